@@ -1,0 +1,160 @@
+/*
+ * sift_mi.h -- C ABI of the MI355X-native SIFT hot path (libsift_mi.so).
+ *
+ * Drop-in boundary for tnibler/sift-features (src/lib.rs @ 2024-10-22).
+ * Plain pointers and sizes only (no HIP, torch or Rust types), so that the
+ * crate's `sift()` can be re-implemented as a thin `extern "C"` shim (see
+ * INTEGRATION.md for the Rust binding a maintainer would add).
+ *
+ * Every entry point names the reference interface it replaces (file:line).
+ * All functions return 0 (SIFT_MI_OK) on success or a negative
+ * sift_mi_status; sift_mi_last_error() describes the last failure of the
+ * calling thread.  The reference is infallible (it panics); the Rust shim
+ * panics with sift_mi_last_error() to keep that signature.
+ *
+ * Threading: a context is not thread-safe; use one context per thread (and
+ * per GPU).  Distinct contexts run concurrently.
+ * Ownership: inputs are borrowed for the duration of a call.  Results live
+ * in context-owned buffers until the next extraction call or destroy.
+ */
+#ifndef SIFT_MI_H
+#define SIFT_MI_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SIFT_MI_DESCRIPTOR_SIZE 128
+
+/* src/lib.rs:48-56 `KeyPoint` (the Rust struct is not repr(C); the shim
+ * converts field by field).  x, y, size are in input-image pixels (the
+ * reference's final `* DELTA_MIN`, src/lib.rs:163-176, is applied). */
+typedef struct {
+    float x, y, size, angle, response;
+} sift_mi_keypoint;
+
+/* src/lib.rs:86-90 `trait Processing`: which blur / resize arithmetic the
+ * pyramid uses.  OPENCV = `OpenCVProcessing` (src/opencv_processing.rs:38-74,
+ * the backend the reference's golden snapshots pin).  IMAGEPROC =
+ * `ImageprocProcessing` (src/lib.rs:993-1007) -- not implemented yet, the
+ * calls return SIFT_MI_EUNSUPPORTED. */
+typedef enum { SIFT_MI_PROFILE_OPENCV = 0, SIFT_MI_PROFILE_IMAGEPROC = 1 } sift_mi_profile;
+
+typedef enum {
+    SIFT_MI_OK = 0,
+    SIFT_MI_EINVAL = -1,      /* bad argument (null pointer, zero size, stride < width ...) */
+    SIFT_MI_ENOMEM = -2,      /* device or host allocation failed */
+    SIFT_MI_EHIP = -3,        /* HIP runtime error (message in sift_mi_last_error) */
+    SIFT_MI_ENODEV = -4,      /* no usable gfx950 device */
+    SIFT_MI_EUNSUPPORTED = -5,/* profile / feature not implemented */
+    SIFT_MI_ESTATE = -6       /* call sequence error (e.g. fetch before extract) */
+} sift_mi_status;
+
+typedef struct sift_mi_ctx sift_mi_ctx;
+
+/* Create a context on HIP device `device_ordinal`; owns one HIP stream and
+ * pooled device buffers.  Fails with SIFT_MI_ENODEV on a non-gfx950 device. */
+int sift_mi_create(int device_ordinal, sift_mi_profile profile, sift_mi_ctx** out);
+void sift_mi_destroy(sift_mi_ctx* ctx);
+
+/* Run subsequent work on an external hipStream_t (e.g. torch's current
+ * stream); NULL restores the context-owned stream. */
+int sift_mi_set_stream(sift_mi_ctx* ctx, void* hip_stream);
+
+/* Images per internal pipeline chunk for batch calls (0 = automatic). */
+int sift_mi_set_chunk(sift_mi_ctx* ctx, uint32_t images_per_chunk);
+
+/* ---- src/lib.rs:71 `sift(img, features_limit) -> SiftResult` ------------
+ * `pixels`: row-major u8 GrayImage, `row_stride` >= width bytes per row.
+ * features_limit < 0 == None.  With a limit the result is ordered by
+ * response, descending (src/lib.rs:156-161); ties keep emission order (the
+ * reference's sort_unstable_by leaves them unspecified).
+ * Writes the keypoint count to *n_keypoints; fetch with sift_mi_fetch. */
+int sift_mi_extract(sift_mi_ctx* ctx, const uint8_t* pixels, uint32_t width, uint32_t height,
+                    size_t row_stride, int64_t features_limit, size_t* n_keypoints);
+
+/* Copy the last result: `kps[cap]`, `desc[cap * 128]` (row i <-> keypoint i,
+ * the (n,128) C-order `Array2<u8>` of SiftResult::descriptors).  Either
+ * pointer may be NULL.  cap must be >= the result size. */
+int sift_mi_fetch(sift_mi_ctx* ctx, sift_mi_keypoint* kps, uint8_t* desc, size_t cap);
+
+/* Emission keys of the last result, for parity checks: bits
+ * [40,64) image, [36,40) octave, [34,36) initial scale, [20,34) initial y,
+ * [6,20) initial x, [0,6) orientation peak -- the reference's emission order
+ * (src/lib.rs:281-294, :324-332, :397-431). */
+int sift_mi_fetch_keys(sift_mi_ctx* ctx, uint64_t* keys, size_t cap);
+
+/* ---- batch of equal-size frames (throughput path; one `sift()` per frame)
+ * `offsets[n+1]` receives the per-frame ranges in the concatenated result. */
+int sift_mi_extract_batch(sift_mi_ctx* ctx, const uint8_t* const* frames, uint32_t n, uint32_t width,
+                          uint32_t height, size_t row_stride, int64_t features_limit, size_t* offsets);
+
+/* Same, frames already resident in device memory: frame i starts at
+ * d_frames + i * frame_pitch (bytes).  The timed path of bench.py. */
+int sift_mi_extract_batch_device(sift_mi_ctx* ctx, const uint8_t* d_frames, size_t frame_pitch, uint32_t n,
+                                 uint32_t width, uint32_t height, size_t row_stride, int64_t features_limit,
+                                 size_t* offsets);
+
+/* Skip the device->host copy of results in batch calls (results stay in
+ * device memory; see sift_mi_device_results).  Default 0 = copy. */
+int sift_mi_set_keep_on_device(sift_mi_ctx* ctx, int keep);
+
+/* Device pointers of the last (single-chunk) result; valid until the next call. */
+int sift_mi_device_results(sift_mi_ctx* ctx, const sift_mi_keypoint** d_kps, const uint8_t** d_desc, size_t* n);
+
+/* ---- src/lib.rs:123-143 `precompute_images` / `PrecomputedImages` ------- */
+int sift_mi_precompute(sift_mi_ctx* ctx, const uint8_t* pixels, uint32_t width, uint32_t height,
+                       size_t row_stride, size_t* n_octaves);
+int sift_mi_octave_dims(sift_mi_ctx* ctx, size_t octave, uint32_t* width, uint32_t* height);
+/* scale_space[octave]: (6, h, w) f32; dog[octave]: (5, h, w) f32 */
+int sift_mi_read_scale_space(sift_mi_ctx* ctx, size_t octave, float* out);
+int sift_mi_read_dog(sift_mi_ctx* ctx, size_t octave, float* out);
+
+/* ---- src/lib.rs:147 `sift_with_precomputed(&PrecomputedImages, limit)` -- */
+int sift_mi_sift_with_precomputed(sift_mi_ctx* ctx, int64_t features_limit, size_t* n_keypoints);
+
+/* ---- src/lib.rs:785 `compute_descriptor(img, x, y, scale, orientation)` -
+ * `img`: host f32 image (h, w); writes 128 bytes. */
+int sift_mi_compute_descriptor(sift_mi_ctx* ctx, const float* img, uint32_t width, uint32_t height, float x,
+                               float y, float scale, float orientation, uint8_t* out);
+
+/* ---- src/lib.rs:86-90 `Processing` ops on host f32 images (op-level parity;
+ * not the performance path) ------------------------------------------------ */
+int sift_mi_gaussian_blur(sift_mi_ctx* ctx, const float* src, uint32_t width, uint32_t height, double sigma,
+                          float* dst);
+int sift_mi_resize_linear(sift_mi_ctx* ctx, const float* src, uint32_t width, uint32_t height, uint32_t dst_width,
+                          uint32_t dst_height, float* dst);
+int sift_mi_resize_nearest(sift_mi_ctx* ctx, const float* src, uint32_t width, uint32_t height, uint32_t dst_width,
+                           uint32_t dst_height, float* dst);
+
+/* ---- measurement ---------------------------------------------------------
+ * Cumulative since the last reset, from HIP events on the context stream.
+ * pyramid_* covers the seed + octave blur/DoG kernels (the HBM-bound stage);
+ * pyramid_bytes is the algorithmic byte count W*H + 44*sum(P_o) per frame. */
+typedef struct {
+    double pyramid_ms;
+    double detect_ms;
+    double orient_ms;
+    double order_ms;
+    double descriptor_ms;
+    double total_ms;
+    uint64_t pyramid_bytes;
+    uint64_t pyramid_launches;
+    uint64_t frames;
+    uint64_t extrema;
+    uint64_t keypoints;
+} sift_mi_stats;
+int sift_mi_get_stats(sift_mi_ctx* ctx, sift_mi_stats* out);
+int sift_mi_reset_stats(sift_mi_ctx* ctx);
+
+/* Library version string and last error (thread-local). */
+const char* sift_mi_version(void);
+const char* sift_mi_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* SIFT_MI_H */

@@ -1,0 +1,179 @@
+// 4x4x8 SIFT descriptors on MI355X: one wave per keypoint, four keypoints
+// per workgroup, the 6x6x8 trilinear histogram kept in the wave's LDS slice.
+//
+// Reference: compute_descriptors / compute_descriptor (src/lib.rs:759-990).
+// Per-sample arithmetic keeps the reference's operand order; the histogram is
+// accumulated with LDS float atomics (ds_add_f32), so the order of additions
+// into a bin differs from the reference's sequential sample order: bins
+// agree to f32 rounding and the final u8 components to +-1 (tolerance stated
+// in tests/test_gpu_parity.py).  The L2 norms use the reference's exact
+// chunk-of-4 summation order (src/lib.rs:957-976).
+#include <float.h>
+
+#include "sift_common.h"
+#include "sift_kernels.h"
+
+namespace siftmi {
+
+constexpr int HIST_FLOATS = 6 * 6 * kDescBins;  // 288
+
+// Wave-cooperative compute_descriptor.  `hist` is this wave's LDS slice.
+__device__ void describe_wave(const float* __restrict__ img, int width, int height, float xf, float yf,
+                              float scale, float orientation, float* hist, uint8_t* __restrict__ out, int lane) {
+    for (int i = lane; i < HIST_FLOATS; i += 64) hist[i] = 0.0f;
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int32_t x = (int32_t)sat_u32(roundf(xf));
+    const int32_t y = (int32_t)sat_u32(roundf(yf));
+    const float BIN_ANGLE_STEP = (float)kDescBins / 360.0f;
+    const float hist_width = kLambdaDescr * scale;
+    const int radius =
+        sat_i32(roundf(kLambdaDescr * scale * 1.41421356237309504880f * (float)(kDescHist + 1) * 0.5f));
+    const float rad = orientation * (3.14159265358979323846f / 180.0f);  // f32::to_radians
+    const float sin_ori = (float)sin((double)rad), cos_ori = (float)cos((double)rad);
+    const float sin_s = sin_ori / hist_width, cos_s = cos_ori / hist_width;
+    const int n = 2 * radius + 1;
+    const int N = n * n;
+    for (int idx = lane; idx < N; idx += 64) {
+        const int iy = idx / n;
+        const int yi = iy - radius, xi = idx - iy * n - radius;
+        const float col_rot = (float)xi * cos_s - (float)yi * sin_s;
+        const float row_rot = (float)xi * sin_s + (float)yi * cos_s;
+        float row_bin = row_rot + (float)(kDescHist / 2);
+        float col_bin = col_rot + (float)(kDescHist / 2);
+        const int32_t ay = y + yi, ax = x + xi;
+        if (!(row_bin > -0.5f && row_bin < (float)kDescHist + 0.5f && col_bin > -0.5f &&
+              col_bin < (float)kDescHist + 0.5f && ay > 0 && ay < height - 1 && ax > 0 && ax < width - 1))
+            continue;
+        const float* rw = img + (size_t)ay * width;
+        const float dx = rw[ax + 1] - rw[ax - 1];
+        const float dy = img[(size_t)(ay - 1) * width + ax] - img[(size_t)(ay + 1) * width + ax];
+        const float wsq = col_rot * col_rot + row_rot * row_rot;
+        const float weight = exp_f32(wsq * (-2.f / (float)(kDescHist * kDescHist)));
+        const double deg = atan2((double)dy, (double)dx) * (180.0 / 3.14159265358979323846);
+        const float ori = (float)fmod(deg + 360.0, 360.0) - orientation;
+        float mag = sqrtf(dx * dx + dy * dy);
+        row_bin = row_bin - 0.5f;
+        col_bin = col_bin - 0.5f;
+        mag = mag * weight;
+        const float obin = ori * BIN_ANGLE_STEP;
+        const float row_floor = floorf(row_bin), col_floor = floorf(col_bin), ori_floor = floorf(obin);
+        const float row_frac = row_bin - row_floor, col_frac = col_bin - col_floor, ori_frac = obin - ori_floor;
+        const float c1 = mag * row_frac, c0 = mag - c1;
+        const float c11 = c1 * col_frac, c10 = c1 - c11;
+        const float c01 = c0 * col_frac, c00 = c0 - c01;
+        const float c111 = c11 * ori_frac, c110 = c11 - c111;
+        const float c101 = c10 * ori_frac, c100 = c10 - c101;
+        const float c011 = c01 * ori_frac, c010 = c01 - c011;
+        const float c001 = c00 * ori_frac, c000 = c00 - c001;
+        const uint32_t r1 = sat_u32(row_floor + 1.f), q1 = sat_u32(col_floor + 1.f);
+        const uint32_t r2 = sat_u32(row_floor + 2.f), q2 = sat_u32(col_floor + 2.f);
+        float of = ori_floor;
+        if (of < 0.f)
+            of = of + (float)kDescBins;
+        else if (of >= (float)kDescBins)
+            of = of - (float)kDescBins;
+        const uint32_t o0 = sat_u32(of);
+        const uint32_t o1 = o0 + 1 >= (uint32_t)kDescBins ? 0u : o0 + 1;
+        float* h11 = hist + (r1 * 6 + q1) * kDescBins;
+        float* h12 = hist + (r1 * 6 + q2) * kDescBins;
+        float* h21 = hist + (r2 * 6 + q1) * kDescBins;
+        float* h22 = hist + (r2 * 6 + q2) * kDescBins;
+        atomicAdd(h11 + o0, c000);
+        atomicAdd(h11 + o1, c001);
+        atomicAdd(h12 + o0, c010);
+        atomicAdd(h12 + o1, c011);
+        atomicAdd(h21 + o0, c100);
+        atomicAdd(h21 + o1, c101);
+        atomicAdd(h22 + o0, c110);
+        atomicAdd(h22 + o1, c111);
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    // lane l < 32 owns flat components 4l..4l+3 (= reference chunk l)
+    float v[4];
+    const int l = lane & 31;
+#pragma unroll
+    for (int j = 0; j < 4; j++) {
+        const int i = 4 * l + j;
+        const int rr = 1 + (i >> 5), cc = 1 + ((i >> 3) & 3), oo = i & 7;
+        v[j] = hist[(rr * 6 + cc) * kDescBins + oo];
+    }
+    float s = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 4; j++) s += v[j] * v[j];
+    float l2 = __shfl(s, 0);
+    for (int c = 1; c < 32; c++) l2 = l2 + __shfl(s, c);
+    l2 = sqrtf(l2);
+    const float cap = l2 * 0.2f;
+#pragma unroll
+    for (int j = 0; j < 4; j++) v[j] = fminf(v[j], cap);
+    s = 0.0f;
+#pragma unroll
+    for (int j = 0; j < 4; j++) s += v[j] * v[j];
+    float l2c = __shfl(s, 0);
+    for (int c = 1; c < 32; c++) l2c = l2c + __shfl(s, c);
+    l2c = sqrtf(l2c);
+    const float norm = 512.0f / fmaxf(l2c, FLT_EPSILON);
+    if (lane < 32) {
+        uint32_t packed = 0;
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            const int32_t q = sat_i32(roundf(v[j] * norm));
+            const uint32_t u = q > 255 ? 255u : (uint32_t)(uint8_t)q;
+            packed |= u << (8 * j);
+        }
+        reinterpret_cast<uint32_t*>(out)[lane] = packed;
+    }
+}
+
+__global__ __launch_bounds__(256) void k_describe(const DescLaunch L) {
+    __shared__ float hist[4][HIST_FLOATS];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t i = blockIdx.x * 4 + wave;
+    if (i >= L.n) return;  // whole wave; no workgroup barrier below
+    const KpRec kp = L.kp[L.idx ? L.idx[i] : i];
+    const int o = kp.octave;
+    const int W = L.ow[o], H = L.oh[o];
+    const float* img =
+        L.gauss[o] + (size_t)(kp.img - L.img_base) * L.gauss_img_stride[o] + (size_t)kp.scale * W * H;
+    // compute_descriptors (src/lib.rs:759-782)
+    const float angle = 360.0f - kp.angle;
+    const float osf = 1.0f / (float)(1u << o);  // 2_f32.powi(-octave)
+    const float kp_size = kp.size * osf;
+    describe_wave(img, W, H, kp.x * osf, kp.y * osf, kp_size, angle, hist[wave], L.out_desc + (size_t)i * kDescSize,
+                  lane);
+    if (lane == 0) {
+        if (L.out_kp) {
+            OutKp k;
+            k.x = kp.x * 0.5f;  // DELTA_MIN (src/lib.rs:163-176)
+            k.y = kp.y * 0.5f;
+            k.size = kp.size * 0.5f;
+            k.angle = kp.angle;
+            k.response = kp.response;
+            L.out_kp[i] = k;
+        }
+        if (L.out_key) L.out_key[i] = kp.key;
+    }
+}
+
+void launch_describe(const DescLaunch& L, hipStream_t st) {
+    if (L.n == 0) return;
+    dim3 grid((L.n + 3) / 4);
+    hipLaunchKernelGGL(k_describe, grid, dim3(256), 0, st, L);
+}
+
+__global__ __launch_bounds__(64) void k_describe_one(const float* img, int w, int h, float x, float y, float scale,
+                                                     float orientation, uint8_t* out) {
+    __shared__ float hist[HIST_FLOATS];
+    describe_wave(img, w, h, x, y, scale, orientation, hist, out, threadIdx.x);
+}
+
+void launch_describe_one(const float* img, int w, int h, float x, float y, float scale, float orientation,
+                         uint8_t* out, hipStream_t st) {
+    hipLaunchKernelGGL(k_describe_one, dim3(1), dim3(64), 0, st, img, w, h, x, y, scale, orientation, out);
+}
+
+}  // namespace siftmi

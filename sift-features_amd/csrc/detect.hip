@@ -1,0 +1,311 @@
+// Keypoint detection on MI355X: DoG extrema + sub-pixel refinement + contrast
+// and edge rejection (k_detect), then 36-bin orientation histograms and
+// reference orientations (k_orient).
+//
+// Reference: find_keypoints / find_extrema_in_dog_img / point_is_local_extremum
+// / interpolate_extremum / extremum_contrast / extremum_is_on_edge /
+// gradient_direction_histogram (src/lib.rs:281-757).
+//
+// Parity: every arithmetic expression keeps the reference's operand order
+// (compiled with -ffp-contract=off).  The orientation histogram accumulates
+// each bin in the reference's sequential row-major sample order (one lane
+// per bin scanning the wave's LDS sample list), so bins are bit-identical to
+// the CPU path and the keypoint count/order does not depend on reduction
+// order.  Emission order (octave, s_init, y_init, x_init, peak) is restored
+// by sorting the 64-bit emission keys afterwards (order.hip).
+#include "sift_common.h"
+#include "sift_kernels.h"
+
+namespace siftmi {
+
+// ---------------------------------------------------------------------------
+// interpolate_extremum (src/lib.rs:525-603) on the DoG stack of one frame.
+// ---------------------------------------------------------------------------
+__device__ bool interpolate(const float* __restrict__ dog, int W, int H, int& scale, int& x, int& y, float& os,
+                            float& ox, float& oy) {
+    const size_t P = (size_t)W * H;
+    for (int it = 0; it < kMaxInterpSteps; it++) {
+        const float* prev = dog + (size_t)(scale - 1) * P;
+        const float* curr = dog + (size_t)scale * P;
+        const float* next = dog + (size_t)(scale + 1) * P;
+#define AT(a, yy, xx) (a)[(size_t)(yy) * W + (xx)]
+        const float g1 = (AT(next, y, x) - AT(prev, y, x)) / 2.f;
+        const float g2 = (AT(curr, y + 1, x) - AT(curr, y - 1, x)) / 2.f;
+        const float g3 = (AT(curr, y, x + 1) - AT(curr, y, x - 1)) / 2.f;
+        const float v2 = AT(curr, y, x) * 2.f;
+        const float h11 = AT(next, y, x) + AT(prev, y, x) - v2;
+        const float h12 = (AT(next, y + 1, x) - AT(next, y - 1, x) - AT(prev, y + 1, x) + AT(prev, y - 1, x)) / 4.f;
+        const float h13 = (AT(next, y, x + 1) - AT(next, y, x - 1) - AT(prev, y, x + 1) + AT(prev, y, x - 1)) / 4.f;
+        const float h22 = AT(curr, y + 1, x) + AT(curr, y - 1, x) - v2;
+        const float h33 = AT(curr, y, x + 1) + AT(curr, y, x - 1) - v2;
+        const float h23 =
+            (AT(curr, y + 1, x + 1) - AT(curr, y + 1, x - 1) - AT(curr, y - 1, x + 1) + AT(curr, y - 1, x - 1)) / 4.f;
+#undef AT
+        const float det =
+            h11 * h22 * h33 - h11 * h23 * h23 - h12 * h12 * h33 + 2.f * h12 * h13 * h23 - h13 * h13 * h22;
+        const float i11 = (h22 * h33 - h23 * h23) / det;
+        const float i12 = (h13 * h23 - h12 * h33) / det;
+        const float i13 = (h12 * h23 - h13 * h22) / det;
+        const float i22 = (h11 * h33 - h13 * h13) / det;
+        const float i23 = (h12 * h13 - h11 * h23) / det;
+        const float i33 = (h11 * h22 - h12 * h12) / det;
+        const float s_ = -(i11 * g1 + i12 * g2 + i13 * g3);
+        const float x_ = -(i13 * g1 + i23 * g2 + i33 * g3);
+        const float y_ = -(i12 * g1 + i22 * g2 + i23 * g3);
+        if (fabsf(s_) < 0.5f && fabsf(x_) < 0.5f && fabsf(y_) < 0.5f) {
+            os = s_;
+            ox = x_;
+            oy = y_;
+            return true;
+        }
+        // `x as isize + offset.round() as isize` (saturating), then bounds
+        const int64_t LIM = (int64_t)1 << 40;
+        const int64_t rx = sat_i64(roundf(x_)), ry = sat_i64(roundf(y_)), rs = sat_i64(roundf(s_));
+        if (rx > LIM || rx < -LIM || ry > LIM || ry < -LIM || rs > LIM || rs < -LIM) return false;
+        const int64_t nx = x + rx, ny = y + ry, ns = scale + rs;
+        if (!(ns >= 1 && ns <= kScalesPerOctave) || nx < kImageBorder || nx >= W - kImageBorder ||
+            ny < kImageBorder || ny >= H - kImageBorder)
+            return false;
+        x = (int)nx;
+        y = (int)ny;
+        scale = (int)ns;
+    }
+    return false;
+}
+
+// ---------------------------------------------------------------------------
+// k_detect: one thread per (x, y), all three scale triples of the octave.
+// The 5 DoG planes of a 64x4 tile (+1 px halo) are staged in LDS; the rare
+// extrema run the refinement chain from global memory.
+// ---------------------------------------------------------------------------
+constexpr int DT_W = 64, DT_H = 4, DT_LW = DT_W + 2, DT_LH = DT_H + 2;
+
+__global__ __launch_bounds__(256) void k_detect(const DetectLaunch L) {
+    __shared__ float t[kDogPerOctave][DT_LH][DT_LW];
+    const int W = L.W, H = L.H;
+    const int x0 = blockIdx.x * DT_W, y0 = blockIdx.y * DT_H;
+    const int b = blockIdx.z;
+    const float* dog = L.dog + (size_t)b * L.img_stride;
+    const size_t P = (size_t)W * H;
+    for (int i = threadIdx.x; i < kDogPerOctave * DT_LH * DT_LW; i += 256) {
+        const int p = i / (DT_LH * DT_LW), r = i - p * (DT_LH * DT_LW);
+        const int ly = r / DT_LW, lx = r - ly * DT_LW;
+        int gy = y0 - 1 + ly, gx = x0 - 1 + lx;
+        gy = gy < 0 ? 0 : (gy >= H ? H - 1 : gy);
+        gx = gx < 0 ? 0 : (gx >= W ? W - 1 : gx);
+        t[p][ly][lx] = dog[(size_t)p * P + (size_t)gy * W + gx];
+    }
+    __syncthreads();
+    const int lx = (threadIdx.x & 63) + 1, ly = (threadIdx.x >> 6) + 1;
+    const int x = x0 + lx - 1, y = y0 + ly - 1;
+    if (x < kImageBorder || x >= W - kImageBorder || y < kImageBorder || y >= H - kImageBorder) return;
+    // threshold = floor(0.5 * 0.04 / 3) = 0 (src/lib.rs:460)
+    const float threshold = floorf(0.5f * kContrastThreshold / (float)kScalesPerOctave);
+    for (int s_in = 1; s_in <= kScalesPerOctave; s_in++) {
+        const float val = t[s_in][ly][lx];
+        if (fabsf(val) <= threshold) continue;
+        bool ok = true;
+        if (val > 0.0f) {
+#pragma unroll
+            for (int p = -1; p <= 1; p++)
+#pragma unroll
+                for (int dy = -1; dy <= 1; dy++)
+#pragma unroll
+                    for (int dx = -1; dx <= 1; dx++)
+                        if (p != 0 || dy != 0 || dx != 0) ok = ok && (val >= t[s_in + p][ly + dy][lx + dx]);
+        } else {
+#pragma unroll
+            for (int p = -1; p <= 1; p++)
+#pragma unroll
+                for (int dy = -1; dy <= 1; dy++)
+#pragma unroll
+                    for (int dx = -1; dx <= 1; dx++)
+                        if (p != 0 || dy != 0 || dx != 0) ok = ok && (val <= t[s_in + p][ly + dy][lx + dx]);
+        }
+        if (!ok) continue;
+        // refinement (src/lib.rs:334-367)
+        int sc = s_in, xi = x, yi = y;
+        float os, ox, oy;
+        if (!interpolate(dog, W, H, sc, xi, yi, os, ox, oy)) continue;
+        const float* prev = dog + (size_t)(sc - 1) * P;
+        const float* curr = dog + (size_t)sc * P;
+        const float* next = dog + (size_t)(sc + 1) * P;
+        const size_t c = (size_t)yi * W + xi;
+        // extremum_contrast (src/lib.rs:606-626)
+        const float g1 = (next[c] - prev[c]) / 2.f;
+        const float g2 = (curr[c + W] - curr[c - W]) / 2.f;
+        const float g3 = (curr[c + 1] - curr[c - 1]) / 2.f;
+        const float interp = os * g1 + oy * g2 + ox * g3;
+        const float contrast = fabsf(curr[c] + interp / 2.f);
+        if (contrast * (float)kScalesPerOctave <= kContrastThreshold) continue;
+        // extremum_is_on_edge (src/lib.rs:630-653)
+        const float v2 = curr[c] * 2.0f;
+        const float h11 = curr[c + W] + curr[c - W] - v2;
+        const float d22 = curr[c + 1] + curr[c - 1] - v2;
+        const float h12 = (curr[c + W + 1] - curr[c + W - 1] - curr[c - W + 1] + curr[c - W - 1]) / 4.f;
+        const float tr = d22 + h11;
+        const float det = d22 * h11 - h12 * h12;
+        if (det <= 0.f) continue;
+        if ((tr * tr * kEdgeThreshold) > (kEdgeThreshold + 1.0f) * (kEdgeThreshold + 1.0f) * det) continue;
+        const uint32_t slot = atomicAdd(L.counter, 1u);
+        if (slot >= L.cap) continue;
+        ExtRec e;
+        e.key = make_key((uint32_t)(L.img_base + b), (uint32_t)L.octave, (uint32_t)s_in, (uint32_t)y, (uint32_t)x);
+        e.img = L.img_base + b;
+        e.octave = L.octave;
+        e.scale = sc;
+        e.x = xi;
+        e.y = yi;
+        e.off_s = os;
+        e.off_x = ox;
+        e.off_y = oy;
+        e.response = contrast;
+        e.pad = 0;
+        L.out[slot] = e;
+    }
+}
+
+void launch_detect(const DetectLaunch& L, hipStream_t st) {
+    dim3 grid((L.W + DT_W - 1) / DT_W, (L.H + DT_H - 1) / DT_H, L.n_img);
+    hipLaunchKernelGGL(k_detect, grid, dim3(256), 0, st, L);
+}
+
+// ---------------------------------------------------------------------------
+// k_orient: one wave per accepted extremum (4 per workgroup).
+// gradient_direction_histogram (src/lib.rs:657-757) + peak selection
+// (src/lib.rs:369-431).  Samples are evaluated 64 at a time into the wave's
+// LDS list in the reference's row-major order; lane k < 36 then sums bin k
+// sequentially over the list (bit-identical to `raw_hist[bin + 2] += w*mag`).
+// ---------------------------------------------------------------------------
+constexpr int OR_LDS = 1092;
+
+__global__ __launch_bounds__(256) void k_orient(const OrientLaunch L) {
+    __shared__ __attribute__((aligned(16))) float sval[4][OR_LDS];
+    __shared__ __attribute__((aligned(16))) uint8_t sbin[4][OR_LDS];
+    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
+    const uint32_t r = blockIdx.x * 4 + wave;
+    const bool active = r < L.n_ext;
+    ExtRec e;
+    int W = 1, H = 1, radius = 0, n = 1, N = 0;
+    float kp_scale = 0.f, kp_x = 0.f, kp_y = 0.f, osf = 1.f;
+    const float* img = nullptr;
+    if (active) {
+        e = L.ext[r];
+        W = L.ow[e.octave];
+        H = L.oh[e.octave];
+        img = L.gauss[e.octave] + (size_t)(e.img - L.img_base) * L.gauss_img_stride[e.octave] +
+              (size_t)e.scale * W * H;
+        osf = (float)(1u << e.octave);  // 2_f32.powi(octave)
+        kp_scale = 0.8f * pow2_f32(((float)e.scale + e.off_s) / (float)kScalesPerOctave) * 2.f;
+        kp_x = ((float)e.x + e.off_x) * osf;
+        kp_y = ((float)e.y + e.off_y) * osf;
+        radius = sat_i32(roundf(3.f * kLambdaOri * kp_scale));
+        if (radius > 16) radius = 16;  // unreachable: kp_scale < 3.6 (assert-equivalent guard)
+        if (radius < 0) radius = 0;
+        n = 2 * radius + 1;
+        N = n * n;
+        const float sigma = kLambdaOri * kp_scale;
+        const float gws = -1.0f / (2.0f * sigma * sigma);
+        const float bin_step = (float)kOriBins / (3.14159265358979323846f * 2.f);
+        const int x = e.x, y = e.y;
+        for (int idx = lane; idx < N; idx += 64) {
+            const int iy = idx / n;
+            const int yp = iy - radius, xp = idx - iy * n - radius;
+            const int yy = y + yp, xx = x + xp;
+            uint8_t bin = 0xff;
+            float val = 0.0f;
+            if (yy > 0 && yy < H - 1 && xx > 0 && xx < W - 1) {
+                const float* rw = img + (size_t)yy * W;
+                const float dx = rw[xx + 1] - rw[xx - 1];
+                const float dy = img[(size_t)(yy - 1) * W + xx] - img[(size_t)(yy + 1) * W + xx];
+                const float wexp = (float)(yp * yp + xp * xp) * gws;
+                const float weight = exp_f32(wexp);
+                const float mag = sqrtf(dx * dx + dy * dy);
+                const float ori = (float)atan2((double)dy, (double)dx);
+                int bi = sat_i32(roundf(bin_step * ori));
+                if (bi >= kOriBins)
+                    bi -= kOriBins;
+                else if (bi < 0)
+                    bi += kOriBins;
+                bin = (uint8_t)bi;
+                val = weight * mag;
+            }
+            sval[wave][idx] = val;
+            sbin[wave][idx] = bin;
+        }
+    }
+    __syncthreads();
+    if (!active) return;
+    // sequential per-bin sums (lane = bin)
+    float acc = 0.0f;
+    {
+        const float4* v4 = reinterpret_cast<const float4*>(sval[wave]);
+        const uint32_t* b4 = reinterpret_cast<const uint32_t*>(sbin[wave]);
+        const uint32_t me = (uint32_t)lane;
+        int j = 0;
+        for (; j + 4 <= N; j += 4) {
+            const float4 v = v4[j >> 2];
+            const uint32_t bb = b4[j >> 2];
+            acc += ((bb & 0xff) == me) ? v.x : 0.0f;
+            acc += (((bb >> 8) & 0xff) == me) ? v.y : 0.0f;
+            acc += (((bb >> 16) & 0xff) == me) ? v.z : 0.0f;
+            acc += ((bb >> 24) == me) ? v.w : 0.0f;
+        }
+        for (; j < N; j++) acc += ((uint32_t)sbin[wave][j] == me) ? sval[wave][j] : 0.0f;
+    }
+    // circular [1,4,6,4,1]/16 smoothing (src/lib.rs:742-755)
+    const int k = lane < kOriBins ? lane : 0;
+    const float rm2 = __shfl(acc, (k + kOriBins - 2) % kOriBins);
+    const float rm1 = __shfl(acc, (k + kOriBins - 1) % kOriBins);
+    const float rp1 = __shfl(acc, (k + 1) % kOriBins);
+    const float rp2 = __shfl(acc, (k + 2) % kOriBins);
+    const float r0 = __shfl(acc, k);
+    const float h = (rm2 + rp2) * (1.f / 16.f) + (rm1 + rp1) * (4.f / 16.f) + r0 * 6.f / 16.f;
+    // max over the 36 bins
+    float m = lane < kOriBins ? h : -1.0f;
+#pragma unroll
+    for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+    const float thr = m * kOriPeakRatio;
+    const float hm = __shfl(h, (k + kOriBins - 1) % kOriBins);
+    const float hp = __shfl(h, (k + 1) % kOriBins);
+    const bool peak = lane < kOriBins && h > hm && h > hp && h >= thr;
+    const uint64_t mask = __ballot(peak);
+    const uint32_t npk = (uint32_t)__popcll(mask);
+    if (npk == 0) return;
+    uint32_t base = 0;
+    if (lane == 0) {
+        base = atomicAdd(L.counter, npk);
+        atomicAdd(L.per_img + (e.img - L.img_base), npk);
+    }
+    base = __shfl(base, 0);
+    if (!peak) return;
+    const uint32_t slot = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+    if (slot >= L.cap) return;
+    const float interp = (hm - hp) / (hm - 2.0f * h + hp);
+    float bin = (float)k + 0.5f * interp;
+    if (bin < 0.0f)
+        bin = (float)kOriBins + bin;
+    else if (bin >= (float)kOriBins)
+        bin = bin - (float)kOriBins;
+    KpRec kp;
+    kp.key = e.key | (uint64_t)k;
+    kp.img = e.img;
+    kp.octave = e.octave;
+    kp.scale = e.scale;
+    kp.pad = 0;
+    kp.x = kp_x;
+    kp.y = kp_y;
+    kp.size = kp_scale * osf;
+    kp.angle = 360.0f - (360.0f / (float)kOriBins) * bin;
+    kp.response = e.response;
+    kp.pad2 = 0.f;
+    L.out[slot] = kp;
+}
+
+void launch_orient(const OrientLaunch& L, hipStream_t st) {
+    if (L.n_ext == 0) return;
+    dim3 grid((L.n_ext + 3) / 4);
+    hipLaunchKernelGGL(k_orient, grid, dim3(256), 0, st, L);
+}
+
+}  // namespace siftmi

@@ -1,0 +1,1017 @@
+// libsift_mi.so host side: the C ABI of include/sift_mi.h over the HIP
+// kernels in this directory.  Mirrors the reference's pipeline
+// (src/lib.rs:71-177): precompute_images -> find_keypoints -> [limit] ->
+// compute_descriptors -> KeyPoint mapping, batched over equal-size frames.
+//
+// Host arithmetic that feeds the device (octave count, blur sigmas, OpenCV
+// kernel taps, resize coefficient tables) is computed exactly as the
+// reference / OpenCV compute it (IEEE double / f32, glibc libm).
+#include <hip/hip_runtime.h>
+
+#include <algorithm>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include <vector>
+
+#include "../../include/sift_mi.h"
+#include "sift_common.h"
+#include "sift_kernels.h"
+
+using namespace siftmi;
+
+namespace {
+
+thread_local std::string g_err;
+
+int fail(int code, const std::string& msg) {
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                                     \
+    do {                                                                                                 \
+        hipError_t e_ = (expr);                                                                          \
+        if (e_ != hipSuccess) return fail(SIFT_MI_EHIP, std::string(#expr) + ": " + hipGetErrorString(e_)); \
+    } while (0)
+
+#define CHK(expr)            \
+    do {                     \
+        int rc_ = (expr);    \
+        if (rc_) return rc_; \
+    } while (0)
+
+template <class T>
+struct DevBuf {
+    T* p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t n) {
+        if (n <= cap && p) return 0;
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+        const size_t bytes = std::max<size_t>(n, 1) * sizeof(T);
+        if (hipMalloc(&p, bytes) != hipSuccess) {
+            p = nullptr;
+            return fail(SIFT_MI_ENOMEM, "hipMalloc(" + std::to_string(bytes) + ") failed");
+        }
+        cap = std::max<size_t>(n, 1);
+        return 0;
+    }
+    void release() {
+        if (p) (void)hipFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+template <class T>
+struct PinBuf {
+    T* p = nullptr;
+    size_t cap = 0;
+    int ensure(size_t n, bool keep = false) {
+        if (n <= cap && p) return 0;
+        size_t ncap = std::max<size_t>({n, 1, cap * 2});
+        T* q = nullptr;
+        if (hipHostMalloc(&q, ncap * sizeof(T), hipHostMallocDefault) != hipSuccess)
+            return fail(SIFT_MI_ENOMEM, "hipHostMalloc failed");
+        if (keep && p && cap) std::memcpy(q, p, cap * sizeof(T));
+        if (p) (void)hipHostFree(p);
+        p = q;
+        cap = ncap;
+        return 0;
+    }
+    void release() {
+        if (p) (void)hipHostFree(p);
+        p = nullptr;
+        cap = 0;
+    }
+};
+
+// ---------------------------------------------------------------------------
+// Reference host arithmetic
+// ---------------------------------------------------------------------------
+// n_octaves = round(log2(min(2W,2H)) - 2) as usize + 1  (src/lib.rs:133-134)
+int n_octaves_for(uint32_t w, uint32_t h) {
+    const uint32_t m = std::min(2 * w, 2 * h);
+    const float f = roundf(log2f((float)m) - 2.0f);
+    const size_t u = (f > 0.0f) ? (size_t)f : 0;  // saturating `as usize`
+    return (int)u + 1;
+}
+
+double powi_f64(double a, int b) {  // compiler-rt __powidf2 (llvm.powi)
+    const bool recip = b < 0;
+    double r = 1;
+    for (;;) {
+        if (b & 1) r *= a;
+        b /= 2;
+        if (b == 0) break;
+        a *= a;
+    }
+    return recip ? 1 / r : r;
+}
+
+// src/lib.rs:220-229
+void octave_sigmas(double* sig) {
+    const double m = std::pow(2.0, 2.0 / kScalesPerOctave);
+    for (int s = 0; s < kImagesPerOctave; s++) {
+        const double a = powi_f64(m, s - 1);
+        const double b = a * m;
+        sig[s] = std::sqrt(b - a) * 0.8 * 2.0;
+    }
+}
+// src/lib.rs:207
+double seed_sigma() { return std::sqrt(0.8 * 0.8 - 0.5 * 0.5) * 2.0; }
+
+// cv::GaussianBlur(Size(), sigma), CV_32F: ksize = cvRound(sigma*4*2+1)|1;
+// taps from getGaussianKernelBitExact (IEEE double), cast to f32.
+int cv_blur_taps(double sigma, BlurTaps* t) {
+    const int n = ((int)std::lrint(sigma * 4 * 2 + 1)) | 1;
+    const int r = n / 2;
+    if (r < 1 || r > 24) return -1;
+    const double scale2X = -0.125 / (sigma * sigma);
+    const int n2 = (n - 1) / 2;
+    double values[64];
+    double sum = 0;
+    for (int i = 0, x = 1 - n; i < n2; i++, x += 2) {
+        const double v = std::exp((double)(x * x) * scale2X);
+        values[i] = v;
+        sum += v;
+    }
+    sum *= 2;
+    sum += 1;
+    const double mul1 = 1 / sum;
+    std::memset(t, 0, sizeof(*t));
+    t->k[0] = (float)(1.0 * mul1);
+    for (int i = 0; i < n2; i++) t->k[r - i] = (float)(values[i] * mul1);
+    return r;
+}
+
+// cv::resize INTER_LINEAR coefficient table (resizeGeneric_)
+void cv_linear_coeffs(int ssz, int dsz, std::vector<int>& ofs, std::vector<float>& a0, std::vector<float>& a1,
+                      int* lim) {
+    const double inv = (double)dsz / ssz;
+    const double scale = 1. / inv;
+    int xmax = dsz;
+    ofs.resize(dsz);
+    a0.resize(dsz);
+    a1.resize(dsz);
+    for (int d = 0; d < dsz; d++) {
+        float f = (float)((d + 0.5) * scale - 0.5);
+        int s = (int)floorf(f);
+        f -= (float)s;
+        if (s < 0) {
+            f = 0;
+            s = 0;
+        }
+        if (s + 1 >= ssz) {
+            if (d < xmax) xmax = d;
+            if (s >= ssz - 1) {
+                f = 0;
+                s = ssz - 1;
+            }
+        }
+        ofs[d] = s;
+        a0[d] = 1.f - f;
+        a1[d] = f;
+    }
+    *lim = xmax;
+}
+
+// cv::resize INTER_NEAREST offsets (resizeNN)
+void cv_nearest_ofs(int ssz, int dsz, std::vector<int>& ofs) {
+    const double ifx = 1. / ((double)dsz / ssz);
+    ofs.resize(dsz);
+    for (int d = 0; d < dsz; d++) {
+        const int s = (int)std::floor(d * ifx);
+        ofs[d] = std::min(s, ssz - 1);
+    }
+}
+
+struct ResizeTabDev {
+    DevBuf<int> xofs, yofs;
+    DevBuf<float> xa0, xa1, ya0, ya1;
+    ResizeTab tab{};
+    int upload(int sw, int sh, int dw, int dh, hipStream_t st) {
+        std::vector<int> xo, yo;
+        std::vector<float> xa, xb, ya, yb;
+        int xmax = 0, ymax = 0;
+        cv_linear_coeffs(sw, dw, xo, xa, xb, &xmax);
+        cv_linear_coeffs(sh, dh, yo, ya, yb, &ymax);
+        CHK(xofs.ensure(dw));
+        CHK(xa0.ensure(dw));
+        CHK(xa1.ensure(dw));
+        CHK(yofs.ensure(dh));
+        CHK(ya0.ensure(dh));
+        CHK(ya1.ensure(dh));
+        HIPCHK(hipMemcpyAsync(xofs.p, xo.data(), dw * sizeof(int), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(xa0.p, xa.data(), dw * sizeof(float), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(xa1.p, xb.data(), dw * sizeof(float), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(yofs.p, yo.data(), dh * sizeof(int), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(ya0.p, ya.data(), dh * sizeof(float), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(ya1.p, yb.data(), dh * sizeof(float), hipMemcpyHostToDevice, st));
+        HIPCHK(hipStreamSynchronize(st));  // host vectors go out of scope
+        tab.xofs = xofs.p;
+        tab.xa0 = xa0.p;
+        tab.xa1 = xa1.p;
+        tab.yofs = yofs.p;
+        tab.ya0 = ya0.p;
+        tab.ya1 = ya1.p;
+        tab.xmax = xmax;
+        return 0;
+    }
+    void release() {
+        xofs.release();
+        yofs.release();
+        xa0.release();
+        xa1.release();
+        ya0.release();
+        ya1.release();
+    }
+};
+
+// Frame geometry + pyramid arena for `chunk` frames of w x h.
+struct Plan {
+    uint32_t w = 0, h = 0, chunk = 0;
+    int n_oct = 0;
+    std::vector<int> ow, oh;
+    std::vector<size_t> P;           // pixels per octave image
+    std::vector<size_t> goff, doff;  // float offsets of octave arenas
+    DevBuf<float> arena;             // [G_0 | D_0 | G_1 | D_1 ...], each chunk-major
+    ResizeTabDev seed_tab;
+    DevBuf<const float*> d_gauss;
+    DevBuf<size_t> d_gstride;
+    DevBuf<int> d_ow, d_oh;
+    BlurTaps seed_taps{};
+    int seed_r = 0;
+    BlurTaps oct_taps[kImagesPerOctave]{};
+    int oct_r[kImagesPerOctave]{};
+    uint64_t algo_bytes_per_frame = 0;
+
+    float* gauss(int o) { return arena.p + goff[o]; }
+    float* dog(int o) { return arena.p + doff[o]; }
+    size_t gstride(int o) const { return (size_t)kImagesPerOctave * P[o]; }
+    size_t dstride(int o) const { return (size_t)kDogPerOctave * P[o]; }
+
+    void release() {
+        arena.release();
+        seed_tab.release();
+        d_gauss.release();
+        d_gstride.release();
+        d_ow.release();
+        d_oh.release();
+        w = h = chunk = 0;
+        n_oct = 0;
+    }
+};
+
+}  // namespace
+
+struct sift_mi_ctx {
+    int device = 0;
+    sift_mi_profile profile = SIFT_MI_PROFILE_OPENCV;
+    hipStream_t own = nullptr;
+    hipStream_t stream = nullptr;
+    uint32_t chunk_override = 0;
+    int keep_on_device = 0;
+    Plan plan;
+    DevBuf<uint8_t> staging;  // host-sourced frames
+    // detection / description buffers
+    DevBuf<ExtRec> ext;
+    DevBuf<KpRec> kp;
+    DevBuf<uint32_t> counters;  // [0] extrema, [1] keypoints, [2..] per frame
+    DevBuf<uint64_t> keys_a, keys_b;
+    DevBuf<uint32_t> vals_a, vals_b, fin;
+    DevBuf<uint8_t> sort_tmp;
+    DevBuf<uint32_t> seg_off, out_off;
+    DevBuf<uint8_t> use_resp;
+    DevBuf<OutKp> out_kp;
+    DevBuf<uint8_t> out_desc;
+    DevBuf<uint64_t> out_key;
+    // host results (pinned)
+    PinBuf<OutKp> h_kp;
+    PinBuf<uint8_t> h_desc;
+    PinBuf<uint64_t> h_key;
+    PinBuf<uint32_t> h_counts;
+    size_t n_result = 0;
+    bool have_result = false;
+    bool have_pyramid = false;  // single-frame precompute state
+    size_t dev_result_n = 0;
+    // timing
+    hipEvent_t ev[8] = {};
+    sift_mi_stats stats{};
+};
+
+namespace {
+
+int set_device(sift_mi_ctx* c) {
+    HIPCHK(hipSetDevice(c->device));
+    return 0;
+}
+
+uint32_t auto_chunk(const Plan& p_probe_w_h, uint32_t w, uint32_t h, uint32_t n) {
+    (void)p_probe_w_h;
+    // ~16 GB of pyramid per chunk (288 GB HBM per MI355X leaves room for 2+)
+    double sum_p = 0;
+    uint32_t ow = 2 * w, oh = 2 * h;
+    const int no = n_octaves_for(w, h);
+    for (int o = 0; o < no; o++) {
+        sum_p += (double)ow * oh;
+        ow /= 2;
+        oh /= 2;
+    }
+    const double per_frame = 44.0 * sum_p;
+    uint32_t c = (uint32_t)std::max(1.0, std::floor(16e9 / per_frame));
+    c = std::min<uint32_t>(c, 64);
+    return std::max<uint32_t>(1, std::min(c, n));
+}
+
+int ensure_plan(sift_mi_ctx* c, uint32_t w, uint32_t h, uint32_t chunk) {
+    Plan& p = c->plan;
+    if (p.w == w && p.h == h && p.chunk >= chunk && p.arena.p) return 0;
+    if (!(p.w == w && p.h == h)) p.release();
+    p.w = w;
+    p.h = h;
+    p.chunk = chunk;
+    p.n_oct = n_octaves_for(w, h);
+    p.ow.assign(p.n_oct, 0);
+    p.oh.assign(p.n_oct, 0);
+    p.P.assign(p.n_oct, 0);
+    p.goff.assign(p.n_oct, 0);
+    p.doff.assign(p.n_oct, 0);
+    int ow = 2 * (int)w, oh = 2 * (int)h;
+    size_t total = 0;
+    uint64_t sum_p = 0;
+    for (int o = 0; o < p.n_oct; o++) {
+        if (ow < 1 || oh < 1) return fail(SIFT_MI_EINVAL, "image too small for the octave count");
+        p.ow[o] = ow;
+        p.oh[o] = oh;
+        p.P[o] = (size_t)ow * oh;
+        sum_p += p.P[o];
+        p.goff[o] = total;
+        total += (size_t)chunk * kImagesPerOctave * p.P[o];
+        p.doff[o] = total;
+        total += (size_t)chunk * kDogPerOctave * p.P[o];
+        total = (total + 63) & ~(size_t)63;  // 256-B aligned octave arenas
+        if (o + 1 < p.n_oct) {
+            // nearest 1/2 must be source pixel (2x, 2y) for the fused epilogue
+            std::vector<int> xo, yo;
+            cv_nearest_ofs(ow, ow / 2, xo);
+            cv_nearest_ofs(oh, oh / 2, yo);
+            for (int i = 0; i < (int)xo.size(); i++)
+                if (xo[i] != 2 * i) return fail(SIFT_MI_EUNSUPPORTED, "nearest offset != 2x");
+            for (int i = 0; i < (int)yo.size(); i++)
+                if (yo[i] != 2 * i) return fail(SIFT_MI_EUNSUPPORTED, "nearest offset != 2y");
+        }
+        ow /= 2;
+        oh /= 2;
+    }
+    p.algo_bytes_per_frame = (uint64_t)w * h + 44ull * sum_p;
+    CHK(p.arena.ensure(total));
+    hipStream_t st = c->stream;
+    CHK(p.seed_tab.upload((int)w, (int)h, 2 * (int)w, 2 * (int)h, st));
+    std::vector<const float*> gp(p.n_oct);
+    std::vector<size_t> gs(p.n_oct);
+    for (int o = 0; o < p.n_oct; o++) {
+        gp[o] = p.gauss(o);
+        gs[o] = p.gstride(o);
+    }
+    CHK(p.d_gauss.ensure(p.n_oct));
+    CHK(p.d_gstride.ensure(p.n_oct));
+    CHK(p.d_ow.ensure(p.n_oct));
+    CHK(p.d_oh.ensure(p.n_oct));
+    HIPCHK(hipMemcpyAsync(p.d_gauss.p, gp.data(), p.n_oct * sizeof(float*), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(p.d_gstride.p, gs.data(), p.n_oct * sizeof(size_t), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(p.d_ow.p, p.ow.data(), p.n_oct * sizeof(int), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(p.d_oh.p, p.oh.data(), p.n_oct * sizeof(int), hipMemcpyHostToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));
+    p.seed_r = cv_blur_taps(seed_sigma(), &p.seed_taps);
+    double sig[kImagesPerOctave];
+    octave_sigmas(sig);
+    for (int s = 1; s < kImagesPerOctave; s++) p.oct_r[s] = cv_blur_taps(sig[s], &p.oct_taps[s]);
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Stage 1: Gaussian scale space + DoG for n frames (device-resident u8)
+// ---------------------------------------------------------------------------
+int run_pyramid(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, size_t row_stride, uint32_t n) {
+    Plan& p = c->plan;
+    hipStream_t st = c->stream;
+    // seed: 2x bilinear into plane 5 of octave 0 (scratch), then blur -> plane 0
+    float* g0 = p.gauss(0);
+    const size_t P0 = p.P[0];
+    launch_upsample2x(d_frames, frame_pitch, row_stride, (int)p.w, (int)p.h, p.seed_tab.tab, g0 + 5 * P0,
+                      p.gstride(0), (int)n, st);
+    BlurLaunch L{};
+    L.src = g0 + 5 * P0;
+    L.src_img_stride = p.gstride(0);
+    L.dst = g0;
+    L.dst_img_stride = p.gstride(0);
+    L.W = p.ow[0];
+    L.H = p.oh[0];
+    L.n_img = (int)n;
+    L.taps = p.seed_taps;
+    if (launch_blur(p.seed_r, L, st)) return fail(SIFT_MI_EUNSUPPORTED, "seed blur radius");
+    uint64_t launches = 2;
+    for (int o = 0; o < p.n_oct; o++) {
+        float* G = p.gauss(o);
+        float* D = p.dog(o);
+        const size_t P = p.P[o];
+        for (int s = 1; s < kImagesPerOctave; s++) {
+            BlurLaunch B{};
+            B.src = G + (size_t)(s - 1) * P;
+            B.src_img_stride = p.gstride(o);
+            B.dst = G + (size_t)s * P;
+            B.dst_img_stride = p.gstride(o);
+            B.dog = D + (size_t)(s - 1) * P;
+            B.dog_img_stride = p.dstride(o);
+            if (s == 3 && o + 1 < p.n_oct) {
+                B.nxt = p.gauss(o + 1);
+                B.nxt_img_stride = p.gstride(o + 1);
+                B.wn = p.ow[o + 1];
+                B.hn = p.oh[o + 1];
+            }
+            B.W = p.ow[o];
+            B.H = p.oh[o];
+            B.n_img = (int)n;
+            B.taps = p.oct_taps[s];
+            if (launch_blur(p.oct_r[s], B, st)) return fail(SIFT_MI_EUNSUPPORTED, "octave blur radius");
+            launches++;
+        }
+    }
+    HIPCHK(hipGetLastError());
+    c->stats.pyramid_launches += launches;
+    c->stats.pyramid_bytes += p.algo_bytes_per_frame * n;
+    return 0;
+}
+
+// ---------------------------------------------------------------------------
+// Stage 2-4: detection, orientation, ordering, descriptors for the n frames
+// currently in the pyramid arena.  Appends results (global frame offset
+// `frame_base`) to the host result buffers unless keep_on_device.
+// ---------------------------------------------------------------------------
+int run_keypoints(sift_mi_ctx* c, uint32_t n, int64_t limit, uint32_t frame_base, size_t* offsets_out,
+                  size_t result_base) {
+    Plan& p = c->plan;
+    hipStream_t st = c->stream;
+    uint64_t sum_p = 0;
+    for (int o = 0; o < p.n_oct; o++) sum_p += p.P[o];
+    size_t cap_ext = std::max<size_t>(4096, (size_t)(sum_p * n / 48));
+    if (c->ext.cap > cap_ext) cap_ext = c->ext.cap;
+    CHK(c->counters.ensure(2 + n));
+    uint32_t n_ext = 0;
+    for (int attempt = 0; attempt < 3; attempt++) {
+        CHK(c->ext.ensure(cap_ext));
+        HIPCHK(hipMemsetAsync(c->counters.p, 0, (2 + n) * sizeof(uint32_t), st));
+        for (int o = 0; o < p.n_oct; o++) {
+            if (p.oh[o] < 2 * kImageBorder || p.ow[o] < 2 * kImageBorder) continue;  // src/lib.rs:315
+            DetectLaunch D{};
+            D.dog = p.dog(o);
+            D.img_stride = p.dstride(o);
+            D.W = p.ow[o];
+            D.H = p.oh[o];
+            D.octave = o;
+            D.n_img = (int)n;
+            D.img_base = 0;
+            D.out = c->ext.p;
+            D.counter = c->counters.p;
+            D.cap = (uint32_t)c->ext.cap;
+            launch_detect(D, st);
+        }
+        HIPCHK(hipGetLastError());
+        CHK(c->h_counts.ensure(2 + n));
+        HIPCHK(hipMemcpyAsync(c->h_counts.p, c->counters.p, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        n_ext = c->h_counts.p[0];
+        if (n_ext <= c->ext.cap) break;
+        cap_ext = (size_t)n_ext + n_ext / 4 + 1024;
+        if (attempt == 2) return fail(SIFT_MI_ENOMEM, "extremum buffer overflow");
+    }
+    HIPCHK(hipEventRecord(c->ev[2], st));
+    size_t cap_kp = std::max<size_t>(2 * (size_t)n_ext + 1024, c->kp.cap);
+    uint32_t n_kp = 0;
+    for (int attempt = 0; attempt < 3; attempt++) {
+        CHK(c->kp.ensure(cap_kp));
+        HIPCHK(hipMemsetAsync(c->counters.p + 1, 0, (1 + n) * sizeof(uint32_t), st));
+        OrientLaunch O{};
+        O.ext = c->ext.p;
+        O.n_ext = n_ext;
+        O.gauss = p.d_gauss.p;
+        O.gauss_img_stride = p.d_gstride.p;
+        O.ow = p.d_ow.p;
+        O.oh = p.d_oh.p;
+        O.out = c->kp.p;
+        O.counter = c->counters.p + 1;
+        O.per_img = c->counters.p + 2;
+        O.img_base = 0;
+        O.cap = (uint32_t)c->kp.cap;
+        launch_orient(O, st);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(c->h_counts.p, c->counters.p, (2 + n) * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+        n_kp = c->h_counts.p[1];
+        if (n_kp <= c->kp.cap) break;
+        cap_kp = (size_t)n_kp + n_kp / 4 + 1024;
+        if (attempt == 2) return fail(SIFT_MI_ENOMEM, "keypoint buffer overflow");
+    }
+    HIPCHK(hipEventRecord(c->ev[3], st));
+    std::vector<uint32_t> cnt(c->h_counts.p + 2, c->h_counts.p + 2 + n);
+    // emission order: radix sort of the keys
+    CHK(c->keys_a.ensure(n_kp));
+    CHK(c->keys_b.ensure(n_kp));
+    CHK(c->vals_a.ensure(n_kp));
+    CHK(c->vals_b.ensure(n_kp));
+    int img_bits = 1;
+    while ((1u << img_bits) < n) img_bits++;
+    const int end_bit = kKeyImgShift + img_bits;
+    size_t tmp = sort_pairs_u64(nullptr, 0, c->keys_a.p, c->keys_b.p, c->vals_a.p, c->vals_b.p, n_kp, end_bit, st);
+    if (!tmp && n_kp) return fail(SIFT_MI_EHIP, "radix sort sizing failed");
+    CHK(c->sort_tmp.ensure(tmp));
+    launch_make_sort_keys(c->kp.p, n_kp, c->keys_a.p, c->vals_a.p, st);
+    if (n_kp && !sort_pairs_u64(c->sort_tmp.p, c->sort_tmp.cap, c->keys_a.p, c->keys_b.p, c->vals_a.p, c->vals_b.p,
+                                n_kp, end_bit, st))
+        return fail(SIFT_MI_EHIP, "radix sort failed");
+    const uint32_t* order = c->vals_b.p;  // emission order -> kp index
+    // features_limit (src/lib.rs:156-161)
+    std::vector<uint32_t> out_cnt(cnt);
+    bool any_limit = false;
+    if (limit >= 0)
+        for (uint32_t f = 0; f < n; f++)
+            if ((uint64_t)limit < cnt[f]) {
+                out_cnt[f] = (uint32_t)limit;
+                any_limit = true;
+            }
+    uint32_t n_out = 0;
+    for (uint32_t f = 0; f < n; f++) n_out += out_cnt[f];
+    if (any_limit) {
+        std::vector<uint32_t> seg(n), oo(n);
+        std::vector<uint8_t> ur(n);
+        uint32_t a = 0, b = 0;
+        for (uint32_t f = 0; f < n; f++) {
+            seg[f] = a;
+            oo[f] = b;
+            ur[f] = (uint64_t)limit < cnt[f];
+            a += cnt[f];
+            b += out_cnt[f];
+        }
+        launch_make_resp_keys(c->kp.p, order, n_kp, 0, c->keys_a.p, c->vals_a.p, st);
+        const int rb = 32 + img_bits;
+        size_t tmp2 = sort_pairs_u64(nullptr, 0, c->keys_a.p, c->keys_b.p, c->vals_a.p, c->fin.p, n_kp, rb, st);
+        CHK(c->sort_tmp.ensure(tmp2));
+        CHK(c->fin.ensure(n_kp));
+        // stable sort: response-descending within each frame, emission order on ties
+        CHK(c->vals_a.ensure(n_kp));
+        DevBuf<uint32_t>& resp_order = c->fin;
+        if (!sort_pairs_u64(c->sort_tmp.p, c->sort_tmp.cap, c->keys_a.p, c->keys_b.p, c->vals_a.p, resp_order.p, n_kp,
+                            rb, st))
+            return fail(SIFT_MI_EHIP, "response sort failed");
+        CHK(c->seg_off.ensure(n));
+        CHK(c->out_off.ensure(n));
+        CHK(c->use_resp.ensure(n));
+        HIPCHK(hipMemcpyAsync(c->seg_off.p, seg.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(c->out_off.p, oo.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(c->use_resp.p, ur.data(), n, hipMemcpyHostToDevice, st));
+        // final index list -> keys_b reused as u32 storage is unsafe; use vals_a
+        launch_select(order, resp_order.p, c->seg_off.p, c->out_off.p, c->use_resp.p, (int)n, n_out, c->vals_a.p, st);
+        order = c->vals_a.p;
+        HIPCHK(hipStreamSynchronize(st));  // seg/oo/ur host vectors
+    }
+    HIPCHK(hipEventRecord(c->ev[4], st));
+    // descriptors
+    CHK(c->out_kp.ensure(n_out));
+    CHK(c->out_desc.ensure((size_t)n_out * kDescSize));
+    CHK(c->out_key.ensure(n_out));
+    DescLaunch DL{};
+    DL.kp = c->kp.p;
+    DL.idx = order;
+    DL.n = n_out;
+    DL.gauss = p.d_gauss.p;
+    DL.gauss_img_stride = p.d_gstride.p;
+    DL.ow = p.d_ow.p;
+    DL.oh = p.d_oh.p;
+    DL.img_base = 0;
+    DL.out_kp = c->out_kp.p;
+    DL.out_key = c->out_key.p;
+    DL.out_desc = c->out_desc.p;
+    launch_describe(DL, st);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev[5], st));
+    c->dev_result_n = n_out;
+    if (!c->keep_on_device) {
+        const size_t need = result_base + n_out;
+        CHK(c->h_kp.ensure(need, true));
+        CHK(c->h_desc.ensure(need * kDescSize, true));
+        CHK(c->h_key.ensure(need, true));
+        if (n_out) {
+            HIPCHK(hipMemcpyAsync(c->h_kp.p + result_base, c->out_kp.p, n_out * sizeof(OutKp), hipMemcpyDeviceToHost,
+                                  st));
+            HIPCHK(hipMemcpyAsync(c->h_desc.p + result_base * kDescSize, c->out_desc.p, (size_t)n_out * kDescSize,
+                                  hipMemcpyDeviceToHost, st));
+            HIPCHK(hipMemcpyAsync(c->h_key.p + result_base, c->out_key.p, n_out * sizeof(uint64_t),
+                                  hipMemcpyDeviceToHost, st));
+        }
+    }
+    HIPCHK(hipEventRecord(c->ev[6], st));
+    HIPCHK(hipStreamSynchronize(st));
+    if (!c->keep_on_device)
+        for (size_t i = 0; i < n_out; i++) c->h_key.p[result_base + i] += (uint64_t)frame_base << kKeyImgShift;
+    if (offsets_out) {
+        size_t acc = result_base;
+        for (uint32_t f = 0; f < n; f++) {
+            offsets_out[f] = acc;
+            acc += out_cnt[f];
+        }
+        offsets_out[n] = acc;
+    }
+    c->stats.extrema += n_ext;
+    c->stats.keypoints += n_out;
+    return 0;
+}
+
+void accumulate_times(sift_mi_ctx* c) {
+    float ms;
+    if (hipEventElapsedTime(&ms, c->ev[0], c->ev[1]) == hipSuccess) c->stats.pyramid_ms += ms;
+    if (hipEventElapsedTime(&ms, c->ev[1], c->ev[2]) == hipSuccess) c->stats.detect_ms += ms;
+    if (hipEventElapsedTime(&ms, c->ev[2], c->ev[3]) == hipSuccess) c->stats.orient_ms += ms;
+    if (hipEventElapsedTime(&ms, c->ev[3], c->ev[4]) == hipSuccess) c->stats.order_ms += ms;
+    if (hipEventElapsedTime(&ms, c->ev[4], c->ev[5]) == hipSuccess) c->stats.descriptor_ms += ms;
+    if (hipEventElapsedTime(&ms, c->ev[0], c->ev[6]) == hipSuccess) c->stats.total_ms += ms;
+}
+
+int check_frame_args(uint32_t w, uint32_t h, size_t stride) {
+    if (w < 1 || h < 1) return fail(SIFT_MI_EINVAL, "empty image");
+    if (stride < w) return fail(SIFT_MI_EINVAL, "row_stride < width");
+    if (w > 8192 * 2 || h > 8192 * 2) return fail(SIFT_MI_EINVAL, "image larger than 16384 px (key field)");
+    return 0;
+}
+
+// Device-resident batch pipeline.
+int extract_device(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, uint32_t n, uint32_t w, uint32_t h,
+                   size_t stride, int64_t limit, size_t* offsets) {
+    CHK(check_frame_args(w, h, stride));
+    if (c->profile != SIFT_MI_PROFILE_OPENCV)
+        return fail(SIFT_MI_EUNSUPPORTED, "IMAGEPROC profile not implemented (parity unpinned)");
+    const uint32_t chunk = c->chunk_override ? std::min(c->chunk_override, n) : auto_chunk(c->plan, w, h, n);
+    CHK(ensure_plan(c, w, h, chunk));
+    c->have_pyramid = false;
+    c->n_result = 0;
+    c->have_result = false;
+    std::vector<size_t> offs(chunk + 1);
+    for (uint32_t f0 = 0; f0 < n; f0 += chunk) {
+        const uint32_t m = std::min(chunk, n - f0);
+        HIPCHK(hipEventRecord(c->ev[0], c->stream));
+        CHK(run_pyramid(c, d_frames + (size_t)f0 * frame_pitch, frame_pitch, stride, m));
+        HIPCHK(hipEventRecord(c->ev[1], c->stream));
+        CHK(run_keypoints(c, m, limit, f0, offs.data(), c->n_result));
+        accumulate_times(c);
+        if (offsets)
+            for (uint32_t f = 0; f < m; f++) offsets[f0 + f] = offs[f];
+        c->n_result = offs[m];
+        c->stats.frames += m;
+    }
+    if (offsets) offsets[n] = c->n_result;
+    c->have_result = true;
+    return 0;
+}
+
+int upload_frames(sift_mi_ctx* c, const uint8_t* const* frames, uint32_t n, uint32_t w, uint32_t h, size_t stride) {
+    const size_t pitch = (size_t)w * h;
+    CHK(c->staging.ensure(pitch * n));
+    for (uint32_t i = 0; i < n; i++) {
+        if (!frames[i]) return fail(SIFT_MI_EINVAL, "null frame");
+        HIPCHK(hipMemcpy2DAsync(c->staging.p + i * pitch, w, frames[i], stride, w, h, hipMemcpyHostToDevice,
+                                c->stream));
+    }
+    return 0;
+}
+
+}  // namespace
+
+// ===========================================================================
+// C ABI
+// ===========================================================================
+extern "C" {
+
+const char* sift_mi_version(void) { return "sift_mi 0.1.0 (gfx950)"; }
+const char* sift_mi_last_error(void) { return g_err.c_str(); }
+
+int sift_mi_create(int device_ordinal, sift_mi_profile profile, sift_mi_ctx** out) {
+    if (!out) return fail(SIFT_MI_EINVAL, "out is null");
+    *out = nullptr;
+    if (profile != SIFT_MI_PROFILE_OPENCV && profile != SIFT_MI_PROFILE_IMAGEPROC)
+        return fail(SIFT_MI_EINVAL, "unknown profile");
+    int ndev = 0;
+    if (hipGetDeviceCount(&ndev) != hipSuccess || ndev <= 0) return fail(SIFT_MI_ENODEV, "no HIP device");
+    if (device_ordinal < 0 || device_ordinal >= ndev) return fail(SIFT_MI_ENODEV, "device ordinal out of range");
+    hipDeviceProp_t prop;
+    HIPCHK(hipGetDeviceProperties(&prop, device_ordinal));
+    if (std::strncmp(prop.gcnArchName, "gfx950", 6) != 0)
+        return fail(SIFT_MI_ENODEV, std::string("device is ") + prop.gcnArchName + ", kernels are built for gfx950");
+    HIPCHK(hipSetDevice(device_ordinal));
+    sift_mi_ctx* c = new sift_mi_ctx();
+    c->device = device_ordinal;
+    c->profile = profile;
+    if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
+        delete c;
+        return fail(SIFT_MI_EHIP, "hipStreamCreate failed");
+    }
+    c->stream = c->own;
+    for (auto& e : c->ev)
+        if (hipEventCreate(&e) != hipSuccess) {
+            delete c;
+            return fail(SIFT_MI_EHIP, "hipEventCreate failed");
+        }
+    *out = c;
+    return 0;
+}
+
+void sift_mi_destroy(sift_mi_ctx* c) {
+    if (!c) return;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    c->plan.release();
+    c->staging.release();
+    c->ext.release();
+    c->kp.release();
+    c->counters.release();
+    c->keys_a.release();
+    c->keys_b.release();
+    c->vals_a.release();
+    c->vals_b.release();
+    c->fin.release();
+    c->sort_tmp.release();
+    c->seg_off.release();
+    c->out_off.release();
+    c->use_resp.release();
+    c->out_kp.release();
+    c->out_desc.release();
+    c->out_key.release();
+    c->h_kp.release();
+    c->h_desc.release();
+    c->h_key.release();
+    c->h_counts.release();
+    for (auto& e : c->ev)
+        if (e) (void)hipEventDestroy(e);
+    if (c->own) (void)hipStreamDestroy(c->own);
+    delete c;
+}
+
+int sift_mi_set_stream(sift_mi_ctx* c, void* s) {
+    if (!c) return fail(SIFT_MI_EINVAL, "ctx is null");
+    c->stream = s ? (hipStream_t)s : c->own;
+    return 0;
+}
+
+int sift_mi_set_chunk(sift_mi_ctx* c, uint32_t k) {
+    if (!c) return fail(SIFT_MI_EINVAL, "ctx is null");
+    c->chunk_override = k;
+    return 0;
+}
+
+int sift_mi_set_keep_on_device(sift_mi_ctx* c, int keep) {
+    if (!c) return fail(SIFT_MI_EINVAL, "ctx is null");
+    c->keep_on_device = keep ? 1 : 0;
+    return 0;
+}
+
+int sift_mi_extract_batch_device(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, uint32_t n,
+                                 uint32_t w, uint32_t h, size_t stride, int64_t limit, size_t* offsets) {
+    if (!c || !d_frames || n == 0) return fail(SIFT_MI_EINVAL, "bad arguments");
+    if (frame_pitch < stride * (h - 1) + w && n > 1) return fail(SIFT_MI_EINVAL, "frame_pitch too small");
+    CHK(set_device(c));
+    return extract_device(c, d_frames, frame_pitch, n, w, h, stride, limit, offsets);
+}
+
+int sift_mi_extract_batch(sift_mi_ctx* c, const uint8_t* const* frames, uint32_t n, uint32_t w, uint32_t h,
+                          size_t stride, int64_t limit, size_t* offsets) {
+    if (!c || !frames || n == 0) return fail(SIFT_MI_EINVAL, "bad arguments");
+    CHK(check_frame_args(w, h, stride));
+    CHK(set_device(c));
+    CHK(upload_frames(c, frames, n, w, h, stride));
+    const int keep = c->keep_on_device;
+    c->keep_on_device = 0;
+    const int rc = extract_device(c, c->staging.p, (size_t)w * h, n, w, h, w, limit, offsets);
+    c->keep_on_device = keep;
+    return rc;
+}
+
+int sift_mi_extract(sift_mi_ctx* c, const uint8_t* pixels, uint32_t w, uint32_t h, size_t stride, int64_t limit,
+                    size_t* n_keypoints) {
+    if (!c || !pixels) return fail(SIFT_MI_EINVAL, "bad arguments");
+    const uint8_t* frames[1] = {pixels};
+    size_t offs[2];
+    CHK(sift_mi_extract_batch(c, frames, 1, w, h, stride, limit, offs));
+    if (n_keypoints) *n_keypoints = offs[1];
+    return 0;
+}
+
+int sift_mi_fetch(sift_mi_ctx* c, sift_mi_keypoint* kps, uint8_t* desc, size_t cap) {
+    if (!c) return fail(SIFT_MI_EINVAL, "ctx is null");
+    if (!c->have_result || c->keep_on_device) return fail(SIFT_MI_ESTATE, "no host result to fetch");
+    if (cap < c->n_result) return fail(SIFT_MI_EINVAL, "cap < result size");
+    static_assert(sizeof(sift_mi_keypoint) == sizeof(OutKp), "layout");
+    if (kps && c->n_result) std::memcpy(kps, c->h_kp.p, c->n_result * sizeof(OutKp));
+    if (desc && c->n_result) std::memcpy(desc, c->h_desc.p, c->n_result * kDescSize);
+    return 0;
+}
+
+int sift_mi_fetch_keys(sift_mi_ctx* c, uint64_t* keys, size_t cap) {
+    if (!c || !keys) return fail(SIFT_MI_EINVAL, "bad arguments");
+    if (!c->have_result || c->keep_on_device) return fail(SIFT_MI_ESTATE, "no host result to fetch");
+    if (cap < c->n_result) return fail(SIFT_MI_EINVAL, "cap < result size");
+    if (c->n_result) std::memcpy(keys, c->h_key.p, c->n_result * sizeof(uint64_t));
+    return 0;
+}
+
+int sift_mi_device_results(sift_mi_ctx* c, const sift_mi_keypoint** d_kps, const uint8_t** d_desc, size_t* n) {
+    if (!c) return fail(SIFT_MI_EINVAL, "ctx is null");
+    if (!c->have_result) return fail(SIFT_MI_ESTATE, "no result");
+    if (d_kps) *d_kps = reinterpret_cast<const sift_mi_keypoint*>(c->out_kp.p);
+    if (d_desc) *d_desc = c->out_desc.p;
+    if (n) *n = c->dev_result_n;
+    return 0;
+}
+
+// ---- precompute_images / sift_with_precomputed (single frame) -------------
+int sift_mi_precompute(sift_mi_ctx* c, const uint8_t* pixels, uint32_t w, uint32_t h, size_t stride,
+                       size_t* n_octaves) {
+    if (!c || !pixels) return fail(SIFT_MI_EINVAL, "bad arguments");
+    CHK(check_frame_args(w, h, stride));
+    if (c->profile != SIFT_MI_PROFILE_OPENCV) return fail(SIFT_MI_EUNSUPPORTED, "IMAGEPROC profile not implemented");
+    CHK(set_device(c));
+    const uint8_t* frames[1] = {pixels};
+    CHK(upload_frames(c, frames, 1, w, h, stride));
+    CHK(ensure_plan(c, w, h, 1));
+    HIPCHK(hipEventRecord(c->ev[0], c->stream));
+    CHK(run_pyramid(c, c->staging.p, (size_t)w * h, w, 1));
+    HIPCHK(hipEventRecord(c->ev[1], c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    c->have_pyramid = true;
+    c->have_result = false;
+    if (n_octaves) *n_octaves = (size_t)c->plan.n_oct;
+    return 0;
+}
+
+int sift_mi_octave_dims(sift_mi_ctx* c, size_t o, uint32_t* w, uint32_t* h) {
+    if (!c || !c->have_pyramid) return fail(SIFT_MI_ESTATE, "no precomputed pyramid");
+    if (o >= (size_t)c->plan.n_oct) return fail(SIFT_MI_EINVAL, "octave out of range");
+    if (w) *w = (uint32_t)c->plan.ow[o];
+    if (h) *h = (uint32_t)c->plan.oh[o];
+    return 0;
+}
+
+int sift_mi_read_scale_space(sift_mi_ctx* c, size_t o, float* out) {
+    if (!c || !out || !c->have_pyramid) return fail(SIFT_MI_ESTATE, "no precomputed pyramid");
+    if (o >= (size_t)c->plan.n_oct) return fail(SIFT_MI_EINVAL, "octave out of range");
+    CHK(set_device(c));
+    HIPCHK(hipMemcpy(out, c->plan.gauss((int)o), c->plan.gstride((int)o) * sizeof(float), hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int sift_mi_read_dog(sift_mi_ctx* c, size_t o, float* out) {
+    if (!c || !out || !c->have_pyramid) return fail(SIFT_MI_ESTATE, "no precomputed pyramid");
+    if (o >= (size_t)c->plan.n_oct) return fail(SIFT_MI_EINVAL, "octave out of range");
+    CHK(set_device(c));
+    HIPCHK(hipMemcpy(out, c->plan.dog((int)o), c->plan.dstride((int)o) * sizeof(float), hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int sift_mi_sift_with_precomputed(sift_mi_ctx* c, int64_t limit, size_t* n_keypoints) {
+    if (!c || !c->have_pyramid) return fail(SIFT_MI_ESTATE, "no precomputed pyramid");
+    CHK(set_device(c));
+    const int keep = c->keep_on_device;
+    c->keep_on_device = 0;
+    size_t offs[2];
+    HIPCHK(hipEventRecord(c->ev[0], c->stream));
+    HIPCHK(hipEventRecord(c->ev[1], c->stream));
+    const int rc = run_keypoints(c, 1, limit, 0, offs, 0);
+    c->keep_on_device = keep;
+    CHK(rc);
+    accumulate_times(c);
+    c->n_result = offs[1];
+    c->have_result = true;
+    if (n_keypoints) *n_keypoints = offs[1];
+    return 0;
+}
+
+// ---- compute_descriptor --------------------------------------------------
+int sift_mi_compute_descriptor(sift_mi_ctx* c, const float* img, uint32_t w, uint32_t h, float x, float y,
+                               float scale, float orientation, uint8_t* out) {
+    if (!c || !img || !out || w < 1 || h < 1) return fail(SIFT_MI_EINVAL, "bad arguments");
+    if (!(scale > 0.f) || scale > 64.f) return fail(SIFT_MI_EINVAL, "scale out of supported range (0, 64]");
+    CHK(set_device(c));
+    DevBuf<float> dimg;
+    DevBuf<uint8_t> dout;
+    CHK(dimg.ensure((size_t)w * h));
+    CHK(dout.ensure(kDescSize));
+    int rc = 0;
+    if (hipMemcpyAsync(dimg.p, img, (size_t)w * h * sizeof(float), hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        rc = fail(SIFT_MI_EHIP, "H2D failed");
+    if (!rc) {
+        launch_describe_one(dimg.p, (int)w, (int)h, x, y, scale, orientation, dout.p, c->stream);
+        if (hipMemcpyAsync(out, dout.p, kDescSize, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+            hipStreamSynchronize(c->stream) != hipSuccess)
+            rc = fail(SIFT_MI_EHIP, "compute_descriptor failed");
+    }
+    dimg.release();
+    dout.release();
+    return rc;
+}
+
+// ---- Processing ops ------------------------------------------------------
+int sift_mi_gaussian_blur(sift_mi_ctx* c, const float* src, uint32_t w, uint32_t h, double sigma, float* dst) {
+    if (!c || !src || !dst || w < 2 || h < 2 || !(sigma > 0)) return fail(SIFT_MI_EINVAL, "bad arguments");
+    if (c->profile != SIFT_MI_PROFILE_OPENCV) return fail(SIFT_MI_EUNSUPPORTED, "IMAGEPROC profile not implemented");
+    CHK(set_device(c));
+    BlurTaps taps;
+    const int r = cv_blur_taps(sigma, &taps);
+    if (r < 1) return fail(SIFT_MI_EUNSUPPORTED, "blur radius outside 1..24");
+    DevBuf<float> a, b;
+    const size_t P = (size_t)w * h;
+    CHK(a.ensure(P));
+    CHK(b.ensure(P));
+    int rc = 0;
+    BlurLaunch L{};
+    L.src = a.p;
+    L.dst = b.p;
+    L.W = (int)w;
+    L.H = (int)h;
+    L.n_img = 1;
+    L.taps = taps;
+    if (hipMemcpyAsync(a.p, src, P * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        launch_blur(r, L, c->stream) != 0 ||
+        hipMemcpyAsync(dst, b.p, P * 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        rc = fail(SIFT_MI_EHIP, "gaussian_blur failed");
+    a.release();
+    b.release();
+    return rc;
+}
+
+int sift_mi_resize_linear(sift_mi_ctx* c, const float* src, uint32_t w, uint32_t h, uint32_t dw, uint32_t dh,
+                          float* dst) {
+    if (!c || !src || !dst || !w || !h || !dw || !dh) return fail(SIFT_MI_EINVAL, "bad arguments");
+    if (c->profile != SIFT_MI_PROFILE_OPENCV) return fail(SIFT_MI_EUNSUPPORTED, "IMAGEPROC profile not implemented");
+    CHK(set_device(c));
+    ResizeTabDev tab;
+    CHK(tab.upload((int)w, (int)h, (int)dw, (int)dh, c->stream));
+    DevBuf<float> a, b;
+    CHK(a.ensure((size_t)w * h));
+    CHK(b.ensure((size_t)dw * dh));
+    int rc = 0;
+    if (hipMemcpyAsync(a.p, src, (size_t)w * h * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess) rc = -1;
+    if (!rc) launch_resize_linear_f32(a.p, (int)w, (int)h, tab.tab, b.p, (int)dw, (int)dh, c->stream);
+    if (rc || hipMemcpyAsync(dst, b.p, (size_t)dw * dh * 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        rc = fail(SIFT_MI_EHIP, "resize_linear failed");
+    a.release();
+    b.release();
+    tab.release();
+    return rc;
+}
+
+int sift_mi_resize_nearest(sift_mi_ctx* c, const float* src, uint32_t w, uint32_t h, uint32_t dw, uint32_t dh,
+                           float* dst) {
+    if (!c || !src || !dst || !w || !h || !dw || !dh) return fail(SIFT_MI_EINVAL, "bad arguments");
+    if (c->profile != SIFT_MI_PROFILE_OPENCV) return fail(SIFT_MI_EUNSUPPORTED, "IMAGEPROC profile not implemented");
+    CHK(set_device(c));
+    std::vector<int> xo, yo;
+    cv_nearest_ofs((int)w, (int)dw, xo);
+    cv_nearest_ofs((int)h, (int)dh, yo);
+    DevBuf<float> a, b;
+    DevBuf<int> dx, dy;
+    CHK(a.ensure((size_t)w * h));
+    CHK(b.ensure((size_t)dw * dh));
+    CHK(dx.ensure(dw));
+    CHK(dy.ensure(dh));
+    int rc = 0;
+    if (hipMemcpyAsync(a.p, src, (size_t)w * h * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        hipMemcpyAsync(dx.p, xo.data(), dw * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+        hipMemcpyAsync(dy.p, yo.data(), dh * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+        rc = -1;
+    if (!rc) launch_resize_nearest_f32(a.p, (int)w, dx.p, dy.p, b.p, (int)dw, (int)dh, c->stream);
+    if (rc || hipMemcpyAsync(dst, b.p, (size_t)dw * dh * 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipStreamSynchronize(c->stream) != hipSuccess)
+        rc = fail(SIFT_MI_EHIP, "resize_nearest failed");
+    a.release();
+    b.release();
+    dx.release();
+    dy.release();
+    return rc;
+}
+
+int sift_mi_get_stats(sift_mi_ctx* c, sift_mi_stats* out) {
+    if (!c || !out) return fail(SIFT_MI_EINVAL, "bad arguments");
+    *out = c->stats;
+    return 0;
+}
+
+int sift_mi_reset_stats(sift_mi_ctx* c) {
+    if (!c) return fail(SIFT_MI_EINVAL, "ctx is null");
+    c->stats = sift_mi_stats{};
+    return 0;
+}
+
+}  // extern "C"

@@ -1,0 +1,106 @@
+// Shared constants, device records and arithmetic helpers of the MI355X SIFT
+// path.  Every constant cites the reference definition in
+// /root/reference/src/lib.rs.
+//
+// Numerics: this code is compiled with -ffp-contract=off (the Rust reference
+// never contracts a*b+c) and only fuses where the reference's OpenCV
+// backend fuses (explicit __builtin_fmaf in the blur passes).  f32 division
+// and sqrt are the IEEE correctly-rounded HIP defaults.
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+
+namespace siftmi {
+
+constexpr int kScalesPerOctave = 3;                  // src/lib.rs:92
+constexpr int kImagesPerOctave = kScalesPerOctave + 3;  // 6 Gaussian images (src/lib.rs:218-221)
+constexpr int kDogPerOctave = kScalesPerOctave + 2;     // 5 DoG images (src/lib.rs:277)
+constexpr float kContrastThreshold = 0.04f;          // src/lib.rs:93
+constexpr float kEdgeThreshold = 10.0f;              // src/lib.rs:94
+constexpr int kImageBorder = 5;                      // src/lib.rs:100
+constexpr int kOriBins = 36;                         // src/lib.rs:102
+constexpr float kLambdaOri = 1.5f;                   // src/lib.rs:104
+constexpr float kLambdaDescr = 3.0f;                 // src/lib.rs:105
+constexpr int kDescHist = 4;                         // src/lib.rs:108
+constexpr int kDescBins = 8;                         // src/lib.rs:110
+constexpr int kDescSize = 128;                       // src/lib.rs:111
+constexpr float kOriPeakRatio = 0.8f;                // src/lib.rs:297
+constexpr int kMaxInterpSteps = 5;                   // src/lib.rs:516
+constexpr int kMaxBlurRadius = 31;                   // taps <= 63 per pass
+
+// Emission key layout (see include/sift_mi.h, sift_mi_fetch_keys).
+constexpr int kKeyImgShift = 40;
+constexpr int kKeyOctShift = 36;
+constexpr int kKeyScaleShift = 34;
+constexpr int kKeyYShift = 20;
+constexpr int kKeyXShift = 6;
+
+__host__ __device__ inline uint64_t make_key(uint32_t img, uint32_t o, uint32_t s, uint32_t y, uint32_t x) {
+    return ((uint64_t)img << kKeyImgShift) | ((uint64_t)o << kKeyOctShift) | ((uint64_t)s << kKeyScaleShift) |
+           ((uint64_t)y << kKeyYShift) | ((uint64_t)x << kKeyXShift);
+}
+
+// Accepted extremum after interpolation + contrast + edge tests
+// (src/lib.rs:334-367).  48 bytes.
+struct ExtRec {
+    uint64_t key;  // emission key without the peak field
+    int32_t img, octave, scale, x, y;  // converged discrete point
+    float off_s, off_x, off_y, response;
+    int32_t pad;
+};
+
+// Keypoint with reference orientation (src/lib.rs:58-68 SiftKeyPoint), in
+// 2x-seed pixel units.  48 bytes.
+struct KpRec {
+    uint64_t key;
+    int32_t img, octave, scale, pad;
+    float x, y, size, angle, response;
+    float pad2;
+};
+
+// Output keypoint (include/sift_mi.h sift_mi_keypoint).
+struct OutKp {
+    float x, y, size, angle, response;
+};
+
+// Blur taps, centre-indexed: k[0] = centre, k[t] = tap at distance t.
+struct BlurTaps {
+    float k[kMaxBlurRadius + 1];
+};
+
+// ---------------------------------------------------------------------------
+// Rust-semantics helpers (saturating `as` casts, `.round()`)
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ int32_t sat_i32(float v) {
+    if (v != v) return 0;
+    if (v >= 2147483647.0f) return INT32_MAX;
+    if (v <= -2147483648.0f) return INT32_MIN;
+    return (int32_t)v;
+}
+__device__ __forceinline__ int64_t sat_i64(float v) {
+    if (v != v) return 0;
+    if (v >= 9.2233720368547758e18f) return INT64_MAX;
+    if (v <= -9.2233720368547758e18f) return INT64_MIN;
+    return (int64_t)v;
+}
+__device__ __forceinline__ uint32_t sat_u32(float v) {  // `as usize` on small non-negative values
+    if (!(v > 0.0f)) return 0;
+    if (v >= 4294967295.0f) return 0xffffffffu;
+    return (uint32_t)v;
+}
+
+// cv::borderInterpolate(BORDER_REFLECT_101)
+__host__ __device__ __forceinline__ int reflect101(int p, int len) {
+    if (len == 1) return 0;
+    while ((unsigned)p >= (unsigned)len) p = p < 0 ? -p : 2 * len - 2 - p;
+    return p;
+}
+
+// Correctly rounded f32 transcendentals evaluated in f64 (the reference calls
+// glibc expf/sinf/cosf/powf, which are correctly rounded in all but rare
+// near-midpoint cases).
+__device__ __forceinline__ float exp_f32(float x) { return (float)exp((double)x); }
+__device__ __forceinline__ float pow2_f32(float x) { return (float)exp2((double)x); }
+
+}  // namespace siftmi

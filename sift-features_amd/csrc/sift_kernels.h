@@ -1,0 +1,105 @@
+// Host-side launch interface of the HIP kernels (internal to libsift_mi.so).
+#pragma once
+
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+#include "sift_common.h"
+
+namespace siftmi {
+
+// cv::resize coefficient tables (device pointers), resizeGeneric_ layout.
+struct ResizeTab {
+    const int* xofs;
+    const float* xa0;
+    const float* xa1;
+    const int* yofs;
+    const float* ya0;
+    const float* ya1;
+    int xmax;
+};
+
+struct BlurLaunch {
+    const float* src;
+    size_t src_img_stride;
+    float* dst;
+    size_t dst_img_stride;
+    float* dog;  // may be null
+    size_t dog_img_stride;
+    float* nxt;  // may be null: next octave base (nearest 1/2)
+    size_t nxt_img_stride;
+    int wn, hn;
+    int W, H;
+    int n_img;
+    BlurTaps taps;
+};
+
+// pyramid.hip
+int launch_blur(int radius, const BlurLaunch& L, hipStream_t st);
+void launch_upsample2x(const uint8_t* frames, size_t frame_pitch, size_t row_stride, int sw, int sh,
+                       const ResizeTab& tab, float* dst, size_t dst_img_stride, int n_img, hipStream_t st);
+void launch_resize_linear_f32(const float* src, int sw, int sh, const ResizeTab& tab, float* dst, int dw, int dh,
+                              hipStream_t st);
+void launch_resize_nearest_f32(const float* src, int sw, const int* xofs, const int* yofs, float* dst, int dw, int dh,
+                               hipStream_t st);
+
+// detect.hip
+struct DetectLaunch {
+    const float* dog;  // octave DoG base, image b at dog + b*img_stride, plane s at + s*W*H
+    size_t img_stride;
+    int W, H, octave, n_img, img_base;
+    ExtRec* out;
+    uint32_t* counter;
+    uint32_t cap;
+};
+void launch_detect(const DetectLaunch& L, hipStream_t st);
+
+struct OrientLaunch {
+    const ExtRec* ext;
+    uint32_t n_ext;
+    const float* const* gauss;     // device array [n_octaves] of octave G bases
+    const size_t* gauss_img_stride;  // device array [n_octaves]
+    const int* ow;                 // device arrays [n_octaves]
+    const int* oh;
+    KpRec* out;
+    uint32_t* counter;
+    uint32_t* per_img;             // [n_img] keypoint counts (indexed by rec.img - img_base)
+    int img_base;
+    uint32_t cap;
+};
+void launch_orient(const OrientLaunch& L, hipStream_t st);
+
+// order.hip
+// keys/vals for the emission-order sort; returns temp bytes when temp == null.
+size_t sort_pairs_u64(void* temp, size_t temp_bytes, const uint64_t* kin, uint64_t* kout, const uint32_t* vin,
+                      uint32_t* vout, uint32_t n, int end_bit, hipStream_t st);
+void launch_make_sort_keys(const KpRec* kp, uint32_t n, uint64_t* keys, uint32_t* vals, hipStream_t st);
+void launch_make_resp_keys(const KpRec* kp, const uint32_t* order, uint32_t n, int img_base, uint64_t* keys,
+                           uint32_t* vals, hipStream_t st);
+// final[i] = src index: for frame f, if take_resp[f] final = resp_order[seg], else emission order
+void launch_select(const uint32_t* emis_order, const uint32_t* resp_order, const uint32_t* seg_off,
+                   const uint32_t* out_off, const uint8_t* use_resp, int n_img, uint32_t n_out, uint32_t* final_idx,
+                   hipStream_t st);
+
+// describe.hip
+struct DescLaunch {
+    const KpRec* kp;
+    const uint32_t* idx;  // final order -> kp index (may be null = identity)
+    uint32_t n;
+    const float* const* gauss;
+    const size_t* gauss_img_stride;
+    const int* ow;
+    const int* oh;
+    int img_base;
+    OutKp* out_kp;     // may be null
+    uint64_t* out_key; // may be null
+    uint8_t* out_desc;
+};
+void launch_describe(const DescLaunch& L, hipStream_t st);
+
+// single-keypoint compute_descriptor on an arbitrary f32 image
+void launch_describe_one(const float* img, int w, int h, float x, float y, float scale, float orientation,
+                         uint8_t* out, hipStream_t st);
+
+}  // namespace siftmi

@@ -1,0 +1,350 @@
+"""Host-side mirror of the reference crate's public API over libsift_mi.so.
+
+Reference: /root/reference/src/lib.rs (tnibler/sift-features @ 2024-10-22)
+
+    pub fn sift(img: &GrayImage, features_limit: Option<usize>) -> SiftResult   (:71)
+    pub fn sift_with_processing::<P: Processing>(img, features_limit)           (:76)
+    pub trait Processing { gaussian_blur, resize_linear, resize_nearest }       (:86-90)
+    pub struct SiftResult { keypoints: Vec<KeyPoint>, descriptors: Array2<u8> } (:41-46)
+    pub struct KeyPoint { x, y, size, angle, response: f32 }                    (:50-56)
+    #[doc(hidden)] precompute_images / sift_with_precomputed / compute_descriptor (:131, :147, :785)
+
+Names, argument meaning and output layout follow the reference; the
+computation is the HIP path (no CPU fallback).  Differences, all documented
+in DESIGN.md:
+  * `sift()` uses the OpenCV arithmetic profile (the one the reference's own
+    golden snapshots pin); `ImageprocProcessing` raises SiftMiError
+    (EUNSUPPORTED) until its profile is implemented.
+  * with a features_limit, ties in response keep emission order (the
+    reference's `sort_unstable_by` leaves their order unspecified).
+  * errors raise SiftMiError where the reference panics.
+"""
+import ctypes
+import threading
+from dataclasses import dataclass
+
+import numpy as np
+
+from . import _lib
+from ._lib import SiftMiError, check, lib
+
+PROFILE_OPENCV = 0
+PROFILE_IMAGEPROC = 1
+DESCRIPTOR_SIZE = 128
+
+
+@dataclass
+class KeyPoint:
+    """src/lib.rs:50-56"""
+    x: float
+    y: float
+    size: float
+    angle: float
+    response: float
+
+
+class SiftResult:
+    """src/lib.rs:41-46.  `keypoints_array` is the (n, 5) f32 table
+    (x, y, size, angle, response); `descriptors` the (n, 128) u8 array whose
+    row i belongs to keypoint i."""
+
+    __slots__ = ("keypoints_array", "descriptors", "keys")
+
+    def __init__(self, keypoints_array, descriptors, keys=None):
+        self.keypoints_array = keypoints_array
+        self.descriptors = descriptors
+        self.keys = keys
+
+    @property
+    def keypoints(self):
+        return [KeyPoint(*map(float, r)) for r in self.keypoints_array]
+
+    def __len__(self):
+        return len(self.keypoints_array)
+
+    def __eq__(self, other):
+        return (isinstance(other, SiftResult) and np.array_equal(self.keypoints_array, other.keypoints_array)
+                and np.array_equal(self.descriptors, other.descriptors))
+
+    def __repr__(self):
+        return f"SiftResult(n={len(self)})"
+
+
+def _u8_image(img):
+    a = np.asarray(img)
+    if a.dtype != np.uint8 or a.ndim != 2:
+        raise TypeError("expected a 2-D uint8 GrayImage array (height, width)")
+    if a.strides[1] != 1 or a.strides[0] < a.shape[1]:
+        a = np.ascontiguousarray(a)
+    return a
+
+
+def _f32_image(img):
+    a = np.ascontiguousarray(img, dtype=np.float32)
+    if a.ndim != 2:
+        raise TypeError("expected a 2-D f32 image (LumaFImage)")
+    return a
+
+
+def _limit(features_limit):
+    if features_limit is None:
+        return -1
+    if features_limit < 0:
+        raise ValueError("features_limit must be >= 0 or None")
+    return int(features_limit)
+
+
+class Context:
+    """One device context (libsift_mi `sift_mi_ctx`): one HIP stream, pooled
+    device buffers.  Not thread-safe; use one per thread / GPU."""
+
+    def __init__(self, device=0, processing=None):
+        processing = processing or OpenCVProcessing
+        self.profile = processing.profile
+        self.device = device
+        h = ctypes.c_void_p()
+        check(lib().sift_mi_create(device, self.profile, ctypes.byref(h)))
+        self._h = h
+        self._generation = 0
+
+    def close(self):
+        if getattr(self, "_h", None):
+            lib().sift_mi_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # -- configuration ----------------------------------------------------
+    def set_stream(self, hip_stream_handle):
+        check(lib().sift_mi_set_stream(self._h, ctypes.c_void_p(hip_stream_handle or 0)))
+
+    def set_chunk(self, images_per_chunk):
+        check(lib().sift_mi_set_chunk(self._h, int(images_per_chunk)))
+
+    def stats(self):
+        s = _lib.Stats()
+        check(lib().sift_mi_get_stats(self._h, ctypes.byref(s)))
+        return s.as_dict()
+
+    def reset_stats(self):
+        check(lib().sift_mi_reset_stats(self._h))
+
+    # -- results ------------------------------------------------------------
+    def _fetch(self, n, with_keys=True):
+        kps = np.empty((n, 5), np.float32)
+        desc = np.empty((n, DESCRIPTOR_SIZE), np.uint8)
+        check(lib().sift_mi_fetch(self._h, kps.ctypes.data, desc.ctypes.data, n))
+        keys = None
+        if with_keys:
+            keys = np.empty(n, np.uint64)
+            check(lib().sift_mi_fetch_keys(self._h, keys.ctypes.data, n))
+        return kps, desc, keys
+
+    # -- sift (src/lib.rs:71-81) ---------------------------------------------
+    def sift(self, img, features_limit=None):
+        a = _u8_image(img)
+        n = ctypes.c_size_t()
+        check(lib().sift_mi_extract(self._h, a.ctypes.data, a.shape[1], a.shape[0], a.strides[0],
+                                    _limit(features_limit), ctypes.byref(n)))
+        return SiftResult(*self._fetch(n.value))
+
+    def sift_batch(self, frames, features_limit=None):
+        """One `sift()` per frame of an (n, h, w) u8 array; returns a list."""
+        f = np.ascontiguousarray(frames, dtype=np.uint8)
+        if f.ndim != 3:
+            raise TypeError("expected (n, height, width) uint8 frames")
+        n, h, w = f.shape
+        ptrs = (ctypes.c_void_p * n)(*[f[i].ctypes.data for i in range(n)])
+        offs = (ctypes.c_size_t * (n + 1))()
+        check(lib().sift_mi_extract_batch(self._h, ptrs, n, w, h, w, _limit(features_limit), offs))
+        kps, desc, keys = self._fetch(offs[n])
+        return [SiftResult(kps[offs[i]:offs[i + 1]], desc[offs[i]:offs[i + 1]], keys[offs[i]:offs[i + 1]])
+                for i in range(n)]
+
+    def sift_batch_device(self, d_frames_ptr, n, width, height, row_stride, frame_pitch,
+                          features_limit=None, fetch=True):
+        """Device-resident frames (e.g. a torch.uint8 cuda tensor's data_ptr()).
+        Returns per-frame offsets and, with fetch, the concatenated results."""
+        offs = (ctypes.c_size_t * (n + 1))()
+        check(lib().sift_mi_set_keep_on_device(self._h, 0 if fetch else 1))
+        check(lib().sift_mi_extract_batch_device(self._h, ctypes.c_void_p(d_frames_ptr), frame_pitch, n, width,
+                                                 height, row_stride, _limit(features_limit), offs))
+        offsets = np.array(offs[:], dtype=np.int64)
+        if not fetch:
+            return offsets, None
+        return offsets, SiftResult(*self._fetch(int(offsets[-1])))
+
+    # -- precompute_images / sift_with_precomputed (src/lib.rs:123-177) ------
+    def precompute_images(self, img):
+        a = _u8_image(img)
+        n = ctypes.c_size_t()
+        check(lib().sift_mi_precompute(self._h, a.ctypes.data, a.shape[1], a.shape[0], a.strides[0],
+                                       ctypes.byref(n)))
+        self._generation += 1
+        return PrecomputedImages(self, n.value, self._generation)
+
+    def sift_with_precomputed(self, pre, features_limit=None):
+        pre._check()
+        n = ctypes.c_size_t()
+        check(lib().sift_mi_sift_with_precomputed(self._h, _limit(features_limit), ctypes.byref(n)))
+        return SiftResult(*self._fetch(n.value))
+
+    # -- compute_descriptor (src/lib.rs:785) -----------------------------------
+    def compute_descriptor(self, img, x, y, scale, orientation):
+        a = _f32_image(img)
+        out = np.zeros(DESCRIPTOR_SIZE, np.uint8)
+        check(lib().sift_mi_compute_descriptor(self._h, a.ctypes.data, a.shape[1], a.shape[0], float(x),
+                                               float(y), float(scale), float(orientation), out.ctypes.data))
+        return out
+
+    # -- Processing ops (src/lib.rs:86-90) ---------------------------------
+    def gaussian_blur(self, img, sigma):
+        a = _f32_image(img)
+        out = np.empty_like(a)
+        check(lib().sift_mi_gaussian_blur(self._h, a.ctypes.data, a.shape[1], a.shape[0], float(sigma),
+                                          out.ctypes.data))
+        return out
+
+    def resize_linear(self, img, width, height):
+        a = _f32_image(img)
+        out = np.empty((height, width), np.float32)
+        check(lib().sift_mi_resize_linear(self._h, a.ctypes.data, a.shape[1], a.shape[0], width, height,
+                                          out.ctypes.data))
+        return out
+
+    def resize_nearest(self, img, width, height):
+        a = _f32_image(img)
+        out = np.empty((height, width), np.float32)
+        check(lib().sift_mi_resize_nearest(self._h, a.ctypes.data, a.shape[1], a.shape[0], width, height,
+                                           out.ctypes.data))
+        return out
+
+
+class PrecomputedImages:
+    """src/lib.rs:123-128: scale_space[o] is (6, h, w) f32, dog[o] (5, h, w)."""
+
+    def __init__(self, ctx, n_octaves, generation):
+        self._ctx = ctx
+        self.n_octaves = n_octaves
+        self._gen = generation
+
+    def _check(self):
+        if self._gen != self._ctx._generation:
+            raise SiftMiError(-6, "PrecomputedImages superseded by a later precompute on this context")
+
+    def dims(self, o):
+        w, h = ctypes.c_uint32(), ctypes.c_uint32()
+        check(lib().sift_mi_octave_dims(self._ctx._h, o, ctypes.byref(w), ctypes.byref(h)))
+        return w.value, h.value
+
+    def scale_space_octave(self, o):
+        self._check()
+        w, h = self.dims(o)
+        out = np.empty((6, h, w), np.float32)
+        check(lib().sift_mi_read_scale_space(self._ctx._h, o, out.ctypes.data))
+        return out
+
+    def dog_octave(self, o):
+        self._check()
+        w, h = self.dims(o)
+        out = np.empty((5, h, w), np.float32)
+        check(lib().sift_mi_read_dog(self._ctx._h, o, out.ctypes.data))
+        return out
+
+    @property
+    def scale_space(self):
+        return [self.scale_space_octave(o) for o in range(self.n_octaves)]
+
+    @property
+    def dog(self):
+        return [self.dog_octave(o) for o in range(self.n_octaves)]
+
+
+# ---------------------------------------------------------------------------
+# Processing backends (src/lib.rs:86-90, :993-1007; src/opencv_processing.rs)
+# ---------------------------------------------------------------------------
+class Processing:
+    profile = None
+
+    @classmethod
+    def gaussian_blur(cls, img, sigma):
+        return default_context(processing=cls).gaussian_blur(img, sigma)
+
+    @classmethod
+    def resize_linear(cls, img, width, height):
+        return default_context(processing=cls).resize_linear(img, width, height)
+
+    @classmethod
+    def resize_nearest(cls, img, width, height):
+        return default_context(processing=cls).resize_nearest(img, width, height)
+
+
+class OpenCVProcessing(Processing):
+    """cv::GaussianBlur / cv::resize arithmetic (src/opencv_processing.rs:38-74)."""
+    profile = PROFILE_OPENCV
+
+
+class ImageprocProcessing(Processing):
+    """imageproc gaussian_blur_f32 / image::resize arithmetic (src/lib.rs:993-1007).
+    Not implemented yet: every call raises SiftMiError(EUNSUPPORTED)."""
+    profile = PROFILE_IMAGEPROC
+
+
+_tls = threading.local()
+
+
+def default_context(device=0, processing=None):
+    processing = processing or OpenCVProcessing
+    cache = getattr(_tls, "ctx", None)
+    if cache is None:
+        cache = _tls.ctx = {}
+    key = (device, processing.profile)
+    if key not in cache:
+        cache[key] = Context(device, processing)
+    return cache[key]
+
+
+def sift(img, features_limit=None):
+    """src/lib.rs:71 (default backend: see module docstring)."""
+    return default_context().sift(img, features_limit)
+
+
+def sift_with_processing(processing, img, features_limit=None):
+    """src/lib.rs:76"""
+    return default_context(processing=processing).sift(img, features_limit)
+
+
+def precompute_images(processing, img):
+    """src/lib.rs:131"""
+    return default_context(processing=processing).precompute_images(img)
+
+
+def sift_with_precomputed(pre, features_limit=None):
+    """src/lib.rs:147"""
+    return pre._ctx.sift_with_precomputed(pre, features_limit)
+
+
+def compute_descriptor(img, x, y, scale, orientation):
+    """src/lib.rs:785"""
+    return default_context().compute_descriptor(img, x, y, scale, orientation)
+
+
+def stable_sort_xy_size(keypoints_array):
+    """Order of the reference test's snapshots (src/lib.rs:1020-1030): stable
+    sort by (x, y, size)."""
+    k = np.asarray(keypoints_array)
+    if not len(k):
+        return np.zeros(0, np.int64)
+    return np.lexsort((k[:, 2], k[:, 1], k[:, 0]))
+
+
+def key_fields(keys):
+    """Decode emission keys (include/sift_mi.h sift_mi_fetch_keys)."""
+    k = np.asarray(keys, dtype=np.uint64)
+    f = lambda s, b: ((k >> np.uint64(s)) & np.uint64((1 << b) - 1)).astype(np.int64)
+    return {"frame": f(40, 24), "octave": f(36, 4), "s_init": f(34, 2), "y_init": f(20, 14),
+            "x_init": f(6, 14), "peak": f(0, 6)}

@@ -1,0 +1,83 @@
+"""Batch / device-resident / chunked paths equal per-image `sift()` results, and
+edge cases (tiny, flat, strided inputs) match the oracle."""
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _frames():
+    import synth
+    return synth.frames(5, 160, 120, seed0=20)
+
+
+def test_batch_equals_single(pkg, ctx):
+    fr = _frames()
+    batch = ctx.sift_batch(fr)
+    for i in range(len(fr)):
+        single = ctx.sift(fr[i])
+        assert single == batch[i], i
+        f = pkg.key_fields(batch[i].keys)
+        assert np.all(f["frame"] == i)
+
+
+def test_chunked_batch(pkg, ctx):
+    fr = _frames()
+    ref = ctx.sift_batch(fr)
+    c2 = pkg.Context(0)
+    c2.set_chunk(2)
+    got = c2.sift_batch(fr)
+    c2.close()
+    assert all(a == b for a, b in zip(ref, got))
+
+
+def test_device_batch_torch(pkg, ctx):
+    import torch
+    fr = _frames()
+    t = torch.from_numpy(fr).cuda()
+    torch.cuda.synchronize()
+    offs, res = ctx.sift_batch_device(t.data_ptr(), t.shape[0], t.shape[2], t.shape[1], t.stride(1),
+                                      t.stride(0))
+    ref = ctx.sift_batch(fr)
+    for i in range(len(fr)):
+        a, b = int(offs[i]), int(offs[i + 1])
+        assert np.array_equal(res.keypoints_array[a:b], ref[i].keypoints_array)
+        assert np.array_equal(res.descriptors[a:b], ref[i].descriptors)
+
+
+def test_deterministic(ctx):
+    import synth
+    img = synth.frame(640, 480, 9)
+    assert ctx.sift(img) == ctx.sift(img)
+
+
+@pytest.mark.parametrize("shape", [(1, 1), (2, 2), (3, 7), (10, 10), (20, 3), (21, 40), (33, 19)])
+def test_tiny_images(pkg, ctx, oracle, shape):
+    from test_gpu_parity import assert_parity
+    rng = np.random.default_rng(sum(shape))
+    img = rng.integers(0, 256, shape, dtype=np.uint8)
+    kp_o, desc_o, ext_o = oracle.sift(img, internal=True)
+    res = ctx.sift(img)
+    assert_parity(pkg, res, kp_o, desc_o, ext_o)
+
+
+def test_flat_image_no_keypoints(ctx, oracle):
+    img = np.full((120, 160), 77, np.uint8)
+    assert len(oracle.sift(img)[0]) == 0
+    assert len(ctx.sift(img)) == 0
+
+
+def test_strided_input(ctx):
+    import synth
+    big = synth.frame(200, 150, 4)
+    view = big[10:130, 7:167]  # non-contiguous rows: row_stride 200 > width 160
+    assert ctx.sift(view) == ctx.sift(np.ascontiguousarray(view))
+
+
+def test_random_noise(pkg, ctx, oracle):
+    """White noise: many plateaus/ties and dense extrema (worst case for ordering)."""
+    from test_gpu_parity import assert_parity
+    img = np.random.default_rng(5).integers(0, 256, (96, 128), dtype=np.uint8)
+    kp_o, desc_o, ext_o = oracle.sift(img, internal=True)
+    res = ctx.sift(img)
+    assert_parity(pkg, res, kp_o, desc_o, ext_o)
