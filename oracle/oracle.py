@@ -89,6 +89,8 @@ def _result(r):
         raise RuntimeError("oracle failed")
     try:
         n = L.oracle_result_n(r)
+        if n == 0:
+            return np.zeros((0, 5), np.float32), np.zeros((0, 128), np.uint8), np.zeros((0, 6), np.int32)
         kp = np.ctypeslib.as_array(ctypes.cast(L.oracle_result_keypoints(r), ctypes.POINTER(ctypes.c_float)),
                                    shape=(max(n, 1) * 5,))[: n * 5].reshape(n, 5).copy()
         ext = np.ctypeslib.as_array(ctypes.cast(L.oracle_result_internal(r), ctypes.POINTER(ctypes.c_int32)),

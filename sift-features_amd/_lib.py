@@ -49,6 +49,14 @@ def lib():
     global _lib
     if _lib is not None:
         return _lib
+    # One HIP runtime per process: torch ships its own libamdhip64.so.7 (same
+    # SONAME as /opt/rocm's).  If torch is importable, load it first so that
+    # libsift_mi.so binds to the already-loaded runtime instead of pulling in a
+    # second copy (which breaks torch.cuda initialisation afterwards).
+    try:
+        import torch  # noqa: F401
+    except ImportError:
+        pass
     if not os.path.exists(LIB_PATH):
         raise ImportError(f"{LIB_PATH} not built; run `make -C {os.path.join(HERE, 'csrc')}` "
                           "(hipcc --offload-arch=gfx950). There is no CPU fallback.")

@@ -17,27 +17,82 @@ namespace siftmi {
 
 constexpr int HIST_FLOATS = 6 * 6 * kDescBins;  // 288
 
-// Wave-cooperative compute_descriptor.  `hist` is this wave's LDS slice.
-__device__ void describe_wave(const float* __restrict__ img, int width, int height, float xf, float yf,
-                              float scale, float orientation, float* hist, uint8_t* __restrict__ out, int lane) {
-    for (int i = lane; i < HIST_FLOATS; i += 64) hist[i] = 0.0f;
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+// Per-wave LDS scratch: 288 histogram bins + the row table of the sample
+// enumeration (first column, prefix count) for up to 2*38+1 = 77 rows.
+constexpr int ROWS_MAX = 80;
+struct DescScratch {
+    float hist[HIST_FLOATS];
+    int rowlo[ROWS_MAX];
+    int rowpre[ROWS_MAX + 1];
+};
+
+// Wave-cooperative compute_descriptor (src/lib.rs:785-990).
+//
+// Only samples whose rotated coordinates fall in the 4x4 histogram region
+// (|col_rot|, |row_rot| < 2.5 bin units, about half of the (2r+1)^2 window)
+// contribute; each row's candidate column interval is computed in f64 and
+// widened by one sample, the compacted (row, col) list is strided over the
+// wave's lanes, and the reference's exact f32 predicate is still evaluated
+// per sample -- so the accepted set is identical to the reference's.
+__device__ __forceinline__ void describe_wave(const float* __restrict__ img, int pitch, int width, int height,
+                                              float xf, float yf, float scale, float orientation,
+                                              DescScratch& sc, uint8_t* __restrict__ out, int lane) {
+    for (int i = lane; i < HIST_FLOATS; i += 64) sc.hist[i] = 0.0f;
     const int32_t x = (int32_t)sat_u32(roundf(xf));
     const int32_t y = (int32_t)sat_u32(roundf(yf));
     const float BIN_ANGLE_STEP = (float)kDescBins / 360.0f;
     const float hist_width = kLambdaDescr * scale;
-    const int radius =
-        sat_i32(roundf(kLambdaDescr * scale * 1.41421356237309504880f * (float)(kDescHist + 1) * 0.5f));
+    int radius = sat_i32(roundf(kLambdaDescr * scale * 1.41421356237309504880f * (float)(kDescHist + 1) * 0.5f));
+    radius = radius < 0 ? 0 : (radius > (ROWS_MAX - 2) / 2 ? (ROWS_MAX - 2) / 2 : radius);
     const float rad = orientation * (3.14159265358979323846f / 180.0f);  // f32::to_radians
     const float sin_ori = (float)sin((double)rad), cos_ori = (float)cos((double)rad);
     const float sin_s = sin_ori / hist_width, cos_s = cos_ori / hist_width;
     const int n = 2 * radius + 1;
-    const int N = n * n;
-    for (int idx = lane; idx < N; idx += 64) {
-        const int iy = idx / n;
-        const int yi = iy - radius, xi = idx - iy * n - radius;
+    // 1. per-row candidate column interval
+    for (int row = lane; row < n; row += 64) {
+        const double yi = (double)(row - radius);
+        const double c = cos_s, s = sin_s;
+        double lo = -radius, hi = radius;
+        bool empty = false;
+        if (fabs(c) > 1e-30) {
+            const double a = (yi * s - 2.5) / c, b = (yi * s + 2.5) / c;
+            lo = fmax(lo, fmin(a, b) - 1.0);
+            hi = fmin(hi, fmax(a, b) + 1.0);
+        } else {
+            empty = !(fabs(yi * s) < 2.5 + 1e-3);
+        }
+        if (fabs(s) > 1e-30) {
+            const double a = (-yi * c - 2.5) / s, b = (-yi * c + 2.5) / s;
+            lo = fmax(lo, fmin(a, b) - 1.0);
+            hi = fmin(hi, fmax(a, b) + 1.0);
+        } else {
+            empty = empty || !(fabs(yi * c) < 2.5 + 1e-3);
+        }
+        const int ilo = (int)floor(lo), ihi = (int)ceil(hi);
+        sc.rowlo[row] = ilo;
+        sc.rowpre[row + 1] = (empty || ihi < ilo) ? 0 : ihi - ilo + 1;
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    if (lane == 0) {
+        int acc = 0;
+        sc.rowpre[0] = 0;
+        for (int r = 1; r <= n; r++) {
+            acc += sc.rowpre[r];
+            sc.rowpre[r] = acc;
+        }
+    }
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    const int total = sc.rowpre[n];
+    // 2. strided walk over the compacted samples
+    int row = 0;
+    for (int k = lane; k < total; k += 64) {
+        while (sc.rowpre[row + 1] <= k) row++;
+        const int yi = row - radius;
+        const int xi = sc.rowlo[row] + (k - sc.rowpre[row]);
         const float col_rot = (float)xi * cos_s - (float)yi * sin_s;
         const float row_rot = (float)xi * sin_s + (float)yi * cos_s;
         float row_bin = row_rot + (float)(kDescHist / 2);
@@ -46,13 +101,16 @@ __device__ void describe_wave(const float* __restrict__ img, int width, int heig
         if (!(row_bin > -0.5f && row_bin < (float)kDescHist + 0.5f && col_bin > -0.5f &&
               col_bin < (float)kDescHist + 0.5f && ay > 0 && ay < height - 1 && ax > 0 && ax < width - 1))
             continue;
-        const float* rw = img + (size_t)ay * width;
+        const float* rw = img + (size_t)ay * pitch;
         const float dx = rw[ax + 1] - rw[ax - 1];
-        const float dy = img[(size_t)(ay - 1) * width + ax] - img[(size_t)(ay + 1) * width + ax];
+        const float dy = rw[ax - pitch] - rw[ax + pitch];
         const float wsq = col_rot * col_rot + row_rot * row_rot;
         const float weight = exp_f32(wsq * (-2.f / (float)(kDescHist * kDescHist)));
-        const double deg = atan2((double)dy, (double)dx) * (180.0 / 3.14159265358979323846);
-        const float ori = (float)fmod(deg + 360.0, 360.0) - orientation;
+        // ((atan2(dy, dx).to_degrees() + 360) % 360) as f32 - orientation; the
+        // f64 remainder of v in [180, 540] by 360 is exactly v or v - 360
+        double deg = atan2((double)dy, (double)dx) * (180.0 / 3.14159265358979323846) + 360.0;
+        deg = deg >= 360.0 ? deg - 360.0 : deg;
+        const float ori = (float)deg - orientation;
         float mag = sqrtf(dx * dx + dy * dy);
         row_bin = row_bin - 0.5f;
         col_bin = col_bin - 0.5f;
@@ -67,19 +125,17 @@ __device__ void describe_wave(const float* __restrict__ img, int width, int heig
         const float c101 = c10 * ori_frac, c100 = c10 - c101;
         const float c011 = c01 * ori_frac, c010 = c01 - c011;
         const float c001 = c00 * ori_frac, c000 = c00 - c001;
-        const uint32_t r1 = sat_u32(row_floor + 1.f), q1 = sat_u32(col_floor + 1.f);
-        const uint32_t r2 = sat_u32(row_floor + 2.f), q2 = sat_u32(col_floor + 2.f);
-        float of = ori_floor;
-        if (of < 0.f)
-            of = of + (float)kDescBins;
-        else if (of >= (float)kDescBins)
-            of = of - (float)kDescBins;
-        const uint32_t o0 = sat_u32(of);
-        const uint32_t o1 = o0 + 1 >= (uint32_t)kDescBins ? 0u : o0 + 1;
-        float* h11 = hist + (r1 * 6 + q1) * kDescBins;
-        float* h12 = hist + (r1 * 6 + q2) * kDescBins;
-        float* h21 = hist + (r2 * 6 + q1) * kDescBins;
-        float* h22 = hist + (r2 * 6 + q2) * kDescBins;
+        // row_floor in [-1, 3], col_floor in [-1, 3] inside the accepted region;
+        // ori_floor in [-8, 7] for orientation in [0, 360] (host-checked)
+        const int r1 = (int)row_floor + 1, q1 = (int)col_floor + 1;
+        int o0 = (int)ori_floor;
+        o0 = o0 < 0 ? o0 + kDescBins : (o0 >= kDescBins ? o0 - kDescBins : o0);
+        if ((unsigned)r1 > 4u || (unsigned)q1 > 4u || (unsigned)o0 >= (unsigned)kDescBins) continue;
+        const int o1 = o0 + 1 >= kDescBins ? 0 : o0 + 1;
+        float* h11 = sc.hist + (r1 * 6 + q1) * kDescBins;
+        float* h12 = h11 + kDescBins;
+        float* h21 = h11 + 6 * kDescBins;
+        float* h22 = h21 + kDescBins;
         atomicAdd(h11 + o0, c000);
         atomicAdd(h11 + o1, c001);
         atomicAdd(h12 + o0, c010);
@@ -99,7 +155,7 @@ __device__ void describe_wave(const float* __restrict__ img, int width, int heig
     for (int j = 0; j < 4; j++) {
         const int i = 4 * l + j;
         const int rr = 1 + (i >> 5), cc = 1 + ((i >> 3) & 3), oo = i & 7;
-        v[j] = hist[(rr * 6 + cc) * kDescBins + oo];
+        v[j] = sc.hist[(rr * 6 + cc) * kDescBins + oo];
     }
     float s = 0.0f;
 #pragma unroll
@@ -130,21 +186,22 @@ __device__ void describe_wave(const float* __restrict__ img, int width, int heig
 }
 
 __global__ __launch_bounds__(256) void k_describe(const DescLaunch L) {
-    __shared__ float hist[4][HIST_FLOATS];
+    __shared__ DescScratch scr[4];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t i = blockIdx.x * 4 + wave;
     if (i >= L.n) return;  // whole wave; no workgroup barrier below
     const KpRec kp = L.kp[L.idx ? L.idx[i] : i];
     const int o = kp.octave;
     const int W = L.ow[o], H = L.oh[o];
+    const int pitch = L.opitch[o];
     const float* img =
-        L.gauss[o] + (size_t)(kp.img - L.img_base) * L.gauss_img_stride[o] + (size_t)kp.scale * W * H;
+        L.gauss[o] + (size_t)(kp.img - L.img_base) * L.gauss_img_stride[o] + (size_t)kp.scale * pitch * H;
     // compute_descriptors (src/lib.rs:759-782)
     const float angle = 360.0f - kp.angle;
     const float osf = 1.0f / (float)(1u << o);  // 2_f32.powi(-octave)
     const float kp_size = kp.size * osf;
-    describe_wave(img, W, H, kp.x * osf, kp.y * osf, kp_size, angle, hist[wave], L.out_desc + (size_t)i * kDescSize,
-                  lane);
+    describe_wave(img, pitch, W, H, kp.x * osf, kp.y * osf, kp_size, angle, scr[wave],
+                  L.out_desc + (size_t)i * kDescSize, lane);
     if (lane == 0) {
         if (L.out_kp) {
             OutKp k;
@@ -167,8 +224,8 @@ void launch_describe(const DescLaunch& L, hipStream_t st) {
 
 __global__ __launch_bounds__(64) void k_describe_one(const float* img, int w, int h, float x, float y, float scale,
                                                      float orientation, uint8_t* out) {
-    __shared__ float hist[HIST_FLOATS];
-    describe_wave(img, w, h, x, y, scale, orientation, hist, out, threadIdx.x);
+    __shared__ DescScratch scr;
+    describe_wave(img, w, w, h, x, y, scale, orientation, scr, out, threadIdx.x);
 }
 
 void launch_describe_one(const float* img, int w, int h, float x, float y, float scale, float orientation,

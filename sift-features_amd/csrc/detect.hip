@@ -21,14 +21,14 @@ namespace siftmi {
 // ---------------------------------------------------------------------------
 // interpolate_extremum (src/lib.rs:525-603) on the DoG stack of one frame.
 // ---------------------------------------------------------------------------
-__device__ bool interpolate(const float* __restrict__ dog, int W, int H, int& scale, int& x, int& y, float& os,
-                            float& ox, float& oy) {
-    const size_t P = (size_t)W * H;
+__device__ __forceinline__ bool interpolate(const float* __restrict__ dog, int W, int H, int pitch, int& scale,
+                                            int& x, int& y, float& os, float& ox, float& oy) {
+    const size_t P = (size_t)pitch * H;
     for (int it = 0; it < kMaxInterpSteps; it++) {
         const float* prev = dog + (size_t)(scale - 1) * P;
         const float* curr = dog + (size_t)scale * P;
         const float* next = dog + (size_t)(scale + 1) * P;
-#define AT(a, yy, xx) (a)[(size_t)(yy) * W + (xx)]
+#define AT(a, yy, xx) (a)[(size_t)(yy) * pitch + (xx)]
         const float g1 = (AT(next, y, x) - AT(prev, y, x)) / 2.f;
         const float g2 = (AT(curr, y + 1, x) - AT(curr, y - 1, x)) / 2.f;
         const float g3 = (AT(curr, y, x + 1) - AT(curr, y, x - 1)) / 2.f;
@@ -74,95 +74,133 @@ __device__ bool interpolate(const float* __restrict__ dog, int W, int H, int& sc
 }
 
 // ---------------------------------------------------------------------------
-// k_detect: one thread per (x, y), all three scale triples of the octave.
-// The 5 DoG planes of a 64x4 tile (+1 px halo) are staged in LDS; the rare
-// extrema run the refinement chain from global memory.
+// k_detect: thread = (column, 4 consecutive rows) of a 64x16 tile, all three
+// scale triples of the octave.  The 5 DoG planes of the tile (+1 px halo)
+// are staged in LDS with 16-B loads on interior tiles; the rare extrema run
+// the refinement chain (interpolate / contrast / edge) from global memory.
 // ---------------------------------------------------------------------------
-constexpr int DT_W = 64, DT_H = 4, DT_LW = DT_W + 2, DT_LH = DT_H + 2;
+constexpr int DT_W = 64, DT_H = 16, DT_RPT = 4;     // rows per thread
+constexpr int DT_LH = DT_H + 2, DT_LWV = DT_W + 8;  // loaded window [x0-4, x0+68)
+constexpr int DT_LP = DT_LWV + 4;                    // LDS pitch
+constexpr int DT_NLOAD4 = kDogPerOctave * DT_LH * (DT_LWV / 4);
+constexpr int DT_LPT = (DT_NLOAD4 + 255) / 256;
 
 __global__ __launch_bounds__(256) void k_detect(const DetectLaunch L) {
-    __shared__ float t[kDogPerOctave][DT_LH][DT_LW];
-    const int W = L.W, H = L.H;
+    __shared__ __attribute__((aligned(16))) float t[kDogPerOctave * DT_LH * DT_LP];
+    const int W = L.W, H = L.H, pitch = L.pitch;
     const int x0 = blockIdx.x * DT_W, y0 = blockIdx.y * DT_H;
     const int b = blockIdx.z;
     const float* dog = L.dog + (size_t)b * L.img_stride;
-    const size_t P = (size_t)W * H;
-    for (int i = threadIdx.x; i < kDogPerOctave * DT_LH * DT_LW; i += 256) {
-        const int p = i / (DT_LH * DT_LW), r = i - p * (DT_LH * DT_LW);
-        const int ly = r / DT_LW, lx = r - ly * DT_LW;
-        int gy = y0 - 1 + ly, gx = x0 - 1 + lx;
-        gy = gy < 0 ? 0 : (gy >= H ? H - 1 : gy);
-        gx = gx < 0 ? 0 : (gx >= W ? W - 1 : gx);
-        t[p][ly][lx] = dog[(size_t)p * P + (size_t)gy * W + gx];
+    const size_t P = (size_t)pitch * H;
+    const int tid = threadIdx.x;
+    const bool interior = x0 >= 4 && x0 + DT_W + 4 <= pitch && y0 >= 1 && y0 + DT_H + 1 <= H;
+    if (interior) {
+        float4 tmp[DT_LPT];
+#pragma unroll
+        for (int j = 0; j < DT_LPT; j++) {  // unconditional (index-clamped) loads, see pyramid.hip
+            const int i = min(tid + 256 * j, DT_NLOAD4 - 1);
+            const int pl = i / (DT_LH * (DT_LWV / 4)), r = i - pl * (DT_LH * (DT_LWV / 4));
+            const int ly = r / (DT_LWV / 4), c4 = r - ly * (DT_LWV / 4);
+            tmp[j] = *reinterpret_cast<const float4*>(dog + (size_t)pl * P + (size_t)(y0 - 1 + ly) * pitch +
+                                                      (x0 - 4 + 4 * c4));
+        }
+#pragma unroll
+        for (int j = 0; j < DT_LPT; j++) {
+            const int i = tid + 256 * j;
+            if (i < DT_NLOAD4) {
+                const int pl = i / (DT_LH * (DT_LWV / 4)), r = i - pl * (DT_LH * (DT_LWV / 4));
+                const int ly = r / (DT_LWV / 4), c4 = r - ly * (DT_LWV / 4);
+                *reinterpret_cast<float4*>(t + (pl * DT_LH + ly) * DT_LP + 4 * c4) = tmp[j];
+            }
+        }
+    } else {
+        for (int i = tid; i < kDogPerOctave * DT_LH * DT_LWV; i += 256) {
+            const int pl = i / (DT_LH * DT_LWV), r = i - pl * (DT_LH * DT_LWV);
+            const int ly = r / DT_LWV, lx = r - ly * DT_LWV;
+            int gy = y0 - 1 + ly, gx = x0 - 4 + lx;
+            gy = gy < 0 ? 0 : (gy >= H ? H - 1 : gy);
+            gx = gx < 0 ? 0 : (gx >= W ? W - 1 : gx);
+            t[(pl * DT_LH + ly) * DT_LP + lx] = dog[(size_t)pl * P + (size_t)gy * pitch + gx];
+        }
     }
     __syncthreads();
-    const int lx = (threadIdx.x & 63) + 1, ly = (threadIdx.x >> 6) + 1;
-    const int x = x0 + lx - 1, y = y0 + ly - 1;
-    if (x < kImageBorder || x >= W - kImageBorder || y < kImageBorder || y >= H - kImageBorder) return;
+    const int lx = (tid & 63) + 4;  // LDS column of this thread's pixel
+    const int x = x0 + (tid & 63);
+    if (x < kImageBorder || x >= W - kImageBorder) return;
     // threshold = floor(0.5 * 0.04 / 3) = 0 (src/lib.rs:460)
     const float threshold = floorf(0.5f * kContrastThreshold / (float)kScalesPerOctave);
-    for (int s_in = 1; s_in <= kScalesPerOctave; s_in++) {
-        const float val = t[s_in][ly][lx];
-        if (fabsf(val) <= threshold) continue;
-        bool ok = true;
-        if (val > 0.0f) {
+#define T(pl, yy, xx) t[((pl) * DT_LH + (yy)) * DT_LP + (xx)]
+    for (int rr = 0; rr < DT_RPT; rr++) {
+        const int ly = (tid >> 6) * DT_RPT + rr + 1;
+        const int y = y0 + ly - 1;
+        if (y < kImageBorder || y >= H - kImageBorder) continue;
+        for (int s_in = 1; s_in <= kScalesPerOctave; s_in++) {
+            // point_is_local_extremum (src/lib.rs:437-506): non-strict vs all 26
+            const float val = T(s_in, ly, lx);
+            if (fabsf(val) <= threshold) continue;
+            bool ok = true;
+            if (val > 0.0f) {
 #pragma unroll
-            for (int p = -1; p <= 1; p++)
+                for (int p = -1; p <= 1; p++)
 #pragma unroll
-                for (int dy = -1; dy <= 1; dy++)
+                    for (int dy = -1; dy <= 1; dy++)
 #pragma unroll
-                    for (int dx = -1; dx <= 1; dx++)
-                        if (p != 0 || dy != 0 || dx != 0) ok = ok && (val >= t[s_in + p][ly + dy][lx + dx]);
-        } else {
+                        for (int dx = -1; dx <= 1; dx++)
+                            if (p != 0 || dy != 0 || dx != 0) ok = ok && (val >= T(s_in + p, ly + dy, lx + dx));
+            } else {
 #pragma unroll
-            for (int p = -1; p <= 1; p++)
+                for (int p = -1; p <= 1; p++)
 #pragma unroll
-                for (int dy = -1; dy <= 1; dy++)
+                    for (int dy = -1; dy <= 1; dy++)
 #pragma unroll
-                    for (int dx = -1; dx <= 1; dx++)
-                        if (p != 0 || dy != 0 || dx != 0) ok = ok && (val <= t[s_in + p][ly + dy][lx + dx]);
+                        for (int dx = -1; dx <= 1; dx++)
+                            if (p != 0 || dy != 0 || dx != 0) ok = ok && (val <= T(s_in + p, ly + dy, lx + dx));
+            }
+            if (!ok) continue;
+            // refinement (src/lib.rs:334-367)
+            int sc = s_in, xi = x, yi = y;
+            float os, ox, oy;
+            if (!interpolate(dog, W, H, pitch, sc, xi, yi, os, ox, oy)) continue;
+            const float* prev = dog + (size_t)(sc - 1) * P;
+            const float* curr = dog + (size_t)sc * P;
+            const float* next = dog + (size_t)(sc + 1) * P;
+            const size_t c = (size_t)yi * pitch + xi;
+            // extremum_contrast (src/lib.rs:606-626)
+            const float g1 = (next[c] - prev[c]) / 2.f;
+            const float g2 = (curr[c + pitch] - curr[c - pitch]) / 2.f;
+            const float g3 = (curr[c + 1] - curr[c - 1]) / 2.f;
+            const float interp = os * g1 + oy * g2 + ox * g3;
+            const float contrast = fabsf(curr[c] + interp / 2.f);
+            if (contrast * (float)kScalesPerOctave <= kContrastThreshold) continue;
+            // extremum_is_on_edge (src/lib.rs:630-653)
+            const float v2 = curr[c] * 2.0f;
+            const float h11 = curr[c + pitch] + curr[c - pitch] - v2;
+            const float d22 = curr[c + 1] + curr[c - 1] - v2;
+            const float h12 =
+                (curr[c + pitch + 1] - curr[c + pitch - 1] - curr[c - pitch + 1] + curr[c - pitch - 1]) / 4.f;
+            const float tr = d22 + h11;
+            const float det = d22 * h11 - h12 * h12;
+            if (det <= 0.f) continue;
+            if ((tr * tr * kEdgeThreshold) > (kEdgeThreshold + 1.0f) * (kEdgeThreshold + 1.0f) * det) continue;
+            const uint32_t slot = atomicAdd(L.counter, 1u);
+            if (slot >= L.cap) continue;
+            ExtRec e;
+            e.key = make_key((uint32_t)(L.img_base + b), (uint32_t)L.octave, (uint32_t)s_in, (uint32_t)y,
+                             (uint32_t)x);
+            e.img = L.img_base + b;
+            e.octave = L.octave;
+            e.scale = sc;
+            e.x = xi;
+            e.y = yi;
+            e.off_s = os;
+            e.off_x = ox;
+            e.off_y = oy;
+            e.response = contrast;
+            e.pad = 0;
+            L.out[slot] = e;
         }
-        if (!ok) continue;
-        // refinement (src/lib.rs:334-367)
-        int sc = s_in, xi = x, yi = y;
-        float os, ox, oy;
-        if (!interpolate(dog, W, H, sc, xi, yi, os, ox, oy)) continue;
-        const float* prev = dog + (size_t)(sc - 1) * P;
-        const float* curr = dog + (size_t)sc * P;
-        const float* next = dog + (size_t)(sc + 1) * P;
-        const size_t c = (size_t)yi * W + xi;
-        // extremum_contrast (src/lib.rs:606-626)
-        const float g1 = (next[c] - prev[c]) / 2.f;
-        const float g2 = (curr[c + W] - curr[c - W]) / 2.f;
-        const float g3 = (curr[c + 1] - curr[c - 1]) / 2.f;
-        const float interp = os * g1 + oy * g2 + ox * g3;
-        const float contrast = fabsf(curr[c] + interp / 2.f);
-        if (contrast * (float)kScalesPerOctave <= kContrastThreshold) continue;
-        // extremum_is_on_edge (src/lib.rs:630-653)
-        const float v2 = curr[c] * 2.0f;
-        const float h11 = curr[c + W] + curr[c - W] - v2;
-        const float d22 = curr[c + 1] + curr[c - 1] - v2;
-        const float h12 = (curr[c + W + 1] - curr[c + W - 1] - curr[c - W + 1] + curr[c - W - 1]) / 4.f;
-        const float tr = d22 + h11;
-        const float det = d22 * h11 - h12 * h12;
-        if (det <= 0.f) continue;
-        if ((tr * tr * kEdgeThreshold) > (kEdgeThreshold + 1.0f) * (kEdgeThreshold + 1.0f) * det) continue;
-        const uint32_t slot = atomicAdd(L.counter, 1u);
-        if (slot >= L.cap) continue;
-        ExtRec e;
-        e.key = make_key((uint32_t)(L.img_base + b), (uint32_t)L.octave, (uint32_t)s_in, (uint32_t)y, (uint32_t)x);
-        e.img = L.img_base + b;
-        e.octave = L.octave;
-        e.scale = sc;
-        e.x = xi;
-        e.y = yi;
-        e.off_s = os;
-        e.off_x = ox;
-        e.off_y = oy;
-        e.response = contrast;
-        e.pad = 0;
-        L.out[slot] = e;
     }
+#undef T
 }
 
 void launch_detect(const DetectLaunch& L, hipStream_t st) {
@@ -186,15 +224,16 @@ __global__ __launch_bounds__(256) void k_orient(const OrientLaunch L) {
     const uint32_t r = blockIdx.x * 4 + wave;
     const bool active = r < L.n_ext;
     ExtRec e;
-    int W = 1, H = 1, radius = 0, n = 1, N = 0;
+    int W = 1, H = 1, pitch = 1, radius = 0, n = 1, N = 0;
     float kp_scale = 0.f, kp_x = 0.f, kp_y = 0.f, osf = 1.f;
     const float* img = nullptr;
     if (active) {
         e = L.ext[r];
         W = L.ow[e.octave];
         H = L.oh[e.octave];
+        pitch = L.opitch[e.octave];
         img = L.gauss[e.octave] + (size_t)(e.img - L.img_base) * L.gauss_img_stride[e.octave] +
-              (size_t)e.scale * W * H;
+              (size_t)e.scale * pitch * H;
         osf = (float)(1u << e.octave);  // 2_f32.powi(octave)
         kp_scale = 0.8f * pow2_f32(((float)e.scale + e.off_s) / (float)kScalesPerOctave) * 2.f;
         kp_x = ((float)e.x + e.off_x) * osf;
@@ -215,9 +254,9 @@ __global__ __launch_bounds__(256) void k_orient(const OrientLaunch L) {
             uint8_t bin = 0xff;
             float val = 0.0f;
             if (yy > 0 && yy < H - 1 && xx > 0 && xx < W - 1) {
-                const float* rw = img + (size_t)yy * W;
+                const float* rw = img + (size_t)yy * pitch;
                 const float dx = rw[xx + 1] - rw[xx - 1];
-                const float dy = img[(size_t)(yy - 1) * W + xx] - img[(size_t)(yy + 1) * W + xx];
+                const float dy = rw[xx - pitch] - rw[xx + pitch];
                 const float wexp = (float)(yp * yp + xp * xp) * gws;
                 const float weight = exp_f32(wexp);
                 const float mag = sqrtf(dx * dx + dy * dy);

@@ -235,14 +235,15 @@ struct ResizeTabDev {
 struct Plan {
     uint32_t w = 0, h = 0, chunk = 0;
     int n_oct = 0;
-    std::vector<int> ow, oh;
-    std::vector<size_t> P;           // pixels per octave image
+    std::vector<int> ow, oh, opitch;
+    std::vector<size_t> P;           // floats per octave image plane (pitch * H)
+    std::vector<size_t> px;          // real pixels per octave image (W * H)
     std::vector<size_t> goff, doff;  // float offsets of octave arenas
     DevBuf<float> arena;             // [G_0 | D_0 | G_1 | D_1 ...], each chunk-major
     ResizeTabDev seed_tab;
     DevBuf<const float*> d_gauss;
     DevBuf<size_t> d_gstride;
-    DevBuf<int> d_ow, d_oh;
+    DevBuf<int> d_ow, d_oh, d_opitch;
     BlurTaps seed_taps{};
     int seed_r = 0;
     BlurTaps oct_taps[kImagesPerOctave]{};
@@ -261,6 +262,7 @@ struct Plan {
         d_gstride.release();
         d_ow.release();
         d_oh.release();
+        d_opitch.release();
         w = h = chunk = 0;
         n_oct = 0;
     }
@@ -337,7 +339,9 @@ int ensure_plan(sift_mi_ctx* c, uint32_t w, uint32_t h, uint32_t chunk) {
     p.n_oct = n_octaves_for(w, h);
     p.ow.assign(p.n_oct, 0);
     p.oh.assign(p.n_oct, 0);
+    p.opitch.assign(p.n_oct, 0);
     p.P.assign(p.n_oct, 0);
+    p.px.assign(p.n_oct, 0);
     p.goff.assign(p.n_oct, 0);
     p.doff.assign(p.n_oct, 0);
     int ow = 2 * (int)w, oh = 2 * (int)h;
@@ -347,8 +351,10 @@ int ensure_plan(sift_mi_ctx* c, uint32_t w, uint32_t h, uint32_t chunk) {
         if (ow < 1 || oh < 1) return fail(SIFT_MI_EINVAL, "image too small for the octave count");
         p.ow[o] = ow;
         p.oh[o] = oh;
-        p.P[o] = (size_t)ow * oh;
-        sum_p += p.P[o];
+        p.opitch[o] = (ow + 63) & ~63;  // 256-B aligned rows
+        p.P[o] = (size_t)p.opitch[o] * oh;
+        p.px[o] = (size_t)ow * oh;
+        sum_p += p.px[o];
         p.goff[o] = total;
         total += (size_t)chunk * kImagesPerOctave * p.P[o];
         p.doff[o] = total;
@@ -381,10 +387,12 @@ int ensure_plan(sift_mi_ctx* c, uint32_t w, uint32_t h, uint32_t chunk) {
     CHK(p.d_gstride.ensure(p.n_oct));
     CHK(p.d_ow.ensure(p.n_oct));
     CHK(p.d_oh.ensure(p.n_oct));
+    CHK(p.d_opitch.ensure(p.n_oct));
     HIPCHK(hipMemcpyAsync(p.d_gauss.p, gp.data(), p.n_oct * sizeof(float*), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(p.d_gstride.p, gs.data(), p.n_oct * sizeof(size_t), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(p.d_ow.p, p.ow.data(), p.n_oct * sizeof(int), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(p.d_oh.p, p.oh.data(), p.n_oct * sizeof(int), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(p.d_opitch.p, p.opitch.data(), p.n_oct * sizeof(int), hipMemcpyHostToDevice, st));
     HIPCHK(hipStreamSynchronize(st));
     p.seed_r = cv_blur_taps(seed_sigma(), &p.seed_taps);
     double sig[kImagesPerOctave];
@@ -399,22 +407,22 @@ int ensure_plan(sift_mi_ctx* c, uint32_t w, uint32_t h, uint32_t chunk) {
 int run_pyramid(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, size_t row_stride, uint32_t n) {
     Plan& p = c->plan;
     hipStream_t st = c->stream;
-    // seed: 2x bilinear into plane 5 of octave 0 (scratch), then blur -> plane 0
-    float* g0 = p.gauss(0);
-    const size_t P0 = p.P[0];
-    launch_upsample2x(d_frames, frame_pitch, row_stride, (int)p.w, (int)p.h, p.seed_tab.tab, g0 + 5 * P0,
-                      p.gstride(0), (int)n, st);
-    BlurLaunch L{};
-    L.src = g0 + 5 * P0;
-    L.src_img_stride = p.gstride(0);
-    L.dst = g0;
-    L.dst_img_stride = p.gstride(0);
-    L.W = p.ow[0];
-    L.H = p.oh[0];
-    L.n_img = (int)n;
-    L.taps = p.seed_taps;
-    if (launch_blur(p.seed_r, L, st)) return fail(SIFT_MI_EUNSUPPORTED, "seed blur radius");
-    uint64_t launches = 2;
+    // seed: u8 -> 2x bilinear -> blur, fused, -> plane 0 of octave 0
+    SeedLaunch S{};
+    S.frames = d_frames;
+    S.frame_pitch = frame_pitch;
+    S.row_stride = row_stride;
+    S.sh = (int)p.h;
+    S.tab = p.seed_tab.tab;
+    S.dst = p.gauss(0);
+    S.dst_img_stride = p.gstride(0);
+    S.W = p.ow[0];
+    S.H = p.oh[0];
+    S.pitch = p.opitch[0];
+    S.n_img = (int)n;
+    S.taps = p.seed_taps;
+    if (launch_seed(p.seed_r, S, st)) return fail(SIFT_MI_EUNSUPPORTED, "seed blur radius");
+    uint64_t launches = 1;
     for (int o = 0; o < p.n_oct; o++) {
         float* G = p.gauss(o);
         float* D = p.dog(o);
@@ -430,11 +438,13 @@ int run_pyramid(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, siz
             if (s == 3 && o + 1 < p.n_oct) {
                 B.nxt = p.gauss(o + 1);
                 B.nxt_img_stride = p.gstride(o + 1);
+                B.pitch_n = p.opitch[o + 1];
                 B.wn = p.ow[o + 1];
                 B.hn = p.oh[o + 1];
             }
             B.W = p.ow[o];
             B.H = p.oh[o];
+            B.pitch = p.opitch[o];
             B.n_img = (int)n;
             B.taps = p.oct_taps[s];
             if (launch_blur(p.oct_r[s], B, st)) return fail(SIFT_MI_EUNSUPPORTED, "octave blur radius");
@@ -457,7 +467,7 @@ int run_keypoints(sift_mi_ctx* c, uint32_t n, int64_t limit, uint32_t frame_base
     Plan& p = c->plan;
     hipStream_t st = c->stream;
     uint64_t sum_p = 0;
-    for (int o = 0; o < p.n_oct; o++) sum_p += p.P[o];
+    for (int o = 0; o < p.n_oct; o++) sum_p += p.px[o];
     size_t cap_ext = std::max<size_t>(4096, (size_t)(sum_p * n / 48));
     if (c->ext.cap > cap_ext) cap_ext = c->ext.cap;
     CHK(c->counters.ensure(2 + n));
@@ -472,6 +482,7 @@ int run_keypoints(sift_mi_ctx* c, uint32_t n, int64_t limit, uint32_t frame_base
             D.img_stride = p.dstride(o);
             D.W = p.ow[o];
             D.H = p.oh[o];
+            D.pitch = p.opitch[o];
             D.octave = o;
             D.n_img = (int)n;
             D.img_base = 0;
@@ -502,6 +513,7 @@ int run_keypoints(sift_mi_ctx* c, uint32_t n, int64_t limit, uint32_t frame_base
         O.gauss_img_stride = p.d_gstride.p;
         O.ow = p.d_ow.p;
         O.oh = p.d_oh.p;
+        O.opitch = p.d_opitch.p;
         O.out = c->kp.p;
         O.counter = c->counters.p + 1;
         O.per_img = c->counters.p + 2;
@@ -591,6 +603,7 @@ int run_keypoints(sift_mi_ctx* c, uint32_t n, int64_t limit, uint32_t frame_base
     DL.gauss_img_stride = p.d_gstride.p;
     DL.ow = p.d_ow.p;
     DL.oh = p.d_oh.p;
+    DL.opitch = p.d_opitch.p;
     DL.img_base = 0;
     DL.out_kp = c->out_kp.p;
     DL.out_key = c->out_key.p;
@@ -866,7 +879,9 @@ int sift_mi_read_scale_space(sift_mi_ctx* c, size_t o, float* out) {
     if (!c || !out || !c->have_pyramid) return fail(SIFT_MI_ESTATE, "no precomputed pyramid");
     if (o >= (size_t)c->plan.n_oct) return fail(SIFT_MI_EINVAL, "octave out of range");
     CHK(set_device(c));
-    HIPCHK(hipMemcpy(out, c->plan.gauss((int)o), c->plan.gstride((int)o) * sizeof(float), hipMemcpyDeviceToHost));
+    const Plan& p = c->plan;
+    HIPCHK(hipMemcpy2D(out, (size_t)p.ow[o] * sizeof(float), c->plan.gauss((int)o), (size_t)p.opitch[o] * sizeof(float),
+                       (size_t)p.ow[o] * sizeof(float), (size_t)kImagesPerOctave * p.oh[o], hipMemcpyDeviceToHost));
     return 0;
 }
 
@@ -874,7 +889,9 @@ int sift_mi_read_dog(sift_mi_ctx* c, size_t o, float* out) {
     if (!c || !out || !c->have_pyramid) return fail(SIFT_MI_ESTATE, "no precomputed pyramid");
     if (o >= (size_t)c->plan.n_oct) return fail(SIFT_MI_EINVAL, "octave out of range");
     CHK(set_device(c));
-    HIPCHK(hipMemcpy(out, c->plan.dog((int)o), c->plan.dstride((int)o) * sizeof(float), hipMemcpyDeviceToHost));
+    const Plan& p = c->plan;
+    HIPCHK(hipMemcpy2D(out, (size_t)p.ow[o] * sizeof(float), c->plan.dog((int)o), (size_t)p.opitch[o] * sizeof(float),
+                       (size_t)p.ow[o] * sizeof(float), (size_t)kDogPerOctave * p.oh[o], hipMemcpyDeviceToHost));
     return 0;
 }
 
@@ -900,7 +917,12 @@ int sift_mi_sift_with_precomputed(sift_mi_ctx* c, int64_t limit, size_t* n_keypo
 int sift_mi_compute_descriptor(sift_mi_ctx* c, const float* img, uint32_t w, uint32_t h, float x, float y,
                                float scale, float orientation, uint8_t* out) {
     if (!c || !img || !out || w < 1 || h < 1) return fail(SIFT_MI_EINVAL, "bad arguments");
-    if (!(scale > 0.f) || scale > 64.f) return fail(SIFT_MI_EINVAL, "scale out of supported range (0, 64]");
+    // window radius round(10.61 * scale) <= 39 (the device scratch); the
+    // pipeline's keypoints have scale < 3.6 (radius <= 38)
+    if (!(scale > 0.f) || roundf(3.0f * scale * 1.41421356f * 5.0f * 0.5f) > 39.0f)
+        return fail(SIFT_MI_EUNSUPPORTED, "scale outside (0, 3.7]: descriptor window radius > 39");
+    // the reference indexes its histogram out of bounds (panics) outside [0, 360]
+    if (!(orientation >= 0.f && orientation <= 360.f)) return fail(SIFT_MI_EINVAL, "orientation outside [0, 360]");
     CHK(set_device(c));
     DevBuf<float> dimg;
     DevBuf<uint8_t> dout;

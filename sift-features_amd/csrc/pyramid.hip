@@ -6,96 +6,61 @@
 // cv::GaussianBlur (separable, BORDER_REFLECT_101) for every blur and
 // cv::resize INTER_NEAREST for the octave step.
 //
-// Kernels (all batched over frames with blockIdx.z):
-//   k_upsample2x  u8 frame -> f32 2x bilinear seed (OpenCV half-pixel
-//                 coefficients, separately rounded products)
-//   k_blur_dog<R> one separable blur G_{s-1} -> G_s staged through LDS:
-//                 coalesced tile+halo load, register-blocked row pass
-//                 (4 outputs/thread, ds_read_b128), register-blocked column
-//                 pass (8 outputs/thread); the epilogue also writes
-//                 D_{s-1} = G_s - G_{s-1} and, for s == 3, the next
-//                 octave's base image (nearest 1/2: pixel (2x, 2y)).
-// The stage is HBM-bound: per octave pixel it must write 6 G + 5 D images
-// (44 B); see DESIGN.md for the roofline accounting.
+// HBM layout: octave o of frame f is a [6][H_o][pitch_o] f32 Gaussian stack
+// followed (per octave arena) by the [5][H_o][pitch_o] DoG stack; pitch_o is
+// W_o rounded up to 64 floats so every row starts 256-B aligned.
+//
+// Kernels (batched over frames with blockIdx.z):
+//   k_seed<TH>    u8 frame -> f32 (LUT v/255) -> 2x bilinear (OpenCV half-pixel
+//                 coefficients, separately rounded products) computed on the fly
+//                 for the tile + halo, then the seed blur (R = 5) -> G_0 of
+//                 octave 0.  The upsampled image never touches HBM.
+//   k_blur<R,TH>  one separable blur G_{s-1} -> G_s: interior tiles load the
+//                 tile + halo with 16-B global loads into LDS (reflect-101
+//                 scalar path only on border tiles), the row pass is register-
+//                 blocked (4 outputs/thread, ds_read_b128), the column pass 8
+//                 outputs/thread; the epilogue writes G_s, D_{s-1} = G_s -
+//                 G_{s-1} and, for s == 3, the next octave's base image
+//                 (nearest 1/2 = pixel (2x, 2y)).
+// The stage is HBM-bound: per octave pixel the reference materialises 6 G + 5 D
+// images (44 B); see DESIGN.md for the roofline accounting.
 #include "sift_common.h"
 #include "sift_kernels.h"
 
 namespace siftmi {
 
 // ---------------------------------------------------------------------------
-// Seed: u8 -> f32 (v / 255, image::ConvertBuffer, src/lib.rs:198) -> 2x
-// bilinear (cv::resize INTER_LINEAR, src/lib.rs:201-205).  Coefficient tables
-// are built on the host with OpenCV's formulas (resizeGeneric_).
+// Tile geometry.  Input window columns [x0 - HWL, x0 + TW + HWL) with
+// HWL = R rounded up to 4 so every row segment is float4-aligned.
 // ---------------------------------------------------------------------------
-__global__ __launch_bounds__(256) void k_upsample2x(const uint8_t* __restrict__ frames, size_t frame_pitch,
-                                                    size_t row_stride, int sw, int sh, const ResizeTab tab,
-                                                    float* __restrict__ dst, size_t dst_img_stride, int dw,
-                                                    int dh) {
-    const int dx = blockIdx.x * 64 + (threadIdx.x & 63);
-    const int dy = blockIdx.y * 4 + (threadIdx.x >> 6);
-    if (dx >= dw || dy >= dh) return;
-    const uint8_t* src = frames + (size_t)blockIdx.z * frame_pitch;
-    const int sx = tab.xofs[dx];
-    const float a0 = tab.xa0[dx], a1 = tab.xa1[dx];
-    const bool two = dx < tab.xmax;
-    const int sy0 = tab.yofs[dy];
-    const int sy1 = sy0 + 1 < sh ? sy0 + 1 : sh - 1;
-    const uint8_t* r0 = src + (size_t)sy0 * row_stride;
-    const uint8_t* r1 = src + (size_t)sy1 * row_stride;
-    const int sx1 = two ? sx + 1 : sx;
-    const float p00 = (float)r0[sx] / 255.0f, p01 = (float)r0[sx1] / 255.0f;
-    const float p10 = (float)r1[sx] / 255.0f, p11 = (float)r1[sx1] / 255.0f;
-    // HResizeLinear: t = S[sx]*a0 + S[sx+1]*a1 (two roundings + add)
-    const float h0 = two ? p00 * a0 + p01 * a1 : p00;
-    const float h1 = two ? p10 * a0 + p11 * a1 : p10;
-    // VResizeLinear: S0*b0 + S1*b1
-    dst[(size_t)blockIdx.z * dst_img_stride + (size_t)dy * dw + dx] = h0 * tab.ya0[dy] + h1 * tab.ya1[dy];
-}
-
-// ---------------------------------------------------------------------------
-// Separable Gaussian blur, OpenCV FilterEngine order:
-//   row pass   RowVec_32f:       acc = x[-R]*k[-R]; acc = fma(x[t], k[t], acc) t = -R+1..R
-//   column pass SymmColumnVec_32f: acc = c*k0; acc = fma(up_t + down_t, k_t, acc) t = 1..R
-// Borders: BORDER_REFLECT_101 on both axes (the column border rows are
-// row-filtered reflected source rows, exactly as FilterEngine builds them).
-// ---------------------------------------------------------------------------
-template <int R>
+template <int R, int TH_>
 struct BlurGeom {
-    static constexpr int TW = 64;                     // output tile width
-    static constexpr int TH = 32;                     // output tile height
-    static constexpr int VB = 8;                      // column outputs per thread
-    static constexpr int IH = TH + 2 * R;             // input / row-pass rows
-    static constexpr int IW = TW + 2 * R;             // input columns used
-    static constexpr int NV = (2 * R + 4 + 3) / 4;    // float4 reads per row-pass item
-    static constexpr int IWP = TW - 4 + 4 * NV;       // padded input pitch (>= IW, %4 == 0)
-    static constexpr int LDS_FLOATS = IH * IWP + IH * TW;
+    static constexpr int TW = 64;
+    static constexpr int TH = TH_;
+    static constexpr int VB = TH / 4;                    // column outputs per thread (256 threads, 64 columns)
+    static constexpr int HWL = (R + 3) & ~3;
+    static constexpr int IH = TH + 2 * R;                // rows of the input window / row-pass output
+    static constexpr int IWV = TW + 2 * HWL;             // loaded columns (multiple of 4)
+    static constexpr int IWP = IWV + 4;                  // LDS pitch (breaks 2^k strides)
+    static constexpr int OFF = HWL - R;                  // first used column inside a float4
+    static constexpr int NV = (HWL + R + 7) / 4;         // float4 reads per row-pass item
+    static constexpr int THP = TW + 4;                   // row-pass output pitch
+    static constexpr int LDS_FLOATS = IH * IWP + IH * THP;
+    static constexpr int NLOAD4 = IH * (IWV / 4);        // float4 per interior tile
+    static constexpr int LOADS_PER_THREAD = (NLOAD4 + 255) / 256;
+    static_assert(4 * NV <= IWV - TW + 4, "row-pass reads stay inside the loaded window");
+    static_assert(TH % 4 == 0, "TH");
 };
 
-template <int R>
-__global__ __launch_bounds__(256) void k_blur_dog(const float* __restrict__ src, size_t src_img_stride,
-                                                  float* __restrict__ dst, size_t dst_img_stride,
-                                                  float* __restrict__ dog, size_t dog_img_stride,
-                                                  float* __restrict__ nxt, size_t nxt_img_stride, int wn, int hn,
-                                                  int W, int H, const BlurTaps taps) {
-    using G = BlurGeom<R>;
-    static_assert(G::IWP >= G::IW, "pitch");
-    __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
-    float* tin = lds;                  // [IH][IWP] G_{s-1} tile + halo
-    float* th = lds + G::IH * G::IWP;  // [IH][TW]  row-pass output
+// Row pass + column pass + epilogue, shared by the seed and octave kernels.
+template <int R, int TH>
+__device__ __forceinline__ void blur_tile_compute(const float* __restrict__ tin, float* __restrict__ th,
+                                                  const BlurTaps& taps, int x0, int y0, int W, int H, int pitch,
+                                                  float* __restrict__ dst, float* __restrict__ dog,
+                                                  float* __restrict__ nxt, int pitch_n, int wn, int hn) {
+    using G = BlurGeom<R, TH>;
     const int tid = threadIdx.x;
-    const int x0 = blockIdx.x * G::TW, y0 = blockIdx.y * G::TH;
-    const size_t b = blockIdx.z;
-    src += b * src_img_stride;
-
-    // 1. tile + halo -> LDS (coalesced along rows, reflect-101 at the borders)
-    for (int i = tid; i < G::IH * G::IW; i += 256) {
-        const int ly = i / G::IW, lx = i - ly * G::IW;
-        const int gy = reflect101(y0 - R + ly, H), gx = reflect101(x0 - R + lx, W);
-        tin[ly * G::IWP + lx] = src[(size_t)gy * W + gx];
-    }
-    __syncthreads();
-
-    // 2. row pass: item = (row, quad of 4 outputs); taps read as float4
+    // row pass: item = (row, quad of 4 outputs); fma chain from the leftmost tap
     for (int i = tid; i < G::IH * (G::TW / 4); i += 256) {
         const int ly = i / (G::TW / 4), q = i - ly * (G::TW / 4);
         const float4* rp = reinterpret_cast<const float4*>(tin + ly * G::IWP + 4 * q);
@@ -110,48 +75,154 @@ __global__ __launch_bounds__(256) void k_blur_dog(const float* __restrict__ src,
         }
         float acc[4];
 #pragma unroll
-        for (int o = 0; o < 4; o++) acc[o] = v[o] * taps.k[R];
+        for (int o = 0; o < 4; o++) acc[o] = v[G::OFF + o] * taps.k[R];
 #pragma unroll
         for (int t = 1; t <= 2 * R; t++) {
             const float kt = taps.k[t > R ? t - R : R - t];
 #pragma unroll
-            for (int o = 0; o < 4; o++) acc[o] = __builtin_fmaf(v[o + t], kt, acc[o]);
+            for (int o = 0; o < 4; o++) acc[o] = __builtin_fmaf(v[G::OFF + o + t], kt, acc[o]);
         }
-        *reinterpret_cast<float4*>(th + ly * G::TW + 4 * q) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+        *reinterpret_cast<float4*>(th + ly * G::THP + 4 * q) = make_float4(acc[0], acc[1], acc[2], acc[3]);
     }
     __syncthreads();
-
-    // 3. column pass: item = (column, VB consecutive outputs)
-    for (int i = tid; i < G::TW * (G::TH / G::VB); i += 256) {
-        const int lx = i & (G::TW - 1), p = i / G::TW;
+    // column pass: thread = (column, VB consecutive rows); centre product then
+    // fma of the (below + above) pair sums outwards
+    {
+        const int lx = tid & (G::TW - 1), p = tid / G::TW;
         const int gx = x0 + lx;
         float v[G::VB + 2 * R];
 #pragma unroll
-        for (int j = 0; j < G::VB + 2 * R; j++) v[j] = th[(p * G::VB + j) * G::TW + lx];
-        if (gx >= W) continue;
+        for (int j = 0; j < G::VB + 2 * R; j++) v[j] = th[(p * G::VB + j) * G::THP + lx];
+        if (gx < W) {
 #pragma unroll
-        for (int o = 0; o < G::VB; o++) {
-            const int ly = p * G::VB + o;
-            const int gy = y0 + ly;
-            if (gy >= H) break;
-            float acc = v[o + R] * taps.k[0];
+            for (int o = 0; o < G::VB; o++) {
+                const int ly = p * G::VB + o;
+                const int gy = y0 + ly;
+                if (gy < H) {
+                    float acc = v[o + R] * taps.k[0];
 #pragma unroll
-            for (int t = 1; t <= R; t++) acc = __builtin_fmaf(v[o + R + t] + v[o + R - t], taps.k[t], acc);
-            const size_t off = (size_t)gy * W + gx;
-            dst[b * dst_img_stride + off] = acc;
-            if (dog) dog[b * dog_img_stride + off] = acc - tin[(ly + R) * G::IWP + lx + R];
-            if (nxt && !(gx & 1) && !(gy & 1) && (gx >> 1) < wn && (gy >> 1) < hn)
-                nxt[b * nxt_img_stride + (size_t)(gy >> 1) * wn + (gx >> 1)] = acc;
+                    for (int t = 1; t <= R; t++) acc = __builtin_fmaf(v[o + R + t] + v[o + R - t], taps.k[t], acc);
+                    const size_t off = (size_t)gy * pitch + gx;
+                    dst[off] = acc;
+                    if (dog) dog[off] = acc - tin[(ly + R) * G::IWP + lx + G::HWL];
+                    if (nxt && !(gx & 1) && !(gy & 1) && (gx >> 1) < wn && (gy >> 1) < hn)
+                        nxt[(size_t)(gy >> 1) * pitch_n + (gx >> 1)] = acc;
+                }
+            }
         }
     }
 }
 
+template <int R, int TH>
+__global__ __launch_bounds__(256) void k_blur(const float* __restrict__ src, size_t src_img_stride,
+                                              float* __restrict__ dst, size_t dst_img_stride,
+                                              float* __restrict__ dog, size_t dog_img_stride,
+                                              float* __restrict__ nxt, size_t nxt_img_stride, int pitch_n, int wn,
+                                              int hn, int W, int H, int pitch, const BlurTaps taps) {
+    using G = BlurGeom<R, TH>;
+    __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
+    float* tin = lds;                  // [IH][IWP]  G_{s-1} window
+    float* th = lds + G::IH * G::IWP;  // [IH][THP]  row-pass output
+    const int tid = threadIdx.x;
+    const int x0 = blockIdx.x * G::TW, y0 = blockIdx.y * G::TH;
+    const size_t b = blockIdx.z;
+    src += b * src_img_stride;
+    const bool interior = x0 >= G::HWL && x0 + G::TW + G::HWL <= W && y0 >= R && y0 + G::TH + R <= H;
+    if (interior) {
+        // all loads in flight before the LDS stores (16 B per lane, coalesced rows)
+        float4 tmp[G::LOADS_PER_THREAD];
+        const float* base = src + (size_t)(y0 - R) * pitch + (x0 - G::HWL);
+        // unconditional (index-clamped) loads: a guarded load makes hipcc wait
+        // vmcnt(0) per element and spill the staging array to scratch
+#pragma unroll
+        for (int j = 0; j < G::LOADS_PER_THREAD; j++) {
+            const int i = min(tid + 256 * j, G::NLOAD4 - 1);
+            const int ly = i / (G::IWV / 4), c4 = i - ly * (G::IWV / 4);
+            tmp[j] = *reinterpret_cast<const float4*>(base + (size_t)ly * pitch + 4 * c4);
+        }
+#pragma unroll
+        for (int j = 0; j < G::LOADS_PER_THREAD; j++) {
+            const int i = tid + 256 * j;
+            if (i < G::NLOAD4) {
+                const int ly = i / (G::IWV / 4), c4 = i - ly * (G::IWV / 4);
+                *reinterpret_cast<float4*>(tin + ly * G::IWP + 4 * c4) = tmp[j];
+            }
+        }
+    } else {
+        for (int i = tid; i < G::IH * G::IWV; i += 256) {
+            const int ly = i / G::IWV, lx = i - ly * G::IWV;
+            const int gy = reflect101(y0 - R + ly, H), gx = reflect101(x0 - G::HWL + lx, W);
+            tin[ly * G::IWP + lx] = src[(size_t)gy * pitch + gx];
+        }
+    }
+    __syncthreads();
+    blur_tile_compute<R, TH>(tin, th, taps, x0, y0, W, H, pitch, dst + b * dst_img_stride,
+                             dog ? dog + b * dog_img_stride : nullptr, nxt ? nxt + b * nxt_img_stride : nullptr,
+                             pitch_n, wn, hn);
+}
+
+// ---------------------------------------------------------------------------
+// Seed: u8 -> f32 (v / 255, image::ConvertBuffer, src/lib.rs:198) -> 2x
+// bilinear (cv::resize INTER_LINEAR, src/lib.rs:201-205) -> GaussianBlur
+// (src/lib.rs:207-209), fused.  Coefficient tables are built on the host
+// with OpenCV's formulas (resizeGeneric_).
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ float upsample_at(const uint8_t* __restrict__ src, size_t row_stride, int sh,
+                                             const ResizeTab& tab, const float* __restrict__ lut, int dx, int dy) {
+    const int sx = tab.xofs[dx];
+    const bool two = dx < tab.xmax;
+    const int sx1 = two ? sx + 1 : sx;
+    const int sy0 = tab.yofs[dy];
+    const int sy1 = sy0 + 1 < sh ? sy0 + 1 : sh - 1;
+    const uint8_t* r0 = src + (size_t)sy0 * row_stride;
+    const uint8_t* r1 = src + (size_t)sy1 * row_stride;
+    const float p00 = lut[r0[sx]], p01 = lut[r0[sx1]];
+    const float p10 = lut[r1[sx]], p11 = lut[r1[sx1]];
+    const float a0 = tab.xa0[dx], a1 = tab.xa1[dx];
+    // HResizeLinear: t = S[sx]*a0 + S[sx+1]*a1 (two roundings + add)
+    const float h0 = two ? p00 * a0 + p01 * a1 : p00;
+    const float h1 = two ? p10 * a0 + p11 * a1 : p10;
+    // VResizeLinear: S0*b0 + S1*b1
+    return h0 * tab.ya0[dy] + h1 * tab.ya1[dy];
+}
+
+template <int R, int TH>
+__global__ __launch_bounds__(256) void k_seed(const uint8_t* __restrict__ frames, size_t frame_pitch,
+                                              size_t row_stride, int sh, const ResizeTab tab,
+                                              float* __restrict__ dst, size_t dst_img_stride, int W, int H,
+                                              int pitch, const BlurTaps taps) {
+    using G = BlurGeom<R, TH>;
+    __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
+    __shared__ float lut[256];
+    float* tin = lds;
+    float* th = lds + G::IH * G::IWP;
+    const int tid = threadIdx.x;
+    lut[tid] = (float)tid / 255.0f;
+    __syncthreads();
+    const int x0 = blockIdx.x * G::TW, y0 = blockIdx.y * G::TH;
+    const size_t b = blockIdx.z;
+    const uint8_t* src = frames + b * frame_pitch;
+    for (int i = tid; i < G::IH * G::IWV; i += 256) {
+        const int ly = i / G::IWV, lx = i - ly * G::IWV;
+        const int gy = reflect101(y0 - R + ly, H), gx = reflect101(x0 - G::HWL + lx, W);
+        tin[ly * G::IWP + lx] = upsample_at(src, row_stride, sh, tab, lut, gx, gy);
+    }
+    __syncthreads();
+    blur_tile_compute<R, TH>(tin, th, taps, x0, y0, W, H, pitch, dst + b * dst_img_stride, nullptr, nullptr, 0, 0,
+                             0);
+}
+
+// ---------------------------------------------------------------------------
+// launchers
+// ---------------------------------------------------------------------------
 template <int R>
 static void launch_blur_r(const BlurLaunch& L, hipStream_t st) {
-    using G = BlurGeom<R>;
+    constexpr int TH = R > 8 ? 64 : 32;
+    using G = BlurGeom<R, TH>;
     dim3 grid((L.W + G::TW - 1) / G::TW, (L.H + G::TH - 1) / G::TH, L.n_img);
-    hipLaunchKernelGGL(k_blur_dog<R>, grid, dim3(256), 0, st, L.src, L.src_img_stride, L.dst, L.dst_img_stride, L.dog,
-                       L.dog_img_stride, L.nxt, L.nxt_img_stride, L.wn, L.hn, L.W, L.H, L.taps);
+    hipLaunchKernelGGL((k_blur<R, TH>), grid, dim3(256), 0, st, L.src, L.src_img_stride, L.dst, L.dst_img_stride,
+                       L.dog, L.dog_img_stride, L.nxt, L.nxt_img_stride, L.pitch_n, L.wn, L.hn, L.W, L.H, L.pitch,
+                       L.taps);
 }
 
 int launch_blur(int R, const BlurLaunch& L, hipStream_t st) {
@@ -167,12 +238,23 @@ int launch_blur(int R, const BlurLaunch& L, hipStream_t st) {
     }
 }
 
-void launch_upsample2x(const uint8_t* frames, size_t frame_pitch, size_t row_stride, int sw, int sh,
-                       const ResizeTab& tab, float* dst, size_t dst_img_stride, int n_img, hipStream_t st) {
-    const int dw = 2 * sw, dh = 2 * sh;
-    dim3 grid((dw + 63) / 64, (dh + 3) / 4, n_img);
-    hipLaunchKernelGGL(k_upsample2x, grid, dim3(256), 0, st, frames, frame_pitch, row_stride, sw, sh, tab, dst,
-                       dst_img_stride, dw, dh);
+template <int R>
+static void launch_seed_r(const SeedLaunch& L, hipStream_t st) {
+    constexpr int TH = 32;
+    using G = BlurGeom<R, TH>;
+    dim3 grid((L.W + G::TW - 1) / G::TW, (L.H + G::TH - 1) / G::TH, L.n_img);
+    hipLaunchKernelGGL((k_seed<R, TH>), grid, dim3(256), 0, st, L.frames, L.frame_pitch, L.row_stride, L.sh, L.tab,
+                       L.dst, L.dst_img_stride, L.W, L.H, L.pitch, L.taps);
+}
+
+int launch_seed(int R, const SeedLaunch& L, hipStream_t st) {
+    switch (R) {
+        case 5:
+            launch_seed_r<5>(L, st);
+            return 0;
+        default:
+            return -1;  // seed sigma is a constant: cvRound(1.249 * 8 + 1) | 1 = 11 taps
+    }
 }
 
 // ---------------------------------------------------------------------------

@@ -20,6 +20,7 @@ struct ResizeTab {
     int xmax;
 };
 
+// Image planes are row-pitched: element (y, x) at plane[y * pitch + x].
 struct BlurLaunch {
     const float* src;
     size_t src_img_stride;
@@ -29,16 +30,27 @@ struct BlurLaunch {
     size_t dog_img_stride;
     float* nxt;  // may be null: next octave base (nearest 1/2)
     size_t nxt_img_stride;
-    int wn, hn;
-    int W, H;
+    int pitch_n, wn, hn;
+    int W, H, pitch;
+    int n_img;
+    BlurTaps taps;
+};
+
+struct SeedLaunch {
+    const uint8_t* frames;
+    size_t frame_pitch, row_stride;
+    int sh;          // source height
+    ResizeTab tab;   // 2x bilinear tables
+    float* dst;      // octave 0, plane 0
+    size_t dst_img_stride;
+    int W, H, pitch;  // seed (2x) geometry
     int n_img;
     BlurTaps taps;
 };
 
 // pyramid.hip
 int launch_blur(int radius, const BlurLaunch& L, hipStream_t st);
-void launch_upsample2x(const uint8_t* frames, size_t frame_pitch, size_t row_stride, int sw, int sh,
-                       const ResizeTab& tab, float* dst, size_t dst_img_stride, int n_img, hipStream_t st);
+int launch_seed(int radius, const SeedLaunch& L, hipStream_t st);
 void launch_resize_linear_f32(const float* src, int sw, int sh, const ResizeTab& tab, float* dst, int dw, int dh,
                               hipStream_t st);
 void launch_resize_nearest_f32(const float* src, int sw, const int* xofs, const int* yofs, float* dst, int dw, int dh,
@@ -48,7 +60,7 @@ void launch_resize_nearest_f32(const float* src, int sw, const int* xofs, const 
 struct DetectLaunch {
     const float* dog;  // octave DoG base, image b at dog + b*img_stride, plane s at + s*W*H
     size_t img_stride;
-    int W, H, octave, n_img, img_base;
+    int W, H, pitch, octave, n_img, img_base;
     ExtRec* out;
     uint32_t* counter;
     uint32_t cap;
@@ -62,6 +74,7 @@ struct OrientLaunch {
     const size_t* gauss_img_stride;  // device array [n_octaves]
     const int* ow;                 // device arrays [n_octaves]
     const int* oh;
+    const int* opitch;
     KpRec* out;
     uint32_t* counter;
     uint32_t* per_img;             // [n_img] keypoint counts (indexed by rec.img - img_base)
@@ -91,6 +104,7 @@ struct DescLaunch {
     const size_t* gauss_img_stride;
     const int* ow;
     const int* oh;
+    const int* opitch;
     int img_base;
     OutKp* out_kp;     // may be null
     uint64_t* out_key; // may be null
