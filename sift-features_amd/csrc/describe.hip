@@ -87,9 +87,27 @@ __device__ __forceinline__ void describe_wave(const float* __restrict__ img, int
     __builtin_amdgcn_wave_barrier();
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
     const int total = sc.rowpre[n];
-    // 2. strided walk over the compacted samples
+    // 2. lane-chunked walk over the compacted samples: lane l takes samples
+    // [l*chunk, (l+1)*chunk), so at any step the 64 lanes sit ~chunk samples
+    // apart across the window and their histogram cells rarely coincide
+    // (a strided walk puts neighbouring lanes on the same cell and serialises
+    // the LDS atomics)
+    const int chunk = (total + 63) >> 6;
+    int k = lane * chunk;
+    const int kend = min(total, k + chunk);
     int row = 0;
-    for (int k = lane; k < total; k += 64) {
+    {
+        int lo = 0, hi = n;  // first row with rowpre[row + 1] > k
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (sc.rowpre[mid + 1] <= k)
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        row = lo;
+    }
+    for (; k < kend; k++) {
         while (sc.rowpre[row + 1] <= k) row++;
         const int yi = row - radius;
         const int xi = sc.rowlo[row] + (k - sc.rowpre[row]);

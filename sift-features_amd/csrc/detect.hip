@@ -134,28 +134,30 @@ __global__ __launch_bounds__(256) void k_detect(const DetectLaunch L) {
         const int ly = (tid >> 6) * DT_RPT + rr + 1;
         const int y = y0 + ly - 1;
         if (y < kImageBorder || y >= H - kImageBorder) continue;
+        // point_is_local_extremum (src/lib.rs:437-506): non-strict vs all 26
+        // neighbours.  Branch-free: per plane the 3x3 max/min (centre excluded
+        // on the middle plane) over registers, then one compare per sign.
+        float pmax[kDogPerOctave], pmin[kDogPerOctave], pc[kDogPerOctave], pmax8[kDogPerOctave],
+            pmin8[kDogPerOctave];
+#pragma unroll
+        for (int pl = 0; pl < kDogPerOctave; pl++) {
+            const float a0 = T(pl, ly - 1, lx - 1), a1 = T(pl, ly - 1, lx), a2 = T(pl, ly - 1, lx + 1);
+            const float b0 = T(pl, ly, lx - 1), b1 = T(pl, ly, lx), b2 = T(pl, ly, lx + 1);
+            const float c0 = T(pl, ly + 1, lx - 1), c1 = T(pl, ly + 1, lx), c2 = T(pl, ly + 1, lx + 1);
+            const float m8 = fmaxf(fmaxf(fmaxf(a0, a1), fmaxf(a2, b0)), fmaxf(fmaxf(b2, c0), fmaxf(c1, c2)));
+            const float n8 = fminf(fminf(fminf(a0, a1), fminf(a2, b0)), fminf(fminf(b2, c0), fminf(c1, c2)));
+            pmax8[pl] = m8;
+            pmin8[pl] = n8;
+            pmax[pl] = fmaxf(m8, b1);
+            pmin[pl] = fminf(n8, b1);
+            pc[pl] = b1;
+        }
         for (int s_in = 1; s_in <= kScalesPerOctave; s_in++) {
-            // point_is_local_extremum (src/lib.rs:437-506): non-strict vs all 26
-            const float val = T(s_in, ly, lx);
+            const float val = pc[s_in];
             if (fabsf(val) <= threshold) continue;
-            bool ok = true;
-            if (val > 0.0f) {
-#pragma unroll
-                for (int p = -1; p <= 1; p++)
-#pragma unroll
-                    for (int dy = -1; dy <= 1; dy++)
-#pragma unroll
-                        for (int dx = -1; dx <= 1; dx++)
-                            if (p != 0 || dy != 0 || dx != 0) ok = ok && (val >= T(s_in + p, ly + dy, lx + dx));
-            } else {
-#pragma unroll
-                for (int p = -1; p <= 1; p++)
-#pragma unroll
-                    for (int dy = -1; dy <= 1; dy++)
-#pragma unroll
-                        for (int dx = -1; dx <= 1; dx++)
-                            if (p != 0 || dy != 0 || dx != 0) ok = ok && (val <= T(s_in + p, ly + dy, lx + dx));
-            }
+            const float mx = fmaxf(fmaxf(pmax[s_in - 1], pmax[s_in + 1]), pmax8[s_in]);
+            const float mn = fminf(fminf(pmin[s_in - 1], pmin[s_in + 1]), pmin8[s_in]);
+            const bool ok = val > 0.0f ? val >= mx : val <= mn;
             if (!ok) continue;
             // refinement (src/lib.rs:334-367)
             int sc = s_in, xi = x, yi = y;

@@ -951,20 +951,23 @@ int sift_mi_gaussian_blur(sift_mi_ctx* c, const float* src, uint32_t w, uint32_t
     const int r = cv_blur_taps(sigma, &taps);
     if (r < 1) return fail(SIFT_MI_EUNSUPPORTED, "blur radius outside 1..24");
     DevBuf<float> a, b;
-    const size_t P = (size_t)w * h;
-    CHK(a.ensure(P));
-    CHK(b.ensure(P));
+    const size_t pitch = ((size_t)w + 63) & ~(size_t)63;  // same row alignment as the pyramid
+    CHK(a.ensure(pitch * h));
+    CHK(b.ensure(pitch * h));
     int rc = 0;
     BlurLaunch L{};
     L.src = a.p;
     L.dst = b.p;
     L.W = (int)w;
     L.H = (int)h;
+    L.pitch = (int)pitch;
     L.n_img = 1;
     L.taps = taps;
-    if (hipMemcpyAsync(a.p, src, P * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess ||
+    if (hipMemcpy2DAsync(a.p, pitch * 4, src, (size_t)w * 4, (size_t)w * 4, h, hipMemcpyHostToDevice, c->stream) !=
+            hipSuccess ||
         launch_blur(r, L, c->stream) != 0 ||
-        hipMemcpyAsync(dst, b.p, P * 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+        hipMemcpy2DAsync(dst, (size_t)w * 4, b.p, pitch * 4, (size_t)w * 4, h, hipMemcpyDeviceToHost, c->stream) !=
+            hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess)
         rc = fail(SIFT_MI_EHIP, "gaussian_blur failed");
     a.release();
