@@ -1,13 +1,12 @@
-// 4x4x8 SIFT descriptors on MI355X: one wave per keypoint, four keypoints
-// per workgroup, the 6x6x8 trilinear histogram kept in the wave's LDS slice.
+// 4x4x8 SIFT descriptors on MI355X: one wave (one workgroup) per keypoint,
+// per-sample records staged in LDS, each lane accumulating two histogram bins
+// in the reference's sequential order (describe_wave), no atomics.
 //
 // Reference: compute_descriptors / compute_descriptor (src/lib.rs:759-990).
-// Per-sample arithmetic keeps the reference's operand order; the histogram is
-// accumulated with LDS float atomics (ds_add_f32), so the order of additions
-// into a bin differs from the reference's sequential sample order: bins
-// agree to f32 rounding and the final u8 components to +-1 (tolerance stated
-// in tests/test_gpu_parity.py).  The L2 norms use the reference's exact
-// chunk-of-4 summation order (src/lib.rs:957-976).
+// Every expression keeps the reference's operand order (-ffp-contract=off);
+// bins, L2 norms (chunk-of-4 order, src/lib.rs:957-976) and the u8 output
+// are bit-identical to the CPU path up to 1-ulp differences of the
+// f64-evaluated exp / atan2 / sin / cos vs glibc.
 #include <float.h>
 
 #include "sift_common.h"
@@ -15,29 +14,55 @@
 
 namespace siftmi {
 
-constexpr int HIST_FLOATS = 6 * 6 * kDescBins;  // 288
 
-// Per-wave LDS scratch: 288 histogram bins + the row table of the sample
-// enumeration (first column, prefix count) for up to 2*38+1 = 77 rows.
+// Per-wave LDS scratch: the row table of the sample enumeration (first
+// column, prefix count; up to 2*39+1 rows) and one band of per-sample records.
 constexpr int ROWS_MAX = 80;
+constexpr int REC_CAP = 1664;  // records per band; a window (<= 3223 samples) needs at most 2 bands
+
 struct DescScratch {
-    float hist[HIST_FLOATS];
+    float2 rec[REC_CAP];  // (mag * weight, obin) per compacted sample; mag < 0 marks a rejected sample
     int rowlo[ROWS_MAX];
     int rowpre[ROWS_MAX + 1];
 };
 
-// Wave-cooperative compute_descriptor (src/lib.rs:785-990).
+__device__ __forceinline__ void wave_sync() {
+    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+    __builtin_amdgcn_wave_barrier();
+    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+}
+
+// xi range (float, widened) where a*xi + b lies in [lo, hi); a ~ 0 -> all or nothing
+__device__ __forceinline__ void lin_range(float a, float b, float lo, float hi, float& xlo, float& xhi) {
+    if (fabsf(a) > 1e-6f) {
+        const float u = (lo - b) / a, v = (hi - b) / a;
+        xlo = fmaxf(xlo, fminf(u, v) - 2.0f);
+        xhi = fminf(xhi, fmaxf(u, v) + 2.0f);
+    } else if (!(b >= lo - 1e-3f && b < hi + 1e-3f)) {
+        xhi = xlo - 1.0f;
+    }
+}
+
+// Wave-cooperative compute_descriptor (src/lib.rs:785-990), bit-exact.
 //
-// Only samples whose rotated coordinates fall in the 4x4 histogram region
-// (|col_rot|, |row_rot| < 2.5 bin units, about half of the (2r+1)^2 window)
-// contribute; each row's candidate column interval is computed in f64 and
-// widened by one sample, the compacted (row, col) list is strided over the
-// wave's lanes, and the reference's exact f32 predicate is still evaluated
-// per sample -- so the accepted set is identical to the reference's.
+// The reference adds every sample's 8 trilinear contributions into a 6x6x8
+// histogram in row-major sample order; only the 4x4 interior (128 bins) is
+// kept.  Here lane l owns the 2 interior bins (cell 1 + l/16 ... , orientation
+// pair l%4): phase A evaluates the per-sample values once (gradient, Gaussian
+// weight, f64 atan2) into LDS records, phase B walks, in row-major order,
+// only the samples whose 2x2-cell footprint covers the lane's cell and adds
+// them to its two bins -- the reference's exact per-bin summation order, with
+// no atomics.  Only samples inside the rotated 4x4 region are enumerated
+// (per-row column intervals computed in float and widened; the reference's f32
+// predicate decides), the window is split into bands of <= REC_CAP samples.
+//
+// kAblate (performance experiments only, tools/ubench_kernels.hip; 0 in the
+// product): bit 0 skip phase B, bit 1 replace atan2, bit 2 replace exp,
+// bit 3 replace the gradient loads.
+template <int kAblate = 0>
 __device__ __forceinline__ void describe_wave(const float* __restrict__ img, int pitch, int width, int height,
                                               float xf, float yf, float scale, float orientation,
                                               DescScratch& sc, uint8_t* __restrict__ out, int lane) {
-    for (int i = lane; i < HIST_FLOATS; i += 64) sc.hist[i] = 0.0f;
     const int32_t x = (int32_t)sat_u32(roundf(xf));
     const int32_t y = (int32_t)sat_u32(roundf(yf));
     const float BIN_ANGLE_STEP = (float)kDescBins / 360.0f;
@@ -48,7 +73,7 @@ __device__ __forceinline__ void describe_wave(const float* __restrict__ img, int
     const float sin_ori = (float)sin((double)rad), cos_ori = (float)cos((double)rad);
     const float sin_s = sin_ori / hist_width, cos_s = cos_ori / hist_width;
     const int n = 2 * radius + 1;
-    // 1. per-row candidate column interval
+    // 1. per-row candidate column interval of the whole 4x4 region
     for (int row = lane; row < n; row += 64) {
         const double yi = (double)(row - radius);
         const double c = cos_s, s = sin_s;
@@ -72,9 +97,7 @@ __device__ __forceinline__ void describe_wave(const float* __restrict__ img, int
         sc.rowlo[row] = ilo;
         sc.rowpre[row + 1] = (empty || ihi < ilo) ? 0 : ihi - ilo + 1;
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+    wave_sync();
     if (lane == 0) {
         int acc = 0;
         sc.rowpre[0] = 0;
@@ -83,130 +106,134 @@ __device__ __forceinline__ void describe_wave(const float* __restrict__ img, int
             sc.rowpre[r] = acc;
         }
     }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    const int total = sc.rowpre[n];
-    // 2. lane-chunked walk over the compacted samples: lane l takes samples
-    // [l*chunk, (l+1)*chunk), so at any step the 64 lanes sit ~chunk samples
-    // apart across the window and their histogram cells rarely coincide
-    // (a strided walk puts neighbouring lanes on the same cell and serialises
-    // the LDS atomics)
-    const int chunk = (total + 63) >> 6;
-    int k = lane * chunk;
-    const int kend = min(total, k + chunk);
-    int row = 0;
-    {
-        int lo = 0, hi = n;  // first row with rowpre[row + 1] > k
-        while (lo < hi) {
-            const int mid = (lo + hi) >> 1;
-            if (sc.rowpre[mid + 1] <= k)
-                lo = mid + 1;
-            else
-                hi = mid;
+    wave_sync();
+    // lane role: interior cell (cr, cc) in 1..4, orientation bins b0, b0 + 1
+    const int ci = lane >> 2;
+    const int cr = 1 + (ci >> 2), cc = 1 + (ci & 3);
+    const int b0 = 2 * (lane & 3), b1 = b0 + 1;
+    float acc0 = 0.0f, acc1 = 0.0f;
+    for (int row0 = 0; row0 < n;) {
+        // band [row0, row1): as many rows as fit in REC_CAP records
+        int row1 = row0 + 1;
+        while (row1 < n && sc.rowpre[row1 + 1] - sc.rowpre[row0] <= REC_CAP) row1++;
+        const int kbase = sc.rowpre[row0], kend = sc.rowpre[row1];
+        // phase A: per-sample values, lane-strided over the band
+        int row = row0;
+        for (int k = kbase + lane; k < kend; k += 64) {
+            while (sc.rowpre[row + 1] <= k) row++;
+            const int yi = row - radius;
+            const int xi = sc.rowlo[row] + (k - sc.rowpre[row]);
+            const float col_rot = (float)xi * cos_s - (float)yi * sin_s;
+            const float row_rot = (float)xi * sin_s + (float)yi * cos_s;
+            const float row_bin = row_rot + (float)(kDescHist / 2);
+            const float col_bin = col_rot + (float)(kDescHist / 2);
+            const int32_t ay = y + yi, ax = x + xi;
+            float2 rc = make_float2(-1.0f, 0.0f);
+            if (row_bin > -0.5f && row_bin < (float)kDescHist + 0.5f && col_bin > -0.5f &&
+                col_bin < (float)kDescHist + 0.5f && ay > 0 && ay < height - 1 && ax > 0 && ax < width - 1) {
+                float dx, dy;
+                if (kAblate & 8) {
+                    dx = (float)xi * 0.01f + 0.001f;
+                    dy = (float)yi * 0.01f - 0.002f;
+                } else {
+                    const float* rw = img + (size_t)ay * pitch;
+                    dx = rw[ax + 1] - rw[ax - 1];
+                    dy = rw[ax - pitch] - rw[ax + pitch];
+                }
+                const float wsq = col_rot * col_rot + row_rot * row_rot;
+                const float weight =
+                    (kAblate & 4) ? 1.0f + wsq * (-0.125f) : exp_f32(wsq * (-2.f / (float)(kDescHist * kDescHist)));
+                // ((atan2(dy, dx).to_degrees() + 360) % 360) as f32 - orientation;
+                // the f64 remainder of v in [180, 540] by 360 is exactly v or v - 360
+                double deg = ((kAblate & 2) ? (double)(dy * 50.0f + dx)
+                                            : atan2((double)dy, (double)dx) * (180.0 / 3.14159265358979323846)) +
+                             360.0;
+                deg = deg >= 360.0 ? deg - 360.0 : deg;
+                const float ori = (float)deg - orientation;
+                const float mag = sqrtf(dx * dx + dy * dy);
+                rc = make_float2(mag * weight, ori * BIN_ANGLE_STEP);
+            }
+            sc.rec[k - kbase] = rc;
         }
-        row = lo;
+        wave_sync();
+        // phase B: this lane's 2x2-cell footprint, row-major
+        if (!(kAblate & 1)) {
+            for (int rw = row0; rw < row1; rw++) {
+                const int yi = rw - radius;
+                const int cnt = sc.rowpre[rw + 1] - sc.rowpre[rw];
+                if (cnt == 0) continue;
+                const int rlo = sc.rowlo[rw];
+                // r1 in {cr-1, cr}  <=>  row_rot in [cr - 3.5, cr - 1.5); same for columns
+                float xlo = (float)rlo, xhi = (float)(rlo + cnt - 1);
+                lin_range(sin_s, (float)yi * cos_s, (float)cr - 3.5f, (float)cr - 1.5f, xlo, xhi);
+                lin_range(cos_s, -(float)yi * sin_s, (float)cc - 3.5f, (float)cc - 1.5f, xlo, xhi);
+                const int xa = max(rlo, (int)ceilf(xlo)), xb = min(rlo + cnt - 1, (int)floorf(xhi));
+                const int kr = sc.rowpre[rw] - rlo - kbase;
+                for (int xi = xa; xi <= xb; xi++) {
+                    const float2 rc = sc.rec[kr + xi];
+                    if (rc.x < 0.0f) continue;
+                    const float col_rot = (float)xi * cos_s - (float)yi * sin_s;
+                    const float row_rot = (float)xi * sin_s + (float)yi * cos_s;
+                    const float rb = (row_rot + (float)(kDescHist / 2)) - 0.5f;
+                    const float cb = (col_rot + (float)(kDescHist / 2)) - 0.5f;
+                    const float rf = floorf(rb), cf = floorf(cb);
+                    const int r1 = (int)rf + 1, q1 = (int)cf + 1;
+                    if ((r1 != cr && r1 + 1 != cr) || (q1 != cc && q1 + 1 != cc)) continue;
+                    const float mag = rc.x, obin = rc.y;
+                    const float of = floorf(obin);
+                    const float ori_frac = obin - of;
+                    int o0 = (int)of;
+                    o0 = o0 < 0 ? o0 + kDescBins : (o0 >= kDescBins ? o0 - kDescBins : o0);
+                    const int o1 = o0 + 1 >= kDescBins ? 0 : o0 + 1;
+                    const float c1 = mag * (rb - rf), c0 = mag - c1;
+                    const float crow = cr == r1 ? c0 : c1;
+                    const float t = crow * (cb - cf);
+                    const float ccol = cc == q1 ? crow - t : t;
+                    const float hi = ccol * ori_frac, lo = ccol - hi;
+                    acc0 += o0 == b0 ? lo : (o1 == b0 ? hi : 0.0f);
+                    acc1 += o0 == b1 ? lo : (o1 == b1 ? hi : 0.0f);
+                }
+            }
+        } else {
+            acc0 += sc.rec[lane].x;
+        }
+        wave_sync();
+        row0 = row1;
     }
-    for (; k < kend; k++) {
-        while (sc.rowpre[row + 1] <= k) row++;
-        const int yi = row - radius;
-        const int xi = sc.rowlo[row] + (k - sc.rowpre[row]);
-        const float col_rot = (float)xi * cos_s - (float)yi * sin_s;
-        const float row_rot = (float)xi * sin_s + (float)yi * cos_s;
-        float row_bin = row_rot + (float)(kDescHist / 2);
-        float col_bin = col_rot + (float)(kDescHist / 2);
-        const int32_t ay = y + yi, ax = x + xi;
-        if (!(row_bin > -0.5f && row_bin < (float)kDescHist + 0.5f && col_bin > -0.5f &&
-              col_bin < (float)kDescHist + 0.5f && ay > 0 && ay < height - 1 && ax > 0 && ax < width - 1))
-            continue;
-        const float* rw = img + (size_t)ay * pitch;
-        const float dx = rw[ax + 1] - rw[ax - 1];
-        const float dy = rw[ax - pitch] - rw[ax + pitch];
-        const float wsq = col_rot * col_rot + row_rot * row_rot;
-        const float weight = exp_f32(wsq * (-2.f / (float)(kDescHist * kDescHist)));
-        // ((atan2(dy, dx).to_degrees() + 360) % 360) as f32 - orientation; the
-        // f64 remainder of v in [180, 540] by 360 is exactly v or v - 360
-        double deg = atan2((double)dy, (double)dx) * (180.0 / 3.14159265358979323846) + 360.0;
-        deg = deg >= 360.0 ? deg - 360.0 : deg;
-        const float ori = (float)deg - orientation;
-        float mag = sqrtf(dx * dx + dy * dy);
-        row_bin = row_bin - 0.5f;
-        col_bin = col_bin - 0.5f;
-        mag = mag * weight;
-        const float obin = ori * BIN_ANGLE_STEP;
-        const float row_floor = floorf(row_bin), col_floor = floorf(col_bin), ori_floor = floorf(obin);
-        const float row_frac = row_bin - row_floor, col_frac = col_bin - col_floor, ori_frac = obin - ori_floor;
-        const float c1 = mag * row_frac, c0 = mag - c1;
-        const float c11 = c1 * col_frac, c10 = c1 - c11;
-        const float c01 = c0 * col_frac, c00 = c0 - c01;
-        const float c111 = c11 * ori_frac, c110 = c11 - c111;
-        const float c101 = c10 * ori_frac, c100 = c10 - c101;
-        const float c011 = c01 * ori_frac, c010 = c01 - c011;
-        const float c001 = c00 * ori_frac, c000 = c00 - c001;
-        // row_floor in [-1, 3], col_floor in [-1, 3] inside the accepted region;
-        // ori_floor in [-8, 7] for orientation in [0, 360] (host-checked)
-        const int r1 = (int)row_floor + 1, q1 = (int)col_floor + 1;
-        int o0 = (int)ori_floor;
-        o0 = o0 < 0 ? o0 + kDescBins : (o0 >= kDescBins ? o0 - kDescBins : o0);
-        if ((unsigned)r1 > 4u || (unsigned)q1 > 4u || (unsigned)o0 >= (unsigned)kDescBins) continue;
-        const int o1 = o0 + 1 >= kDescBins ? 0 : o0 + 1;
-        float* h11 = sc.hist + (r1 * 6 + q1) * kDescBins;
-        float* h12 = h11 + kDescBins;
-        float* h21 = h11 + 6 * kDescBins;
-        float* h22 = h21 + kDescBins;
-        atomicAdd(h11 + o0, c000);
-        atomicAdd(h11 + o1, c001);
-        atomicAdd(h12 + o0, c010);
-        atomicAdd(h12 + o1, c011);
-        atomicAdd(h21 + o0, c100);
-        atomicAdd(h21 + o1, c101);
-        atomicAdd(h22 + o0, c110);
-        atomicAdd(h22 + o1, c111);
-    }
-    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-    __builtin_amdgcn_wave_barrier();
-    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-    // lane l < 32 owns flat components 4l..4l+3 (= reference chunk l)
-    float v[4];
-    const int l = lane & 31;
-#pragma unroll
-    for (int j = 0; j < 4; j++) {
-        const int i = 4 * l + j;
-        const int rr = 1 + (i >> 5), cc = 1 + ((i >> 3) & 3), oo = i & 7;
-        v[j] = sc.hist[(rr * 6 + cc) * kDescBins + oo];
-    }
+    // normalisation (src/lib.rs:951-989): lane l holds flat[2l], flat[2l+1];
+    // chunk j = flat[4j..4j+4) = lanes 2j, 2j+1; exact chunk-of-4 order
+    const float c_hi0 = __shfl(acc0, (lane + 1) & 63), c_hi1 = __shfl(acc1, (lane + 1) & 63);
     float s = 0.0f;
-#pragma unroll
-    for (int j = 0; j < 4; j++) s += v[j] * v[j];
+    s += acc0 * acc0;
+    s += acc1 * acc1;
+    s += c_hi0 * c_hi0;
+    s += c_hi1 * c_hi1;
     float l2 = __shfl(s, 0);
-    for (int c = 1; c < 32; c++) l2 = l2 + __shfl(s, c);
+    for (int j = 1; j < 32; j++) l2 = l2 + __shfl(s, 2 * j);
     l2 = sqrtf(l2);
     const float cap = l2 * 0.2f;
-#pragma unroll
-    for (int j = 0; j < 4; j++) v[j] = fminf(v[j], cap);
+    const float v0 = fminf(acc0, cap), v1 = fminf(acc1, cap);
+    const float d_hi0 = __shfl(v0, (lane + 1) & 63), d_hi1 = __shfl(v1, (lane + 1) & 63);
     s = 0.0f;
-#pragma unroll
-    for (int j = 0; j < 4; j++) s += v[j] * v[j];
+    s += v0 * v0;
+    s += v1 * v1;
+    s += d_hi0 * d_hi0;
+    s += d_hi1 * d_hi1;
     float l2c = __shfl(s, 0);
-    for (int c = 1; c < 32; c++) l2c = l2c + __shfl(s, c);
+    for (int j = 1; j < 32; j++) l2c = l2c + __shfl(s, 2 * j);
     l2c = sqrtf(l2c);
     const float norm = 512.0f / fmaxf(l2c, FLT_EPSILON);
-    if (lane < 32) {
-        uint32_t packed = 0;
-#pragma unroll
-        for (int j = 0; j < 4; j++) {
-            const int32_t q = sat_i32(roundf(v[j] * norm));
-            const uint32_t u = q > 255 ? 255u : (uint32_t)(uint8_t)q;
-            packed |= u << (8 * j);
-        }
-        reinterpret_cast<uint32_t*>(out)[lane] = packed;
-    }
+    const int32_t q0 = sat_i32(roundf(v0 * norm)), q1v = sat_i32(roundf(v1 * norm));
+    const uint32_t u0 = q0 > 255 ? 255u : (uint32_t)(uint8_t)q0;
+    const uint32_t u1 = q1v > 255 ? 255u : (uint32_t)(uint8_t)q1v;
+    reinterpret_cast<uint16_t*>(out)[lane] = (uint16_t)(u0 | (u1 << 8));
 }
 
-__global__ __launch_bounds__(256) void k_describe(const DescLaunch L) {
-    __shared__ DescScratch scr[4];
-    const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t i = blockIdx.x * 4 + wave;
+template <int kAblate>
+__global__ __launch_bounds__(64) void k_describe(const DescLaunch L) {
+    __shared__ DescScratch scr[1];
+    const int wave = 0, lane = threadIdx.x;
+    const uint32_t i = blockIdx.x;
     if (i >= L.n) return;  // whole wave; no workgroup barrier below
     const KpRec kp = L.kp[L.idx ? L.idx[i] : i];
     const int o = kp.octave;
@@ -218,7 +245,7 @@ __global__ __launch_bounds__(256) void k_describe(const DescLaunch L) {
     const float angle = 360.0f - kp.angle;
     const float osf = 1.0f / (float)(1u << o);  // 2_f32.powi(-octave)
     const float kp_size = kp.size * osf;
-    describe_wave(img, pitch, W, H, kp.x * osf, kp.y * osf, kp_size, angle, scr[wave],
+    describe_wave<kAblate>(img, pitch, W, H, kp.x * osf, kp.y * osf, kp_size, angle, scr[wave],
                   L.out_desc + (size_t)i * kDescSize, lane);
     if (lane == 0) {
         if (L.out_kp) {
@@ -236,8 +263,7 @@ __global__ __launch_bounds__(256) void k_describe(const DescLaunch L) {
 
 void launch_describe(const DescLaunch& L, hipStream_t st) {
     if (L.n == 0) return;
-    dim3 grid((L.n + 3) / 4);
-    hipLaunchKernelGGL(k_describe, grid, dim3(256), 0, st, L);
+    hipLaunchKernelGGL(k_describe<0>, dim3(L.n), dim3(64), 0, st, L);
 }
 
 __global__ __launch_bounds__(64) void k_describe_one(const float* img, int w, int h, float x, float y, float scale,

@@ -76,8 +76,8 @@ __device__ __forceinline__ bool interpolate(const float* __restrict__ dog, int W
 // ---------------------------------------------------------------------------
 // k_detect: thread = (column, 4 consecutive rows) of a 64x16 tile, all three
 // scale triples of the octave.  The 5 DoG planes of the tile (+1 px halo)
-// are staged in LDS with 16-B loads on interior tiles; the rare extrema run
-// the refinement chain (interpolate / contrast / edge) from global memory.
+// are staged in LDS with 16-B loads on interior tiles.  Extrema are appended
+// as packed emission keys for k_refine.
 // ---------------------------------------------------------------------------
 constexpr int DT_W = 64, DT_H = 16, DT_RPT = 4;     // rows per thread
 constexpr int DT_LH = DT_H + 2, DT_LWV = DT_W + 8;  // loaded window [x0-4, x0+68)
@@ -85,14 +85,19 @@ constexpr int DT_LP = DT_LWV + 4;                    // LDS pitch
 constexpr int DT_NLOAD4 = kDogPerOctave * DT_LH * (DT_LWV / 4);
 constexpr int DT_LPT = (DT_NLOAD4 + 255) / 256;
 
+constexpr int DT_LCAP = 512;  // per-block LDS candidate list (overflow goes straight to global)
+
 __global__ __launch_bounds__(256) void k_detect(const DetectLaunch L) {
     __shared__ __attribute__((aligned(16))) float t[kDogPerOctave * DT_LH * DT_LP];
+    __shared__ uint64_t lcand[DT_LCAP];
+    __shared__ uint32_t lcount, gbase;
     const int W = L.W, H = L.H, pitch = L.pitch;
     const int x0 = blockIdx.x * DT_W, y0 = blockIdx.y * DT_H;
     const int b = blockIdx.z;
     const float* dog = L.dog + (size_t)b * L.img_stride;
     const size_t P = (size_t)pitch * H;
     const int tid = threadIdx.x;
+    if (tid == 0) lcount = 0;
     const bool interior = x0 >= 4 && x0 + DT_W + 4 <= pitch && y0 >= 1 && y0 + DT_H + 1 <= H;
     if (interior) {
         float4 tmp[DT_LPT];
@@ -126,14 +131,14 @@ __global__ __launch_bounds__(256) void k_detect(const DetectLaunch L) {
     __syncthreads();
     const int lx = (tid & 63) + 4;  // LDS column of this thread's pixel
     const int x = x0 + (tid & 63);
-    if (x < kImageBorder || x >= W - kImageBorder) return;
+    const bool xin = x >= kImageBorder && x < W - kImageBorder;
     // threshold = floor(0.5 * 0.04 / 3) = 0 (src/lib.rs:460)
     const float threshold = floorf(0.5f * kContrastThreshold / (float)kScalesPerOctave);
 #define T(pl, yy, xx) t[((pl) * DT_LH + (yy)) * DT_LP + (xx)]
     for (int rr = 0; rr < DT_RPT; rr++) {
         const int ly = (tid >> 6) * DT_RPT + rr + 1;
         const int y = y0 + ly - 1;
-        if (y < kImageBorder || y >= H - kImageBorder) continue;
+        if (!xin || y < kImageBorder || y >= H - kImageBorder) continue;
         // point_is_local_extremum (src/lib.rs:437-506): non-strict vs all 26
         // neighbours.  Branch-free: per plane the 3x3 max/min (centre excluded
         // on the middle plane) over registers, then one compare per sign.
@@ -159,55 +164,106 @@ __global__ __launch_bounds__(256) void k_detect(const DetectLaunch L) {
             const float mn = fminf(fminf(pmin[s_in - 1], pmin[s_in + 1]), pmin8[s_in]);
             const bool ok = val > 0.0f ? val >= mx : val <= mn;
             if (!ok) continue;
-            // refinement (src/lib.rs:334-367)
-            int sc = s_in, xi = x, yi = y;
-            float os, ox, oy;
-            if (!interpolate(dog, W, H, pitch, sc, xi, yi, os, ox, oy)) continue;
-            const float* prev = dog + (size_t)(sc - 1) * P;
-            const float* curr = dog + (size_t)sc * P;
-            const float* next = dog + (size_t)(sc + 1) * P;
-            const size_t c = (size_t)yi * pitch + xi;
-            // extremum_contrast (src/lib.rs:606-626)
-            const float g1 = (next[c] - prev[c]) / 2.f;
-            const float g2 = (curr[c + pitch] - curr[c - pitch]) / 2.f;
-            const float g3 = (curr[c + 1] - curr[c - 1]) / 2.f;
-            const float interp = os * g1 + oy * g2 + ox * g3;
-            const float contrast = fabsf(curr[c] + interp / 2.f);
-            if (contrast * (float)kScalesPerOctave <= kContrastThreshold) continue;
-            // extremum_is_on_edge (src/lib.rs:630-653)
-            const float v2 = curr[c] * 2.0f;
-            const float h11 = curr[c + pitch] + curr[c - pitch] - v2;
-            const float d22 = curr[c + 1] + curr[c - 1] - v2;
-            const float h12 =
-                (curr[c + pitch + 1] - curr[c + pitch - 1] - curr[c - pitch + 1] + curr[c - pitch - 1]) / 4.f;
-            const float tr = d22 + h11;
-            const float det = d22 * h11 - h12 * h12;
-            if (det <= 0.f) continue;
-            if ((tr * tr * kEdgeThreshold) > (kEdgeThreshold + 1.0f) * (kEdgeThreshold + 1.0f) * det) continue;
-            const uint32_t slot = atomicAdd(L.counter, 1u);
-            if (slot >= L.cap) continue;
-            ExtRec e;
-            e.key = make_key((uint32_t)(L.img_base + b), (uint32_t)L.octave, (uint32_t)s_in, (uint32_t)y,
-                             (uint32_t)x);
-            e.img = L.img_base + b;
-            e.octave = L.octave;
-            e.scale = sc;
-            e.x = xi;
-            e.y = yi;
-            e.off_s = os;
-            e.off_x = ox;
-            e.off_y = oy;
-            e.response = contrast;
-            e.pad = 0;
-            L.out[slot] = e;
+            // candidate -> refinement kernel (dense, so its dependent global
+            // loads overlap across many threads instead of stalling this tile)
+            const uint64_t key =
+                make_key((uint32_t)(L.img_base + b), (uint32_t)L.octave, (uint32_t)s_in, (uint32_t)y, (uint32_t)x);
+            const uint32_t li = atomicAdd(&lcount, 1u);
+            if (li < DT_LCAP) {
+                lcand[li] = key;
+            } else {
+                const uint32_t slot = atomicAdd(L.counter, 1u);
+                if (slot < L.cap) L.cand[slot] = key;
+            }
         }
     }
+    // one global atomic per block (a single hot counter serialises at the
+    // memory side), then a coalesced copy of the block's list
+    __syncthreads();
+    const uint32_t nl = lcount < DT_LCAP ? lcount : DT_LCAP;
+    if (nl == 0) return;
+    if (tid == 0) gbase = atomicAdd(L.counter, nl);
+    __syncthreads();
+    for (uint32_t i = tid; i < nl; i += 256)
+        if (gbase + i < L.cap) L.cand[gbase + i] = lcand[i];
 #undef T
 }
 
 void launch_detect(const DetectLaunch& L, hipStream_t st) {
     dim3 grid((L.W + DT_W - 1) / DT_W, (L.H + DT_H - 1) / DT_H, L.n_img);
     hipLaunchKernelGGL(k_detect, grid, dim3(256), 0, st, L);
+}
+
+// ---------------------------------------------------------------------------
+// k_refine: one thread per candidate extremum -- interpolate_extremum,
+// extremum_contrast, extremum_is_on_edge (src/lib.rs:334-367); accepted
+// extrema are appended with one atomic per wave.
+// ---------------------------------------------------------------------------
+__device__ __forceinline__ bool refine_one(const RefineLaunch& L, uint64_t key, ExtRec& e) {
+    const int b = (int)(key >> kKeyImgShift);
+    const int o = (int)((key >> kKeyOctShift) & 15);
+    const int s_in = (int)((key >> kKeyScaleShift) & 3);
+    const int y = (int)((key >> kKeyYShift) & 0x3fff);
+    const int x = (int)((key >> kKeyXShift) & 0x3fff);
+    const int W = L.ow[o], H = L.oh[o], pitch = L.opitch[o];
+    const float* dog = L.dog[o] + (size_t)(b - L.img_base) * L.dog_img_stride[o];
+    const size_t P = (size_t)pitch * H;
+    int sc = s_in, xi = x, yi = y;
+    float os, ox, oy;
+    if (!interpolate(dog, W, H, pitch, sc, xi, yi, os, ox, oy)) return false;
+    const float* prev = dog + (size_t)(sc - 1) * P;
+    const float* curr = dog + (size_t)sc * P;
+    const float* next = dog + (size_t)(sc + 1) * P;
+    const size_t c = (size_t)yi * pitch + xi;
+    // extremum_contrast (src/lib.rs:606-626)
+    const float g1 = (next[c] - prev[c]) / 2.f;
+    const float g2 = (curr[c + pitch] - curr[c - pitch]) / 2.f;
+    const float g3 = (curr[c + 1] - curr[c - 1]) / 2.f;
+    const float interp = os * g1 + oy * g2 + ox * g3;
+    const float contrast = fabsf(curr[c] + interp / 2.f);
+    if (contrast * (float)kScalesPerOctave <= kContrastThreshold) return false;
+    // extremum_is_on_edge (src/lib.rs:630-653)
+    const float v2 = curr[c] * 2.0f;
+    const float h11 = curr[c + pitch] + curr[c - pitch] - v2;
+    const float d22 = curr[c + 1] + curr[c - 1] - v2;
+    const float h12 = (curr[c + pitch + 1] - curr[c + pitch - 1] - curr[c - pitch + 1] + curr[c - pitch - 1]) / 4.f;
+    const float tr = d22 + h11;
+    const float det = d22 * h11 - h12 * h12;
+    if (det <= 0.f) return false;
+    if ((tr * tr * kEdgeThreshold) > (kEdgeThreshold + 1.0f) * (kEdgeThreshold + 1.0f) * det) return false;
+    e.key = key;
+    e.img = b;
+    e.octave = o;
+    e.scale = sc;
+    e.x = xi;
+    e.y = yi;
+    e.off_s = os;
+    e.off_x = ox;
+    e.off_y = oy;
+    e.response = contrast;
+    e.pad = 0;
+    return true;
+}
+
+__global__ __launch_bounds__(256) void k_refine(const RefineLaunch L) {
+    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
+    ExtRec e;
+    const bool keep = i < L.n_cand && refine_one(L, L.cand[i], e);
+    const uint64_t mask = __ballot(keep);
+    if (!mask) return;
+    const int lane = threadIdx.x & 63;
+    const int leader = __ffsll((unsigned long long)mask) - 1;
+    uint32_t base = 0;
+    if (lane == leader) base = atomicAdd(L.counter, (uint32_t)__popcll(mask));
+    base = __shfl(base, leader);
+    if (!keep) return;
+    const uint32_t slot = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+    if (slot < L.cap) L.out[slot] = e;
+}
+
+void launch_refine(const RefineLaunch& L, hipStream_t st) {
+    if (L.n_cand == 0) return;
+    hipLaunchKernelGGL(k_refine, dim3((L.n_cand + 255) / 256), dim3(256), 0, st, L);
 }
 
 // ---------------------------------------------------------------------------
@@ -222,6 +278,7 @@ constexpr int OR_LDS = 1092;
 __global__ __launch_bounds__(256) void k_orient(const OrientLaunch L) {
     __shared__ __attribute__((aligned(16))) float sval[4][OR_LDS];
     __shared__ __attribute__((aligned(16))) uint8_t sbin[4][OR_LDS];
+    __shared__ uint32_t wcount[4], wbase;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t r = blockIdx.x * 4 + wave;
     const bool active = r < L.n_ext;
@@ -276,8 +333,8 @@ __global__ __launch_bounds__(256) void k_orient(const OrientLaunch L) {
         }
     }
     __syncthreads();
-    if (!active) return;
-    // sequential per-bin sums (lane = bin)
+    // sequential per-bin sums (lane = bin); inactive waves run on an empty list
+    if (!active) N = 0;
     float acc = 0.0f;
     {
         const float4* v4 = reinterpret_cast<const float4*>(sval[wave]);
@@ -312,14 +369,17 @@ __global__ __launch_bounds__(256) void k_orient(const OrientLaunch L) {
     const bool peak = lane < kOriBins && h > hm && h > hp && h >= thr;
     const uint64_t mask = __ballot(peak);
     const uint32_t npk = (uint32_t)__popcll(mask);
-    if (npk == 0) return;
-    uint32_t base = 0;
-    if (lane == 0) {
-        base = atomicAdd(L.counter, npk);
-        atomicAdd(L.per_img + (e.img - L.img_base), npk);
+    // one global atomic per workgroup (4 waves)
+    if (lane == 0) wcount[wave] = npk;
+    __syncthreads();
+    if (threadIdx.x == 0) {
+        const uint32_t tot = wcount[0] + wcount[1] + wcount[2] + wcount[3];
+        wbase = tot ? atomicAdd(L.counter, tot) : 0u;
     }
-    base = __shfl(base, 0);
+    __syncthreads();
     if (!peak) return;
+    uint32_t base = wbase;
+    for (int w = 0; w < wave; w++) base += wcount[w];
     const uint32_t slot = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
     if (slot >= L.cap) return;
     const float interp = (hm - hp) / (hm - 2.0f * h + hp);

@@ -241,8 +241,8 @@ struct Plan {
     std::vector<size_t> goff, doff;  // float offsets of octave arenas
     DevBuf<float> arena;             // [G_0 | D_0 | G_1 | D_1 ...], each chunk-major
     ResizeTabDev seed_tab;
-    DevBuf<const float*> d_gauss;
-    DevBuf<size_t> d_gstride;
+    DevBuf<const float*> d_gauss, d_dog;
+    DevBuf<size_t> d_gstride, d_dstride;
     DevBuf<int> d_ow, d_oh, d_opitch;
     BlurTaps seed_taps{};
     int seed_r = 0;
@@ -260,6 +260,8 @@ struct Plan {
         seed_tab.release();
         d_gauss.release();
         d_gstride.release();
+        d_dog.release();
+        d_dstride.release();
         d_ow.release();
         d_oh.release();
         d_opitch.release();
@@ -280,6 +282,7 @@ struct sift_mi_ctx {
     Plan plan;
     DevBuf<uint8_t> staging;  // host-sourced frames
     // detection / description buffers
+    DevBuf<uint64_t> cand;
     DevBuf<ExtRec> ext;
     DevBuf<KpRec> kp;
     DevBuf<uint32_t> counters;  // [0] extrema, [1] keypoints, [2..] per frame
@@ -377,14 +380,20 @@ int ensure_plan(sift_mi_ctx* c, uint32_t w, uint32_t h, uint32_t chunk) {
     CHK(p.arena.ensure(total));
     hipStream_t st = c->stream;
     CHK(p.seed_tab.upload((int)w, (int)h, 2 * (int)w, 2 * (int)h, st));
-    std::vector<const float*> gp(p.n_oct);
-    std::vector<size_t> gs(p.n_oct);
+    std::vector<const float*> gp(p.n_oct), dp(p.n_oct);
+    std::vector<size_t> gs(p.n_oct), ds(p.n_oct);
     for (int o = 0; o < p.n_oct; o++) {
         gp[o] = p.gauss(o);
         gs[o] = p.gstride(o);
+        dp[o] = p.dog(o);
+        ds[o] = p.dstride(o);
     }
     CHK(p.d_gauss.ensure(p.n_oct));
     CHK(p.d_gstride.ensure(p.n_oct));
+    CHK(p.d_dog.ensure(p.n_oct));
+    CHK(p.d_dstride.ensure(p.n_oct));
+    HIPCHK(hipMemcpyAsync(p.d_dog.p, dp.data(), p.n_oct * sizeof(float*), hipMemcpyHostToDevice, st));
+    HIPCHK(hipMemcpyAsync(p.d_dstride.p, ds.data(), p.n_oct * sizeof(size_t), hipMemcpyHostToDevice, st));
     CHK(p.d_ow.ensure(p.n_oct));
     CHK(p.d_oh.ensure(p.n_oct));
     CHK(p.d_opitch.ensure(p.n_oct));
@@ -468,13 +477,14 @@ int run_keypoints(sift_mi_ctx* c, uint32_t n, int64_t limit, uint32_t frame_base
     hipStream_t st = c->stream;
     uint64_t sum_p = 0;
     for (int o = 0; o < p.n_oct; o++) sum_p += p.px[o];
-    size_t cap_ext = std::max<size_t>(4096, (size_t)(sum_p * n / 48));
-    if (c->ext.cap > cap_ext) cap_ext = c->ext.cap;
-    CHK(c->counters.ensure(2 + n));
-    uint32_t n_ext = 0;
+    // counters: [0] candidates, [1] extrema, [2] keypoints, [3..3+n) per frame
+    size_t cap_cand = std::max<size_t>({8192, (size_t)(sum_p * n / 256), c->cand.cap});
+    CHK(c->counters.ensure(3 + n));
+    CHK(c->h_counts.ensure(3 + n));
+    uint32_t n_cand = 0;
     for (int attempt = 0; attempt < 3; attempt++) {
-        CHK(c->ext.ensure(cap_ext));
-        HIPCHK(hipMemsetAsync(c->counters.p, 0, (2 + n) * sizeof(uint32_t), st));
+        CHK(c->cand.ensure(cap_cand));
+        HIPCHK(hipMemsetAsync(c->counters.p, 0, (3 + n) * sizeof(uint32_t), st));
         for (int o = 0; o < p.n_oct; o++) {
             if (p.oh[o] < 2 * kImageBorder || p.ow[o] < 2 * kImageBorder) continue;  // src/lib.rs:315
             DetectLaunch D{};
@@ -486,26 +496,47 @@ int run_keypoints(sift_mi_ctx* c, uint32_t n, int64_t limit, uint32_t frame_base
             D.octave = o;
             D.n_img = (int)n;
             D.img_base = 0;
-            D.out = c->ext.p;
+            D.cand = c->cand.p;
             D.counter = c->counters.p;
-            D.cap = (uint32_t)c->ext.cap;
+            D.cap = (uint32_t)c->cand.cap;
             launch_detect(D, st);
         }
         HIPCHK(hipGetLastError());
-        CHK(c->h_counts.ensure(2 + n));
         HIPCHK(hipMemcpyAsync(c->h_counts.p, c->counters.p, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
-        n_ext = c->h_counts.p[0];
-        if (n_ext <= c->ext.cap) break;
-        cap_ext = (size_t)n_ext + n_ext / 4 + 1024;
-        if (attempt == 2) return fail(SIFT_MI_ENOMEM, "extremum buffer overflow");
+        n_cand = c->h_counts.p[0];
+        if (n_cand <= c->cand.cap) break;
+        cap_cand = (size_t)n_cand + n_cand / 4 + 4096;
+        if (attempt == 2) return fail(SIFT_MI_ENOMEM, "candidate buffer overflow");
     }
+    size_t cap_ext = std::max<size_t>((size_t)n_cand, 1024);
+    if (c->ext.cap > cap_ext) cap_ext = c->ext.cap;
+    CHK(c->ext.ensure(cap_ext));  // every candidate yields at most one extremum
+    {
+        RefineLaunch R{};
+        R.cand = c->cand.p;
+        R.n_cand = n_cand;
+        R.dog = p.d_dog.p;
+        R.dog_img_stride = p.d_dstride.p;
+        R.ow = p.d_ow.p;
+        R.oh = p.d_oh.p;
+        R.opitch = p.d_opitch.p;
+        R.img_base = 0;
+        R.out = c->ext.p;
+        R.counter = c->counters.p + 1;
+        R.cap = (uint32_t)c->ext.cap;
+        launch_refine(R, st);
+        HIPCHK(hipGetLastError());
+        HIPCHK(hipMemcpyAsync(c->h_counts.p + 1, c->counters.p + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipStreamSynchronize(st));
+    }
+    const uint32_t n_ext = c->h_counts.p[1];
     HIPCHK(hipEventRecord(c->ev[2], st));
     size_t cap_kp = std::max<size_t>(2 * (size_t)n_ext + 1024, c->kp.cap);
     uint32_t n_kp = 0;
     for (int attempt = 0; attempt < 3; attempt++) {
         CHK(c->kp.ensure(cap_kp));
-        HIPCHK(hipMemsetAsync(c->counters.p + 1, 0, (1 + n) * sizeof(uint32_t), st));
+        HIPCHK(hipMemsetAsync(c->counters.p + 2, 0, sizeof(uint32_t), st));
         OrientLaunch O{};
         O.ext = c->ext.p;
         O.n_ext = n_ext;
@@ -515,21 +546,19 @@ int run_keypoints(sift_mi_ctx* c, uint32_t n, int64_t limit, uint32_t frame_base
         O.oh = p.d_oh.p;
         O.opitch = p.d_opitch.p;
         O.out = c->kp.p;
-        O.counter = c->counters.p + 1;
-        O.per_img = c->counters.p + 2;
+        O.counter = c->counters.p + 2;
         O.img_base = 0;
         O.cap = (uint32_t)c->kp.cap;
         launch_orient(O, st);
         HIPCHK(hipGetLastError());
-        HIPCHK(hipMemcpyAsync(c->h_counts.p, c->counters.p, (2 + n) * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+        HIPCHK(hipMemcpyAsync(c->h_counts.p, c->counters.p, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
         HIPCHK(hipStreamSynchronize(st));
-        n_kp = c->h_counts.p[1];
+        n_kp = c->h_counts.p[2];
         if (n_kp <= c->kp.cap) break;
         cap_kp = (size_t)n_kp + n_kp / 4 + 1024;
         if (attempt == 2) return fail(SIFT_MI_ENOMEM, "keypoint buffer overflow");
     }
     HIPCHK(hipEventRecord(c->ev[3], st));
-    std::vector<uint32_t> cnt(c->h_counts.p + 2, c->h_counts.p + 2 + n);
     // emission order: radix sort of the keys
     CHK(c->keys_a.ensure(n_kp));
     CHK(c->keys_b.ensure(n_kp));
@@ -546,6 +575,23 @@ int run_keypoints(sift_mi_ctx* c, uint32_t n, int64_t limit, uint32_t frame_base
                                 n_kp, end_bit, st))
         return fail(SIFT_MI_EHIP, "radix sort failed");
     const uint32_t* order = c->vals_b.p;  // emission order -> kp index
+    // per-frame counts from the frame boundaries of the sorted keys
+    uint32_t* d_starts = c->counters.p + 3;
+    HIPCHK(hipMemsetAsync(d_starts, 0xff, n * sizeof(uint32_t), st));
+    launch_frame_starts(c->keys_b.p, n_kp, d_starts, st);
+    HIPCHK(hipMemcpyAsync(c->h_counts.p + 3, d_starts, n * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipStreamSynchronize(st));
+    std::vector<uint32_t> cnt(n, 0);
+    {
+        uint32_t next = n_kp;
+        for (int f = (int)n - 1; f >= 0; f--) {
+            const uint32_t s0 = c->h_counts.p[3 + f];
+            if (s0 != 0xffffffffu) {
+                cnt[f] = next - s0;
+                next = s0;
+            }
+        }
+    }
     // features_limit (src/lib.rs:156-161)
     std::vector<uint32_t> out_cnt(cnt);
     bool any_limit = false;
@@ -746,6 +792,7 @@ void sift_mi_destroy(sift_mi_ctx* c) {
     (void)hipStreamSynchronize(c->stream);
     c->plan.release();
     c->staging.release();
+    c->cand.release();
     c->ext.release();
     c->kp.release();
     c->counters.release();

@@ -35,6 +35,18 @@ void launch_make_sort_keys(const KpRec* kp, uint32_t n, uint64_t* keys, uint32_t
     hipLaunchKernelGGL(k_make_sort_keys, dim3((n + 255) / 256), dim3(256), 0, st, kp, n, keys, vals);
 }
 
+__global__ void k_frame_starts(const uint64_t* __restrict__ keys, uint32_t n, uint32_t* __restrict__ starts) {
+    const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i >= n) return;
+    const uint32_t f = (uint32_t)(keys[i] >> kKeyImgShift);
+    if (i == 0 || (uint32_t)(keys[i - 1] >> kKeyImgShift) != f) starts[f] = i;
+}
+
+void launch_frame_starts(const uint64_t* sorted_keys, uint32_t n, uint32_t* starts, hipStream_t st) {
+    if (!n) return;
+    hipLaunchKernelGGL(k_frame_starts, dim3((n + 255) / 256), dim3(256), 0, st, sorted_keys, n, starts);
+}
+
 // key = (frame << 32) | ~bits(response)  (response >= 0, so bit order == value order)
 __global__ void k_make_resp_keys(const KpRec* __restrict__ kp, const uint32_t* __restrict__ order, uint32_t n,
                                  int img_base, uint64_t* __restrict__ keys, uint32_t* __restrict__ vals) {

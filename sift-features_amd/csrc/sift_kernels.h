@@ -61,11 +61,26 @@ struct DetectLaunch {
     const float* dog;  // octave DoG base, image b at dog + b*img_stride, plane s at + s*W*H
     size_t img_stride;
     int W, H, pitch, octave, n_img, img_base;
-    ExtRec* out;
+    uint64_t* cand;  // packed candidate keys (frame, octave, scale, y, x)
     uint32_t* counter;
     uint32_t cap;
 };
 void launch_detect(const DetectLaunch& L, hipStream_t st);
+
+struct RefineLaunch {
+    const uint64_t* cand;
+    uint32_t n_cand;
+    const float* const* dog;       // device array [n_octaves] of octave D bases
+    const size_t* dog_img_stride;  // device array [n_octaves]
+    const int* ow;
+    const int* oh;
+    const int* opitch;
+    int img_base;
+    ExtRec* out;
+    uint32_t* counter;
+    uint32_t cap;
+};
+void launch_refine(const RefineLaunch& L, hipStream_t st);
 
 struct OrientLaunch {
     const ExtRec* ext;
@@ -77,7 +92,6 @@ struct OrientLaunch {
     const int* opitch;
     KpRec* out;
     uint32_t* counter;
-    uint32_t* per_img;             // [n_img] keypoint counts (indexed by rec.img - img_base)
     int img_base;
     uint32_t cap;
 };
@@ -88,6 +102,9 @@ void launch_orient(const OrientLaunch& L, hipStream_t st);
 size_t sort_pairs_u64(void* temp, size_t temp_bytes, const uint64_t* kin, uint64_t* kout, const uint32_t* vin,
                       uint32_t* vout, uint32_t n, int end_bit, hipStream_t st);
 void launch_make_sort_keys(const KpRec* kp, uint32_t n, uint64_t* keys, uint32_t* vals, hipStream_t st);
+// starts[f] = first index of frame f in the sorted keys (0xffffffff if none);
+// starts must be pre-filled with 0xff bytes
+void launch_frame_starts(const uint64_t* sorted_keys, uint32_t n, uint32_t* starts, hipStream_t st);
 void launch_make_resp_keys(const KpRec* kp, const uint32_t* order, uint32_t n, int img_base, uint64_t* keys,
                            uint32_t* vals, hipStream_t st);
 // final[i] = src index: for frame f, if take_resp[f] final = resp_order[seg], else emission order
