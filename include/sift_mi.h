@@ -98,6 +98,12 @@ int sift_mi_extract_batch_device(sift_mi_ctx* ctx, const uint8_t* d_frames, size
                                  uint32_t width, uint32_t height, size_t row_stride, int64_t features_limit,
                                  size_t* offsets);
 
+/* Descriptor accumulation order.  0 (default): lane-private histograms summed
+ * per bin -- components within +-1 of the reference.  1: bins accumulated in
+ * the reference's sequential sample order (src/lib.rs:883-948) -- bit-exact
+ * descriptors, slower.  Keypoints are identical in both modes. */
+int sift_mi_set_exact_descriptors(sift_mi_ctx* ctx, int exact);
+
 /* Skip the device->host copy of results in batch calls (results stay in
  * device memory; see sift_mi_device_results).  Default 0 = copy. */
 int sift_mi_set_keep_on_device(sift_mi_ctx* ctx, int keep);

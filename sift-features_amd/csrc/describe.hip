@@ -1,13 +1,18 @@
 // 4x4x8 SIFT descriptors on MI355X: one wave (one workgroup) per keypoint,
-// per-sample records staged in LDS, each lane accumulating two histogram bins
-// in the reference's sequential order (describe_wave), no atomics.
+// no atomics.  Two accumulation strategies over the same per-sample math:
+//   describe_wave_fast  (default) lane-private LDS histograms, summed per bin;
+//                       u8 components within +-1 of the reference;
+//   describe_wave_exact bin-owner lanes adding in the reference's sequential
+//                       sample order -- bit-identical bins and bytes (up to
+//                       1-ulp differences of the f64-evaluated exp / atan2 /
+//                       sin / cos vs glibc), ~7x slower.
 //
 // Reference: compute_descriptors / compute_descriptor (src/lib.rs:759-990).
 // Every expression keeps the reference's operand order (-ffp-contract=off);
-// bins, L2 norms (chunk-of-4 order, src/lib.rs:957-976) and the u8 output
-// are bit-identical to the CPU path up to 1-ulp differences of the
-// f64-evaluated exp / atan2 / sin / cos vs glibc.
+// the L2 norms use the reference's chunk-of-4 order (src/lib.rs:957-976).
 #include <float.h>
+
+#include <type_traits>
 
 #include "sift_common.h"
 #include "sift_kernels.h"
@@ -32,15 +37,59 @@ __device__ __forceinline__ void wave_sync() {
     __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
 }
 
-// xi range (float, widened) where a*xi + b lies in [lo, hi); a ~ 0 -> all or nothing
-__device__ __forceinline__ void lin_range(float a, float b, float lo, float hi, float& xlo, float& xhi) {
-    if (fabsf(a) > 1e-6f) {
-        const float u = (lo - b) / a, v = (hi - b) / a;
-        xlo = fmaxf(xlo, fminf(u, v) - 2.0f);
-        xhi = fminf(xhi, fmaxf(u, v) + 2.0f);
-    } else if (!(b >= lo - 1e-3f && b < hi + 1e-3f)) {
-        xhi = xlo - 1.0f;
-    }
+// Footprint of a cell on one axis: a*xi + k*yi in [c - 3.5, c - 1.5).  For
+// |a| > 1e-6 the xi bounds are lo(yi) = lo0 + kk*yi, hi(yi) = hi0 + kk*yi
+// (widened by 2 columns; the exact f32 floor test decides membership).
+// Otherwise the constraint does not depend on xi: the whole row is in or out.
+__device__ __forceinline__ void lin_bounds(float a, float k, float c, float& lo0, float& hi0, float& kk,
+                                           bool& row_only) {
+    row_only = !(fabsf(a) > 1e-6f);
+    const float inv = row_only ? 0.0f : 1.0f / a;
+    const float u = (c - 3.5f) * inv, v = (c - 1.5f) * inv;
+    lo0 = fminf(u, v) - 2.0f;
+    hi0 = fmaxf(u, v) + 2.0f;
+    kk = -k * inv;
+}
+__device__ __forceinline__ bool row_in(float fy, float k, float c) {
+    const float b = fy * k;
+    return b >= c - 3.5f - 1e-3f && b < c - 1.5f + 1e-3f;
+}
+__device__ __forceinline__ float row_lo(float lo0, float kk, bool row_only, float fy, float k, float c) {
+    return row_only ? (row_in(fy, k, c) ? -1e9f : 1e9f) : lo0 + kk * fy;
+}
+__device__ __forceinline__ float row_hi(float hi0, float kk, bool row_only, float fy, float k, float c) {
+    return row_only ? (row_in(fy, k, c) ? 1e9f : -1e9f) : hi0 + kk * fy;
+}
+
+// Normalisation (src/lib.rs:951-989) of the 128 interior bins held two per
+// lane (lane l: flat[2l], flat[2l+1]); chunk j = flat[4j..4j+4) = lanes 2j,
+// 2j+1, summed in the reference's exact chunk-of-4 order.
+__device__ __forceinline__ void describe_normalize(float acc0, float acc1, uint8_t* __restrict__ out, int lane) {
+    const float c_hi0 = __shfl(acc0, (lane + 1) & 63), c_hi1 = __shfl(acc1, (lane + 1) & 63);
+    float s = 0.0f;
+    s += acc0 * acc0;
+    s += acc1 * acc1;
+    s += c_hi0 * c_hi0;
+    s += c_hi1 * c_hi1;
+    float l2 = __shfl(s, 0);
+    for (int j = 1; j < 32; j++) l2 = l2 + __shfl(s, 2 * j);
+    l2 = sqrtf(l2);
+    const float cap = l2 * 0.2f;
+    const float v0 = fminf(acc0, cap), v1 = fminf(acc1, cap);
+    const float d_hi0 = __shfl(v0, (lane + 1) & 63), d_hi1 = __shfl(v1, (lane + 1) & 63);
+    s = 0.0f;
+    s += v0 * v0;
+    s += v1 * v1;
+    s += d_hi0 * d_hi0;
+    s += d_hi1 * d_hi1;
+    float l2c = __shfl(s, 0);
+    for (int j = 1; j < 32; j++) l2c = l2c + __shfl(s, 2 * j);
+    l2c = sqrtf(l2c);
+    const float norm = 512.0f / fmaxf(l2c, FLT_EPSILON);
+    const int32_t q0 = sat_i32(roundf(v0 * norm)), q1v = sat_i32(roundf(v1 * norm));
+    const uint32_t u0 = q0 > 255 ? 255u : (uint32_t)(uint8_t)q0;
+    const uint32_t u1 = q1v > 255 ? 255u : (uint32_t)(uint8_t)q1v;
+    reinterpret_cast<uint16_t*>(out)[lane] = (uint16_t)(u0 | (u1 << 8));
 }
 
 // Wave-cooperative compute_descriptor (src/lib.rs:785-990), bit-exact.
@@ -60,9 +109,9 @@ __device__ __forceinline__ void lin_range(float a, float b, float lo, float hi, 
 // product): bit 0 skip phase B, bit 1 replace atan2, bit 2 replace exp,
 // bit 3 replace the gradient loads.
 template <int kAblate = 0>
-__device__ __forceinline__ void describe_wave(const float* __restrict__ img, int pitch, int width, int height,
-                                              float xf, float yf, float scale, float orientation,
-                                              DescScratch& sc, uint8_t* __restrict__ out, int lane) {
+__device__ __forceinline__ void describe_wave_exact(const float* __restrict__ img, int pitch, int width, int height,
+                                                    float xf, float yf, float scale, float orientation,
+                                                    DescScratch& sc, uint8_t* __restrict__ out, int lane) {
     const int32_t x = (int32_t)sat_u32(roundf(xf));
     const int32_t y = (int32_t)sat_u32(roundf(yf));
     const float BIN_ANGLE_STEP = (float)kDescBins / 360.0f;
@@ -112,6 +161,14 @@ __device__ __forceinline__ void describe_wave(const float* __restrict__ img, int
     const int cr = 1 + (ci >> 2), cc = 1 + (ci & 3);
     const int b0 = 2 * (lane & 3), b1 = b0 + 1;
     float acc0 = 0.0f, acc1 = 0.0f;
+    // footprint bounds per row as linear functions of yi (widened by 2 columns):
+    //   r1 in {cr-1, cr}  <=>  row_rot = xi*sin_s + yi*cos_s in [cr - 3.5, cr - 1.5)
+    //   q1 in {cc-1, cc}  <=>  col_rot = xi*cos_s - yi*sin_s in [cc - 3.5, cc - 1.5)
+    // (a ~ 0 coefficient makes the constraint row-only; see lin_bounds)
+    float aLo, aHi, aK, bLo, bHi, bK;
+    bool aRow, bRow;
+    lin_bounds(sin_s, cos_s, (float)cr, aLo, aHi, aK, aRow);
+    lin_bounds(cos_s, -sin_s, (float)cc, bLo, bHi, bK, bRow);
     for (int row0 = 0; row0 < n;) {
         // band [row0, row1): as many rows as fit in REC_CAP records
         int row1 = row0 + 1;
@@ -156,43 +213,51 @@ __device__ __forceinline__ void describe_wave(const float* __restrict__ img, int
             sc.rec[k - kbase] = rc;
         }
         wave_sync();
-        // phase B: this lane's 2x2-cell footprint, row-major
+        // phase B: this lane's 2x2-cell footprint, row-major.  Each lane walks
+        // its own flattened (row, column) cursor so the wave iterates
+        // max-over-lanes(footprint) times instead of sum-over-rows(max).
         if (!(kAblate & 1)) {
-            for (int rw = row0; rw < row1; rw++) {
-                const int yi = rw - radius;
-                const int cnt = sc.rowpre[rw + 1] - sc.rowpre[rw];
-                if (cnt == 0) continue;
-                const int rlo = sc.rowlo[rw];
-                // r1 in {cr-1, cr}  <=>  row_rot in [cr - 3.5, cr - 1.5); same for columns
-                float xlo = (float)rlo, xhi = (float)(rlo + cnt - 1);
-                lin_range(sin_s, (float)yi * cos_s, (float)cr - 3.5f, (float)cr - 1.5f, xlo, xhi);
-                lin_range(cos_s, -(float)yi * sin_s, (float)cc - 3.5f, (float)cc - 1.5f, xlo, xhi);
-                const int xa = max(rlo, (int)ceilf(xlo)), xb = min(rlo + cnt - 1, (int)floorf(xhi));
-                const int kr = sc.rowpre[rw] - rlo - kbase;
-                for (int xi = xa; xi <= xb; xi++) {
-                    const float2 rc = sc.rec[kr + xi];
-                    if (rc.x < 0.0f) continue;
-                    const float col_rot = (float)xi * cos_s - (float)yi * sin_s;
-                    const float row_rot = (float)xi * sin_s + (float)yi * cos_s;
-                    const float rb = (row_rot + (float)(kDescHist / 2)) - 0.5f;
-                    const float cb = (col_rot + (float)(kDescHist / 2)) - 0.5f;
-                    const float rf = floorf(rb), cf = floorf(cb);
-                    const int r1 = (int)rf + 1, q1 = (int)cf + 1;
-                    if ((r1 != cr && r1 + 1 != cr) || (q1 != cc && q1 + 1 != cc)) continue;
-                    const float mag = rc.x, obin = rc.y;
-                    const float of = floorf(obin);
-                    const float ori_frac = obin - of;
-                    int o0 = (int)of;
-                    o0 = o0 < 0 ? o0 + kDescBins : (o0 >= kDescBins ? o0 - kDescBins : o0);
-                    const int o1 = o0 + 1 >= kDescBins ? 0 : o0 + 1;
-                    const float c1 = mag * (rb - rf), c0 = mag - c1;
-                    const float crow = cr == r1 ? c0 : c1;
-                    const float t = crow * (cb - cf);
-                    const float ccol = cc == q1 ? crow - t : t;
-                    const float hi = ccol * ori_frac, lo = ccol - hi;
-                    acc0 += o0 == b0 ? lo : (o1 == b0 ? hi : 0.0f);
-                    acc1 += o0 == b1 ? lo : (o1 == b1 ? hi : 0.0f);
+            int rw = row0 - 1, xi = 1, xb = 0, kr = 0, yi = 0;
+            for (;;) {
+                if (xi > xb) {  // advance to the next row with a non-empty interval
+                    if (++rw >= row1) break;
+                    yi = rw - radius;
+                    const int pre = sc.rowpre[rw];
+                    const int cnt = sc.rowpre[rw + 1] - pre;
+                    const int rlo = sc.rowlo[rw];
+                    const float fy = (float)yi;
+                    float xlo = fmaxf(row_lo(aLo, aK, aRow, fy, cos_s, (float)cr),
+                                      row_lo(bLo, bK, bRow, fy, -sin_s, (float)cc));
+                    float xhi = fminf(row_hi(aHi, aK, aRow, fy, cos_s, (float)cr),
+                                      row_hi(bHi, bK, bRow, fy, -sin_s, (float)cc));
+                    xi = max(rlo, (int)ceilf(xlo));
+                    xb = min(rlo + cnt - 1, (int)floorf(xhi));
+                    kr = pre - rlo - kbase;
+                    continue;
                 }
+                const float2 rc = sc.rec[kr + xi];
+                const float col_rot = (float)xi * cos_s - (float)yi * sin_s;
+                const float row_rot = (float)xi * sin_s + (float)yi * cos_s;
+                xi++;
+                if (rc.x < 0.0f) continue;
+                const float rb = (row_rot + (float)(kDescHist / 2)) - 0.5f;
+                const float cb = (col_rot + (float)(kDescHist / 2)) - 0.5f;
+                const float rf = floorf(rb), cf = floorf(cb);
+                const int r1 = (int)rf + 1, q1 = (int)cf + 1;
+                if ((r1 != cr && r1 + 1 != cr) || (q1 != cc && q1 + 1 != cc)) continue;
+                const float mag = rc.x, obin = rc.y;
+                const float of = floorf(obin);
+                const float ori_frac = obin - of;
+                int o0 = (int)of;
+                o0 = o0 < 0 ? o0 + kDescBins : (o0 >= kDescBins ? o0 - kDescBins : o0);
+                const int o1 = o0 + 1 >= kDescBins ? 0 : o0 + 1;
+                const float c1 = mag * (rb - rf), c0 = mag - c1;
+                const float crow = cr == r1 ? c0 : c1;
+                const float t = crow * (cb - cf);
+                const float ccol = cc == q1 ? crow - t : t;
+                const float hi = ccol * ori_frac, lo = ccol - hi;
+                acc0 += o0 == b0 ? lo : (o1 == b0 ? hi : 0.0f);
+                acc1 += o0 == b1 ? lo : (o1 == b1 ? hi : 0.0f);
             }
         } else {
             acc0 += sc.rec[lane].x;
@@ -200,41 +265,176 @@ __device__ __forceinline__ void describe_wave(const float* __restrict__ img, int
         wave_sync();
         row0 = row1;
     }
-    // normalisation (src/lib.rs:951-989): lane l holds flat[2l], flat[2l+1];
-    // chunk j = flat[4j..4j+4) = lanes 2j, 2j+1; exact chunk-of-4 order
-    const float c_hi0 = __shfl(acc0, (lane + 1) & 63), c_hi1 = __shfl(acc1, (lane + 1) & 63);
-    float s = 0.0f;
-    s += acc0 * acc0;
-    s += acc1 * acc1;
-    s += c_hi0 * c_hi0;
-    s += c_hi1 * c_hi1;
-    float l2 = __shfl(s, 0);
-    for (int j = 1; j < 32; j++) l2 = l2 + __shfl(s, 2 * j);
-    l2 = sqrtf(l2);
-    const float cap = l2 * 0.2f;
-    const float v0 = fminf(acc0, cap), v1 = fminf(acc1, cap);
-    const float d_hi0 = __shfl(v0, (lane + 1) & 63), d_hi1 = __shfl(v1, (lane + 1) & 63);
-    s = 0.0f;
-    s += v0 * v0;
-    s += v1 * v1;
-    s += d_hi0 * d_hi0;
-    s += d_hi1 * d_hi1;
-    float l2c = __shfl(s, 0);
-    for (int j = 1; j < 32; j++) l2c = l2c + __shfl(s, 2 * j);
-    l2c = sqrtf(l2c);
-    const float norm = 512.0f / fmaxf(l2c, FLT_EPSILON);
-    const int32_t q0 = sat_i32(roundf(v0 * norm)), q1v = sat_i32(roundf(v1 * norm));
-    const uint32_t u0 = q0 > 255 ? 255u : (uint32_t)(uint8_t)q0;
-    const uint32_t u1 = q1v > 255 ? 255u : (uint32_t)(uint8_t)q1v;
-    reinterpret_cast<uint16_t*>(out)[lane] = (uint16_t)(u0 | (u1 << 8));
+    describe_normalize(acc0, acc1, out, lane);
 }
 
-template <int kAblate>
+// Fast path (the default): lane-private 4x4x8 histograms.
+//
+// Lanes walk contiguous chunks of the compacted samples and add each sample's
+// interior contributions (cells 1..4 x 1..4; the reference discards the
+// border ring, src/lib.rs:951) into a private 128-bin slice of LDS with plain
+// read-add-write (LDS float atomics cost ~3 cycles per lane on gfx950,
+// tools/ubench_lds.hip); the 64 slices are then summed per bin.  Per-sample
+// arithmetic is the reference's; only the order of the bin additions differs,
+// so bins agree to f32 rounding and the u8 components to +-1 (the tolerance
+// tests/test_gpu_parity.py states).  describe_wave_exact is the bit-exact
+// alternative (sift_mi_set_exact_descriptors).
+constexpr int PRIV_STRIDE = 132;  // 128 bins + 4 dummy slots (border-ring contributions)
+
+struct DescScratchFast {
+    float h[64 * PRIV_STRIDE];
+    int rowlo[ROWS_MAX];
+    int rowpre[ROWS_MAX + 1];
+};
+
+template <int kAblate = 0>
+__device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img, int pitch, int width, int height,
+                                                   float xf, float yf, float scale, float orientation,
+                                                   DescScratchFast& sc, uint8_t* __restrict__ out, int lane) {
+    const int32_t x = (int32_t)sat_u32(roundf(xf));
+    const int32_t y = (int32_t)sat_u32(roundf(yf));
+    const float BIN_ANGLE_STEP = (float)kDescBins / 360.0f;
+    const float hist_width = kLambdaDescr * scale;
+    int radius = sat_i32(roundf(kLambdaDescr * scale * 1.41421356237309504880f * (float)(kDescHist + 1) * 0.5f));
+    radius = radius < 0 ? 0 : (radius > (ROWS_MAX - 2) / 2 ? (ROWS_MAX - 2) / 2 : radius);
+    const float rad = orientation * (3.14159265358979323846f / 180.0f);  // f32::to_radians
+    const float sin_ori = (float)sin((double)rad), cos_ori = (float)cos((double)rad);
+    const float sin_s = sin_ori / hist_width, cos_s = cos_ori / hist_width;
+    const int n = 2 * radius + 1;
+    float* hp = sc.h + lane * PRIV_STRIDE;
+#pragma unroll
+    for (int i = 0; i < PRIV_STRIDE; i += 4) *reinterpret_cast<float4*>(hp + i) = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int row = lane; row < n; row += 64) {
+        const double yi = (double)(row - radius);
+        const double c = cos_s, s = sin_s;
+        double lo = -radius, hi = radius;
+        bool empty = false;
+        if (fabs(c) > 1e-30) {
+            const double a = (yi * s - 2.5) / c, b = (yi * s + 2.5) / c;
+            lo = fmax(lo, fmin(a, b) - 1.0);
+            hi = fmin(hi, fmax(a, b) + 1.0);
+        } else {
+            empty = !(fabs(yi * s) < 2.5 + 1e-3);
+        }
+        if (fabs(s) > 1e-30) {
+            const double a = (-yi * c - 2.5) / s, b = (-yi * c + 2.5) / s;
+            lo = fmax(lo, fmin(a, b) - 1.0);
+            hi = fmin(hi, fmax(a, b) + 1.0);
+        } else {
+            empty = empty || !(fabs(yi * c) < 2.5 + 1e-3);
+        }
+        const int ilo = (int)floor(lo), ihi = (int)ceil(hi);
+        sc.rowlo[row] = ilo;
+        sc.rowpre[row + 1] = (empty || ihi < ilo) ? 0 : ihi - ilo + 1;
+    }
+    wave_sync();
+    if (lane == 0) {
+        int acc = 0;
+        sc.rowpre[0] = 0;
+        for (int r = 1; r <= n; r++) {
+            acc += sc.rowpre[r];
+            sc.rowpre[r] = acc;
+        }
+    }
+    wave_sync();
+    const int total = sc.rowpre[n];
+    const int chunk = (total + 63) >> 6;
+    int k = lane * chunk;
+    const int kend = min(total, k + chunk);
+    int row = 0;
+    {
+        int lo = 0, hi = n;  // first row with rowpre[row + 1] > k
+        while (lo < hi) {
+            const int mid = (lo + hi) >> 1;
+            if (sc.rowpre[mid + 1] <= k)
+                lo = mid + 1;
+            else
+                hi = mid;
+        }
+        row = lo;
+    }
+    for (; k < kend; k++) {
+        while (sc.rowpre[row + 1] <= k) row++;
+        const int yi = row - radius;
+        const int xi = sc.rowlo[row] + (k - sc.rowpre[row]);
+        const float col_rot = (float)xi * cos_s - (float)yi * sin_s;
+        const float row_rot = (float)xi * sin_s + (float)yi * cos_s;
+        float row_bin = row_rot + (float)(kDescHist / 2);
+        float col_bin = col_rot + (float)(kDescHist / 2);
+        const int32_t ay = y + yi, ax = x + xi;
+        if (!(row_bin > -0.5f && row_bin < (float)kDescHist + 0.5f && col_bin > -0.5f &&
+              col_bin < (float)kDescHist + 0.5f && ay > 0 && ay < height - 1 && ax > 0 && ax < width - 1))
+            continue;
+        float dx, dy;
+        if (kAblate & 8) {
+            dx = (float)xi * 0.01f + 0.001f;
+            dy = (float)yi * 0.01f - 0.002f;
+        } else {
+            const float* rw = img + (size_t)ay * pitch;
+            dx = rw[ax + 1] - rw[ax - 1];
+            dy = rw[ax - pitch] - rw[ax + pitch];
+        }
+        const float wsq = col_rot * col_rot + row_rot * row_rot;
+        const float weight =
+            (kAblate & 4) ? 1.0f + wsq * (-0.125f) : exp_f32(wsq * (-2.f / (float)(kDescHist * kDescHist)));
+        double deg = ((kAblate & 2) ? (double)(dy * 50.0f + dx)
+                                    : atan2((double)dy, (double)dx) * (180.0 / 3.14159265358979323846)) +
+                     360.0;
+        deg = deg >= 360.0 ? deg - 360.0 : deg;  // f64 `% 360.0` of a value in [180, 540]
+        const float ori = (float)deg - orientation;
+        float mag = sqrtf(dx * dx + dy * dy);
+        row_bin = row_bin - 0.5f;
+        col_bin = col_bin - 0.5f;
+        mag = mag * weight;
+        const float obin = ori * BIN_ANGLE_STEP;
+        const float row_floor = floorf(row_bin), col_floor = floorf(col_bin), ori_floor = floorf(obin);
+        const float row_frac = row_bin - row_floor, col_frac = col_bin - col_floor, ori_frac = obin - ori_floor;
+        const float c1 = mag * row_frac, c0 = mag - c1;
+        const float c11 = c1 * col_frac, c10 = c1 - c11;
+        const float c01 = c0 * col_frac, c00 = c0 - c01;
+        const float c111 = c11 * ori_frac, c110 = c11 - c111;
+        const float c101 = c10 * ori_frac, c100 = c10 - c101;
+        const float c011 = c01 * ori_frac, c010 = c01 - c011;
+        const float c001 = c00 * ori_frac, c000 = c00 - c001;
+        const int r1 = (int)row_floor + 1, q1 = (int)col_floor + 1;  // 0..4
+        int o0 = (int)ori_floor;
+        o0 = o0 < 0 ? o0 + kDescBins : (o0 >= kDescBins ? o0 - kDescBins : o0);
+        o0 &= kDescBins - 1;
+        const int o1 = (o0 + 1) & (kDescBins - 1);
+        // interior slice offset of cell (r, q), or the dummy slots for the border ring
+        auto cell = [](int r, int q) { return (r >= 1 && r <= 4 && q >= 1 && q <= 4) ? ((r - 1) * 4 + (q - 1)) * 8 : 128; };
+        const int b11 = cell(r1, q1), b12 = cell(r1, q1 + 1), b21 = cell(r1 + 1, q1), b22 = cell(r1 + 1, q1 + 1);
+        const int d0 = o0 & (b11 == 128 ? 3 : 7), d1 = o1 & (b11 == 128 ? 3 : 7);
+        hp[b11 + d0] += c000;
+        hp[b11 + d1] += c001;
+        const int e0 = o0 & (b12 == 128 ? 3 : 7), e1 = o1 & (b12 == 128 ? 3 : 7);
+        hp[b12 + e0] += c010;
+        hp[b12 + e1] += c011;
+        const int f0 = o0 & (b21 == 128 ? 3 : 7), f1 = o1 & (b21 == 128 ? 3 : 7);
+        hp[b21 + f0] += c100;
+        hp[b21 + f1] += c101;
+        const int g0 = o0 & (b22 == 128 ? 3 : 7), g1 = o1 & (b22 == 128 ? 3 : 7);
+        hp[b22 + g0] += c110;
+        hp[b22 + g1] += c111;
+    }
+    wave_sync();
+    // per-bin sum of the 64 private slices: lane l owns flat bins 2l, 2l+1
+    float acc0 = 0.0f, acc1 = 0.0f;
+#pragma unroll 8
+    for (int j = 0; j < 64; j++) {
+        const float2 v = *reinterpret_cast<const float2*>(sc.h + j * PRIV_STRIDE + 2 * lane);
+        acc0 += v.x;
+        acc1 += v.y;
+    }
+    describe_normalize(acc0, acc1, out, lane);
+}
+
+template <bool kExact, int kAblate>
 __global__ __launch_bounds__(64) void k_describe(const DescLaunch L) {
-    __shared__ DescScratch scr[1];
-    const int wave = 0, lane = threadIdx.x;
+    using Scratch = typename std::conditional<kExact, DescScratch, DescScratchFast>::type;
+    __shared__ __attribute__((aligned(16))) Scratch scr;
+    const int lane = threadIdx.x;
     const uint32_t i = blockIdx.x;
-    if (i >= L.n) return;  // whole wave; no workgroup barrier below
     const KpRec kp = L.kp[L.idx ? L.idx[i] : i];
     const int o = kp.octave;
     const int W = L.ow[o], H = L.oh[o];
@@ -245,8 +445,11 @@ __global__ __launch_bounds__(64) void k_describe(const DescLaunch L) {
     const float angle = 360.0f - kp.angle;
     const float osf = 1.0f / (float)(1u << o);  // 2_f32.powi(-octave)
     const float kp_size = kp.size * osf;
-    describe_wave<kAblate>(img, pitch, W, H, kp.x * osf, kp.y * osf, kp_size, angle, scr[wave],
-                  L.out_desc + (size_t)i * kDescSize, lane);
+    uint8_t* out = L.out_desc + (size_t)i * kDescSize;
+    if constexpr (kExact)
+        describe_wave_exact<kAblate>(img, pitch, W, H, kp.x * osf, kp.y * osf, kp_size, angle, scr, out, lane);
+    else
+        describe_wave_fast<kAblate>(img, pitch, W, H, kp.x * osf, kp.y * osf, kp_size, angle, scr, out, lane);
     if (lane == 0) {
         if (L.out_kp) {
             OutKp k;
@@ -263,13 +466,16 @@ __global__ __launch_bounds__(64) void k_describe(const DescLaunch L) {
 
 void launch_describe(const DescLaunch& L, hipStream_t st) {
     if (L.n == 0) return;
-    hipLaunchKernelGGL(k_describe<0>, dim3(L.n), dim3(64), 0, st, L);
+    if (L.exact)
+        hipLaunchKernelGGL((k_describe<true, 0>), dim3(L.n), dim3(64), 0, st, L);
+    else
+        hipLaunchKernelGGL((k_describe<false, 0>), dim3(L.n), dim3(64), 0, st, L);
 }
 
 __global__ __launch_bounds__(64) void k_describe_one(const float* img, int w, int h, float x, float y, float scale,
                                                      float orientation, uint8_t* out) {
-    __shared__ DescScratch scr;
-    describe_wave(img, w, w, h, x, y, scale, orientation, scr, out, threadIdx.x);
+    __shared__ __attribute__((aligned(16))) DescScratch scr;
+    describe_wave_exact(img, w, w, h, x, y, scale, orientation, scr, out, threadIdx.x);
 }
 
 void launch_describe_one(const float* img, int w, int h, float x, float y, float scale, float orientation,

@@ -279,6 +279,7 @@ struct sift_mi_ctx {
     hipStream_t stream = nullptr;
     uint32_t chunk_override = 0;
     int keep_on_device = 0;
+    int exact_descriptors = 0;
     Plan plan;
     DevBuf<uint8_t> staging;  // host-sourced frames
     // detection / description buffers
@@ -654,6 +655,7 @@ int run_keypoints(sift_mi_ctx* c, uint32_t n, int64_t limit, uint32_t frame_base
     DL.out_kp = c->out_kp.p;
     DL.out_key = c->out_key.p;
     DL.out_desc = c->out_desc.p;
+    DL.exact = c->exact_descriptors;
     launch_describe(DL, st);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[5], st));
@@ -827,6 +829,12 @@ int sift_mi_set_stream(sift_mi_ctx* c, void* s) {
 int sift_mi_set_chunk(sift_mi_ctx* c, uint32_t k) {
     if (!c) return fail(SIFT_MI_EINVAL, "ctx is null");
     c->chunk_override = k;
+    return 0;
+}
+
+int sift_mi_set_exact_descriptors(sift_mi_ctx* c, int exact) {
+    if (!c) return fail(SIFT_MI_EINVAL, "ctx is null");
+    c->exact_descriptors = exact ? 1 : 0;
     return 0;
 }
 

@@ -126,6 +126,7 @@ struct DescLaunch {
     OutKp* out_kp;     // may be null
     uint64_t* out_key; // may be null
     uint8_t* out_desc;
+    int exact;         // 1: bit-exact bin-owner accumulation (describe_wave_exact)
 };
 void launch_describe(const DescLaunch& L, hipStream_t st);
 

@@ -122,6 +122,10 @@ class Context:
     def set_stream(self, hip_stream_handle):
         check(lib().sift_mi_set_stream(self._h, ctypes.c_void_p(hip_stream_handle or 0)))
 
+    def set_exact_descriptors(self, exact=True):
+        """Bit-exact descriptor accumulation order (slower); default off."""
+        check(lib().sift_mi_set_exact_descriptors(self._h, 1 if exact else 0))
+
     def set_chunk(self, images_per_chunk):
         check(lib().sift_mi_set_chunk(self._h, int(images_per_chunk)))
 

@@ -40,4 +40,4 @@ def test_compute_descriptor(ctx, oracle):
         d = np.abs(g.astype(int) - o.astype(int))
         assert d.max() <= 1, (x, y, s, a, d.max())
         same += (d == 0).sum()
-    assert same / (128 * len(cases)) >= 0.99
+    assert same == 128 * len(cases)  # sift_mi_compute_descriptor uses the exact accumulation order

@@ -116,3 +116,18 @@ def test_golden_snapshots_gpu(pkg, ctx, oracle):
         g = load_golden(name)
         res = ctx.sift(g["image"])
         assert abs(len(res) - count) <= max(3, 0.02 * count)
+
+
+@pytest.mark.parametrize("name", ["bird_small", "tree_small", "synth_640x480", "synth_97x61"])
+def test_exact_descriptors_bit_identical(pkg, oracle, name):
+    """sift_mi_set_exact_descriptors(1): bins accumulated in the reference's
+    sequential sample order -> descriptors byte-identical to the CPU path."""
+    img = INPUTS[name]
+    kp_o, desc_o, ext_o = oracle.sift(img, internal=True)
+    c = pkg.Context(0)
+    c.set_exact_descriptors(True)
+    res = c.sift(img)
+    c.close()
+    assert_parity(pkg, res, kp_o, desc_o, ext_o)
+    assert np.array_equal(res.descriptors, desc_o), (res.descriptors != desc_o).sum()
+    assert np.array_equal(res.keypoints_array, kp_o)

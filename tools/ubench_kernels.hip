@@ -19,15 +19,15 @@ using namespace siftmi;
         }                                                                        \
     } while (0)
 
-template <int A>
+template <bool E, int A>
 float time_describe(const DescLaunch& L, int reps) {
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
     dim3 grid(L.n);
-    hipLaunchKernelGGL(k_describe<A>, grid, dim3(64), 0, 0, L);
+    hipLaunchKernelGGL((k_describe<E, A>), grid, dim3(64), 0, 0, L);
     CK(hipEventRecord(a));
-    for (int i = 0; i < reps; i++) hipLaunchKernelGGL(k_describe<A>, grid, dim3(64), 0, 0, L);
+    for (int i = 0; i < reps; i++) hipLaunchKernelGGL((k_describe<E, A>), grid, dim3(64), 0, 0, L);
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
     float ms;
@@ -92,12 +92,12 @@ int main(int argc, char** argv) {
     L.out_desc = d_desc;
     const int reps = 5;
     std::printf("describe n=%d\n", NKP);
-    std::printf("  full            %8.3f ms\n", time_describe<0>(L, reps));
-    std::printf("  -phaseB         %8.3f ms\n", time_describe<1>(L, reps));
-    std::printf("  -atan2          %8.3f ms\n", time_describe<2>(L, reps));
-    std::printf("  -exp            %8.3f ms\n", time_describe<4>(L, reps));
-    std::printf("  -loads          %8.3f ms\n", time_describe<8>(L, reps));
-    std::printf("  -atan2-exp      %8.3f ms\n", time_describe<6>(L, reps));
-    std::printf("  -all            %8.3f ms\n", time_describe<15>(L, reps));
+    std::printf("  exact           %8.3f ms\n", time_describe<true, 0>(L, reps));
+    std::printf("  exact -phaseB   %8.3f ms\n", time_describe<true, 1>(L, reps));
+    std::printf("  fast            %8.3f ms\n", time_describe<false, 0>(L, reps));
+    std::printf("  fast -atan2     %8.3f ms\n", time_describe<false, 2>(L, reps));
+    std::printf("  fast -exp       %8.3f ms\n", time_describe<false, 4>(L, reps));
+    std::printf("  fast -loads     %8.3f ms\n", time_describe<false, 8>(L, reps));
+    std::printf("  fast -all       %8.3f ms\n", time_describe<false, 14>(L, reps));
     return 0;
 }
