@@ -162,6 +162,94 @@ __global__ __launch_bounds__(256) void k_blur(const float* __restrict__ src, siz
 }
 
 // ---------------------------------------------------------------------------
+// Persistent, software-pipelined variant: each workgroup walks tiles
+// (frame, ty, tx) with stride gridDim.x; the 16-B global loads of the next
+// interior tile are issued into registers before the current tile's row and
+// column passes, so HBM latency hides behind LDS/VALU work (border tiles use
+// the synchronous reflect-101 path).
+// ---------------------------------------------------------------------------
+template <int R, int TH>
+__global__ __launch_bounds__(256) void k_blur_pp(const float* __restrict__ src, size_t src_img_stride,
+                                                 float* __restrict__ dst, size_t dst_img_stride,
+                                                 float* __restrict__ dog, size_t dog_img_stride,
+                                                 float* __restrict__ nxt, size_t nxt_img_stride, int pitch_n, int wn,
+                                                 int hn, int W, int H, int pitch, int tiles_x, int tiles_y,
+                                                 int n_tiles, const BlurTaps taps) {
+    using G = BlurGeom<R, TH>;
+    __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
+    float* tin = lds;
+    float* th = lds + G::IH * G::IWP;
+    const int tid = threadIdx.x;
+    float4 tmp[G::LOADS_PER_THREAD];
+    auto tile_xy = [&](int t, int& b, int& x0, int& y0) {
+        const int per = tiles_x * tiles_y;
+        b = t / per;
+        const int r = t - b * per;
+        const int ty = r / tiles_x;
+        x0 = (r - ty * tiles_x) * G::TW;
+        y0 = ty * G::TH;
+    };
+    auto interior = [&](int x0, int y0) {
+        return x0 >= G::HWL && x0 + G::TW + G::HWL <= W && y0 >= R && y0 + G::TH + R <= H;
+    };
+    auto issue = [&](int b, int x0, int y0) {
+        const float* base = src + (size_t)b * src_img_stride + (size_t)(y0 - R) * pitch + (x0 - G::HWL);
+#pragma unroll
+        for (int j = 0; j < G::LOADS_PER_THREAD; j++) {
+            const int i = min(tid + 256 * j, G::NLOAD4 - 1);
+            const int ly = i / (G::IWV / 4), c4 = i - ly * (G::IWV / 4);
+            tmp[j] = *reinterpret_cast<const float4*>(base + (size_t)ly * pitch + 4 * c4);
+        }
+    };
+    int t = blockIdx.x;
+    if (t >= n_tiles) return;
+    int b, x0, y0;
+    tile_xy(t, b, x0, y0);
+    bool inner = interior(x0, y0);
+    if (inner) issue(b, x0, y0);
+    for (;;) {
+        // current tile -> LDS
+        if (inner) {
+#pragma unroll
+            for (int j = 0; j < G::LOADS_PER_THREAD; j++) {
+                const int i = tid + 256 * j;
+                if (i < G::NLOAD4) {
+                    const int ly = i / (G::IWV / 4), c4 = i - ly * (G::IWV / 4);
+                    *reinterpret_cast<float4*>(tin + ly * G::IWP + 4 * c4) = tmp[j];
+                }
+            }
+        } else {
+            const float* sb = src + (size_t)b * src_img_stride;
+            for (int i = tid; i < G::IH * G::IWV; i += 256) {
+                const int ly = i / G::IWV, lx = i - ly * G::IWV;
+                const int gy = reflect101(y0 - R + ly, H), gx = reflect101(x0 - G::HWL + lx, W);
+                tin[ly * G::IWP + lx] = sb[(size_t)gy * pitch + gx];
+            }
+        }
+        __syncthreads();
+        // prefetch the next interior tile while this one is filtered
+        const int tn = t + gridDim.x;
+        int bn = 0, xn = 0, yn = 0;
+        bool inner_n = false;
+        if (tn < n_tiles) {
+            tile_xy(tn, bn, xn, yn);
+            inner_n = interior(xn, yn);
+            if (inner_n) issue(bn, xn, yn);
+        }
+        blur_tile_compute<R, TH>(tin, th, taps, x0, y0, W, H, pitch, dst + (size_t)b * dst_img_stride,
+                                 dog ? dog + (size_t)b * dog_img_stride : nullptr,
+                                 nxt ? nxt + (size_t)b * nxt_img_stride : nullptr, pitch_n, wn, hn);
+        if (tn >= n_tiles) break;
+        __syncthreads();  // tin / th are rewritten by the next tile
+        t = tn;
+        b = bn;
+        x0 = xn;
+        y0 = yn;
+        inner = inner_n;
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Seed: u8 -> f32 (v / 255, image::ConvertBuffer, src/lib.rs:198) -> 2x
 // bilinear (cv::resize INTER_LINEAR, src/lib.rs:201-205) -> GaussianBlur
 // (src/lib.rs:207-209), fused.  Coefficient tables are built on the host

@@ -3,6 +3,7 @@
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -I sift-features_amd/csrc \
 //         tools/ubench_kernels.hip -o tools/ubench_kernels
 #include "../sift-features_amd/csrc/describe.hip"
+#include "../sift-features_amd/csrc/pyramid.hip"
 
 #include <cstdio>
 #include <cstdlib>
@@ -35,7 +36,61 @@ float time_describe(const DescLaunch& L, int reps) {
     return ms / reps;
 }
 
+// blur variants on an octave-0-sized batch (3840x2160, pitch 3840, 32 frames)
+template <int R, int TH, int PP>
+float time_blur(const float* src, float* dst, float* dog, int W, int H, int pitch, int nimg, int reps) {
+    using G = BlurGeom<R, TH>;
+    BlurTaps taps{};
+    for (int t = 0; t <= R; t++) taps.k[t] = 1.0f / (2 * R + 1);
+    const size_t img = (size_t)pitch * H;
+    const int tx = (W + G::TW - 1) / G::TW, ty = (H + G::TH - 1) / G::TH;
+    dim3 grid(tx, ty, nimg);
+    auto go = [&]() {
+        if (PP)
+            hipLaunchKernelGGL((k_blur_pp<R, TH>), dim3(256 * PP), dim3(256), 0, 0, src, img, dst, img, dog, img,
+                               (float*)nullptr, (size_t)0, 0, 0, 0, W, H, pitch, tx, ty, tx * ty * nimg, taps);
+        else
+            hipLaunchKernelGGL((k_blur<R, TH>), grid, dim3(256), 0, 0, src, img, dst, img, dog, img, (float*)nullptr,
+                               (size_t)0, 0, 0, 0, W, H, pitch, taps);
+    };
+    go();
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    CK(hipEventRecord(a));
+    for (int i = 0; i < reps; i++) go();
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    return ms / reps;
+}
+
+void bench_blur() {
+    const int W = 3840, H = 2160, pitch = 3840, N = 16;
+    const size_t n = (size_t)pitch * H * N;
+    float *s, *d, *g;
+    CK(hipMalloc(&s, n * 4));
+    CK(hipMalloc(&d, n * 4));
+    CK(hipMalloc(&g, n * 4));
+    CK(hipMemset(s, 0, n * 4));
+    const double bytes = 12.0 * W * H * N;  // read G_{s-1}, write G_s + D_{s-1}
+    std::printf("blur octave-0 batch (%d x %dx%d): ms, effective GB/s (12 B/px)\n", N, W, H);
+#define B(R, TH, PP)                                                                                      \
+    {                                                                                                     \
+        const float ms = time_blur<R, TH, PP>(s, d, g, W, H, pitch, N, 5);                                \
+        std::printf("  R=%2d TH=%2d pp=%d %8.3f ms %8.1f GB/s\n", R, TH, PP, ms, bytes / (ms * 1e-3) / 1e9); \
+    }
+    B(5, 32, 0) B(5, 64, 0) B(8, 32, 0) B(8, 64, 0) B(13, 32, 0) B(13, 64, 0)
+    B(5, 32, 4) B(5, 32, 6) B(8, 32, 4) B(13, 32, 3) B(13, 32, 4) B(13, 64, 2) B(13, 64, 3)
+#undef B
+    CK(hipFree(s));
+    CK(hipFree(d));
+    CK(hipFree(g));
+}
+
 int main(int argc, char** argv) {
+    bench_blur();
     const int W = 3840, H = 2160, pitch = 3840, NKP = argc > 1 ? atoi(argv[1]) : 200000;
     // one octave image stack (6 planes) with smooth synthetic content
     std::vector<float> img((size_t)6 * pitch * H);
