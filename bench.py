@@ -165,7 +165,7 @@ def main():
             "latency_1frame_ms": latency_ms,
             "roofline": {"bound": "hbm", "achieved": pyr_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": pyr_gbs / HBM_PEAK_GBS, "traffic": None,
-                         "kernel": "pyramid stage (k_upsample2x + k_blur_dog<R>), rank 0",
+                         "kernel": "pyramid stage (k_seed + k_blur<R>), rank 0",
                          "algorithmic_bytes_per_launch": per_launch_bytes,
                          "avg_launch_ms": per_launch_ms},
             "cpu_baseline": cpu,

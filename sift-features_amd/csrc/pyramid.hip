@@ -33,83 +33,141 @@ namespace siftmi {
 // Tile geometry.  Input window columns [x0 - HWL, x0 + TW + HWL) with
 // HWL = R rounded up to 4 so every row segment is float4-aligned.
 // ---------------------------------------------------------------------------
-template <int R, int TH_>
+template <int R, int TH_, int QW_ = 8>
 struct BlurGeom {
     static constexpr int TW = 64;
     static constexpr int TH = TH_;
-    static constexpr int VB = TH / 4;                    // column outputs per thread (256 threads, 64 columns)
+    static constexpr int QW = QW_;                       // row-pass outputs per item (4 or 8)
     static constexpr int HWL = (R + 3) & ~3;
     static constexpr int IH = TH + 2 * R;                // rows of the input window / row-pass output
     static constexpr int IWV = TW + 2 * HWL;             // loaded columns (multiple of 4)
     static constexpr int IWP = IWV + 4;                  // LDS pitch (breaks 2^k strides)
     static constexpr int OFF = HWL - R;                  // first used column inside a float4
-    static constexpr int NV = (HWL + R + 7) / 4;         // float4 reads per row-pass item
-    static constexpr int THP = TW + 4;                   // row-pass output pitch
-    static constexpr int LDS_FLOATS = IH * IWP + IH * THP;
+    static constexpr int NV = (HWL + R + QW + 3) / 4;    // float4 reads per row-pass item
+    static constexpr int THP = IWP;                      // row-pass output written in place (see below)
+    static constexpr int LDS_FLOATS = IH * IWP;
     static constexpr int NLOAD4 = IH * (IWV / 4);        // float4 per interior tile
     static constexpr int LOADS_PER_THREAD = (NLOAD4 + 255) / 256;
-    static_assert(4 * NV <= IWV - TW + 4, "row-pass reads stay inside the loaded window");
-    static_assert(TH % 4 == 0, "TH");
+    static_assert(4 * NV <= IWV - TW + QW, "row-pass reads stay inside the loaded window");
+    static_assert(TH % 8 == 0, "TH: the column pass gives each thread TH/8 rows");
 };
 
 // Row pass + column pass + epilogue, shared by the seed and octave kernels.
+// The row pass writes its output in place over the input window (`th` ==
+// `tin`): every row is filtered by 8 lanes of one wave, which read the whole
+// row window into registers before any of them stores (LDS executes a wave's
+// instructions in order), so no lane overwrites a value another still needs.
+// The DoG needs G_{s-1} at the tile centre: each thread copies its centre
+// values to registers before the row pass.
+// Both passes use packed f32 arithmetic (v_pk_fma_f32 / v_pk_add_f32: two
+// independent, individually rounded lanes -- the same results as scalar fma /
+// add): the row pass pairs adjacent outputs of a row, the column pass
+// adjacent columns.
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+// volatile LDS view: keeps each row-window read one ds_read_b128 (the compiler
+// otherwise narrows the unused edge lanes into ds_read2_b32 pairs)
+typedef __attribute__((address_space(3))) volatile f4v lds_f4v;
+// and each column-pass read one ds_read_b64 (256 B/clk; the compiler would
+// pair them into ds_read2_b64, which runs at half that rate)
+typedef __attribute__((address_space(3))) volatile f2v lds_f2v;
+
 template <int R, int TH>
 __device__ __forceinline__ void blur_tile_compute(const float* __restrict__ tin, float* __restrict__ th,
                                                   const BlurTaps& taps, int x0, int y0, int W, int H, int pitch,
                                                   float* __restrict__ dst, float* __restrict__ dog,
                                                   float* __restrict__ nxt, int pitch_n, int wn, int hn) {
     using G = BlurGeom<R, TH>;
+    constexpr int VB2 = TH / 8;  // column pass: thread = (column pair, VB2 consecutive rows)
     const int tid = threadIdx.x;
-    // row pass: item = (row, quad of 4 outputs); fma chain from the leftmost tap
-    for (int i = tid; i < G::IH * (G::TW / 4); i += 256) {
-        const int ly = i / (G::TW / 4), q = i - ly * (G::TW / 4);
-        const float4* rp = reinterpret_cast<const float4*>(tin + ly * G::IWP + 4 * q);
+    const int cp = tid & 31, band = tid >> 5;
+    f2v centre[VB2];
+    if (dog) {
+#pragma unroll
+        for (int o = 0; o < VB2; o++)
+            centre[o] = *reinterpret_cast<const f2v*>(tin + (band * VB2 + o + R) * G::IWP + G::HWL + 2 * cp);
+        __syncthreads();  // other waves overwrite these rows in place below
+    }
+    // row pass: item = (row, QW consecutive outputs); fma chain from the leftmost tap.
+    // A wave filters 8 whole rows per iteration.  Lane -> (row, item) follows
+    // the ds_read_b128 lane groups ({0-3,12-15,20-27}, {4-11,16-19,28-31} per
+    // 32-lane half): each group reads two adjacent rows, whose float4 slots are
+    // the even / odd slots of a bank row (IWP/4 is odd) -> conflict-free.
+    static_assert(G::QW == 8 && (G::IWP / 4) % 2 == 1, "row-pass lane map assumes 8 items per row, odd pitch");
+    const int lane = tid & 63, wv = tid >> 6;
+    int rq;  // (row in wave) * 8 + item
+    {
+        const int l = lane & 31;
+        int g, k;
+        if (l < 4) { g = 0; k = l; }
+        else if (l < 12) { g = 1; k = l - 4; }
+        else if (l < 16) { g = 0; k = l - 8; }
+        else if (l < 20) { g = 1; k = l - 8; }
+        else if (l < 28) { g = 0; k = l - 12; }
+        else { g = 1; k = l - 16; }
+        rq = ((lane >> 5) * 4 + g * 2) * 8 + k;
+    }
+    for (int i = wv * 64 + rq; i < G::IH * 8; i += 256) {
+        const int ly = i >> 3, q = i & 7;
+        const lds_f4v* rp = (const lds_f4v*)(tin + ly * G::IWP + G::QW * q);
         float v[4 * G::NV];
 #pragma unroll
         for (int j = 0; j < G::NV; j++) {
-            const float4 f = rp[j];
+            const f4v f = rp[j];
             v[4 * j + 0] = f.x;
             v[4 * j + 1] = f.y;
             v[4 * j + 2] = f.z;
             v[4 * j + 3] = f.w;
         }
-        float acc[4];
+        float acc[G::QW];
 #pragma unroll
-        for (int o = 0; o < 4; o++) acc[o] = v[G::OFF + o] * taps.k[R];
+        for (int o = 0; o < G::QW; o++) acc[o] = v[G::OFF + o] * taps.k[R];
 #pragma unroll
         for (int t = 1; t <= 2 * R; t++) {
             const float kt = taps.k[t > R ? t - R : R - t];
 #pragma unroll
-            for (int o = 0; o < 4; o++) acc[o] = __builtin_fmaf(v[G::OFF + o + t], kt, acc[o]);
+            for (int o = 0; o < G::QW; o++) acc[o] = __builtin_fmaf(v[G::OFF + o + t], kt, acc[o]);
         }
-        *reinterpret_cast<float4*>(th + ly * G::THP + 4 * q) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+        // all lanes of this row have their window in registers (in-order LDS)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+#pragma unroll
+        for (int o = 0; o < G::QW; o += 4)
+            *reinterpret_cast<float4*>(th + ly * G::THP + G::QW * q + o) =
+                make_float4(acc[o], acc[o + 1], acc[o + 2], acc[o + 3]);
     }
     __syncthreads();
-    // column pass: thread = (column, VB consecutive rows); centre product then
-    // fma of the (below + above) pair sums outwards
-    {
-        const int lx = tid & (G::TW - 1), p = tid / G::TW;
-        const int gx = x0 + lx;
-        float v[G::VB + 2 * R];
+    // column pass: centre product then fma of the (below + above) pair sums outwards
+    f2v v[VB2 + 2 * R];
 #pragma unroll
-        for (int j = 0; j < G::VB + 2 * R; j++) v[j] = th[(p * G::VB + j) * G::THP + lx];
-        if (gx < W) {
+    for (int j = 0; j < VB2 + 2 * R; j++)
+        v[j] = *(const lds_f2v*)(th + (band * VB2 + j) * G::THP + 2 * cp);
+    const int gx = x0 + 2 * cp;  // even
+    if (gx >= W) return;
+    const bool pair = gx + 1 < W;
+    const bool full = y0 + TH <= H;
+    const f2v k0 = {taps.k[0], taps.k[0]};
 #pragma unroll
-            for (int o = 0; o < G::VB; o++) {
-                const int ly = p * G::VB + o;
-                const int gy = y0 + ly;
-                if (gy < H) {
-                    float acc = v[o + R] * taps.k[0];
+    for (int o = 0; o < VB2; o++) {
+        const int gy = y0 + band * VB2 + o;
+        if (!full && gy >= H) break;
+        f2v acc = v[o + R] * k0;
 #pragma unroll
-                    for (int t = 1; t <= R; t++) acc = __builtin_fmaf(v[o + R + t] + v[o + R - t], taps.k[t], acc);
-                    const size_t off = (size_t)gy * pitch + gx;
-                    dst[off] = acc;
-                    if (dog) dog[off] = acc - tin[(ly + R) * G::IWP + lx + G::HWL];
-                    if (nxt && !(gx & 1) && !(gy & 1) && (gx >> 1) < wn && (gy >> 1) < hn)
-                        nxt[(size_t)(gy >> 1) * pitch_n + (gx >> 1)] = acc;
-                }
-            }
+        for (int t = 1; t <= R; t++) {
+            const f2v kt = {taps.k[t], taps.k[t]};
+            acc = __builtin_elementwise_fma(v[o + R + t] + v[o + R - t], kt, acc);
         }
+        const size_t off = (size_t)gy * pitch + gx;
+        if (pair) {
+            *reinterpret_cast<f2v*>(dst + off) = acc;
+            if (dog) *reinterpret_cast<f2v*>(dog + off) = acc - centre[o];
+        } else {
+            dst[off] = acc.x;
+            if (dog) dog[off] = acc.x - centre[o].x;
+        }
+        // nearest 1/2 (cv::resize INTER_NEAREST): pixel (2x, 2y); gy parity == o parity
+        if ((o & 1) == 0 && nxt && (gx >> 1) < wn && (gy >> 1) < hn)
+            nxt[(size_t)(gy >> 1) * pitch_n + (gx >> 1)] = acc.x;
     }
 }
 
@@ -121,8 +179,8 @@ __global__ __launch_bounds__(256) void k_blur(const float* __restrict__ src, siz
                                               int hn, int W, int H, int pitch, const BlurTaps taps) {
     using G = BlurGeom<R, TH>;
     __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
-    float* tin = lds;                  // [IH][IWP]  G_{s-1} window
-    float* th = lds + G::IH * G::IWP;  // [IH][THP]  row-pass output
+    float* tin = lds;  // [IH][IWP]  G_{s-1} window, then (in place) the row-pass output
+    float* th = lds;
     const int tid = threadIdx.x;
     const int x0 = blockIdx.x * G::TW, y0 = blockIdx.y * G::TH;
     const size_t b = blockIdx.z;
@@ -162,94 +220,6 @@ __global__ __launch_bounds__(256) void k_blur(const float* __restrict__ src, siz
 }
 
 // ---------------------------------------------------------------------------
-// Persistent, software-pipelined variant: each workgroup walks tiles
-// (frame, ty, tx) with stride gridDim.x; the 16-B global loads of the next
-// interior tile are issued into registers before the current tile's row and
-// column passes, so HBM latency hides behind LDS/VALU work (border tiles use
-// the synchronous reflect-101 path).
-// ---------------------------------------------------------------------------
-template <int R, int TH>
-__global__ __launch_bounds__(256) void k_blur_pp(const float* __restrict__ src, size_t src_img_stride,
-                                                 float* __restrict__ dst, size_t dst_img_stride,
-                                                 float* __restrict__ dog, size_t dog_img_stride,
-                                                 float* __restrict__ nxt, size_t nxt_img_stride, int pitch_n, int wn,
-                                                 int hn, int W, int H, int pitch, int tiles_x, int tiles_y,
-                                                 int n_tiles, const BlurTaps taps) {
-    using G = BlurGeom<R, TH>;
-    __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
-    float* tin = lds;
-    float* th = lds + G::IH * G::IWP;
-    const int tid = threadIdx.x;
-    float4 tmp[G::LOADS_PER_THREAD];
-    auto tile_xy = [&](int t, int& b, int& x0, int& y0) {
-        const int per = tiles_x * tiles_y;
-        b = t / per;
-        const int r = t - b * per;
-        const int ty = r / tiles_x;
-        x0 = (r - ty * tiles_x) * G::TW;
-        y0 = ty * G::TH;
-    };
-    auto interior = [&](int x0, int y0) {
-        return x0 >= G::HWL && x0 + G::TW + G::HWL <= W && y0 >= R && y0 + G::TH + R <= H;
-    };
-    auto issue = [&](int b, int x0, int y0) {
-        const float* base = src + (size_t)b * src_img_stride + (size_t)(y0 - R) * pitch + (x0 - G::HWL);
-#pragma unroll
-        for (int j = 0; j < G::LOADS_PER_THREAD; j++) {
-            const int i = min(tid + 256 * j, G::NLOAD4 - 1);
-            const int ly = i / (G::IWV / 4), c4 = i - ly * (G::IWV / 4);
-            tmp[j] = *reinterpret_cast<const float4*>(base + (size_t)ly * pitch + 4 * c4);
-        }
-    };
-    int t = blockIdx.x;
-    if (t >= n_tiles) return;
-    int b, x0, y0;
-    tile_xy(t, b, x0, y0);
-    bool inner = interior(x0, y0);
-    if (inner) issue(b, x0, y0);
-    for (;;) {
-        // current tile -> LDS
-        if (inner) {
-#pragma unroll
-            for (int j = 0; j < G::LOADS_PER_THREAD; j++) {
-                const int i = tid + 256 * j;
-                if (i < G::NLOAD4) {
-                    const int ly = i / (G::IWV / 4), c4 = i - ly * (G::IWV / 4);
-                    *reinterpret_cast<float4*>(tin + ly * G::IWP + 4 * c4) = tmp[j];
-                }
-            }
-        } else {
-            const float* sb = src + (size_t)b * src_img_stride;
-            for (int i = tid; i < G::IH * G::IWV; i += 256) {
-                const int ly = i / G::IWV, lx = i - ly * G::IWV;
-                const int gy = reflect101(y0 - R + ly, H), gx = reflect101(x0 - G::HWL + lx, W);
-                tin[ly * G::IWP + lx] = sb[(size_t)gy * pitch + gx];
-            }
-        }
-        __syncthreads();
-        // prefetch the next interior tile while this one is filtered
-        const int tn = t + gridDim.x;
-        int bn = 0, xn = 0, yn = 0;
-        bool inner_n = false;
-        if (tn < n_tiles) {
-            tile_xy(tn, bn, xn, yn);
-            inner_n = interior(xn, yn);
-            if (inner_n) issue(bn, xn, yn);
-        }
-        blur_tile_compute<R, TH>(tin, th, taps, x0, y0, W, H, pitch, dst + (size_t)b * dst_img_stride,
-                                 dog ? dog + (size_t)b * dog_img_stride : nullptr,
-                                 nxt ? nxt + (size_t)b * nxt_img_stride : nullptr, pitch_n, wn, hn);
-        if (tn >= n_tiles) break;
-        __syncthreads();  // tin / th are rewritten by the next tile
-        t = tn;
-        b = bn;
-        x0 = xn;
-        y0 = yn;
-        inner = inner_n;
-    }
-}
-
-// ---------------------------------------------------------------------------
 // Seed: u8 -> f32 (v / 255, image::ConvertBuffer, src/lib.rs:198) -> 2x
 // bilinear (cv::resize INTER_LINEAR, src/lib.rs:201-205) -> GaussianBlur
 // (src/lib.rs:207-209), fused.  Coefficient tables are built on the host
@@ -283,7 +253,7 @@ __global__ __launch_bounds__(256) void k_seed(const uint8_t* __restrict__ frames
     __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
     __shared__ float lut[256];
     float* tin = lds;
-    float* th = lds + G::IH * G::IWP;
+    float* th = lds;
     const int tid = threadIdx.x;
     lut[tid] = (float)tid / 255.0f;
     __syncthreads();
@@ -305,7 +275,7 @@ __global__ __launch_bounds__(256) void k_seed(const uint8_t* __restrict__ frames
 // ---------------------------------------------------------------------------
 template <int R>
 static void launch_blur_r(const BlurLaunch& L, hipStream_t st) {
-    constexpr int TH = R > 8 ? 64 : 32;
+    constexpr int TH = R >= 10 ? 64 : 32;  // measured: tools/ubench_kernels.hip blur
     using G = BlurGeom<R, TH>;
     dim3 grid((L.W + G::TW - 1) / G::TW, (L.H + G::TH - 1) / G::TH, L.n_img);
     hipLaunchKernelGGL((k_blur<R, TH>), grid, dim3(256), 0, st, L.src, L.src_img_stride, L.dst, L.dst_img_stride,

@@ -18,6 +18,11 @@ if [[ ,$STEPS, == *,ubench,* ]]; then
   rc=$?; echo "ubench rc=$rc"; cat gpurun_out/ubench.log
   [ $rc -eq 0 ] || exit $rc
 fi
+if [[ ,$STEPS, == *,blur,* ]]; then
+  timeout -k 10 120 ./tools/ubench_kernels blur > gpurun_out/ubench_blur.log 2>&1
+  rc=$?; echo "ubench blur rc=$rc"; cat gpurun_out/ubench_blur.log
+  [ $rc -eq 0 ] || exit $rc
+fi
 if [[ ,$STEPS, == *,bench,* ]]; then
   timeout -k 10 600 python bench.py --steps 3 --warmup 1 --frames $FRAMES --cpu-seconds 6 > gpurun_out/bench.log 2>&1
   rc=$?; echo "bench rc=$rc"; tail -3 gpurun_out/bench.log

@@ -6,6 +6,7 @@
 #include "../sift-features_amd/csrc/pyramid.hip"
 
 #include <cstdio>
+#include <cstring>
 #include <cstdlib>
 #include <vector>
 
@@ -46,12 +47,8 @@ float time_blur(const float* src, float* dst, float* dog, int W, int H, int pitc
     const int tx = (W + G::TW - 1) / G::TW, ty = (H + G::TH - 1) / G::TH;
     dim3 grid(tx, ty, nimg);
     auto go = [&]() {
-        if (PP)
-            hipLaunchKernelGGL((k_blur_pp<R, TH>), dim3(256 * PP), dim3(256), 0, 0, src, img, dst, img, dog, img,
-                               (float*)nullptr, (size_t)0, 0, 0, 0, W, H, pitch, tx, ty, tx * ty * nimg, taps);
-        else
-            hipLaunchKernelGGL((k_blur<R, TH>), grid, dim3(256), 0, 0, src, img, dst, img, dog, img, (float*)nullptr,
-                               (size_t)0, 0, 0, 0, W, H, pitch, taps);
+        hipLaunchKernelGGL((k_blur<R, TH>), grid, dim3(256), 0, 0, src, img, dst, img, dog, img, (float*)nullptr,
+                           (size_t)0, 0, 0, 0, W, H, pitch, taps);
     };
     go();
     hipEvent_t a, b;
@@ -66,8 +63,8 @@ float time_blur(const float* src, float* dst, float* dog, int W, int H, int pitc
     return ms / reps;
 }
 
-void bench_blur() {
-    const int W = 3840, H = 2160, pitch = 3840, N = 16;
+void bench_blur(int N) {
+    const int W = 3840, H = 2160, pitch = 3840;
     const size_t n = (size_t)pitch * H * N;
     float *s, *d, *g;
     CK(hipMalloc(&s, n * 4));
@@ -81,8 +78,7 @@ void bench_blur() {
         const float ms = time_blur<R, TH, PP>(s, d, g, W, H, pitch, N, 5);                                \
         std::printf("  R=%2d TH=%2d pp=%d %8.3f ms %8.1f GB/s\n", R, TH, PP, ms, bytes / (ms * 1e-3) / 1e9); \
     }
-    B(5, 32, 0) B(5, 64, 0) B(8, 32, 0) B(8, 64, 0) B(13, 32, 0) B(13, 64, 0)
-    B(5, 32, 4) B(5, 32, 6) B(8, 32, 4) B(13, 32, 3) B(13, 32, 4) B(13, 64, 2) B(13, 64, 3)
+    B(5, 32, 0) B(6, 32, 0) B(8, 32, 0) B(10, 32, 0) B(10, 64, 0) B(13, 32, 0) B(13, 64, 0)
 #undef B
     CK(hipFree(s));
     CK(hipFree(d));
@@ -90,8 +86,13 @@ void bench_blur() {
 }
 
 int main(int argc, char** argv) {
-    bench_blur();
-    const int W = 3840, H = 2160, pitch = 3840, NKP = argc > 1 ? atoi(argv[1]) : 200000;
+    const char* mode = argc > 1 ? argv[1] : "all";
+    if (!strcmp(mode, "all") || !strcmp(mode, "blur")) {
+        bench_blur(16);
+        bench_blur(2);
+    }
+    if (strcmp(mode, "all") && strcmp(mode, "desc")) return 0;
+    const int W = 3840, H = 2160, pitch = 3840, NKP = 200000;
     // one octave image stack (6 planes) with smooth synthetic content
     std::vector<float> img((size_t)6 * pitch * H);
     for (int y = 0; y < H; y++)
