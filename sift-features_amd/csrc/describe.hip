@@ -272,8 +272,8 @@ __device__ __forceinline__ void describe_wave_exact(const float* __restrict__ im
 //
 // Lanes walk contiguous chunks of the compacted samples and add each sample's
 // interior contributions (cells 1..4 x 1..4; the reference discards the
-// border ring, src/lib.rs:951) into a private 128-bin slice of LDS with plain
-// read-add-write (LDS float atomics cost ~3 cycles per lane on gfx950,
+// border ring, src/lib.rs:951) into a private 128-bin slice of LDS (bin-major,
+// lane-minor layout: conflict-free) with plain read-add-write (LDS float atomics cost ~3 cycles per lane on gfx950,
 // tools/ubench_lds.hip); the 64 slices are then summed per bin.  Per-sample
 // arithmetic is the reference's; only the order of the bin additions differs,
 // so bins agree to f32 rounding and the u8 components to +-1 (the tolerance
@@ -301,9 +301,12 @@ __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img
     const float sin_ori = (float)sin((double)rad), cos_ori = (float)cos((double)rad);
     const float sin_s = sin_ori / hist_width, cos_s = cos_ori / hist_width;
     const int n = 2 * radius + 1;
-    float* hp = sc.h + lane * PRIV_STRIDE;
+    // bin b of lane l's slice lives at h[b * 64 + l]: every lane's read-add-write
+    // of any bin hits its own bank (l mod 32) -> conflict-free scatter
+    float* hp = sc.h + lane;
 #pragma unroll
-    for (int i = 0; i < PRIV_STRIDE; i += 4) *reinterpret_cast<float4*>(hp + i) = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = 0; i < PRIV_STRIDE * 64 / 4; i += 64)
+        reinterpret_cast<float4*>(sc.h)[i + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int row = lane; row < n; row += 64) {
         const double yi = (double)(row - radius);
         const double c = cos_s, s = sin_s;
@@ -405,26 +408,29 @@ __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img
         auto cell = [](int r, int q) { return (r >= 1 && r <= 4 && q >= 1 && q <= 4) ? ((r - 1) * 4 + (q - 1)) * 8 : 128; };
         const int b11 = cell(r1, q1), b12 = cell(r1, q1 + 1), b21 = cell(r1 + 1, q1), b22 = cell(r1 + 1, q1 + 1);
         const int d0 = o0 & (b11 == 128 ? 3 : 7), d1 = o1 & (b11 == 128 ? 3 : 7);
-        hp[b11 + d0] += c000;
-        hp[b11 + d1] += c001;
+        hp[(b11 + d0) * 64] += c000;
+        hp[(b11 + d1) * 64] += c001;
         const int e0 = o0 & (b12 == 128 ? 3 : 7), e1 = o1 & (b12 == 128 ? 3 : 7);
-        hp[b12 + e0] += c010;
-        hp[b12 + e1] += c011;
+        hp[(b12 + e0) * 64] += c010;
+        hp[(b12 + e1) * 64] += c011;
         const int f0 = o0 & (b21 == 128 ? 3 : 7), f1 = o1 & (b21 == 128 ? 3 : 7);
-        hp[b21 + f0] += c100;
-        hp[b21 + f1] += c101;
+        hp[(b21 + f0) * 64] += c100;
+        hp[(b21 + f1) * 64] += c101;
         const int g0 = o0 & (b22 == 128 ? 3 : 7), g1 = o1 & (b22 == 128 ? 3 : 7);
-        hp[b22 + g0] += c110;
-        hp[b22 + g1] += c111;
+        hp[(b22 + g0) * 64] += c110;
+        hp[(b22 + g1) * 64] += c111;
     }
     wave_sync();
-    // per-bin sum of the 64 private slices: lane l owns flat bins 2l, 2l+1
+    // per-bin sum of the 64 private slices: lane l owns flat bins 2l, 2l+1 and
+    // starts at slice l (rotated start: the 32 lanes of a half hit 32 banks)
     float acc0 = 0.0f, acc1 = 0.0f;
+    const float* r0 = sc.h + (2 * lane) * 64;
+    const float* r1 = r0 + 64;
 #pragma unroll 8
     for (int j = 0; j < 64; j++) {
-        const float2 v = *reinterpret_cast<const float2*>(sc.h + j * PRIV_STRIDE + 2 * lane);
-        acc0 += v.x;
-        acc1 += v.y;
+        const int jj = (j + lane) & 63;
+        acc0 += r0[jj];
+        acc1 += r1[jj];
     }
     describe_normalize(acc0, acc1, out, lane);
 }

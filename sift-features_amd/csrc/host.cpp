@@ -423,6 +423,7 @@ int run_pyramid(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, siz
     S.frame_pitch = frame_pitch;
     S.row_stride = row_stride;
     S.sh = (int)p.h;
+    S.sw = (int)p.w;
     S.tab = p.seed_tab.tab;
     S.dst = p.gauss(0);
     S.dst_img_stride = p.gstride(0);

@@ -246,24 +246,89 @@ __device__ __forceinline__ float upsample_at(const uint8_t* __restrict__ src, si
 
 template <int R, int TH>
 __global__ __launch_bounds__(256) void k_seed(const uint8_t* __restrict__ frames, size_t frame_pitch,
-                                              size_t row_stride, int sh, const ResizeTab tab,
+                                              size_t row_stride, int sh, int sw, const ResizeTab tab,
                                               float* __restrict__ dst, size_t dst_img_stride, int W, int H,
                                               int pitch, const BlurTaps taps) {
     using G = BlurGeom<R, TH>;
+    // source window: a span of D upsampled pixels needs <= D/2 + 2 source pixels
+    constexpr int SR = G::IH / 2 + 3, SC = G::IWV / 2 + 3;
+    static_assert(G::IH <= 128 && G::IWV <= 128, "span reduction covers 128 positions per axis");
     __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
+    __shared__ float srcf[SR * SC];         // u8 -> f32 source window
+    __shared__ float hbuf[SR * G::IWV];     // horizontal pass (HResizeLinear) per source row
     __shared__ float lut[256];
+    __shared__ int span[4][4];              // per wave: min/max upsampled x (waves 0,1) / y (waves 2,3)
+    __shared__ int txo[G::IWV], tyo[G::IH];  // per window column / row: source index (resize tables)
+    __shared__ float txa0[G::IWV], txa1[G::IWV], tya0[G::IH], tya1[G::IH];
     float* tin = lds;
     float* th = lds;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     lut[tid] = (float)tid / 255.0f;
-    __syncthreads();
     const int x0 = blockIdx.x * G::TW, y0 = blockIdx.y * G::TH;
     const size_t b = blockIdx.z;
     const uint8_t* src = frames + b * frame_pitch;
-    for (int i = tid; i < G::IH * G::IWV; i += 256) {
-        const int ly = i / G::IWV, lx = i - ly * G::IWV;
-        const int gy = reflect101(y0 - R + ly, H), gx = reflect101(x0 - G::HWL + lx, W);
-        tin[ly * G::IWP + lx] = upsample_at(src, row_stride, sh, tab, lut, gx, gy);
+    // upsampled-coordinate spans of the tile window after reflect-101
+    {
+        const int t = tid & 127;
+        const bool isx = tid < 128;
+        const bool act = isx ? t < G::IWV : t < G::IH;
+        const int g = act ? (isx ? reflect101(x0 - G::HWL + t, W) : reflect101(y0 - R + t, H)) : 0;
+        // this window position's table entries, fetched once (all in flight together)
+        if (act && isx) {
+            txo[t] = g < tab.xmax ? tab.xofs[g] : -1 - tab.xofs[g];  // < 0: single-tap right border
+            txa0[t] = tab.xa0[g];
+            txa1[t] = tab.xa1[g];
+        } else if (act) {
+            tyo[t] = tab.yofs[g];
+            tya0[t] = tab.ya0[g];
+            tya1[t] = tab.ya1[g];
+        }
+        int mn = act ? g : INT_MAX, mx = act ? g : INT_MIN;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            mn = min(mn, __shfl_xor(mn, o));
+            mx = max(mx, __shfl_xor(mx, o));
+        }
+        if (lane == 0) {
+            span[wv][0] = mn;
+            span[wv][1] = mx;
+        }
+    }
+    __syncthreads();
+    const int gxa = min(span[0][0], span[1][0]), gxb = max(span[0][1], span[1][1]);
+    const int gya = min(span[2][0], span[3][0]), gyb = max(span[2][1], span[3][1]);
+    const int sxa = tab.xofs[gxa], sxb = min(tab.xofs[gxb] + 1, sw - 1);
+    const int sya = tab.yofs[gya], syb = min(tab.yofs[gyb] + 1, sh - 1);
+    const int nc = sxb - sxa + 1, nr = syb - sya + 1;
+    if (nc <= SC && nr <= SR) {
+        for (int i = tid; i < nr * nc; i += 256) {
+            const int r = i / nc, c = i - r * nc;
+            srcf[r * SC + c] = lut[src[(size_t)(sya + r) * row_stride + sxa + c]];
+        }
+        __syncthreads();
+        // HResizeLinear: t = S[sx]*a0 + S[sx+1]*a1 (two roundings + add)
+        for (int i = tid; i < nr * G::IWV; i += 256) {
+            const int r = i / G::IWV, lx = i - r * G::IWV;
+            const int xo = txo[lx];
+            const bool two = xo >= 0;
+            const int sx = (two ? xo : -1 - xo) - sxa;
+            const float p0 = srcf[r * SC + sx];
+            hbuf[i] = two ? p0 * txa0[lx] + srcf[r * SC + sx + 1] * txa1[lx] : p0;
+        }
+        __syncthreads();
+        // VResizeLinear: S0*b0 + S1*b1
+        for (int i = tid; i < G::IH * G::IWV; i += 256) {
+            const int ly = i / G::IWV, lx = i - ly * G::IWV;
+            const int s0 = tyo[ly];
+            const int r0 = s0 - sya, r1 = min(s0 + 1, sh - 1) - sya;
+            tin[ly * G::IWP + lx] = hbuf[r0 * G::IWV + lx] * tya0[ly] + hbuf[r1 * G::IWV + lx] * tya1[ly];
+        }
+    } else {  // not reached for a 2x seed; kept for safety on degenerate shapes
+        for (int i = tid; i < G::IH * G::IWV; i += 256) {
+            const int ly = i / G::IWV, lx = i - ly * G::IWV;
+            const int gy = reflect101(y0 - R + ly, H), gx = reflect101(x0 - G::HWL + lx, W);
+            tin[ly * G::IWP + lx] = upsample_at(src, row_stride, sh, tab, lut, gx, gy);
+        }
     }
     __syncthreads();
     blur_tile_compute<R, TH>(tin, th, taps, x0, y0, W, H, pitch, dst + b * dst_img_stride, nullptr, nullptr, 0, 0,
@@ -301,7 +366,7 @@ static void launch_seed_r(const SeedLaunch& L, hipStream_t st) {
     constexpr int TH = 32;
     using G = BlurGeom<R, TH>;
     dim3 grid((L.W + G::TW - 1) / G::TW, (L.H + G::TH - 1) / G::TH, L.n_img);
-    hipLaunchKernelGGL((k_seed<R, TH>), grid, dim3(256), 0, st, L.frames, L.frame_pitch, L.row_stride, L.sh, L.tab,
+    hipLaunchKernelGGL((k_seed<R, TH>), grid, dim3(256), 0, st, L.frames, L.frame_pitch, L.row_stride, L.sh, L.sw, L.tab,
                        L.dst, L.dst_img_stride, L.W, L.H, L.pitch, L.taps);
 }
 

@@ -39,7 +39,7 @@ struct BlurLaunch {
 struct SeedLaunch {
     const uint8_t* frames;
     size_t frame_pitch, row_stride;
-    int sh;          // source height
+    int sh, sw;      // source height, width
     ResizeTab tab;   // 2x bilinear tables
     float* dst;      // octave 0, plane 0
     size_t dst_img_stride;

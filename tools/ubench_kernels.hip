@@ -38,17 +38,29 @@ float time_describe(const DescLaunch& L, int reps) {
 }
 
 // blur variants on an octave-0-sized batch (3840x2160, pitch 3840, 32 frames)
-template <int R, int TH, int PP>
-float time_blur(const float* src, float* dst, float* dog, int W, int H, int pitch, int nimg, int reps) {
+__global__ void k_fill(float* p, size_t n) {
+    for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        uint32_t h = (uint32_t)i * 2654435761u;
+        h ^= h >> 15;
+        h *= 2246822519u;
+        h ^= h >> 13;
+        p[i] = (float)(h & 0xffff) / 65536.0f;
+    }
+}
+
+// stride = distance between frames (floats); arena layout puts G_{s-1}, G_s,
+// D_{s-1} of one frame inside an 11-plane octave arena, like the product.
+template <int R, int TH>
+float time_blur(const float* src, float* dst, float* dog, size_t stride, int W, int H, int pitch, int nimg,
+                int reps) {
     using G = BlurGeom<R, TH>;
     BlurTaps taps{};
     for (int t = 0; t <= R; t++) taps.k[t] = 1.0f / (2 * R + 1);
-    const size_t img = (size_t)pitch * H;
     const int tx = (W + G::TW - 1) / G::TW, ty = (H + G::TH - 1) / G::TH;
     dim3 grid(tx, ty, nimg);
     auto go = [&]() {
-        hipLaunchKernelGGL((k_blur<R, TH>), grid, dim3(256), 0, 0, src, img, dst, img, dog, img, (float*)nullptr,
-                           (size_t)0, 0, 0, 0, W, H, pitch, taps);
+        hipLaunchKernelGGL((k_blur<R, TH>), grid, dim3(256), 0, 0, src, stride, dst, stride, dog, stride,
+                           (float*)nullptr, (size_t)0, 0, 0, 0, W, H, pitch, taps);
     };
     go();
     hipEvent_t a, b;
@@ -63,33 +75,49 @@ float time_blur(const float* src, float* dst, float* dog, int W, int H, int pitc
     return ms / reps;
 }
 
-void bench_blur(int N) {
+void bench_blur(int N, bool arena, bool random) {
     const int W = 3840, H = 2160, pitch = 3840;
-    const size_t n = (size_t)pitch * H * N;
-    float *s, *d, *g;
-    CK(hipMalloc(&s, n * 4));
-    CK(hipMalloc(&d, n * 4));
-    CK(hipMalloc(&g, n * 4));
-    CK(hipMemset(s, 0, n * 4));
-    const double bytes = 12.0 * W * H * N;  // read G_{s-1}, write G_s + D_{s-1}
-    std::printf("blur octave-0 batch (%d x %dx%d): ms, effective GB/s (12 B/px)\n", N, W, H);
-#define B(R, TH, PP)                                                                                      \
-    {                                                                                                     \
-        const float ms = time_blur<R, TH, PP>(s, d, g, W, H, pitch, N, 5);                                \
-        std::printf("  R=%2d TH=%2d pp=%d %8.3f ms %8.1f GB/s\n", R, TH, PP, ms, bytes / (ms * 1e-3) / 1e9); \
+    const size_t plane = (size_t)pitch * H;
+    float *base, *s, *d, *g;
+    size_t stride;
+    if (arena) {
+        CK(hipMalloc(&base, plane * 11 * N * 4));
+        stride = plane * 11;
+        s = base;
+        d = base + plane;
+        g = base + 6 * plane;
+        if (random) hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, base, plane * 11 * N);
+        else CK(hipMemset(base, 0, plane * 11 * N * 4));
+    } else {
+        CK(hipMalloc(&base, plane * 3 * N * 4));
+        stride = plane;
+        s = base;
+        d = base + plane * N;
+        g = base + 2 * plane * N;
+        if (random) hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, base, plane * 3 * N);
+        else CK(hipMemset(base, 0, plane * 3 * N * 4));
     }
-    B(5, 32, 0) B(6, 32, 0) B(8, 32, 0) B(10, 32, 0) B(10, 64, 0) B(13, 32, 0) B(13, 64, 0)
+    CK(hipDeviceSynchronize());
+    const double bytes = 12.0 * W * H * N;  // read G_{s-1}, write G_s + D_{s-1}
+    std::printf("blur octave-0 batch (%d x %dx%d, %s layout, %s data): ms, effective GB/s (12 B/px)\n", N, W, H,
+                arena ? "arena" : "planar", random ? "random" : "zero");
+#define B(R, TH)                                                                                         \
+    {                                                                                                    \
+        const float ms = time_blur<R, TH>(s, d, g, stride, W, H, pitch, N, 5);                           \
+        std::printf("  R=%2d TH=%2d %8.3f ms %8.1f GB/s\n", R, TH, ms, bytes / (ms * 1e-3) / 1e9);        \
+    }
+    B(5, 32) B(6, 32) B(8, 32) B(10, 32) B(10, 64) B(13, 32) B(13, 64)
 #undef B
-    CK(hipFree(s));
-    CK(hipFree(d));
-    CK(hipFree(g));
+    CK(hipFree(base));
 }
 
 int main(int argc, char** argv) {
     const char* mode = argc > 1 ? argv[1] : "all";
     if (!strcmp(mode, "all") || !strcmp(mode, "blur")) {
-        bench_blur(16);
-        bench_blur(2);
+        bench_blur(16, false, false);
+        bench_blur(16, false, true);
+        bench_blur(16, true, true);
+        bench_blur(2, true, true);
     }
     if (strcmp(mode, "all") && strcmp(mode, "desc")) return 0;
     const int W = 3840, H = 2160, pitch = 3840, NKP = 200000;
