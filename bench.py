@@ -80,8 +80,10 @@ def main():
         ctx.set_chunk(args.chunk)
     ptr, stride, pitch = frames.data_ptr(), frames.stride(1), frames.stride(0)
 
+    out = pkg.ResultBuffers()  # streaming caller: host result arrays reused across batches
+
     def step():
-        offs, res = ctx.sift_batch_device(ptr, B, W, H, stride, pitch, fetch=True)
+        offs, res = ctx.sift_batch_device(ptr, B, W, H, stride, pitch, fetch=True, out=out)
         return int(offs[-1])
 
     def barrier():

@@ -6,6 +6,7 @@ See sift.py for the reference API mirror and DESIGN.md for the design.
 from ._lib import SiftMiError, lib  # noqa: F401
 from .sift import (  # noqa: F401
     DESCRIPTOR_SIZE, Context, ImageprocProcessing, KeyPoint, OpenCVProcessing, PrecomputedImages, Processing,
+    ResultBuffers,
     SiftResult, compute_descriptor, default_context, key_fields, precompute_images, sift, sift_with_precomputed,
     sift_with_processing, stable_sort_xy_size)
 

@@ -12,6 +12,7 @@
 // the L2 norms use the reference's chunk-of-4 order (src/lib.rs:957-976).
 #include <float.h>
 
+#include <algorithm>
 #include <type_traits>
 
 #include "sift_common.h"
@@ -279,18 +280,29 @@ __device__ __forceinline__ void describe_wave_exact(const float* __restrict__ im
 // so bins agree to f32 rounding and the u8 components to +-1 (the tolerance
 // tests/test_gpu_parity.py states).  describe_wave_exact is the bit-exact
 // alternative (sift_mi_set_exact_descriptors).
+//
+// kShare lanes share one slice (64 / kShare slices per wave): their updates
+// are issued group by group (lanes [g*S, (g+1)*S) in step g), so no two lanes
+// of a slice write in the same instruction.  Sharing trades LDS instructions
+// for LDS footprint -- 33.8 KB per wave at kShare = 1 (one wave per SIMD),
+// 16.9 KB at 2, 8.4 KB at 4 -- i.e. for occupancy.
 constexpr int PRIV_STRIDE = 132;  // 128 bins + 4 dummy slots (border-ring contributions)
 
+template <int kShare>
 struct DescScratchFast {
-    float h[64 * PRIV_STRIDE];
+    float h[64 / kShare * PRIV_STRIDE];
     int rowlo[ROWS_MAX];
     int rowpre[ROWS_MAX + 1];
 };
 
-template <int kAblate = 0>
+// kAblate bit 4: f32 atan2 / exp (ocml) instead of the reference's f64 atan2
+// and the correctly rounded f32 exp -- results stay within the fast path's
+// +-1 tolerance (the sample angle moves by < 1e-5 degree).
+template <int kShare, int kAblate = 0>
 __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img, int pitch, int width, int height,
                                                    float xf, float yf, float scale, float orientation,
-                                                   DescScratchFast& sc, uint8_t* __restrict__ out, int lane) {
+                                                   DescScratchFast<kShare>& sc, uint8_t* __restrict__ out, int lane) {
+    constexpr int NS = 64 / kShare;  // slices
     const int32_t x = (int32_t)sat_u32(roundf(xf));
     const int32_t y = (int32_t)sat_u32(roundf(yf));
     const float BIN_ANGLE_STEP = (float)kDescBins / 360.0f;
@@ -303,10 +315,11 @@ __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img
     const int n = 2 * radius + 1;
     // bin b of lane l's slice lives at h[b * 64 + l]: every lane's read-add-write
     // of any bin hits its own bank (l mod 32) -> conflict-free scatter
-    float* hp = sc.h + lane;
+    float* hp = sc.h + (lane & (NS - 1));
+    const int grp = lane / NS;
 #pragma unroll
-    for (int i = 0; i < PRIV_STRIDE * 64 / 4; i += 64)
-        reinterpret_cast<float4*>(sc.h)[i + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (int i = 0; i < PRIV_STRIDE * NS / 4; i += 64)
+        if (i + lane < PRIV_STRIDE * NS / 4) reinterpret_cast<float4*>(sc.h)[i + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
     for (int row = lane; row < n; row += 64) {
         const double yi = (double)(row - radius);
         const double c = cos_s, s = sin_s;
@@ -365,9 +378,10 @@ __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img
         float row_bin = row_rot + (float)(kDescHist / 2);
         float col_bin = col_rot + (float)(kDescHist / 2);
         const int32_t ay = y + yi, ax = x + xi;
-        if (!(row_bin > -0.5f && row_bin < (float)kDescHist + 0.5f && col_bin > -0.5f &&
-              col_bin < (float)kDescHist + 0.5f && ay > 0 && ay < height - 1 && ax > 0 && ax < width - 1))
-            continue;
+        const bool inside = row_bin > -0.5f && row_bin < (float)kDescHist + 0.5f && col_bin > -0.5f &&
+                            col_bin < (float)kDescHist + 0.5f && ay > 0 && ay < height - 1 && ax > 0 &&
+                            ax < width - 1;
+        if (kShare == 1 && !inside) continue;
         float dx, dy;
         if (kAblate & 8) {
             dx = (float)xi * 0.01f + 0.001f;
@@ -378,10 +392,11 @@ __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img
             dy = rw[ax - pitch] - rw[ax + pitch];
         }
         const float wsq = col_rot * col_rot + row_rot * row_rot;
-        const float weight =
-            (kAblate & 4) ? 1.0f + wsq * (-0.125f) : exp_f32(wsq * (-2.f / (float)(kDescHist * kDescHist)));
-        double deg = ((kAblate & 2) ? (double)(dy * 50.0f + dx)
-                                    : atan2((double)dy, (double)dx) * (180.0 / 3.14159265358979323846)) +
+        const float earg = wsq * (-2.f / (float)(kDescHist * kDescHist));
+        const float weight = (kAblate & 4) ? 1.0f + wsq * (-0.125f) : ((kAblate & 16) ? expf(earg) : exp_f32(earg));
+        double deg = ((kAblate & 2)    ? (double)(dy * 50.0f + dx)
+                      : (kAblate & 16) ? (double)(atan2f(dy, dx) * (180.0f / 3.14159265358979323846f))
+                                       : atan2((double)dy, (double)dx) * (180.0 / 3.14159265358979323846)) +
                      360.0;
         deg = deg >= 360.0 ? deg - 360.0 : deg;  // f64 `% 360.0` of a value in [180, 540]
         const float ori = (float)deg - orientation;
@@ -408,74 +423,93 @@ __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img
         auto cell = [](int r, int q) { return (r >= 1 && r <= 4 && q >= 1 && q <= 4) ? ((r - 1) * 4 + (q - 1)) * 8 : 128; };
         const int b11 = cell(r1, q1), b12 = cell(r1, q1 + 1), b21 = cell(r1 + 1, q1), b22 = cell(r1 + 1, q1 + 1);
         const int d0 = o0 & (b11 == 128 ? 3 : 7), d1 = o1 & (b11 == 128 ? 3 : 7);
-        hp[(b11 + d0) * 64] += c000;
-        hp[(b11 + d1) * 64] += c001;
         const int e0 = o0 & (b12 == 128 ? 3 : 7), e1 = o1 & (b12 == 128 ? 3 : 7);
-        hp[(b12 + e0) * 64] += c010;
-        hp[(b12 + e1) * 64] += c011;
         const int f0 = o0 & (b21 == 128 ? 3 : 7), f1 = o1 & (b21 == 128 ? 3 : 7);
-        hp[(b21 + f0) * 64] += c100;
-        hp[(b21 + f1) * 64] += c101;
         const int g0 = o0 & (b22 == 128 ? 3 : 7), g1 = o1 & (b22 == 128 ? 3 : 7);
-        hp[(b22 + g0) * 64] += c110;
-        hp[(b22 + g1) * 64] += c111;
+#pragma unroll
+        for (int g = 0; g < kShare; g++) {
+            if (kShare > 1 && !(inside && grp == g)) continue;
+            hp[(b11 + d0) * NS] += c000;
+            hp[(b11 + d1) * NS] += c001;
+            hp[(b12 + e0) * NS] += c010;
+            hp[(b12 + e1) * NS] += c011;
+            hp[(b21 + f0) * NS] += c100;
+            hp[(b21 + f1) * NS] += c101;
+            hp[(b22 + g0) * NS] += c110;
+            hp[(b22 + g1) * NS] += c111;
+        }
     }
     wave_sync();
     // per-bin sum of the 64 private slices: lane l owns flat bins 2l, 2l+1 and
     // starts at slice l (rotated start: the 32 lanes of a half hit 32 banks)
     float acc0 = 0.0f, acc1 = 0.0f;
-    const float* r0 = sc.h + (2 * lane) * 64;
-    const float* r1 = r0 + 64;
+    const float* r0 = sc.h + (2 * lane) * NS;
+    const float* r1 = r0 + NS;
 #pragma unroll 8
-    for (int j = 0; j < 64; j++) {
-        const int jj = (j + lane) & 63;
+    for (int j = 0; j < NS; j++) {
+        const int jj = (j + lane) & (NS - 1);
         acc0 += r0[jj];
         acc1 += r1[jj];
     }
     describe_normalize(acc0, acc1, out, lane);
 }
 
-template <bool kExact, int kAblate>
+// kMode 0: bit-exact (describe_wave_exact); 1 / 2 / 4: fast path with that
+// slice-sharing factor.
+template <int kMode, int kAblate>
 __global__ __launch_bounds__(64) void k_describe(const DescLaunch L) {
-    using Scratch = typename std::conditional<kExact, DescScratch, DescScratchFast>::type;
+    constexpr bool kExact = kMode == 0;
+    using Scratch = typename std::conditional<kExact, DescScratch, DescScratchFast<kExact ? 1 : kMode>>::type;
     __shared__ __attribute__((aligned(16))) Scratch scr;
     const int lane = threadIdx.x;
-    const uint32_t i = blockIdx.x;
-    const KpRec kp = L.kp[L.idx ? L.idx[i] : i];
-    const int o = kp.octave;
-    const int W = L.ow[o], H = L.oh[o];
-    const int pitch = L.opitch[o];
-    const float* img =
-        L.gauss[o] + (size_t)(kp.img - L.img_base) * L.gauss_img_stride[o] + (size_t)kp.scale * pitch * H;
-    // compute_descriptors (src/lib.rs:759-782)
-    const float angle = 360.0f - kp.angle;
-    const float osf = 1.0f / (float)(1u << o);  // 2_f32.powi(-octave)
-    const float kp_size = kp.size * osf;
-    uint8_t* out = L.out_desc + (size_t)i * kDescSize;
-    if constexpr (kExact)
-        describe_wave_exact<kAblate>(img, pitch, W, H, kp.x * osf, kp.y * osf, kp_size, angle, scr, out, lane);
-    else
-        describe_wave_fast<kAblate>(img, pitch, W, H, kp.x * osf, kp.y * osf, kp_size, angle, scr, out, lane);
-    if (lane == 0) {
-        if (L.out_kp) {
-            OutKp k;
-            k.x = kp.x * 0.5f;  // DELTA_MIN (src/lib.rs:163-176)
-            k.y = kp.y * 0.5f;
-            k.size = kp.size * 0.5f;
-            k.angle = kp.angle;
-            k.response = kp.response;
-            L.out_kp[i] = k;
+    const uint32_t n = min(*L.n, L.bound);
+    // one wave per keypoint, taken from a work counter: window sizes (and
+    // costs) vary ~20x, a static stride would leave a long tail
+    for (;;) {
+        uint32_t i = 0;
+        if (lane == 0) i = atomicAdd(L.work, 1u);
+        i = __shfl(i, 0);
+        if (i >= n) break;
+        const KpRec kp = L.kp[L.idx ? L.idx[i] : i];
+        const int o = kp.octave;
+        const int W = L.ow[o], H = L.oh[o];
+        const int pitch = L.opitch[o];
+        const float* img =
+            L.gauss[o] + (size_t)(kp.img - L.img_base) * L.gauss_img_stride[o] + (size_t)kp.scale * pitch * H;
+        // compute_descriptors (src/lib.rs:759-782)
+        const float angle = 360.0f - kp.angle;
+        const float osf = 1.0f / (float)(1u << o);  // 2_f32.powi(-octave)
+        const float kp_size = kp.size * osf;
+        uint8_t* out = L.out_desc + (size_t)i * kDescSize;
+        if constexpr (kExact)
+            describe_wave_exact<kAblate>(img, pitch, W, H, kp.x * osf, kp.y * osf, kp_size, angle, scr, out, lane);
+        else
+            describe_wave_fast<kExact ? 1 : kMode, kAblate>(img, pitch, W, H, kp.x * osf, kp.y * osf, kp_size, angle,
+                                                            scr, out, lane);
+        if (lane == 0) {
+            if (L.out_kp) {
+                OutKp k;
+                k.x = kp.x * 0.5f;  // DELTA_MIN (src/lib.rs:163-176)
+                k.y = kp.y * 0.5f;
+                k.size = kp.size * 0.5f;
+                k.angle = kp.angle;
+                k.response = kp.response;
+                L.out_kp[i] = k;
+            }
+            if (L.out_key) L.out_key[i] = kp.key + L.key_base;
         }
-        if (L.out_key) L.out_key[i] = kp.key;
+        wave_sync();  // the scratch is reused by the next keypoint
     }
 }
 
 void launch_describe(const DescLaunch& L, hipStream_t st) {
-    if (L.n == 0) return;
+    if (L.bound == 0) return;
+    // fast path: 17 KB of LDS per wave -> 9 resident per CU (exact: 14 KB)
+    const dim3 grid(std::min<uint32_t>(L.bound, 256 * 9));
     if (L.exact)
-        hipLaunchKernelGGL((k_describe<true, 0>), dim3(L.n), dim3(64), 0, st, L);
+        hipLaunchKernelGGL((k_describe<0, 0>), grid, dim3(64), 0, st, L);
     else
-        hipLaunchKernelGGL((k_describe<false, 0>), dim3(L.n), dim3(64), 0, st, L);
+        hipLaunchKernelGGL((k_describe<2, 0>), grid, dim3(64), 0, st, L);
 }
 
 __global__ __launch_bounds__(64) void k_describe_one(const float* img, int w, int h, float x, float y, float scale,

@@ -13,6 +13,8 @@
 // the CPU path and the keypoint count/order does not depend on reduction
 // order.  Emission order (octave, s_init, y_init, x_init, peak) is restored
 // by sorting the 64-bit emission keys afterwards (order.hip).
+#include <algorithm>
+
 #include "sift_common.h"
 #include "sift_kernels.h"
 
@@ -246,24 +248,26 @@ __device__ __forceinline__ bool refine_one(const RefineLaunch& L, uint64_t key, 
 }
 
 __global__ __launch_bounds__(256) void k_refine(const RefineLaunch L) {
-    const uint32_t i = blockIdx.x * 256 + threadIdx.x;
-    ExtRec e;
-    const bool keep = i < L.n_cand && refine_one(L, L.cand[i], e);
-    const uint64_t mask = __ballot(keep);
-    if (!mask) return;
+    const uint32_t n = min(*L.n_cand, L.cand_cap);
     const int lane = threadIdx.x & 63;
-    const int leader = __ffsll((unsigned long long)mask) - 1;
-    uint32_t base = 0;
-    if (lane == leader) base = atomicAdd(L.counter, (uint32_t)__popcll(mask));
-    base = __shfl(base, leader);
-    if (!keep) return;
-    const uint32_t slot = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
-    if (slot < L.cap) L.out[slot] = e;
+    for (uint32_t base = blockIdx.x * 256; base < n; base += gridDim.x * 256) {
+        const uint32_t i = base + threadIdx.x;
+        ExtRec e;
+        const bool keep = i < n && refine_one(L, L.cand[i], e);
+        const uint64_t mask = __ballot(keep);
+        if (!mask) continue;
+        const int leader = __ffsll((unsigned long long)mask) - 1;
+        uint32_t b = 0;
+        if (lane == leader) b = atomicAdd(L.counter, (uint32_t)__popcll(mask));
+        b = __shfl(b, leader);
+        const uint32_t slot = b + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+        if (keep && slot < L.cap) L.out[slot] = e;
+    }
 }
 
 void launch_refine(const RefineLaunch& L, hipStream_t st) {
-    if (L.n_cand == 0) return;
-    hipLaunchKernelGGL(k_refine, dim3((L.n_cand + 255) / 256), dim3(256), 0, st, L);
+    if (L.cand_cap == 0) return;
+    hipLaunchKernelGGL(k_refine, dim3(std::min<uint32_t>((L.cand_cap + 255) / 256, 2048)), dim3(256), 0, st, L);
 }
 
 // ---------------------------------------------------------------------------
@@ -280,132 +284,138 @@ __global__ __launch_bounds__(256) void k_orient(const OrientLaunch L) {
     __shared__ __attribute__((aligned(16))) uint8_t sbin[4][OR_LDS];
     __shared__ uint32_t wcount[4], wbase;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t r = blockIdx.x * 4 + wave;
-    const bool active = r < L.n_ext;
-    ExtRec e;
-    int W = 1, H = 1, pitch = 1, radius = 0, n = 1, N = 0;
-    float kp_scale = 0.f, kp_x = 0.f, kp_y = 0.f, osf = 1.f;
-    const float* img = nullptr;
-    if (active) {
-        e = L.ext[r];
-        W = L.ow[e.octave];
-        H = L.oh[e.octave];
-        pitch = L.opitch[e.octave];
-        img = L.gauss[e.octave] + (size_t)(e.img - L.img_base) * L.gauss_img_stride[e.octave] +
-              (size_t)e.scale * pitch * H;
-        osf = (float)(1u << e.octave);  // 2_f32.powi(octave)
-        kp_scale = 0.8f * pow2_f32(((float)e.scale + e.off_s) / (float)kScalesPerOctave) * 2.f;
-        kp_x = ((float)e.x + e.off_x) * osf;
-        kp_y = ((float)e.y + e.off_y) * osf;
-        radius = sat_i32(roundf(3.f * kLambdaOri * kp_scale));
-        if (radius > 16) radius = 16;  // unreachable: kp_scale < 3.6 (assert-equivalent guard)
-        if (radius < 0) radius = 0;
-        n = 2 * radius + 1;
-        N = n * n;
-        const float sigma = kLambdaOri * kp_scale;
-        const float gws = -1.0f / (2.0f * sigma * sigma);
-        const float bin_step = (float)kOriBins / (3.14159265358979323846f * 2.f);
-        const int x = e.x, y = e.y;
-        for (int idx = lane; idx < N; idx += 64) {
-            const int iy = idx / n;
-            const int yp = iy - radius, xp = idx - iy * n - radius;
-            const int yy = y + yp, xx = x + xp;
-            uint8_t bin = 0xff;
-            float val = 0.0f;
-            if (yy > 0 && yy < H - 1 && xx > 0 && xx < W - 1) {
-                const float* rw = img + (size_t)yy * pitch;
-                const float dx = rw[xx + 1] - rw[xx - 1];
-                const float dy = rw[xx - pitch] - rw[xx + pitch];
-                const float wexp = (float)(yp * yp + xp * xp) * gws;
-                const float weight = exp_f32(wexp);
-                const float mag = sqrtf(dx * dx + dy * dy);
-                const float ori = (float)atan2((double)dy, (double)dx);
-                int bi = sat_i32(roundf(bin_step * ori));
-                if (bi >= kOriBins)
-                    bi -= kOriBins;
-                else if (bi < 0)
-                    bi += kOriBins;
-                bin = (uint8_t)bi;
-                val = weight * mag;
-            }
-            sval[wave][idx] = val;
-            sbin[wave][idx] = bin;
-        }
-    }
-    __syncthreads();
-    // sequential per-bin sums (lane = bin); inactive waves run on an empty list
-    if (!active) N = 0;
-    float acc = 0.0f;
+    const uint32_t n_ext = min(*L.n_ext, L.ext_cap);
+    // one group of 4 extrema per workgroup; the grid covers the bound, the
+    // device count ends it early (block-uniform)
     {
-        const float4* v4 = reinterpret_cast<const float4*>(sval[wave]);
-        const uint32_t* b4 = reinterpret_cast<const uint32_t*>(sbin[wave]);
-        const uint32_t me = (uint32_t)lane;
-        int j = 0;
-        for (; j + 4 <= N; j += 4) {
-            const float4 v = v4[j >> 2];
-            const uint32_t bb = b4[j >> 2];
-            acc += ((bb & 0xff) == me) ? v.x : 0.0f;
-            acc += (((bb >> 8) & 0xff) == me) ? v.y : 0.0f;
-            acc += (((bb >> 16) & 0xff) == me) ? v.z : 0.0f;
-            acc += ((bb >> 24) == me) ? v.w : 0.0f;
+        const uint32_t rg = blockIdx.x * 4;
+        if (rg >= n_ext) return;
+        const uint32_t r = rg + wave;
+        const bool active = r < n_ext;
+        ExtRec e;
+        int W = 1, H = 1, pitch = 1, radius = 0, n = 1, N = 0;
+        float kp_scale = 0.f, kp_x = 0.f, kp_y = 0.f, osf = 1.f;
+        const float* img = nullptr;
+        if (active) {
+            e = L.ext[r];
+            W = L.ow[e.octave];
+            H = L.oh[e.octave];
+            pitch = L.opitch[e.octave];
+            img = L.gauss[e.octave] + (size_t)(e.img - L.img_base) * L.gauss_img_stride[e.octave] +
+                  (size_t)e.scale * pitch * H;
+            osf = (float)(1u << e.octave);  // 2_f32.powi(octave)
+            kp_scale = 0.8f * pow2_f32(((float)e.scale + e.off_s) / (float)kScalesPerOctave) * 2.f;
+            kp_x = ((float)e.x + e.off_x) * osf;
+            kp_y = ((float)e.y + e.off_y) * osf;
+            radius = sat_i32(roundf(3.f * kLambdaOri * kp_scale));
+            if (radius > 16) radius = 16;  // unreachable: kp_scale < 3.6 (assert-equivalent guard)
+            if (radius < 0) radius = 0;
+            n = 2 * radius + 1;
+            N = n * n;
+            const float sigma = kLambdaOri * kp_scale;
+            const float gws = -1.0f / (2.0f * sigma * sigma);
+            const float bin_step = (float)kOriBins / (3.14159265358979323846f * 2.f);
+            const int x = e.x, y = e.y;
+            for (int idx = lane; idx < N; idx += 64) {
+                const int iy = idx / n;
+                const int yp = iy - radius, xp = idx - iy * n - radius;
+                const int yy = y + yp, xx = x + xp;
+                uint8_t bin = 0xff;
+                float val = 0.0f;
+                if (yy > 0 && yy < H - 1 && xx > 0 && xx < W - 1) {
+                    const float* rw = img + (size_t)yy * pitch;
+                    const float dx = rw[xx + 1] - rw[xx - 1];
+                    const float dy = rw[xx - pitch] - rw[xx + pitch];
+                    const float wexp = (float)(yp * yp + xp * xp) * gws;
+                    const float weight = exp_f32(wexp);
+                    const float mag = sqrtf(dx * dx + dy * dy);
+                    const float ori = (float)atan2((double)dy, (double)dx);
+                    int bi = sat_i32(roundf(bin_step * ori));
+                    if (bi >= kOriBins)
+                        bi -= kOriBins;
+                    else if (bi < 0)
+                        bi += kOriBins;
+                    bin = (uint8_t)bi;
+                    val = weight * mag;
+                }
+                sval[wave][idx] = val;
+                sbin[wave][idx] = bin;
+            }
         }
-        for (; j < N; j++) acc += ((uint32_t)sbin[wave][j] == me) ? sval[wave][j] : 0.0f;
+        __syncthreads();
+        // sequential per-bin sums (lane = bin); inactive waves run on an empty list
+        if (!active) N = 0;
+        float acc = 0.0f;
+        {
+            const float4* v4 = reinterpret_cast<const float4*>(sval[wave]);
+            const uint32_t* b4 = reinterpret_cast<const uint32_t*>(sbin[wave]);
+            const uint32_t me = (uint32_t)lane;
+            int j = 0;
+            for (; j + 4 <= N; j += 4) {
+                const float4 v = v4[j >> 2];
+                const uint32_t bb = b4[j >> 2];
+                acc += ((bb & 0xff) == me) ? v.x : 0.0f;
+                acc += (((bb >> 8) & 0xff) == me) ? v.y : 0.0f;
+                acc += (((bb >> 16) & 0xff) == me) ? v.z : 0.0f;
+                acc += ((bb >> 24) == me) ? v.w : 0.0f;
+            }
+            for (; j < N; j++) acc += ((uint32_t)sbin[wave][j] == me) ? sval[wave][j] : 0.0f;
+        }
+        // circular [1,4,6,4,1]/16 smoothing (src/lib.rs:742-755)
+        const int k = lane < kOriBins ? lane : 0;
+        const float rm2 = __shfl(acc, (k + kOriBins - 2) % kOriBins);
+        const float rm1 = __shfl(acc, (k + kOriBins - 1) % kOriBins);
+        const float rp1 = __shfl(acc, (k + 1) % kOriBins);
+        const float rp2 = __shfl(acc, (k + 2) % kOriBins);
+        const float r0 = __shfl(acc, k);
+        const float h = (rm2 + rp2) * (1.f / 16.f) + (rm1 + rp1) * (4.f / 16.f) + r0 * 6.f / 16.f;
+        // max over the 36 bins
+        float m = lane < kOriBins ? h : -1.0f;
+    #pragma unroll
+        for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
+        const float thr = m * kOriPeakRatio;
+        const float hm = __shfl(h, (k + kOriBins - 1) % kOriBins);
+        const float hp = __shfl(h, (k + 1) % kOriBins);
+        const bool peak = lane < kOriBins && h > hm && h > hp && h >= thr;
+        const uint64_t mask = __ballot(peak);
+        const uint32_t npk = (uint32_t)__popcll(mask);
+        // one global atomic per workgroup (4 waves)
+        if (lane == 0) wcount[wave] = npk;
+        __syncthreads();
+        if (threadIdx.x == 0) {
+            const uint32_t tot = wcount[0] + wcount[1] + wcount[2] + wcount[3];
+            wbase = tot ? atomicAdd(L.counter, tot) : 0u;
+        }
+        __syncthreads();
+        uint32_t base = wbase;
+        for (int w = 0; w < wave; w++) base += wcount[w];
+        const uint32_t slot = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+        if (!peak || slot >= L.cap) return;
+        const float interp = (hm - hp) / (hm - 2.0f * h + hp);
+        float bin = (float)k + 0.5f * interp;
+        if (bin < 0.0f)
+            bin = (float)kOriBins + bin;
+        else if (bin >= (float)kOriBins)
+            bin = bin - (float)kOriBins;
+        KpRec kp;
+        kp.key = e.key | (uint64_t)k;
+        kp.img = e.img;
+        kp.octave = e.octave;
+        kp.scale = e.scale;
+        kp.pad = 0;
+        kp.x = kp_x;
+        kp.y = kp_y;
+        kp.size = kp_scale * osf;
+        kp.angle = 360.0f - (360.0f / (float)kOriBins) * bin;
+        kp.response = e.response;
+        kp.pad2 = 0.f;
+        L.out[slot] = kp;
     }
-    // circular [1,4,6,4,1]/16 smoothing (src/lib.rs:742-755)
-    const int k = lane < kOriBins ? lane : 0;
-    const float rm2 = __shfl(acc, (k + kOriBins - 2) % kOriBins);
-    const float rm1 = __shfl(acc, (k + kOriBins - 1) % kOriBins);
-    const float rp1 = __shfl(acc, (k + 1) % kOriBins);
-    const float rp2 = __shfl(acc, (k + 2) % kOriBins);
-    const float r0 = __shfl(acc, k);
-    const float h = (rm2 + rp2) * (1.f / 16.f) + (rm1 + rp1) * (4.f / 16.f) + r0 * 6.f / 16.f;
-    // max over the 36 bins
-    float m = lane < kOriBins ? h : -1.0f;
-#pragma unroll
-    for (int off = 32; off >= 1; off >>= 1) m = fmaxf(m, __shfl_xor(m, off));
-    const float thr = m * kOriPeakRatio;
-    const float hm = __shfl(h, (k + kOriBins - 1) % kOriBins);
-    const float hp = __shfl(h, (k + 1) % kOriBins);
-    const bool peak = lane < kOriBins && h > hm && h > hp && h >= thr;
-    const uint64_t mask = __ballot(peak);
-    const uint32_t npk = (uint32_t)__popcll(mask);
-    // one global atomic per workgroup (4 waves)
-    if (lane == 0) wcount[wave] = npk;
-    __syncthreads();
-    if (threadIdx.x == 0) {
-        const uint32_t tot = wcount[0] + wcount[1] + wcount[2] + wcount[3];
-        wbase = tot ? atomicAdd(L.counter, tot) : 0u;
-    }
-    __syncthreads();
-    if (!peak) return;
-    uint32_t base = wbase;
-    for (int w = 0; w < wave; w++) base += wcount[w];
-    const uint32_t slot = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
-    if (slot >= L.cap) return;
-    const float interp = (hm - hp) / (hm - 2.0f * h + hp);
-    float bin = (float)k + 0.5f * interp;
-    if (bin < 0.0f)
-        bin = (float)kOriBins + bin;
-    else if (bin >= (float)kOriBins)
-        bin = bin - (float)kOriBins;
-    KpRec kp;
-    kp.key = e.key | (uint64_t)k;
-    kp.img = e.img;
-    kp.octave = e.octave;
-    kp.scale = e.scale;
-    kp.pad = 0;
-    kp.x = kp_x;
-    kp.y = kp_y;
-    kp.size = kp_scale * osf;
-    kp.angle = 360.0f - (360.0f / (float)kOriBins) * bin;
-    kp.response = e.response;
-    kp.pad2 = 0.f;
-    L.out[slot] = kp;
 }
 
 void launch_orient(const OrientLaunch& L, hipStream_t st) {
-    if (L.n_ext == 0) return;
-    dim3 grid((L.n_ext + 3) / 4);
+    if (L.ext_cap == 0) return;
+    dim3 grid((L.ext_cap + 3) / 4);
     hipLaunchKernelGGL(k_orient, grid, dim3(256), 0, st, L);
 }
 

@@ -13,6 +13,7 @@
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/sift_mi.h"
@@ -272,40 +273,56 @@ struct Plan {
 
 }  // namespace
 
+// Per-chunk state that outlives the enqueue: device counters, final outputs
+// and the events of one in-flight chunk.  Two slots alternate, so chunk k+1's
+// kernels run while the host waits for chunk k and copies its results out.
+struct Slot {
+    // [0] candidates [1] extrema [2] keypoints [3] outputs [4..4+F) frame starts
+    // [4+F..4+2F) per-frame outputs [4+2F..6+2F) work counters
+    DevBuf<uint32_t> counters;
+    PinBuf<uint32_t> h_counts;
+    DevBuf<OutKp> out_kp;
+    DevBuf<uint8_t> out_desc;
+    DevBuf<uint64_t> out_key;
+    hipEvent_t ev[7] = {};   // stage boundaries on the compute stream (ev[6] = chunk done)
+    hipEvent_t copied = {};  // results copied to the host (copy stream)
+    bool pending_copy = false;
+    uint32_t m = 0, frame_base = 0, cap_frames = 0;
+    uint32_t bc = 0, be = 0, bk = 0;  // candidate / extremum / keypoint bounds used by this chunk
+};
+
 struct sift_mi_ctx {
     int device = 0;
     sift_mi_profile profile = SIFT_MI_PROFILE_OPENCV;
     hipStream_t own = nullptr;
-    hipStream_t stream = nullptr;
+    hipStream_t stream = nullptr;  // compute stream (own or the caller's)
+    hipStream_t cstream = nullptr; // device->host result copies
     uint32_t chunk_override = 0;
     int keep_on_device = 0;
     int exact_descriptors = 0;
     Plan plan;
     DevBuf<uint8_t> staging;  // host-sourced frames
-    // detection / description buffers
+    // detection / description buffers (shared by the slots: chunks run in stream order)
     DevBuf<uint64_t> cand;
     DevBuf<ExtRec> ext;
     DevBuf<KpRec> kp;
-    DevBuf<uint32_t> counters;  // [0] extrema, [1] keypoints, [2..] per frame
     DevBuf<uint64_t> keys_a, keys_b;
     DevBuf<uint32_t> vals_a, vals_b, fin;
     DevBuf<uint8_t> sort_tmp;
     DevBuf<uint32_t> seg_off, out_off;
     DevBuf<uint8_t> use_resp;
-    DevBuf<OutKp> out_kp;
-    DevBuf<uint8_t> out_desc;
-    DevBuf<uint64_t> out_key;
+    Slot slot[2];
+    int last_slot = 0;
+    // per-frame high-water marks that size the next chunk's bounds
+    double pf_cand = 0, pf_ext = 0, pf_kp = 0;
     // host results (pinned)
     PinBuf<OutKp> h_kp;
     PinBuf<uint8_t> h_desc;
     PinBuf<uint64_t> h_key;
-    PinBuf<uint32_t> h_counts;
     size_t n_result = 0;
     bool have_result = false;
     bool have_pyramid = false;  // single-frame precompute state
     size_t dev_result_n = 0;
-    // timing
-    hipEvent_t ev[8] = {};
     sift_mi_stats stats{};
 };
 
@@ -469,237 +486,291 @@ int run_pyramid(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, siz
 }
 
 // ---------------------------------------------------------------------------
-// Stage 2-4: detection, orientation, ordering, descriptors for the n frames
-// currently in the pyramid arena.  Appends results (global frame offset
-// `frame_base`) to the host result buffers unless keep_on_device.
+// Stages 2-4 for the m frames in the pyramid arena: detection, refinement,
+// orientation, ordering, features_limit, descriptors -- enqueued on the
+// compute stream with no host round trip.  Every stage reads its input count
+// from device memory (Slot::counters) and is bounded by a host-side estimate
+// (bc / be / bk); finalize_chunk detects a count above its bound and the chunk
+// is re-run with larger bounds.
 // ---------------------------------------------------------------------------
-int run_keypoints(sift_mi_ctx* c, uint32_t n, int64_t limit, uint32_t frame_base, size_t* offsets_out,
-                  size_t result_base) {
-    Plan& p = c->plan;
-    hipStream_t st = c->stream;
+constexpr uint32_t kMaxChunk = 64;  // frames per chunk (one wave plans the output)
+
+struct Bounds {
+    uint32_t bc, be, bk;
+};
+
+Bounds chunk_bounds(sift_mi_ctx* c, uint32_t m) {
     uint64_t sum_p = 0;
-    for (int o = 0; o < p.n_oct; o++) sum_p += p.px[o];
-    // counters: [0] candidates, [1] extrema, [2] keypoints, [3..3+n) per frame
-    size_t cap_cand = std::max<size_t>({8192, (size_t)(sum_p * n / 256), c->cand.cap});
-    CHK(c->counters.ensure(3 + n));
-    CHK(c->h_counts.ensure(3 + n));
-    uint32_t n_cand = 0;
-    for (int attempt = 0; attempt < 3; attempt++) {
-        CHK(c->cand.ensure(cap_cand));
-        HIPCHK(hipMemsetAsync(c->counters.p, 0, (3 + n) * sizeof(uint32_t), st));
-        for (int o = 0; o < p.n_oct; o++) {
-            if (p.oh[o] < 2 * kImageBorder || p.ow[o] < 2 * kImageBorder) continue;  // src/lib.rs:315
-            DetectLaunch D{};
-            D.dog = p.dog(o);
-            D.img_stride = p.dstride(o);
-            D.W = p.ow[o];
-            D.H = p.oh[o];
-            D.pitch = p.opitch[o];
-            D.octave = o;
-            D.n_img = (int)n;
-            D.img_base = 0;
-            D.cand = c->cand.p;
-            D.counter = c->counters.p;
-            D.cap = (uint32_t)c->cand.cap;
-            launch_detect(D, st);
-        }
-        HIPCHK(hipGetLastError());
-        HIPCHK(hipMemcpyAsync(c->h_counts.p, c->counters.p, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
-        n_cand = c->h_counts.p[0];
-        if (n_cand <= c->cand.cap) break;
-        cap_cand = (size_t)n_cand + n_cand / 4 + 4096;
-        if (attempt == 2) return fail(SIFT_MI_ENOMEM, "candidate buffer overflow");
+    for (int o = 0; o < c->plan.n_oct; o++) sum_p += c->plan.px[o];
+    auto est = [&](double pf, double floor_pf) {
+        const double per = std::max(pf * 1.3, floor_pf);
+        return (uint32_t)std::min<double>(std::ceil(per * m) + 1024, 0x7fffffff);
+    };
+    Bounds B;
+    // first chunk: one candidate per 256 octave pixels; later chunks: 1.3x
+    // the per-frame high-water mark
+    B.bc = est(c->pf_cand, c->pf_cand > 0 ? 64.0 : sum_p / 256.0);
+    B.be = est(c->pf_ext, c->pf_ext > 0 ? 64.0 : sum_p / 512.0);
+    B.bk = est(c->pf_kp, c->pf_kp > 0 ? 64.0 : sum_p / 384.0);
+    B.be = std::min(B.be, B.bc);  // one extremum per candidate at most
+    return B;
+}
+
+// Grows the shared buffers for bounds B (waits for in-flight work first when a
+// buffer has to be reallocated).
+int reserve_chunk(sift_mi_ctx* c, const Bounds& B, uint32_t frames) {
+    const bool grow = B.bc > c->cand.cap || B.be > c->ext.cap || B.bk > c->kp.cap || B.bk > c->keys_a.cap ||
+                      frames > c->seg_off.cap;
+    bool grow_out = false;
+    for (auto& S : c->slot)
+        grow_out |= B.bk > S.out_kp.cap || 6 + 2 * frames > S.counters.cap;
+    if (grow || grow_out) {
+        HIPCHK(hipStreamSynchronize(c->stream));
+        HIPCHK(hipStreamSynchronize(c->cstream));
     }
-    size_t cap_ext = std::max<size_t>((size_t)n_cand, 1024);
-    if (c->ext.cap > cap_ext) cap_ext = c->ext.cap;
-    CHK(c->ext.ensure(cap_ext));  // every candidate yields at most one extremum
-    {
-        RefineLaunch R{};
-        R.cand = c->cand.p;
-        R.n_cand = n_cand;
-        R.dog = p.d_dog.p;
-        R.dog_img_stride = p.d_dstride.p;
-        R.ow = p.d_ow.p;
-        R.oh = p.d_oh.p;
-        R.opitch = p.d_opitch.p;
-        R.img_base = 0;
-        R.out = c->ext.p;
-        R.counter = c->counters.p + 1;
-        R.cap = (uint32_t)c->ext.cap;
-        launch_refine(R, st);
-        HIPCHK(hipGetLastError());
-        HIPCHK(hipMemcpyAsync(c->h_counts.p + 1, c->counters.p + 1, sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
+    CHK(c->cand.ensure(B.bc));
+    CHK(c->ext.ensure(B.be));
+    CHK(c->kp.ensure(B.bk));
+    CHK(c->keys_a.ensure(B.bk));
+    CHK(c->keys_b.ensure(B.bk));
+    CHK(c->vals_a.ensure(B.bk));
+    CHK(c->vals_b.ensure(B.bk));
+    CHK(c->fin.ensure(B.bk));
+    CHK(c->seg_off.ensure(frames));
+    CHK(c->out_off.ensure(frames));
+    CHK(c->use_resp.ensure(frames));
+    for (auto& S : c->slot) {
+        CHK(S.counters.ensure(6 + 2 * frames));
+        CHK(S.h_counts.ensure(4 + 2 * frames));
+        CHK(S.out_kp.ensure(B.bk));
+        CHK(S.out_desc.ensure((size_t)B.bk * kDescSize));
+        CHK(S.out_key.ensure(B.bk));
     }
-    const uint32_t n_ext = c->h_counts.p[1];
-    HIPCHK(hipEventRecord(c->ev[2], st));
-    size_t cap_kp = std::max<size_t>(2 * (size_t)n_ext + 1024, c->kp.cap);
-    uint32_t n_kp = 0;
-    for (int attempt = 0; attempt < 3; attempt++) {
-        CHK(c->kp.ensure(cap_kp));
-        HIPCHK(hipMemsetAsync(c->counters.p + 2, 0, sizeof(uint32_t), st));
-        OrientLaunch O{};
-        O.ext = c->ext.p;
-        O.n_ext = n_ext;
-        O.gauss = p.d_gauss.p;
-        O.gauss_img_stride = p.d_gstride.p;
-        O.ow = p.d_ow.p;
-        O.oh = p.d_oh.p;
-        O.opitch = p.d_opitch.p;
-        O.out = c->kp.p;
-        O.counter = c->counters.p + 2;
-        O.img_base = 0;
-        O.cap = (uint32_t)c->kp.cap;
-        launch_orient(O, st);
-        HIPCHK(hipGetLastError());
-        HIPCHK(hipMemcpyAsync(c->h_counts.p, c->counters.p, 3 * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-        HIPCHK(hipStreamSynchronize(st));
-        n_kp = c->h_counts.p[2];
-        if (n_kp <= c->kp.cap) break;
-        cap_kp = (size_t)n_kp + n_kp / 4 + 1024;
-        if (attempt == 2) return fail(SIFT_MI_ENOMEM, "keypoint buffer overflow");
+    return 0;
+}
+
+int img_bits_for(uint32_t m) {
+    int b = 1;
+    while ((1u << b) <= m) b++;  // strictly above the largest frame index: the padding key sorts last
+    return b;
+}
+
+int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_t frame_base, const Bounds& B) {
+    Plan& p = c->plan;
+    Slot& S = c->slot[si];
+    hipStream_t st = c->stream;
+    S.m = m;
+    S.frame_base = frame_base;
+    S.cap_frames = m;
+    S.bc = B.bc;
+    S.be = B.be;
+    S.bk = B.bk;
+    uint32_t* cnt = S.counters.p;
+    uint32_t* starts = cnt + 4;
+    uint32_t* out_cnt = cnt + 4 + m;
+    uint32_t* work = cnt + 4 + 2 * m;  // [1]: descriptor work counter
+    HIPCHK(hipMemsetAsync(cnt, 0, 4 * sizeof(uint32_t), st));
+    HIPCHK(hipMemsetAsync(work, 0, 2 * sizeof(uint32_t), st));
+    HIPCHK(hipMemsetAsync(starts, 0xff, m * sizeof(uint32_t), st));
+    for (int o = 0; o < p.n_oct; o++) {
+        if (p.oh[o] < 2 * kImageBorder || p.ow[o] < 2 * kImageBorder) continue;  // src/lib.rs:315
+        DetectLaunch D{};
+        D.dog = p.dog(o);
+        D.img_stride = p.dstride(o);
+        D.W = p.ow[o];
+        D.H = p.oh[o];
+        D.pitch = p.opitch[o];
+        D.octave = o;
+        D.n_img = (int)m;
+        D.img_base = 0;
+        D.cand = c->cand.p;
+        D.counter = cnt + 0;
+        D.cap = B.bc;
+        launch_detect(D, st);
     }
-    HIPCHK(hipEventRecord(c->ev[3], st));
-    // emission order: radix sort of the keys
-    CHK(c->keys_a.ensure(n_kp));
-    CHK(c->keys_b.ensure(n_kp));
-    CHK(c->vals_a.ensure(n_kp));
-    CHK(c->vals_b.ensure(n_kp));
-    int img_bits = 1;
-    while ((1u << img_bits) < n) img_bits++;
+    RefineLaunch R{};
+    R.cand = c->cand.p;
+    R.n_cand = cnt + 0;
+    R.cand_cap = B.bc;
+    R.dog = p.d_dog.p;
+    R.dog_img_stride = p.d_dstride.p;
+    R.ow = p.d_ow.p;
+    R.oh = p.d_oh.p;
+    R.opitch = p.d_opitch.p;
+    R.img_base = 0;
+    R.out = c->ext.p;
+    R.counter = cnt + 1;
+    R.cap = B.be;
+    launch_refine(R, st);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(S.ev[2], st));
+    OrientLaunch O{};
+    O.ext = c->ext.p;
+    O.n_ext = cnt + 1;
+    O.ext_cap = B.be;
+    O.gauss = p.d_gauss.p;
+    O.gauss_img_stride = p.d_gstride.p;
+    O.ow = p.d_ow.p;
+    O.oh = p.d_oh.p;
+    O.opitch = p.d_opitch.p;
+    O.out = c->kp.p;
+    O.counter = cnt + 2;
+    O.img_base = 0;
+    O.cap = B.bk;
+    launch_orient(O, st);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(S.ev[3], st));
+    // emission order: radix sort of the keys (padding sorts last)
+    const int img_bits = img_bits_for(m);
     const int end_bit = kKeyImgShift + img_bits;
-    size_t tmp = sort_pairs_u64(nullptr, 0, c->keys_a.p, c->keys_b.p, c->vals_a.p, c->vals_b.p, n_kp, end_bit, st);
-    if (!tmp && n_kp) return fail(SIFT_MI_EHIP, "radix sort sizing failed");
-    CHK(c->sort_tmp.ensure(tmp));
-    launch_make_sort_keys(c->kp.p, n_kp, c->keys_a.p, c->vals_a.p, st);
-    if (n_kp && !sort_pairs_u64(c->sort_tmp.p, c->sort_tmp.cap, c->keys_a.p, c->keys_b.p, c->vals_a.p, c->vals_b.p,
-                                n_kp, end_bit, st))
+    const uint64_t pad = (end_bit >= 64) ? ~0ull : ((1ull << end_bit) - 1);
+    size_t tmp = sort_pairs_u64(nullptr, 0, c->keys_a.p, c->keys_b.p, c->vals_a.p, c->vals_b.p, B.bk, end_bit, st);
+    const int rb = 32 + img_bits;
+    const uint64_t rpad = (1ull << rb) - 1;
+    if (limit >= 0)
+        tmp = std::max(tmp, sort_pairs_u64(nullptr, 0, c->keys_a.p, c->keys_b.p, c->vals_a.p, c->fin.p, B.bk, rb, st));
+    if (!tmp) return fail(SIFT_MI_EHIP, "radix sort sizing failed");
+    if (tmp > c->sort_tmp.cap) {
+        HIPCHK(hipStreamSynchronize(st));
+        CHK(c->sort_tmp.ensure(tmp));
+    }
+    launch_make_sort_keys(c->kp.p, cnt + 2, B.bk, pad, c->keys_a.p, c->vals_a.p, st);
+    if (!sort_pairs_u64(c->sort_tmp.p, c->sort_tmp.cap, c->keys_a.p, c->keys_b.p, c->vals_a.p, c->vals_b.p, B.bk,
+                        end_bit, st))
         return fail(SIFT_MI_EHIP, "radix sort failed");
     const uint32_t* order = c->vals_b.p;  // emission order -> kp index
-    // per-frame counts from the frame boundaries of the sorted keys
-    uint32_t* d_starts = c->counters.p + 3;
-    HIPCHK(hipMemsetAsync(d_starts, 0xff, n * sizeof(uint32_t), st));
-    launch_frame_starts(c->keys_b.p, n_kp, d_starts, st);
-    HIPCHK(hipMemcpyAsync(c->h_counts.p + 3, d_starts, n * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    HIPCHK(hipStreamSynchronize(st));
-    std::vector<uint32_t> cnt(n, 0);
-    {
-        uint32_t next = n_kp;
-        for (int f = (int)n - 1; f >= 0; f--) {
-            const uint32_t s0 = c->h_counts.p[3 + f];
-            if (s0 != 0xffffffffu) {
-                cnt[f] = next - s0;
-                next = s0;
-            }
-        }
-    }
-    // features_limit (src/lib.rs:156-161)
-    std::vector<uint32_t> out_cnt(cnt);
-    bool any_limit = false;
-    if (limit >= 0)
-        for (uint32_t f = 0; f < n; f++)
-            if ((uint64_t)limit < cnt[f]) {
-                out_cnt[f] = (uint32_t)limit;
-                any_limit = true;
-            }
-    uint32_t n_out = 0;
-    for (uint32_t f = 0; f < n; f++) n_out += out_cnt[f];
-    if (any_limit) {
-        std::vector<uint32_t> seg(n), oo(n);
-        std::vector<uint8_t> ur(n);
-        uint32_t a = 0, b = 0;
-        for (uint32_t f = 0; f < n; f++) {
-            seg[f] = a;
-            oo[f] = b;
-            ur[f] = (uint64_t)limit < cnt[f];
-            a += cnt[f];
-            b += out_cnt[f];
-        }
-        launch_make_resp_keys(c->kp.p, order, n_kp, 0, c->keys_a.p, c->vals_a.p, st);
-        const int rb = 32 + img_bits;
-        size_t tmp2 = sort_pairs_u64(nullptr, 0, c->keys_a.p, c->keys_b.p, c->vals_a.p, c->fin.p, n_kp, rb, st);
-        CHK(c->sort_tmp.ensure(tmp2));
-        CHK(c->fin.ensure(n_kp));
+    launch_frame_starts(c->keys_b.p, cnt + 2, B.bk, starts, st);
+    // features_limit (src/lib.rs:156-161): per-frame plan on the device
+    launch_limit_plan(starts, cnt + 2, B.bk, (int)m, limit, out_cnt, c->seg_off.p, c->out_off.p, c->use_resp.p,
+                      cnt + 3, st);
+    if (limit >= 0) {
         // stable sort: response-descending within each frame, emission order on ties
-        CHK(c->vals_a.ensure(n_kp));
-        DevBuf<uint32_t>& resp_order = c->fin;
-        if (!sort_pairs_u64(c->sort_tmp.p, c->sort_tmp.cap, c->keys_a.p, c->keys_b.p, c->vals_a.p, resp_order.p, n_kp,
-                            rb, st))
+        launch_make_resp_keys(c->kp.p, order, cnt + 2, B.bk, 0, rpad, c->keys_a.p, c->vals_a.p, st);
+        if (!sort_pairs_u64(c->sort_tmp.p, c->sort_tmp.cap, c->keys_a.p, c->keys_b.p, c->vals_a.p, c->fin.p, B.bk, rb,
+                            st))
             return fail(SIFT_MI_EHIP, "response sort failed");
-        CHK(c->seg_off.ensure(n));
-        CHK(c->out_off.ensure(n));
-        CHK(c->use_resp.ensure(n));
-        HIPCHK(hipMemcpyAsync(c->seg_off.p, seg.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemcpyAsync(c->out_off.p, oo.data(), n * sizeof(uint32_t), hipMemcpyHostToDevice, st));
-        HIPCHK(hipMemcpyAsync(c->use_resp.p, ur.data(), n, hipMemcpyHostToDevice, st));
-        // final index list -> keys_b reused as u32 storage is unsafe; use vals_a
-        launch_select(order, resp_order.p, c->seg_off.p, c->out_off.p, c->use_resp.p, (int)n, n_out, c->vals_a.p, st);
+        launch_select(order, c->fin.p, c->seg_off.p, c->out_off.p, c->use_resp.p, (int)m, cnt + 3, B.bk, c->vals_a.p,
+                      st);
         order = c->vals_a.p;
-        HIPCHK(hipStreamSynchronize(st));  // seg/oo/ur host vectors
     }
-    HIPCHK(hipEventRecord(c->ev[4], st));
-    // descriptors
-    CHK(c->out_kp.ensure(n_out));
-    CHK(c->out_desc.ensure((size_t)n_out * kDescSize));
-    CHK(c->out_key.ensure(n_out));
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(S.ev[4], st));
+    // descriptors into this slot's outputs, once its previous copy-out is done
+    if (S.pending_copy) HIPCHK(hipStreamWaitEvent(st, S.copied, 0));
     DescLaunch DL{};
     DL.kp = c->kp.p;
     DL.idx = order;
-    DL.n = n_out;
+    DL.n = cnt + 3;
+    DL.bound = B.bk;
+    DL.work = work + 1;
+    DL.key_base = (uint64_t)frame_base << kKeyImgShift;
     DL.gauss = p.d_gauss.p;
     DL.gauss_img_stride = p.d_gstride.p;
     DL.ow = p.d_ow.p;
     DL.oh = p.d_oh.p;
     DL.opitch = p.d_opitch.p;
     DL.img_base = 0;
-    DL.out_kp = c->out_kp.p;
-    DL.out_key = c->out_key.p;
-    DL.out_desc = c->out_desc.p;
+    DL.out_kp = S.out_kp.p;
+    DL.out_key = S.out_key.p;
+    DL.out_desc = S.out_desc.p;
     DL.exact = c->exact_descriptors;
     launch_describe(DL, st);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(c->ev[5], st));
-    c->dev_result_n = n_out;
-    if (!c->keep_on_device) {
-        const size_t need = result_base + n_out;
-        CHK(c->h_kp.ensure(need, true));
-        CHK(c->h_desc.ensure(need * kDescSize, true));
-        CHK(c->h_key.ensure(need, true));
-        if (n_out) {
-            HIPCHK(hipMemcpyAsync(c->h_kp.p + result_base, c->out_kp.p, n_out * sizeof(OutKp), hipMemcpyDeviceToHost,
-                                  st));
-            HIPCHK(hipMemcpyAsync(c->h_desc.p + result_base * kDescSize, c->out_desc.p, (size_t)n_out * kDescSize,
-                                  hipMemcpyDeviceToHost, st));
-            HIPCHK(hipMemcpyAsync(c->h_key.p + result_base, c->out_key.p, n_out * sizeof(uint64_t),
-                                  hipMemcpyDeviceToHost, st));
-        }
-    }
-    HIPCHK(hipEventRecord(c->ev[6], st));
-    HIPCHK(hipStreamSynchronize(st));
-    if (!c->keep_on_device)
-        for (size_t i = 0; i < n_out; i++) c->h_key.p[result_base + i] += (uint64_t)frame_base << kKeyImgShift;
-    if (offsets_out) {
-        size_t acc = result_base;
-        for (uint32_t f = 0; f < n; f++) {
-            offsets_out[f] = acc;
-            acc += out_cnt[f];
-        }
-        offsets_out[n] = acc;
-    }
-    c->stats.extrema += n_ext;
-    c->stats.keypoints += n_out;
+    HIPCHK(hipEventRecord(S.ev[5], st));
+    HIPCHK(hipMemcpyAsync(S.h_counts.p, cnt, (4 + 2 * m) * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    HIPCHK(hipEventRecord(S.ev[6], st));
     return 0;
 }
 
-void accumulate_times(sift_mi_ctx* c) {
+void accumulate_times(sift_mi_ctx* c, Slot& S) {
     float ms;
-    if (hipEventElapsedTime(&ms, c->ev[0], c->ev[1]) == hipSuccess) c->stats.pyramid_ms += ms;
-    if (hipEventElapsedTime(&ms, c->ev[1], c->ev[2]) == hipSuccess) c->stats.detect_ms += ms;
-    if (hipEventElapsedTime(&ms, c->ev[2], c->ev[3]) == hipSuccess) c->stats.orient_ms += ms;
-    if (hipEventElapsedTime(&ms, c->ev[3], c->ev[4]) == hipSuccess) c->stats.order_ms += ms;
-    if (hipEventElapsedTime(&ms, c->ev[4], c->ev[5]) == hipSuccess) c->stats.descriptor_ms += ms;
-    if (hipEventElapsedTime(&ms, c->ev[0], c->ev[6]) == hipSuccess) c->stats.total_ms += ms;
+    if (hipEventElapsedTime(&ms, S.ev[0], S.ev[1]) == hipSuccess) c->stats.pyramid_ms += ms;
+    if (hipEventElapsedTime(&ms, S.ev[1], S.ev[2]) == hipSuccess) c->stats.detect_ms += ms;
+    if (hipEventElapsedTime(&ms, S.ev[2], S.ev[3]) == hipSuccess) c->stats.orient_ms += ms;
+    if (hipEventElapsedTime(&ms, S.ev[3], S.ev[4]) == hipSuccess) c->stats.order_ms += ms;
+    if (hipEventElapsedTime(&ms, S.ev[4], S.ev[5]) == hipSuccess) c->stats.descriptor_ms += ms;
+    if (hipEventElapsedTime(&ms, S.ev[0], S.ev[6]) == hipSuccess) c->stats.total_ms += ms;
+}
+
+// Enqueue pyramid (optional) + keypoint stages of one chunk on slot si.
+int enqueue_chunk(sift_mi_ctx* c, int si, const uint8_t* d_frames, size_t frame_pitch, size_t stride, uint32_t m,
+                  int64_t limit, uint32_t frame_base, bool pyramid) {
+    Slot& S = c->slot[si];
+    const Bounds B = chunk_bounds(c, m);
+    CHK(reserve_chunk(c, B, c->plan.chunk));
+    HIPCHK(hipEventRecord(S.ev[0], c->stream));
+    if (pyramid) CHK(run_pyramid(c, d_frames, frame_pitch, stride, m));
+    HIPCHK(hipEventRecord(S.ev[1], c->stream));
+    return enqueue_keypoints(c, si, m, limit, frame_base, B);
+}
+
+// Wait for slot si's chunk; on success append its per-frame offsets and start
+// the copy of its results to the host.  Returns 1 when a stage count exceeded
+// its bound (the caller re-runs the chunk; the high-water marks now cover it).
+int finalize_chunk(sift_mi_ctx* c, int si, size_t* offsets) {
+    Slot& S = c->slot[si];
+    HIPCHK(hipEventSynchronize(S.ev[6]));
+    const uint32_t* h = S.h_counts.p;
+    const uint32_t m = S.m;
+    const double fm = (double)m;
+    c->pf_cand = std::max(c->pf_cand, h[0] / fm);
+    c->pf_ext = std::max(c->pf_ext, h[1] / fm);
+    c->pf_kp = std::max(c->pf_kp, h[2] / fm);
+    if (h[0] > S.bc || h[1] > S.be || h[2] > S.bk) return 1;
+    const uint32_t n_out = h[3];
+    accumulate_times(c, S);
+    const size_t base = c->n_result;
+    if (offsets) {
+        size_t acc = base;
+        for (uint32_t f = 0; f < m; f++) {
+            offsets[S.frame_base + f] = acc;
+            acc += h[4 + m + f];
+        }
+    }
+    c->dev_result_n = n_out;
+    c->last_slot = si;
+    if (!c->keep_on_device) {
+        const size_t need = base + n_out;
+        if (need > c->h_kp.cap || need * kDescSize > c->h_desc.cap || need > c->h_key.cap) {
+            HIPCHK(hipStreamSynchronize(c->cstream));  // copies in flight into the old buffers
+            CHK(c->h_kp.ensure(need, true));
+            CHK(c->h_desc.ensure(need * kDescSize, true));
+            CHK(c->h_key.ensure(need, true));
+        }
+        if (n_out) {
+            HIPCHK(hipStreamWaitEvent(c->cstream, S.ev[6], 0));
+            HIPCHK(hipMemcpyAsync(c->h_kp.p + base, S.out_kp.p, n_out * sizeof(OutKp), hipMemcpyDeviceToHost,
+                                  c->cstream));
+            HIPCHK(hipMemcpyAsync(c->h_desc.p + base * kDescSize, S.out_desc.p, (size_t)n_out * kDescSize,
+                                  hipMemcpyDeviceToHost, c->cstream));
+            HIPCHK(hipMemcpyAsync(c->h_key.p + base, S.out_key.p, n_out * sizeof(uint64_t), hipMemcpyDeviceToHost,
+                                  c->cstream));
+            HIPCHK(hipEventRecord(S.copied, c->cstream));
+            S.pending_copy = true;
+        }
+    }
+    c->n_result = base + n_out;
+    c->stats.extrema += h[1];
+    c->stats.keypoints += n_out;
+    c->stats.frames += m;
+    return 0;
+}
+
+// Single chunk, synchronous (precompute / sift_with_precomputed paths).
+int run_chunk_sync(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, size_t stride, uint32_t m,
+                   int64_t limit, bool pyramid, size_t* offsets) {
+    c->n_result = 0;
+    for (int attempt = 0; attempt < 4; attempt++) {
+        CHK(enqueue_chunk(c, 0, d_frames, frame_pitch, stride, m, limit, 0, pyramid));
+        const int rc = finalize_chunk(c, 0, offsets);
+        if (rc < 0) return rc;
+        if (rc == 0) {
+            if (offsets) offsets[m] = c->n_result;
+            HIPCHK(hipStreamSynchronize(c->cstream));
+            return 0;
+        }
+    }
+    return fail(SIFT_MI_ENOMEM, "stage count kept exceeding its buffer bound");
 }
 
 int check_frame_args(uint32_t w, uint32_t h, size_t stride) {
@@ -709,30 +780,43 @@ int check_frame_args(uint32_t w, uint32_t h, size_t stride) {
     return 0;
 }
 
-// Device-resident batch pipeline.
+// Device-resident batch pipeline: chunks alternate between the two slots;
+// chunk k+1 is enqueued before the host waits for chunk k, so the GPU never
+// idles on host round trips, and chunk k's results travel to the host on the
+// copy stream while chunk k+1 computes.
 int extract_device(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, uint32_t n, uint32_t w, uint32_t h,
                    size_t stride, int64_t limit, size_t* offsets) {
     CHK(check_frame_args(w, h, stride));
     if (c->profile != SIFT_MI_PROFILE_OPENCV)
         return fail(SIFT_MI_EUNSUPPORTED, "IMAGEPROC profile not implemented (parity unpinned)");
-    const uint32_t chunk = c->chunk_override ? std::min(c->chunk_override, n) : auto_chunk(c->plan, w, h, n);
+    const uint32_t chunk =
+        std::min(kMaxChunk, c->chunk_override ? std::min(c->chunk_override, n) : auto_chunk(c->plan, w, h, n));
     CHK(ensure_plan(c, w, h, chunk));
     c->have_pyramid = false;
     c->n_result = 0;
     c->have_result = false;
-    std::vector<size_t> offs(chunk + 1);
-    for (uint32_t f0 = 0; f0 < n; f0 += chunk) {
-        const uint32_t m = std::min(chunk, n - f0);
-        HIPCHK(hipEventRecord(c->ev[0], c->stream));
-        CHK(run_pyramid(c, d_frames + (size_t)f0 * frame_pitch, frame_pitch, stride, m));
-        HIPCHK(hipEventRecord(c->ev[1], c->stream));
-        CHK(run_keypoints(c, m, limit, f0, offs.data(), c->n_result));
-        accumulate_times(c);
-        if (offsets)
-            for (uint32_t f = 0; f < m; f++) offsets[f0 + f] = offs[f];
-        c->n_result = offs[m];
-        c->stats.frames += m;
+    const uint32_t n_chunks = (n + chunk - 1) / chunk;
+    auto frames_of = [&](uint32_t k) { return std::min(chunk, n - k * chunk); };
+    auto enqueue = [&](uint32_t k) {
+        return enqueue_chunk(c, (int)(k & 1), d_frames + (size_t)k * chunk * frame_pitch, frame_pitch, stride,
+                             frames_of(k), limit, k * chunk, true);
+    };
+    CHK(enqueue(0));
+    for (uint32_t k = 0; k < n_chunks; k++) {
+        if (k + 1 < n_chunks) CHK(enqueue(k + 1));
+        int rc = finalize_chunk(c, (int)(k & 1), offsets);
+        if (rc < 0) return rc;
+        for (int attempt = 0; rc == 1; attempt++) {
+            // a stage overflowed its bound: drain (the already enqueued chunk
+            // k+1 completes first, its results are unaffected), then re-run k
+            if (attempt == 3) return fail(SIFT_MI_ENOMEM, "stage count kept exceeding its buffer bound");
+            HIPCHK(hipStreamSynchronize(c->stream));
+            CHK(enqueue(k));
+            rc = finalize_chunk(c, (int)(k & 1), offsets);
+            if (rc < 0) return rc;
+        }
     }
+    HIPCHK(hipStreamSynchronize(c->cstream));
     if (offsets) offsets[n] = c->n_result;
     c->have_result = true;
     return 0;
@@ -780,11 +864,15 @@ int sift_mi_create(int device_ordinal, sift_mi_profile profile, sift_mi_ctx** ou
         return fail(SIFT_MI_EHIP, "hipStreamCreate failed");
     }
     c->stream = c->own;
-    for (auto& e : c->ev)
-        if (hipEventCreate(&e) != hipSuccess) {
-            delete c;
-            return fail(SIFT_MI_EHIP, "hipEventCreate failed");
-        }
+    bool ok = hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking) == hipSuccess;
+    for (auto& S : c->slot) {
+        for (auto& e : S.ev) ok = ok && hipEventCreate(&e) == hipSuccess;
+        ok = ok && hipEventCreateWithFlags(&S.copied, hipEventDisableTiming) == hipSuccess;
+    }
+    if (!ok) {
+        sift_mi_destroy(c);
+        return fail(SIFT_MI_EHIP, "stream / event creation failed");
+    }
     *out = c;
     return 0;
 }
@@ -792,13 +880,13 @@ int sift_mi_create(int device_ordinal, sift_mi_profile profile, sift_mi_ctx** ou
 void sift_mi_destroy(sift_mi_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    (void)hipStreamSynchronize(c->stream);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->cstream) (void)hipStreamSynchronize(c->cstream);
     c->plan.release();
     c->staging.release();
     c->cand.release();
     c->ext.release();
     c->kp.release();
-    c->counters.release();
     c->keys_a.release();
     c->keys_b.release();
     c->vals_a.release();
@@ -808,15 +896,20 @@ void sift_mi_destroy(sift_mi_ctx* c) {
     c->seg_off.release();
     c->out_off.release();
     c->use_resp.release();
-    c->out_kp.release();
-    c->out_desc.release();
-    c->out_key.release();
+    for (auto& S : c->slot) {
+        S.counters.release();
+        S.h_counts.release();
+        S.out_kp.release();
+        S.out_desc.release();
+        S.out_key.release();
+        for (auto& e : S.ev)
+            if (e) (void)hipEventDestroy(e);
+        if (S.copied) (void)hipEventDestroy(S.copied);
+    }
     c->h_kp.release();
     c->h_desc.release();
     c->h_key.release();
-    c->h_counts.release();
-    for (auto& e : c->ev)
-        if (e) (void)hipEventDestroy(e);
+    if (c->cstream) (void)hipStreamDestroy(c->cstream);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
 }
@@ -876,13 +969,41 @@ int sift_mi_extract(sift_mi_ctx* c, const uint8_t* pixels, uint32_t w, uint32_t 
     return 0;
 }
 
+}  // extern "C"
+
+namespace {
+// Host copy of large results: split across threads (the copy is bound by
+// page faults on freshly allocated destinations as much as by bandwidth).
+void par_memcpy(void* dst, const void* src, size_t bytes) {
+    constexpr size_t kPerThread = 4u << 20;
+    const unsigned hw = std::max(1u, std::min(8u, std::thread::hardware_concurrency()));
+    const unsigned nt = (unsigned)std::min<size_t>(hw, bytes / kPerThread);
+    if (nt <= 1) {
+        std::memcpy(dst, src, bytes);
+        return;
+    }
+    const size_t part = (bytes / nt + 4095) & ~(size_t)4095;
+    std::vector<std::thread> th;
+    for (unsigned t = 1; t < nt; t++) {
+        const size_t a = t * part;
+        if (a >= bytes) break;
+        const size_t b = std::min(bytes, a + part);
+        th.emplace_back([=] { std::memcpy((char*)dst + a, (const char*)src + a, b - a); });
+    }
+    std::memcpy(dst, src, std::min(bytes, part));
+    for (auto& x : th) x.join();
+}
+}  // namespace
+
+extern "C" {
+
 int sift_mi_fetch(sift_mi_ctx* c, sift_mi_keypoint* kps, uint8_t* desc, size_t cap) {
     if (!c) return fail(SIFT_MI_EINVAL, "ctx is null");
     if (!c->have_result || c->keep_on_device) return fail(SIFT_MI_ESTATE, "no host result to fetch");
     if (cap < c->n_result) return fail(SIFT_MI_EINVAL, "cap < result size");
     static_assert(sizeof(sift_mi_keypoint) == sizeof(OutKp), "layout");
-    if (kps && c->n_result) std::memcpy(kps, c->h_kp.p, c->n_result * sizeof(OutKp));
-    if (desc && c->n_result) std::memcpy(desc, c->h_desc.p, c->n_result * kDescSize);
+    if (kps && c->n_result) par_memcpy(kps, c->h_kp.p, c->n_result * sizeof(OutKp));
+    if (desc && c->n_result) par_memcpy(desc, c->h_desc.p, c->n_result * kDescSize);
     return 0;
 }
 
@@ -890,15 +1011,16 @@ int sift_mi_fetch_keys(sift_mi_ctx* c, uint64_t* keys, size_t cap) {
     if (!c || !keys) return fail(SIFT_MI_EINVAL, "bad arguments");
     if (!c->have_result || c->keep_on_device) return fail(SIFT_MI_ESTATE, "no host result to fetch");
     if (cap < c->n_result) return fail(SIFT_MI_EINVAL, "cap < result size");
-    if (c->n_result) std::memcpy(keys, c->h_key.p, c->n_result * sizeof(uint64_t));
+    if (c->n_result) par_memcpy(keys, c->h_key.p, c->n_result * sizeof(uint64_t));
     return 0;
 }
 
 int sift_mi_device_results(sift_mi_ctx* c, const sift_mi_keypoint** d_kps, const uint8_t** d_desc, size_t* n) {
     if (!c) return fail(SIFT_MI_EINVAL, "ctx is null");
     if (!c->have_result) return fail(SIFT_MI_ESTATE, "no result");
-    if (d_kps) *d_kps = reinterpret_cast<const sift_mi_keypoint*>(c->out_kp.p);
-    if (d_desc) *d_desc = c->out_desc.p;
+    const Slot& S = c->slot[c->last_slot];
+    if (d_kps) *d_kps = reinterpret_cast<const sift_mi_keypoint*>(S.out_kp.p);
+    if (d_desc) *d_desc = S.out_desc.p;
     if (n) *n = c->dev_result_n;
     return 0;
 }
@@ -913,9 +1035,7 @@ int sift_mi_precompute(sift_mi_ctx* c, const uint8_t* pixels, uint32_t w, uint32
     const uint8_t* frames[1] = {pixels};
     CHK(upload_frames(c, frames, 1, w, h, stride));
     CHK(ensure_plan(c, w, h, 1));
-    HIPCHK(hipEventRecord(c->ev[0], c->stream));
     CHK(run_pyramid(c, c->staging.p, (size_t)w * h, w, 1));
-    HIPCHK(hipEventRecord(c->ev[1], c->stream));
     HIPCHK(hipStreamSynchronize(c->stream));
     c->have_pyramid = true;
     c->have_result = false;
@@ -957,13 +1077,9 @@ int sift_mi_sift_with_precomputed(sift_mi_ctx* c, int64_t limit, size_t* n_keypo
     const int keep = c->keep_on_device;
     c->keep_on_device = 0;
     size_t offs[2];
-    HIPCHK(hipEventRecord(c->ev[0], c->stream));
-    HIPCHK(hipEventRecord(c->ev[1], c->stream));
-    const int rc = run_keypoints(c, 1, limit, 0, offs, 0);
+    const int rc = run_chunk_sync(c, nullptr, 0, 0, 1, limit, false, offs);
     c->keep_on_device = keep;
     CHK(rc);
-    accumulate_times(c);
-    c->n_result = offs[1];
     c->have_result = true;
     if (n_keypoints) *n_keypoints = offs[1];
     return 0;

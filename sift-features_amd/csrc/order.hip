@@ -22,52 +22,108 @@ size_t sort_pairs_u64(void* temp, size_t temp_bytes, const uint64_t* kin, uint64
     return bytes;
 }
 
-__global__ void k_make_sort_keys(const KpRec* __restrict__ kp, uint32_t n, uint64_t* __restrict__ keys,
-                                 uint32_t* __restrict__ vals) {
+__global__ void k_make_sort_keys(const KpRec* __restrict__ kp, const uint32_t* __restrict__ n_dev, uint32_t bound,
+                                 uint64_t pad, uint64_t* __restrict__ keys, uint32_t* __restrict__ vals) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
-    keys[i] = kp[i].key;
+    if (i >= bound) return;
+    const uint32_t n = min(*n_dev, bound);
+    keys[i] = i < n ? kp[i].key : pad;
     vals[i] = i;
 }
 
-void launch_make_sort_keys(const KpRec* kp, uint32_t n, uint64_t* keys, uint32_t* vals, hipStream_t st) {
-    if (!n) return;
-    hipLaunchKernelGGL(k_make_sort_keys, dim3((n + 255) / 256), dim3(256), 0, st, kp, n, keys, vals);
+void launch_make_sort_keys(const KpRec* kp, const uint32_t* n, uint32_t bound, uint64_t pad, uint64_t* keys,
+                           uint32_t* vals, hipStream_t st) {
+    if (!bound) return;
+    hipLaunchKernelGGL(k_make_sort_keys, dim3((bound + 255) / 256), dim3(256), 0, st, kp, n, bound, pad, keys, vals);
 }
 
-__global__ void k_frame_starts(const uint64_t* __restrict__ keys, uint32_t n, uint32_t* __restrict__ starts) {
+__global__ void k_frame_starts(const uint64_t* __restrict__ keys, const uint32_t* __restrict__ n_dev, uint32_t bound,
+                               uint32_t* __restrict__ starts) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t n = min(*n_dev, bound);
     if (i >= n) return;
     const uint32_t f = (uint32_t)(keys[i] >> kKeyImgShift);
     if (i == 0 || (uint32_t)(keys[i - 1] >> kKeyImgShift) != f) starts[f] = i;
 }
 
-void launch_frame_starts(const uint64_t* sorted_keys, uint32_t n, uint32_t* starts, hipStream_t st) {
-    if (!n) return;
-    hipLaunchKernelGGL(k_frame_starts, dim3((n + 255) / 256), dim3(256), 0, st, sorted_keys, n, starts);
+void launch_frame_starts(const uint64_t* sorted_keys, const uint32_t* n, uint32_t bound, uint32_t* starts,
+                         hipStream_t st) {
+    if (!bound) return;
+    hipLaunchKernelGGL(k_frame_starts, dim3((bound + 255) / 256), dim3(256), 0, st, sorted_keys, n, bound, starts);
+}
+
+// One wave; frame f = lane (n_img <= 64).  cnt[f] = next non-empty start - start[f].
+__global__ void k_limit_plan(const uint32_t* __restrict__ starts, const uint32_t* __restrict__ n_kp, uint32_t bound,
+                             int n_img, int64_t limit, uint32_t* __restrict__ out_cnt, uint32_t* __restrict__ seg_off,
+                             uint32_t* __restrict__ out_off, uint8_t* __restrict__ use_resp,
+                             uint32_t* __restrict__ n_out) {
+    const int f = threadIdx.x;
+    const uint32_t n = min(*n_kp, bound);
+    const uint32_t s = f < n_img ? starts[f] : 0xffffffffu;
+    // end of frame f: the smallest start among later frames (suffix min), else n
+    uint32_t nxt = 0xffffffffu;
+    for (int g = n_img - 1; g > f; g--) nxt = min(nxt, starts[g]);
+    const uint32_t end = nxt == 0xffffffffu ? n : nxt;
+    const uint32_t cnt = s == 0xffffffffu ? 0u : end - s;
+    const bool trunc = limit >= 0 && (uint64_t)limit < cnt;
+    const uint32_t oc = trunc ? (uint32_t)limit : cnt;
+    // exclusive prefix sums over the wave (frames are in sorted order)
+    uint32_t seg = cnt, out = oc;
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const uint32_t a = __shfl_up(seg, o), b = __shfl_up(out, o);
+        if (f >= o) {
+            seg += a;
+            out += b;
+        }
+    }
+    if (f < n_img) {
+        out_cnt[f] = oc;
+        seg_off[f] = seg - cnt;
+        out_off[f] = out - oc;
+        use_resp[f] = trunc ? 1 : 0;
+    }
+    if (f == 63) *n_out = out;
+}
+
+void launch_limit_plan(const uint32_t* starts, const uint32_t* n_kp, uint32_t bound, int n_img, int64_t limit,
+                       uint32_t* out_cnt, uint32_t* seg_off, uint32_t* out_off, uint8_t* use_resp, uint32_t* n_out,
+                       hipStream_t st) {
+    hipLaunchKernelGGL(k_limit_plan, dim3(1), dim3(64), 0, st, starts, n_kp, bound, n_img, limit, out_cnt, seg_off,
+                       out_off, use_resp, n_out);
 }
 
 // key = (frame << 32) | ~bits(response)  (response >= 0, so bit order == value order)
-__global__ void k_make_resp_keys(const KpRec* __restrict__ kp, const uint32_t* __restrict__ order, uint32_t n,
-                                 int img_base, uint64_t* __restrict__ keys, uint32_t* __restrict__ vals) {
+__global__ void k_make_resp_keys(const KpRec* __restrict__ kp, const uint32_t* __restrict__ order,
+                                 const uint32_t* __restrict__ n_dev, uint32_t bound, int img_base, uint64_t pad,
+                                 uint64_t* __restrict__ keys, uint32_t* __restrict__ vals) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
-    if (i >= n) return;
+    if (i >= bound) return;
+    const uint32_t n = min(*n_dev, bound);
+    if (i >= n) {
+        keys[i] = pad;
+        vals[i] = 0;
+        return;
+    }
     const KpRec k = kp[order[i]];
     const uint32_t bits = __float_as_uint(k.response);
     keys[i] = ((uint64_t)(uint32_t)(k.img - img_base) << 32) | (uint64_t)(~bits);
     vals[i] = order[i];
 }
 
-void launch_make_resp_keys(const KpRec* kp, const uint32_t* order, uint32_t n, int img_base, uint64_t* keys,
-                           uint32_t* vals, hipStream_t st) {
-    if (!n) return;
-    hipLaunchKernelGGL(k_make_resp_keys, dim3((n + 255) / 256), dim3(256), 0, st, kp, order, n, img_base, keys, vals);
+void launch_make_resp_keys(const KpRec* kp, const uint32_t* order, const uint32_t* n, uint32_t bound, int img_base,
+                           uint64_t pad, uint64_t* keys, uint32_t* vals, hipStream_t st) {
+    if (!bound) return;
+    hipLaunchKernelGGL(k_make_resp_keys, dim3((bound + 255) / 256), dim3(256), 0, st, kp, order, n, bound, img_base,
+                       pad, keys, vals);
 }
 
 __global__ void k_select(const uint32_t* __restrict__ emis, const uint32_t* __restrict__ resp,
                          const uint32_t* __restrict__ seg_off, const uint32_t* __restrict__ out_off,
-                         const uint8_t* __restrict__ use_resp, int n_img, uint32_t n_out, uint32_t* __restrict__ fin) {
+                         const uint8_t* __restrict__ use_resp, int n_img, const uint32_t* __restrict__ n_out_dev,
+                         uint32_t bound, uint32_t* __restrict__ fin) {
     const uint32_t i = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t n_out = min(*n_out_dev, bound);
     if (i >= n_out) return;
     int lo = 0, hi = n_img - 1;  // frame f with out_off[f] <= i < out_off[f+1]
     while (lo < hi) {
@@ -82,11 +138,11 @@ __global__ void k_select(const uint32_t* __restrict__ emis, const uint32_t* __re
 }
 
 void launch_select(const uint32_t* emis_order, const uint32_t* resp_order, const uint32_t* seg_off,
-                   const uint32_t* out_off, const uint8_t* use_resp, int n_img, uint32_t n_out, uint32_t* final_idx,
-                   hipStream_t st) {
-    if (!n_out) return;
-    hipLaunchKernelGGL(k_select, dim3((n_out + 255) / 256), dim3(256), 0, st, emis_order, resp_order, seg_off, out_off,
-                       use_resp, n_img, n_out, final_idx);
+                   const uint32_t* out_off, const uint8_t* use_resp, int n_img, const uint32_t* n_out, uint32_t bound,
+                   uint32_t* final_idx, hipStream_t st) {
+    if (!bound) return;
+    hipLaunchKernelGGL(k_select, dim3((bound + 255) / 256), dim3(256), 0, st, emis_order, resp_order, seg_off, out_off,
+                       use_resp, n_img, n_out, bound, final_idx);
 }
 
 }  // namespace siftmi

@@ -67,9 +67,13 @@ struct DetectLaunch {
 };
 void launch_detect(const DetectLaunch& L, hipStream_t st);
 
+// Stage sizes live in device counters (no host round trip between stages):
+// every consumer reads its count from device memory, clamps it to the buffer
+// bound, and walks the items with a grid-stride loop.
 struct RefineLaunch {
     const uint64_t* cand;
-    uint32_t n_cand;
+    const uint32_t* n_cand;  // device count (may exceed cand_cap: overflow, clamped)
+    uint32_t cand_cap;
     const float* const* dog;       // device array [n_octaves] of octave D bases
     const size_t* dog_img_stride;  // device array [n_octaves]
     const int* ow;
@@ -84,7 +88,8 @@ void launch_refine(const RefineLaunch& L, hipStream_t st);
 
 struct OrientLaunch {
     const ExtRec* ext;
-    uint32_t n_ext;
+    const uint32_t* n_ext;  // device count, clamped to ext_cap
+    uint32_t ext_cap;
     const float* const* gauss;     // device array [n_octaves] of octave G bases
     const size_t* gauss_img_stride;  // device array [n_octaves]
     const int* ow;                 // device arrays [n_octaves]
@@ -101,22 +106,37 @@ void launch_orient(const OrientLaunch& L, hipStream_t st);
 // keys/vals for the emission-order sort; returns temp bytes when temp == null.
 size_t sort_pairs_u64(void* temp, size_t temp_bytes, const uint64_t* kin, uint64_t* kout, const uint32_t* vin,
                       uint32_t* vout, uint32_t n, int end_bit, hipStream_t st);
-void launch_make_sort_keys(const KpRec* kp, uint32_t n, uint64_t* keys, uint32_t* vals, hipStream_t st);
+// keys[i] = emission key of kp i for i < min(*n, bound); keys beyond are
+// padded with `pad` (sorts last); vals[i] = i
+void launch_make_sort_keys(const KpRec* kp, const uint32_t* n, uint32_t bound, uint64_t pad, uint64_t* keys,
+                           uint32_t* vals, hipStream_t st);
 // starts[f] = first index of frame f in the sorted keys (0xffffffff if none);
 // starts must be pre-filled with 0xff bytes
-void launch_frame_starts(const uint64_t* sorted_keys, uint32_t n, uint32_t* starts, hipStream_t st);
-void launch_make_resp_keys(const KpRec* kp, const uint32_t* order, uint32_t n, int img_base, uint64_t* keys,
-                           uint32_t* vals, hipStream_t st);
-// final[i] = src index: for frame f, if take_resp[f] final = resp_order[seg], else emission order
+void launch_frame_starts(const uint64_t* sorted_keys, const uint32_t* n, uint32_t bound, uint32_t* starts,
+                         hipStream_t st);
+// Per-frame output plan (features_limit, src/lib.rs:156-161), one wave:
+// out_cnt[f], seg_off[f] (first sorted index of frame f), out_off[f] (first
+// output index), use_resp[f] (frame truncated by response) and *n_out.
+void launch_limit_plan(const uint32_t* starts, const uint32_t* n_kp, uint32_t bound, int n_img, int64_t limit,
+                       uint32_t* out_cnt, uint32_t* seg_off, uint32_t* out_off, uint8_t* use_resp, uint32_t* n_out,
+                       hipStream_t st);
+// key = (frame << 32) | ~bits(response) over the emission order; padded beyond *n
+void launch_make_resp_keys(const KpRec* kp, const uint32_t* order, const uint32_t* n, uint32_t bound, int img_base,
+                           uint64_t pad, uint64_t* keys, uint32_t* vals, hipStream_t st);
+// final[i] = src index for i < *n_out: for frame f, if use_resp[f] the
+// response order, else the emission order
 void launch_select(const uint32_t* emis_order, const uint32_t* resp_order, const uint32_t* seg_off,
-                   const uint32_t* out_off, const uint8_t* use_resp, int n_img, uint32_t n_out, uint32_t* final_idx,
-                   hipStream_t st);
+                   const uint32_t* out_off, const uint8_t* use_resp, int n_img, const uint32_t* n_out, uint32_t bound,
+                   uint32_t* final_idx, hipStream_t st);
 
 // describe.hip
 struct DescLaunch {
     const KpRec* kp;
     const uint32_t* idx;  // final order -> kp index (may be null = identity)
-    uint32_t n;
+    const uint32_t* n;    // device count, clamped to bound
+    uint32_t bound;
+    uint32_t* work;       // zeroed work counter: waves take keypoints dynamically (costs vary ~20x)
+    uint64_t key_base;    // added to the emission keys (frame offset of the chunk)
     const float* const* gauss;
     const size_t* gauss_img_stride;
     const int* ow;

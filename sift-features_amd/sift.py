@@ -70,6 +70,24 @@ class SiftResult:
         return f"SiftResult(n={len(self)})"
 
 
+class ResultBuffers:
+    """Reusable host arrays for batch results (streaming callers: avoids a
+    fresh allocation -- and its page faults -- per batch).  Grows on demand."""
+
+    def __init__(self, capacity=0):
+        self._alloc(capacity)
+
+    def _alloc(self, n):
+        self.kps = np.empty((n, 5), np.float32)
+        self.desc = np.empty((n, DESCRIPTOR_SIZE), np.uint8)
+        self.keys = np.empty(n, np.uint64)
+
+    def views(self, n):
+        if n > len(self.kps):
+            self._alloc(max(n, 2 * len(self.kps)))
+        return self.kps[:n], self.desc[:n], self.keys[:n]
+
+
 def _u8_image(img):
     a = np.asarray(img)
     if a.dtype != np.uint8 or a.ndim != 2:
@@ -138,14 +156,18 @@ class Context:
         check(lib().sift_mi_reset_stats(self._h))
 
     # -- results ------------------------------------------------------------
-    def _fetch(self, n, with_keys=True):
-        kps = np.empty((n, 5), np.float32)
-        desc = np.empty((n, DESCRIPTOR_SIZE), np.uint8)
+    def _fetch(self, n, with_keys=True, out=None):
+        if out is not None:
+            kps, desc, keys = out.views(n)
+        else:
+            kps = np.empty((n, 5), np.float32)
+            desc = np.empty((n, DESCRIPTOR_SIZE), np.uint8)
+            keys = np.empty(n, np.uint64) if with_keys else None
         check(lib().sift_mi_fetch(self._h, kps.ctypes.data, desc.ctypes.data, n))
-        keys = None
         if with_keys:
-            keys = np.empty(n, np.uint64)
             check(lib().sift_mi_fetch_keys(self._h, keys.ctypes.data, n))
+        else:
+            keys = None
         return kps, desc, keys
 
     # -- sift (src/lib.rs:71-81) ---------------------------------------------
@@ -170,9 +192,12 @@ class Context:
                 for i in range(n)]
 
     def sift_batch_device(self, d_frames_ptr, n, width, height, row_stride, frame_pitch,
-                          features_limit=None, fetch=True):
+                          features_limit=None, fetch=True, out=None):
         """Device-resident frames (e.g. a torch.uint8 cuda tensor's data_ptr()).
-        Returns per-frame offsets and, with fetch, the concatenated results."""
+        Returns per-frame offsets and, with fetch, the concatenated results.
+        `out` (a ResultBuffers) receives the results in reused host arrays;
+        the returned SiftResult then holds views into it, valid until the
+        buffers are reused."""
         offs = (ctypes.c_size_t * (n + 1))()
         check(lib().sift_mi_set_keep_on_device(self._h, 0 if fetch else 1))
         check(lib().sift_mi_extract_batch_device(self._h, ctypes.c_void_p(d_frames_ptr), frame_pitch, n, width,
@@ -180,7 +205,7 @@ class Context:
         offsets = np.array(offs[:], dtype=np.int64)
         if not fetch:
             return offsets, None
-        return offsets, SiftResult(*self._fetch(int(offsets[-1])))
+        return offsets, SiftResult(*self._fetch(int(offsets[-1]), out=out))
 
     # -- precompute_images / sift_with_precomputed (src/lib.rs:123-177) ------
     def precompute_images(self, img):

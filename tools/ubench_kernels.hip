@@ -5,6 +5,7 @@
 #include "../sift-features_amd/csrc/describe.hip"
 #include "../sift-features_amd/csrc/pyramid.hip"
 
+#include <algorithm>
 #include <cstdio>
 #include <cstring>
 #include <cstdlib>
@@ -21,15 +22,19 @@ using namespace siftmi;
         }                                                                        \
     } while (0)
 
-template <bool E, int A>
+template <int E, int A>
 float time_describe(const DescLaunch& L, int reps) {
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
-    dim3 grid(L.n);
+    dim3 grid(std::min<uint32_t>(L.bound, 2048));
+    CK(hipMemset(L.work, 0, 4));
     hipLaunchKernelGGL((k_describe<E, A>), grid, dim3(64), 0, 0, L);
     CK(hipEventRecord(a));
-    for (int i = 0; i < reps; i++) hipLaunchKernelGGL((k_describe<E, A>), grid, dim3(64), 0, 0, L);
+    for (int i = 0; i < reps; i++) {
+        CK(hipMemsetAsync(L.work, 0, 4, 0));
+        hipLaunchKernelGGL((k_describe<E, A>), grid, dim3(64), 0, 0, L);
+    }
     CK(hipEventRecord(b));
     CK(hipEventSynchronize(b));
     float ms;
@@ -167,7 +172,14 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(d_p, &pitch, 4, hipMemcpyHostToDevice));
     DescLaunch L{};
     L.kp = d_kp;
-    L.n = NKP;
+    uint32_t* d_n;
+    CK(hipMalloc(&d_n, 4));
+    CK(hipMemcpy(d_n, &NKP, 4, hipMemcpyHostToDevice));
+    L.n = d_n;
+    L.bound = NKP;
+    uint32_t* d_work;
+    CK(hipMalloc(&d_work, 4));
+    L.work = d_work;
     L.gauss = d_g;
     L.gauss_img_stride = d_gs;
     L.ow = d_w;
@@ -176,12 +188,16 @@ int main(int argc, char** argv) {
     L.out_desc = d_desc;
     const int reps = 5;
     std::printf("describe n=%d\n", NKP);
-    std::printf("  exact           %8.3f ms\n", time_describe<true, 0>(L, reps));
-    std::printf("  exact -phaseB   %8.3f ms\n", time_describe<true, 1>(L, reps));
-    std::printf("  fast            %8.3f ms\n", time_describe<false, 0>(L, reps));
-    std::printf("  fast -atan2     %8.3f ms\n", time_describe<false, 2>(L, reps));
-    std::printf("  fast -exp       %8.3f ms\n", time_describe<false, 4>(L, reps));
-    std::printf("  fast -loads     %8.3f ms\n", time_describe<false, 8>(L, reps));
-    std::printf("  fast -all       %8.3f ms\n", time_describe<false, 14>(L, reps));
+    std::printf("  exact           %8.3f ms\n", time_describe<0, 0>(L, reps));
+    std::printf("  exact -phaseB   %8.3f ms\n", time_describe<0, 1>(L, reps));
+    std::printf("  fast s1         %8.3f ms\n", time_describe<1, 0>(L, reps));
+    std::printf("  fast s2         %8.3f ms\n", time_describe<2, 0>(L, reps));
+    std::printf("  fast s4         %8.3f ms\n", time_describe<4, 0>(L, reps));
+    std::printf("  fast s1 f32     %8.3f ms\n", time_describe<1, 16>(L, reps));
+    std::printf("  fast s2 f32     %8.3f ms\n", time_describe<2, 16>(L, reps));
+    std::printf("  fast s4 f32     %8.3f ms\n", time_describe<4, 16>(L, reps));
+    std::printf("  fast s2 -atan2  %8.3f ms\n", time_describe<2, 2>(L, reps));
+    std::printf("  fast s2 -loads  %8.3f ms\n", time_describe<2, 8>(L, reps));
+    std::printf("  fast s2 -all    %8.3f ms\n", time_describe<2, 14>(L, reps));
     return 0;
 }
