@@ -142,6 +142,20 @@ def main():
                "sample": f"{nfr} of the {B} benchmark frames ({W}x{H}), full sift() each, "
                          f"single-threaded C oracle (oracle/sift_oracle.c), {el:.1f} s"}
 
+    # HBM traffic of the same launch group from the committed PMC passes
+    # (tools/round_profile.sh -> profiles/pmc_traffic.json), scaled to one
+    # launch like `achieved`; null when no measurement matches this frame size
+    traffic, traffic_src = None, None
+    try:
+        with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
+            t = json.load(f)
+        if t["frame"] == f"{W}x{H}" and st["pyramid_launches"]:
+            frames_done = st["frames"]
+            traffic = t["pyramid_hbm_bytes_per_frame"] * frames_done / st["pyramid_launches"]
+            traffic_src = t["source"]
+    except (OSError, KeyError, ValueError):
+        pass
+
     if rank == 0:
         n_oct = int(round(np.log2(min(2 * W, 2 * H)) - 2)) + 1
         out = {
@@ -166,7 +180,8 @@ def main():
                                   ("pyramid_ms", "detect_ms", "orient_ms", "order_ms", "descriptor_ms", "total_ms")},
             "latency_1frame_ms": latency_ms,
             "roofline": {"bound": "hbm", "achieved": pyr_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
-                         "frac": pyr_gbs / HBM_PEAK_GBS, "traffic": None,
+                         "frac": pyr_gbs / HBM_PEAK_GBS, "traffic": traffic,
+                         "traffic_source": traffic_src,
                          "kernel": "pyramid stage (k_seed + k_blur<R>), rank 0",
                          "algorithmic_bytes_per_launch": per_launch_bytes,
                          "avg_launch_ms": per_launch_ms},

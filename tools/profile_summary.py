@@ -1,0 +1,110 @@
+"""Summarise a round profile (tools/round_profile.sh) into profiles/.
+
+Writes
+  profiles/<round>_kernel_stats.csv   rocprofv3 --stats output (copied)
+  profiles/<round>_summary.md         per-kernel table, the pyramid stage from
+                                      the trace next to bench.py's own number,
+                                      and HBM traffic from the PMC passes
+  profiles/pmc_traffic.json           per-frame pyramid traffic, read by
+                                      bench.py for roofline.traffic
+HBM bytes follow MI355X_MICROARCH.md (HBM section): FETCH_SIZE and WRITE_SIZE
+are in KiB; on gfx950 FETCH_SIZE counts half the bytes of 16-B-per-lane
+streaming reads (doubled here); WRITE_SIZE is exact for 16-B stores.
+"""
+import csv
+import glob
+import json
+import os
+import re
+import shutil
+import sys
+from collections import defaultdict
+
+ROUND, OUT, FRAMES = sys.argv[1], sys.argv[2], int(sys.argv[3])
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+PROF = os.path.join(ROOT, "profiles")
+os.makedirs(PROF, exist_ok=True)
+PYR = ("k_seed", "k_blur")
+
+
+def short(n):
+    return re.sub(r"\(.*", "", n).replace("void ", "").replace("siftmi::", "")
+
+
+def one(pattern):
+    f = glob.glob(os.path.join(OUT, pattern), recursive=True)
+    return f[0] if f else None
+
+
+def bench_line(log):
+    for line in open(log):
+        if line.startswith("{"):
+            return json.loads(line)
+    return None
+
+
+trace = one("trace/**/run_kernel_trace.csv")
+stats = one("trace/**/run_kernel_stats.csv")
+shutil.copy(stats, os.path.join(PROF, f"{ROUND}_kernel_stats.csv"))
+b = bench_line(os.path.join(OUT, "bench_trace.log"))
+steps_total = b["steps"] + b["warmup"] if b else 4
+
+agg = defaultdict(lambda: [0, 0.0])
+for r in csv.DictReader(open(trace)):
+    k = short(r["Kernel_Name"])
+    agg[k][0] += 1
+    agg[k][1] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
+tot = sum(v[1] for k, v in agg.items() if "siftmi" in k or k.startswith("k_"))
+pyr_us = sum(v[1] for k, v in agg.items() if k.startswith(PYR))
+pyr_n = sum(v[0] for k, v in agg.items() if k.startswith(PYR))
+
+
+def pmc(kind, name):
+    f = one(f"{kind}/**/run_counter_collection.csv")
+    v = 0.0
+    for r in csv.DictReader(open(f)):
+        if r["Counter_Name"] == name and short(r["Kernel_Name"]).startswith(PYR):
+            v += float(r["Counter_Value"])
+    return v * 1024.0  # KiB -> bytes
+
+
+fetch = 2.0 * pmc("fetch", "FETCH_SIZE")  # gfx950: half of 16-B streaming reads counted
+write = pmc("write", "WRITE_SIZE")
+frames_total = FRAMES * steps_total  # the PMC passes run the same command (warmup + steps)
+traffic_pf = (fetch + write) / frames_total
+W, H = 1920, 1080
+sum_p, ow, oh = 0, 2 * W, 2 * H
+for _ in range(int(round(__import__("math").log2(min(2 * W, 2 * H)) - 2)) + 1):
+    sum_p += ow * oh
+    ow //= 2
+    oh //= 2
+algo_pf = W * H + 44 * sum_p
+json.dump({"round": ROUND, "frame": f"{W}x{H}", "frames_per_call": FRAMES,
+           "pyramid_hbm_bytes_per_frame": traffic_pf, "fetch_bytes_per_frame": fetch / frames_total,
+           "write_bytes_per_frame": write / frames_total, "algorithmic_bytes_per_frame": algo_pf,
+           "source": f"profiles/{ROUND}_summary.md (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)"},
+          open(os.path.join(PROF, "pmc_traffic.json"), "w"), indent=1)
+
+with open(os.path.join(PROF, f"{ROUND}_summary.md"), "w") as f:
+    f.write(f"# {ROUND} profile: `bench.py --frames {FRAMES} --steps 3 --warmup 1` on one MI355X\n\n")
+    f.write("Command: `bash tools/round_profile.sh` (rocprofv3 --kernel-trace --stats; then separate "
+            "--pmc FETCH_SIZE and --pmc WRITE_SIZE passes of the same command).\n\n")
+    if b:
+        f.write(f"bench line (traced run): value = {b['value']:.4g} keypoints/s, ms_per_step = "
+                f"{b['ms_per_step']:.2f}, stage_ms_per_step = {json.dumps(b['stage_ms_per_step'])}\n\n")
+    f.write("## Pyramid stage (the roofline kernel group: k_seed + k_blur<R>)\n\n")
+    f.write(f"* trace: {pyr_n} launches over {steps_total} calls, {pyr_us / 1e3:.3f} ms total -> "
+            f"{pyr_us / 1e3 / steps_total:.3f} ms per call, {pyr_us / max(1, pyr_n):.1f} us per launch\n")
+    if b:
+        f.write(f"* bench.py (HIP events on the compute stream, timed steps only): pyramid_ms per step = "
+                f"{b['stage_ms_per_step']['pyramid_ms']:.3f}, avg launch = {b['roofline']['avg_launch_ms'] * 1e3:.1f} us\n")
+    f.write(f"* algorithmic bytes per frame (W*H + 44*sum P_o) = {algo_pf / 1e6:.1f} MB\n")
+    f.write(f"* HBM traffic per frame (PMC, FETCH_SIZE x2 + WRITE_SIZE) = {traffic_pf / 1e6:.1f} MB "
+            f"(read {fetch / frames_total / 1e6:.1f} MB, write {write / frames_total / 1e6:.1f} MB); "
+            f"traffic / algorithmic = {traffic_pf / algo_pf:.2f}\n\n")
+    f.write("## Kernels (trace, all calls)\n\n| kernel | launches | total ms | avg us | share |\n|---|---|---|---|---|\n")
+    for k, (n, us) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
+        if not (k.startswith("k_") or "hipcub" in k or "rocprim" in k):
+            continue
+        f.write(f"| `{k}` | {n} | {us / 1e3:.3f} | {us / n:.1f} | {100 * us / tot:.1f}% |\n")
+print(open(os.path.join(PROF, f"{ROUND}_summary.md")).read())
