@@ -18,4 +18,6 @@ timeout -k 10 600 rocprofv3 --pmc FETCH_SIZE -d $OUT/fetch -o run --output-forma
 rc=$?; echo "fetch rc=$rc"; [ $rc -eq 0 ] || exit $rc
 timeout -k 10 600 rocprofv3 --pmc WRITE_SIZE -d $OUT/write -o run --output-format csv -- $CMD > $OUT/bench_write.log 2>&1
 rc=$?; echo "write rc=$rc"; [ $rc -eq 0 ] || exit $rc
-python3 tools/profile_summary.py $ROUND $OUT $FRAMES
+# summarise locally after gpurun merges gpurun_out/ back:
+#   python3 tools/profile_summary.py $ROUND $OUT $FRAMES
+python3 tools/profile_summary.py $ROUND $OUT $FRAMES > $OUT/summary.md
