@@ -94,8 +94,9 @@ __global__ __launch_bounds__(256) void k_detect(const DetectLaunch L) {
     __shared__ uint64_t lcand[DT_LCAP];
     __shared__ uint32_t lcount, gbase;
     const int W = L.W, H = L.H, pitch = L.pitch;
-    const int x0 = blockIdx.x * DT_W, y0 = blockIdx.y * DT_H;
-    const int b = blockIdx.z;
+    const TileId tile = xcd_tile();
+    const int x0 = tile.x * DT_W, y0 = tile.y * DT_H;
+    const int b = tile.z;
     const float* dog = L.dog + (size_t)b * L.img_stride;
     const size_t P = (size_t)pitch * H;
     const int tid = threadIdx.x;

@@ -182,8 +182,9 @@ __global__ __launch_bounds__(256) void k_blur(const float* __restrict__ src, siz
     float* tin = lds;  // [IH][IWP]  G_{s-1} window, then (in place) the row-pass output
     float* th = lds;
     const int tid = threadIdx.x;
-    const int x0 = blockIdx.x * G::TW, y0 = blockIdx.y * G::TH;
-    const size_t b = blockIdx.z;
+    const TileId tile = xcd_tile();
+    const int x0 = tile.x * G::TW, y0 = tile.y * G::TH;
+    const size_t b = tile.z;
     src += b * src_img_stride;
     const bool interior = x0 >= G::HWL && x0 + G::TW + G::HWL <= W && y0 >= R && y0 + G::TH + R <= H;
     if (interior) {
@@ -264,8 +265,9 @@ __global__ __launch_bounds__(256) void k_seed(const uint8_t* __restrict__ frames
     float* th = lds;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     lut[tid] = (float)tid / 255.0f;
-    const int x0 = blockIdx.x * G::TW, y0 = blockIdx.y * G::TH;
-    const size_t b = blockIdx.z;
+    const TileId tile = xcd_tile();
+    const int x0 = tile.x * G::TW, y0 = tile.y * G::TH;
+    const size_t b = tile.z;
     const uint8_t* src = frames + b * frame_pitch;
     // upsampled-coordinate spans of the tile window after reflect-101
     {

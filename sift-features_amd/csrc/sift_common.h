@@ -97,6 +97,29 @@ __host__ __device__ __forceinline__ int reflect101(int p, int len) {
     return p;
 }
 
+// XCD-aware tile order for (tx, ty, frames) grids.  The dispatcher deals
+// workgroups round-robin over the 8 XCDs (each with a private 4 MB L2), so
+// neighbouring tiles of a plain grid land on different XCDs and every halo
+// row is re-read from HBM / Infinity Cache.  The bijective remap below gives
+// each XCD a contiguous range of tile ids (cdna_hip_programming.md T1), walked
+// row-major inside a frame: consecutive tiles of one XCD are horizontal
+// neighbours (shared column halos, adjacent 256-B write segments), and the
+// tile row above -- the vertical halo -- was loaded one tile row earlier
+// (still in L2).
+struct TileId {
+    int x, y, z;
+};
+__device__ __forceinline__ TileId xcd_tile() {
+    const uint32_t tx = gridDim.x, ty = gridDim.y;
+    const uint32_t nwg = tx * ty * gridDim.z;
+    const uint32_t orig = blockIdx.x + tx * (blockIdx.y + ty * blockIdx.z);
+    const uint32_t q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+    const uint32_t t = (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+    const uint32_t per = tx * ty;
+    const uint32_t z = t / per, rem = t - z * per;
+    return {(int)(rem - (rem / tx) * tx), (int)(rem / tx), (int)z};
+}
+
 // Correctly rounded f32 transcendentals evaluated in f64 (the reference calls
 // glibc expf/sinf/cosf/powf, which are correctly rounded in all but rare
 // near-midpoint cases).
