@@ -256,11 +256,15 @@ __global__ __launch_bounds__(256) void k_seed(const uint8_t* __restrict__ frames
     static_assert(G::IH <= 128 && G::IWV <= 128, "span reduction covers 128 positions per axis");
     __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
     __shared__ float srcf[SR * SC];         // u8 -> f32 source window
-    __shared__ float hbuf[SR * G::IWV];     // horizontal pass (HResizeLinear) per source row
+    __shared__ __attribute__((aligned(16))) float hbuf[SR * G::IWV];  // HResizeLinear per source row
     __shared__ float lut[256];
     __shared__ int span[4][4];              // per wave: min/max upsampled x (waves 0,1) / y (waves 2,3)
-    __shared__ int txo[G::IWV], tyo[G::IH];  // per window column / row: source index (resize tables)
-    __shared__ float txa0[G::IWV], txa1[G::IWV], tya0[G::IH], tya1[G::IH];
+    // per window column / row: source index and coefficients (resize tables)
+    __shared__ __attribute__((aligned(16))) int txo[G::IWV];
+    __shared__ __attribute__((aligned(16))) float txa0[G::IWV], txa1[G::IWV];
+    __shared__ int tyo[G::IH];
+    __shared__ float tya0[G::IH], tya1[G::IH];
+    static_assert(G::IWV % 4 == 0, "float4 passes");
     float* tin = lds;
     float* th = lds;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
@@ -269,23 +273,29 @@ __global__ __launch_bounds__(256) void k_seed(const uint8_t* __restrict__ frames
     const int x0 = tile.x * G::TW, y0 = tile.y * G::TH;
     const size_t b = tile.z;
     const uint8_t* src = frames + b * frame_pitch;
-    // upsampled-coordinate spans of the tile window after reflect-101
+    // per window column (threads 0..127) / row (128..255): reflect-101 position,
+    // its resize table entries (all loads in flight together), and the span of
+    // source columns / rows the window needs
     {
         const int t = tid & 127;
         const bool isx = tid < 128;
         const bool act = isx ? t < G::IWV : t < G::IH;
         const int g = act ? (isx ? reflect101(x0 - G::HWL + t, W) : reflect101(y0 - R + t, H)) : 0;
-        // this window position's table entries, fetched once (all in flight together)
+        int s0 = 0, s1 = 0;
         if (act && isx) {
-            txo[t] = g < tab.xmax ? tab.xofs[g] : -1 - tab.xofs[g];  // < 0: single-tap right border
+            s0 = tab.xofs[g];
+            s1 = min(s0 + 1, sw - 1);
+            txo[t] = g < tab.xmax ? s0 : -1 - s0;  // < 0: single-tap right border
             txa0[t] = tab.xa0[g];
             txa1[t] = tab.xa1[g];
         } else if (act) {
-            tyo[t] = tab.yofs[g];
+            s0 = tab.yofs[g];
+            s1 = min(s0 + 1, sh - 1);
+            tyo[t] = s0;
             tya0[t] = tab.ya0[g];
             tya1[t] = tab.ya1[g];
         }
-        int mn = act ? g : INT_MAX, mx = act ? g : INT_MIN;
+        int mn = act ? s0 : INT_MAX, mx = act ? s1 : INT_MIN;
 #pragma unroll
         for (int o = 32; o >= 1; o >>= 1) {
             mn = min(mn, __shfl_xor(mn, o));
@@ -297,33 +307,43 @@ __global__ __launch_bounds__(256) void k_seed(const uint8_t* __restrict__ frames
         }
     }
     __syncthreads();
-    const int gxa = min(span[0][0], span[1][0]), gxb = max(span[0][1], span[1][1]);
-    const int gya = min(span[2][0], span[3][0]), gyb = max(span[2][1], span[3][1]);
-    const int sxa = tab.xofs[gxa], sxb = min(tab.xofs[gxb] + 1, sw - 1);
-    const int sya = tab.yofs[gya], syb = min(tab.yofs[gyb] + 1, sh - 1);
+    const int sxa = min(span[0][0], span[1][0]), sxb = max(span[0][1], span[1][1]);
+    const int sya = min(span[2][0], span[3][0]), syb = max(span[2][1], span[3][1]);
     const int nc = sxb - sxa + 1, nr = syb - sya + 1;
     if (nc <= SC && nr <= SR) {
-        for (int i = tid; i < nr * nc; i += 256) {
-            const int r = i / nc, c = i - r * nc;
-            srcf[r * SC + c] = lut[src[(size_t)(sya + r) * row_stride + sxa + c]];
+        for (int r = wv; r < nr; r += 4)
+            for (int c = lane; c < nc; c += 64)
+                srcf[r * SC + c] = lut[src[(size_t)(sya + r) * row_stride + sxa + c]];
+        __syncthreads();
+        // HResizeLinear: t = S[sx]*a0 + S[sx+1]*a1 (two roundings + add); 4 columns per item
+        constexpr int Q = G::IWV / 4;
+        for (int i = tid; i < nr * Q; i += 256) {
+            const int r = i / Q, c = (i - r * Q) * 4;
+            const int4 xo = *reinterpret_cast<const int4*>(txo + c);
+            const float4 a0 = *reinterpret_cast<const float4*>(txa0 + c);
+            const float4 a1 = *reinterpret_cast<const float4*>(txa1 + c);
+            const float* sr = srcf + r * SC - sxa;
+            auto hres = [&](int o, float w0, float w1) {
+                const bool two = o >= 0;
+                const int sx = two ? o : -1 - o;
+                const float p0 = sr[sx];
+                return two ? p0 * w0 + sr[sx + 1] * w1 : p0;
+            };
+            *reinterpret_cast<float4*>(hbuf + r * G::IWV + c) =
+                make_float4(hres(xo.x, a0.x, a1.x), hres(xo.y, a0.y, a1.y), hres(xo.z, a0.z, a1.z),
+                            hres(xo.w, a0.w, a1.w));
         }
         __syncthreads();
-        // HResizeLinear: t = S[sx]*a0 + S[sx+1]*a1 (two roundings + add)
-        for (int i = tid; i < nr * G::IWV; i += 256) {
-            const int r = i / G::IWV, lx = i - r * G::IWV;
-            const int xo = txo[lx];
-            const bool two = xo >= 0;
-            const int sx = (two ? xo : -1 - xo) - sxa;
-            const float p0 = srcf[r * SC + sx];
-            hbuf[i] = two ? p0 * txa0[lx] + srcf[r * SC + sx + 1] * txa1[lx] : p0;
-        }
-        __syncthreads();
-        // VResizeLinear: S0*b0 + S1*b1
-        for (int i = tid; i < G::IH * G::IWV; i += 256) {
-            const int ly = i / G::IWV, lx = i - ly * G::IWV;
+        // VResizeLinear: S0*b0 + S1*b1; 4 columns per item
+        for (int i = tid; i < G::IH * Q; i += 256) {
+            const int ly = i / Q, c = (i - ly * Q) * 4;
             const int s0 = tyo[ly];
             const int r0 = s0 - sya, r1 = min(s0 + 1, sh - 1) - sya;
-            tin[ly * G::IWP + lx] = hbuf[r0 * G::IWV + lx] * tya0[ly] + hbuf[r1 * G::IWV + lx] * tya1[ly];
+            const float4 u = *reinterpret_cast<const float4*>(hbuf + r0 * G::IWV + c);
+            const float4 v = *reinterpret_cast<const float4*>(hbuf + r1 * G::IWV + c);
+            const float b0 = tya0[ly], b1 = tya1[ly];
+            *reinterpret_cast<float4*>(tin + ly * G::IWP + c) =
+                make_float4(u.x * b0 + v.x * b1, u.y * b0 + v.y * b1, u.z * b0 + v.z * b1, u.w * b0 + v.w * b1);
         }
     } else {  // not reached for a 2x seed; kept for safety on degenerate shapes
         for (int i = tid; i < G::IH * G::IWV; i += 256) {
