@@ -72,8 +72,12 @@ def main():
     import synth
     pkg = pkg_loader.load()
 
+    import shard
     B, W, H = args.frames, args.width, args.height
-    frames = synth.frames_torch(B, W, H, seed0=rank * B, device=dev)
+    # weak scaling: a global batch of world*B frames, rank r owns the
+    # contiguous block shard_range(world*B, r, world) (frame i = seed i)
+    f0, f1 = shard.shard_range(world * B, rank, world)
+    frames = synth.frames_torch(f1 - f0, W, H, seed0=f0, device=dev)
     torch.cuda.synchronize()
     ctx = pkg.Context(local, pkg.OpenCVProcessing)
     if args.chunk:
@@ -104,13 +108,7 @@ def main():
     dt = time.perf_counter() - t0
     st = ctx.stats()
 
-    tot = torch.tensor([float(n_kp), float(B * args.steps)], dtype=torch.float64, device=dev)
-    tmax = torch.tensor([dt], dtype=torch.float64, device=dev)
-    if world > 1:
-        dist.all_reduce(tot, op=dist.ReduceOp.SUM)
-        dist.all_reduce(tmax, op=dist.ReduceOp.MAX)
-    total_kp, total_frames = tot.tolist()
-    dt_max = float(tmax.item())
+    dt_max, total_kp, total_frames = shard.reduce_run(dt, n_kp, B * args.steps, dist if world > 1 else None)
 
     pyr_gbs = st["pyramid_bytes"] / (st["pyramid_ms"] * 1e-3) / 1e9 if st["pyramid_ms"] > 0 else 0.0
     per_launch_bytes = st["pyramid_bytes"] / max(1, st["pyramid_launches"])

@@ -1,0 +1,96 @@
+"""Multi-GPU data parallelism for batches of frames.
+
+Frames are independent, so a batch shards by contiguous frame blocks, one
+process per GPU (torch.distributed, RCCL backend on MI355X), with no
+data-path collective: every rank runs the whole path on its own frames.  The
+only collectives are
+  * `reduce_run`    -- the benchmark's max-over-ranks time and summed counts;
+  * `gather_results` -- the optional "trivial keypoint gather" of the north
+                        star: per-rank results concatenated on one rank in
+                        global frame order (sizes first, then padded payloads
+                        in one gather per array).
+Both run unchanged on gloo (CPU tensors; tests/test_shard.py) and RCCL (GPU
+tensors).
+"""
+import numpy as np
+
+
+def shard_range(n_total, rank, world):
+    """Contiguous block [start, stop) of frames owned by `rank`; blocks differ
+    in size by at most one frame and cover 0..n_total exactly once."""
+    if world < 1 or not 0 <= rank < world:
+        raise ValueError("bad rank / world")
+    q, r = divmod(n_total, world)
+    start = rank * q + min(rank, r)
+    return start, start + q + (1 if rank < r else 0)
+
+
+def _device(dist):
+    import torch
+    return torch.device("cuda", torch.cuda.current_device()) if dist.get_backend() == "nccl" else torch.device("cpu")
+
+
+def reduce_run(seconds, keypoints, frames, dist=None):
+    """(max seconds over ranks, total keypoints, total frames)."""
+    import torch
+    if dist is None or not dist.is_initialized() or dist.get_world_size() == 1:
+        return float(seconds), int(keypoints), int(frames)
+    dev = _device(dist)
+    t = torch.tensor([float(seconds)], dtype=torch.float64, device=dev)
+    c = torch.tensor([float(keypoints), float(frames)], dtype=torch.float64, device=dev)
+    dist.all_reduce(t, op=dist.ReduceOp.MAX)
+    dist.all_reduce(c, op=dist.ReduceOp.SUM)
+    return float(t.item()), int(c[0].item()), int(c[1].item())
+
+
+def gather_results(keypoints, descriptors, offsets, dist, dst=0):
+    """Concatenate every rank's (keypoints (n,5) f32, descriptors (n,128) u8,
+    per-frame offsets (m+1,)) on rank `dst`, in rank (= global frame) order.
+
+    Returns (keypoints, descriptors, offsets) on `dst`, None elsewhere.
+    """
+    import torch
+    world = dist.get_world_size()
+    rank = dist.get_rank()
+    dev = _device(dist)
+    kps = np.ascontiguousarray(keypoints, dtype=np.float32).reshape(-1, 5)
+    desc = np.ascontiguousarray(descriptors, dtype=np.uint8).reshape(-1, 128)
+    offs = np.asarray(offsets, dtype=np.int64)
+    n, m = len(kps), len(offs) - 1
+    if len(desc) != n or offs[-1] - offs[0] != n:
+        raise ValueError("keypoints / descriptors / offsets disagree")
+    sizes = torch.tensor([n, m], dtype=torch.int64, device=dev)
+    all_sizes = [torch.zeros_like(sizes) for _ in range(world)]
+    dist.all_gather(all_sizes, sizes)
+    ns = [int(s[0]) for s in all_sizes]
+    ms = [int(s[1]) for s in all_sizes]
+    n_max, m_max = max(max(ns), 1), max(ms)
+
+    def padded(a, rows, dtype):
+        t = torch.zeros((rows,) + a.shape[1:], dtype=dtype, device=dev)
+        if len(a):
+            t[: len(a)] = torch.from_numpy(a).to(dev)
+        return t
+
+    # keypoints as raw 32-bit words, descriptors as bytes (exact bits on any backend)
+    payload = {
+        "kps": padded(kps.view(np.int32), n_max, torch.int32),
+        "desc": padded(desc, n_max, torch.uint8),
+        "offs": padded(offs - offs[0], m_max + 1, torch.int64),
+    }
+    out = {}
+    for key, t in payload.items():
+        lst = [torch.zeros_like(t) for _ in range(world)] if rank == dst else None
+        dist.gather(t, gather_list=lst, dst=dst)
+        out[key] = lst
+    if rank != dst:
+        return None
+    k_all, d_all, o_all, base = [], [], [0], 0
+    for r in range(world):
+        k_all.append(out["kps"][r][: ns[r]].cpu().numpy().view(np.float32))
+        d_all.append(out["desc"][r][: ns[r]].cpu().numpy())
+        o = out["offs"][r][1: ms[r] + 1].cpu().numpy()
+        o_all.extend((o + base).tolist())
+        base += ns[r]
+    return (np.concatenate(k_all).reshape(-1, 5), np.concatenate(d_all).reshape(-1, 128),
+            np.asarray(o_all, dtype=np.int64))
