@@ -151,6 +151,11 @@ static inline int reflect101(int p, int len) {
     return p;
 }
 
+/* Arithmetic-variant switch for pinning experiments against the snapshots
+ * (tools only; 0 = the restatement documented above). */
+static int g_variant = 0;
+void oracle_set_variant(int v) { g_variant = v; }
+
 /* Separable filter: RowFilter<float,float,RowVec_32f> (fma chain from the
  * leftmost tap), then SymmColumnFilter<SymmColumnVec_32f> (centre product,
  * then fma of the (below+above) pair sums outwards). */
@@ -182,8 +187,15 @@ static void cv_blur(const float* src, int w, int h, double sigma, float* dst) {
         const float* s = src + (size_t)y * w;
         float* t = tmp + (size_t)y * w;
         for (int x = 0; x < w; x++) {
-            float acc = s[xo[x]] * kxv[0];
-            for (int k = 1; k < kx; k++) acc = fmaf(s[xo[x + k]], kxv[k], acc);
+            float acc;
+            if (g_variant & 64) {  /* symmetric pairs from the centre */
+                acc = s[xo[x + rx]] * kxv[rx];
+                for (int k = 1; k <= rx; k++) acc = fmaf(s[xo[x + rx - k]] + s[xo[x + rx + k]], kxv[rx + k], acc);
+            } else {
+                acc = s[xo[x]] * kxv[0];
+                for (int k = 1; k < kx; k++)
+                    acc = (g_variant & 8) ? acc + s[xo[x + k]] * kxv[k] : fmaf(s[xo[x + k]], kxv[k], acc);
+            }
             t[x] = acc;
         }
     }
@@ -191,11 +203,20 @@ static void cv_blur(const float* src, int w, int h, double sigma, float* dst) {
     for (int y = 0; y < h; y++) {
         float* d = dst + (size_t)y * w;
         const float* c = tmp + (size_t)y * w;
+        if (g_variant & 32) {  /* plain fma chain from the top tap */
+            for (int x = 0; x < w; x++) {
+                float acc = tmp[(size_t)reflect101(y - ry, h) * w + x] * kyv[0];
+                for (int k = 1; k < ky; k++) acc = fmaf(tmp[(size_t)reflect101(y - ry + k, h) * w + x], kyv[k], acc);
+                d[x] = acc;
+            }
+            continue;
+        }
         for (int x = 0; x < w; x++) d[x] = c[x] * kc[0];
         for (int k = 1; k <= ry; k++) {
             const float* dn = tmp + (size_t)reflect101(y + k, h) * w;
             const float* up = tmp + (size_t)reflect101(y - k, h) * w;
-            for (int x = 0; x < w; x++) d[x] = fmaf(dn[x] + up[x], kc[k], d[x]);
+            for (int x = 0; x < w; x++)
+                d[x] = (g_variant & 16) ? d[x] + (dn[x] + up[x]) * kc[k] : fmaf(dn[x] + up[x], kc[k], d[x]);
         }
     }
     free(xo);
@@ -248,7 +269,7 @@ static void cv_resize_linear(const float* src, int sw, int sh, int dw, int dh, f
         for (int x = 0; x < dw; x++) {
             int sx = xo[x];
             if (x < xmax)
-                t[x] = s[sx] * xa0[x] + s[sx + 1] * xa1[x];
+                t[x] = (g_variant & 4) ? fmaf(s[sx], xa0[x], s[sx + 1] * xa1[x]) : s[sx] * xa0[x] + s[sx + 1] * xa1[x];
             else
                 t[x] = s[sx];
         }
@@ -258,7 +279,10 @@ static void cv_resize_linear(const float* src, int sw, int sh, int dw, int dh, f
         const float* s0 = hb + (size_t)r0 * dw;
         const float* s1 = hb + (size_t)r1 * dw;
         float* d = dst + (size_t)y * dw;
-        for (int x = 0; x < dw; x++) d[x] = s0[x] * ya0[y] + s1[x] * ya1[y];
+        for (int x = 0; x < dw; x++)
+            d[x] = (g_variant & 1)   ? fmaf(s0[x], ya0[y], s1[x] * ya1[y])
+                   : (g_variant & 2) ? fmaf(s1[x], ya1[y], s0[x] * ya0[y])
+                                     : s0[x] * ya0[y] + s1[x] * ya1[y];
     }
     free(hb);
     free(xo);
@@ -578,7 +602,7 @@ static void find_keypoints(const opyr_t* p, kpvec_t* out) {
                     if (on_edge(dog + (size_t)pt.scale * P, w, pt.x, pt.y)) continue;
                     const float osf = powi_f32(2.0f, o);
                     const float kp_scale =
-                        (float)0.8 * powf(2.0f, ((float)pt.scale + pt.off_s) / (float)SCALES_PER_OCTAVE) * 2.f;
+                        (float)0.8 * ((g_variant & 128) ? exp2f(((float)pt.scale + pt.off_s) / (float)SCALES_PER_OCTAVE) : powf(2.0f, ((float)pt.scale + pt.off_s) / (float)SCALES_PER_OCTAVE)) * 2.f;
                     const float kp_x = ((float)pt.x + pt.off_x) * osf;
                     const float kp_y = ((float)pt.y + pt.off_y) * osf;
                     const int radius = sat_i32(roundf(3.f * 1.5f * kp_scale));

@@ -11,11 +11,19 @@ Sources (reference @ /root/reference):
     already stably sorted by (x, y, size) (src/lib.rs:1020-1030).
   * images/*.jpg -- the test inputs (src/lib.rs:1038, :1047).  The reference
     decodes them with `image::load_from_memory(..).grayscale()` (image 0.25.2,
-    zune-jpeg decoder, luma = (2126 R + 7152 G + 722 B) / 10000, integer
-    division).  We decode with PIL (libjpeg-turbo, ISLOW IDCT, fancy
-    upsampling) and apply the same integer luma formula.  The two JPEG
-    decoders may differ by +-1 LSB on some pixels; that is the documented
-    source of residual golden mismatch ("Oracle").
+    whose JPEG backend is zune-jpeg; luma = (2126 R + 7152 G + 722 B) / 10000,
+    integer division).  zune-jpeg is not in /root/reference, so the inputs are
+    decoded here by tests/golden/jpeg_decode.py with the reconstruction
+    arithmetic that reproduces the snapshots (selected by matching them; see
+    DESIGN.md, "Oracle"):  idct="zune" (stb_image 12-bit integer IDCT with the
+    row-pass bias 512 + 65536 + (128 << 17) and the DC-only shortcut
+    (DC >> 3) + 128), upsample="twopass" (vertical then horizontal 3:1
+    triangle, each (3a + b + 2) >> 2), color="zune" (45/32, 11/32, 23/32,
+    113/64 fixed point), edge="pad".  With these inputs the oracle finds the
+    snapshots' exact keypoint counts (1270, 225) with 96-99 % of keypoints at
+    identical positions.  The same decoder with the libjpeg arithmetic
+    reproduces PIL (libjpeg-turbo) bit-exactly on these files (checked below),
+    which validates its entropy decoding.
 
 Usage:  python tests/golden/make_golden.py
 """
@@ -68,10 +76,18 @@ def parse_descriptors(path):
     return arr.astype(np.uint8)
 
 
+sys.path.insert(0, HERE)
+import jpeg_decode  # noqa: E402
+
+ZUNE = dict(idct="zune", upsample="twopass", color="zune", edge="pad")
+
+
 def decode_gray(path):
-    rgb = np.asarray(Image.open(path).convert("RGB")).astype(np.uint32)
-    luma = (2126 * rgb[..., 0] + 7152 * rgb[..., 1] + 722 * rgb[..., 2]) // 10000
-    return np.clip(luma, 0, 255).astype(np.uint8)
+    # entropy-decoding check: the libjpeg arithmetic must reproduce PIL exactly
+    pil = np.asarray(Image.open(path).convert("RGB"))
+    ours = jpeg_decode.decode(path, idct="islow", upsample="libjpeg", color="libjpeg", edge="clamp")
+    assert np.array_equal(pil, ours), "jpeg_decode does not reproduce libjpeg-turbo"
+    return jpeg_decode.luma(jpeg_decode.decode(path, **ZUNE))
 
 
 def main():
