@@ -23,13 +23,13 @@ namespace siftmi {
 // ---------------------------------------------------------------------------
 // interpolate_extremum (src/lib.rs:525-603) on the DoG stack of one frame.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ bool interpolate(const float* __restrict__ dog, int W, int H, int pitch, int& scale,
+__device__ __forceinline__ bool interpolate(const gfloat* __restrict__ dog, int W, int H, int pitch, int& scale,
                                             int& x, int& y, float& os, float& ox, float& oy) {
     const size_t P = (size_t)pitch * H;
     for (int it = 0; it < kMaxInterpSteps; it++) {
-        const float* prev = dog + (size_t)(scale - 1) * P;
-        const float* curr = dog + (size_t)scale * P;
-        const float* next = dog + (size_t)(scale + 1) * P;
+        const gfloat* prev = dog + (size_t)(scale - 1) * P;
+        const gfloat* curr = dog + (size_t)scale * P;
+        const gfloat* next = dog + (size_t)(scale + 1) * P;
 #define AT(a, yy, xx) (a)[(size_t)(yy) * pitch + (xx)]
         const float g1 = (AT(next, y, x) - AT(prev, y, x)) / 2.f;
         const float g2 = (AT(curr, y + 1, x) - AT(curr, y - 1, x)) / 2.f;
@@ -135,37 +135,51 @@ __global__ __launch_bounds__(256) void k_detect(const DetectLaunch L) {
     const int lx = (tid & 63) + 4;  // LDS column of this thread's pixel
     const int x = x0 + (tid & 63);
     const bool xin = x >= kImageBorder && x < W - kImageBorder;
+#define T(pl, yy, xx) t[((pl) * DT_LH + (yy)) * DT_LP + (xx)]
+    // Per plane, the 3-wide row max / min of the DT_RPT + 2 rows this thread
+    // touches are formed once (6 rows x 3 reads instead of 4 x 9), then the
+    // 3x3 maxima of each output row are combined from them.
+    const int ly0 = (tid >> 6) * DT_RPT;  // first LDS row of the window (output row ly0 + 1)
+    float hmax[kDogPerOctave][DT_RPT + 2], hmin[kDogPerOctave][DT_RPT + 2];
+    float lr_max[kDogPerOctave][DT_RPT], lr_min[kDogPerOctave][DT_RPT], ctr[kDogPerOctave][DT_RPT];
+#pragma unroll
+    for (int pl = 0; pl < kDogPerOctave; pl++) {
+#pragma unroll
+        for (int r = 0; r < DT_RPT + 2; r++) {
+            const float l = T(pl, ly0 + r, lx - 1), c = T(pl, ly0 + r, lx), rt = T(pl, ly0 + r, lx + 1);
+            const float m2 = fmaxf(l, rt), n2 = fminf(l, rt);
+            hmax[pl][r] = fmaxf(m2, c);
+            hmin[pl][r] = fminf(n2, c);
+            if (r >= 1 && r <= DT_RPT) {
+                lr_max[pl][r - 1] = m2;
+                lr_min[pl][r - 1] = n2;
+                ctr[pl][r - 1] = c;
+            }
+        }
+    }
     // threshold = floor(0.5 * 0.04 / 3) = 0 (src/lib.rs:460)
     const float threshold = floorf(0.5f * kContrastThreshold / (float)kScalesPerOctave);
-#define T(pl, yy, xx) t[((pl) * DT_LH + (yy)) * DT_LP + (xx)]
+#pragma unroll
     for (int rr = 0; rr < DT_RPT; rr++) {
-        const int ly = (tid >> 6) * DT_RPT + rr + 1;
-        const int y = y0 + ly - 1;
+        const int y = y0 + ly0 + rr;
         if (!xin || y < kImageBorder || y >= H - kImageBorder) continue;
         // point_is_local_extremum (src/lib.rs:437-506): non-strict vs all 26
-        // neighbours.  Branch-free: per plane the 3x3 max/min (centre excluded
-        // on the middle plane) over registers, then one compare per sign.
-        float pmax[kDogPerOctave], pmin[kDogPerOctave], pc[kDogPerOctave], pmax8[kDogPerOctave],
-            pmin8[kDogPerOctave];
+        // neighbours; per plane the 3x3 max / min (centre excluded on the
+        // middle plane), then one compare per sign.
+        float pmax[kDogPerOctave], pmin[kDogPerOctave];
 #pragma unroll
         for (int pl = 0; pl < kDogPerOctave; pl++) {
-            const float a0 = T(pl, ly - 1, lx - 1), a1 = T(pl, ly - 1, lx), a2 = T(pl, ly - 1, lx + 1);
-            const float b0 = T(pl, ly, lx - 1), b1 = T(pl, ly, lx), b2 = T(pl, ly, lx + 1);
-            const float c0 = T(pl, ly + 1, lx - 1), c1 = T(pl, ly + 1, lx), c2 = T(pl, ly + 1, lx + 1);
-            const float m8 = fmaxf(fmaxf(fmaxf(a0, a1), fmaxf(a2, b0)), fmaxf(fmaxf(b2, c0), fmaxf(c1, c2)));
-            const float n8 = fminf(fminf(fminf(a0, a1), fminf(a2, b0)), fminf(fminf(b2, c0), fminf(c1, c2)));
-            pmax8[pl] = m8;
-            pmin8[pl] = n8;
-            pmax[pl] = fmaxf(m8, b1);
-            pmin[pl] = fminf(n8, b1);
-            pc[pl] = b1;
+            pmax[pl] = fmaxf(fmaxf(hmax[pl][rr], hmax[pl][rr + 1]), hmax[pl][rr + 2]);
+            pmin[pl] = fminf(fminf(hmin[pl][rr], hmin[pl][rr + 1]), hmin[pl][rr + 2]);
         }
+#pragma unroll
         for (int s_in = 1; s_in <= kScalesPerOctave; s_in++) {
-            const float val = pc[s_in];
-            if (fabsf(val) <= threshold) continue;
-            const float mx = fmaxf(fmaxf(pmax[s_in - 1], pmax[s_in + 1]), pmax8[s_in]);
-            const float mn = fminf(fminf(pmin[s_in - 1], pmin[s_in + 1]), pmin8[s_in]);
-            const bool ok = val > 0.0f ? val >= mx : val <= mn;
+            const float val = ctr[s_in][rr];
+            const float m8 = fmaxf(fmaxf(hmax[s_in][rr], hmax[s_in][rr + 2]), lr_max[s_in][rr]);
+            const float n8 = fminf(fminf(hmin[s_in][rr], hmin[s_in][rr + 2]), lr_min[s_in][rr]);
+            const float mx = fmaxf(fmaxf(pmax[s_in - 1], pmax[s_in + 1]), m8);
+            const float mn = fminf(fminf(pmin[s_in - 1], pmin[s_in + 1]), n8);
+            const bool ok = fabsf(val) > threshold && (val > 0.0f ? val >= mx : val <= mn);
             if (!ok) continue;
             // candidate -> refinement kernel (dense, so its dependent global
             // loads overlap across many threads instead of stalling this tile)
@@ -209,14 +223,14 @@ __device__ __forceinline__ bool refine_one(const RefineLaunch& L, uint64_t key, 
     const int y = (int)((key >> kKeyYShift) & 0x3fff);
     const int x = (int)((key >> kKeyXShift) & 0x3fff);
     const int W = L.ow[o], H = L.oh[o], pitch = L.opitch[o];
-    const float* dog = L.dog[o] + (size_t)(b - L.img_base) * L.dog_img_stride[o];
+    const gfloat* dog = as_global(L.dog[o]) + (size_t)(b - L.img_base) * L.dog_img_stride[o];
     const size_t P = (size_t)pitch * H;
     int sc = s_in, xi = x, yi = y;
     float os, ox, oy;
     if (!interpolate(dog, W, H, pitch, sc, xi, yi, os, ox, oy)) return false;
-    const float* prev = dog + (size_t)(sc - 1) * P;
-    const float* curr = dog + (size_t)sc * P;
-    const float* next = dog + (size_t)(sc + 1) * P;
+    const gfloat* prev = dog + (size_t)(sc - 1) * P;
+    const gfloat* curr = dog + (size_t)sc * P;
+    const gfloat* next = dog + (size_t)(sc + 1) * P;
     const size_t c = (size_t)yi * pitch + xi;
     // extremum_contrast (src/lib.rs:606-626)
     const float g1 = (next[c] - prev[c]) / 2.f;
@@ -324,7 +338,7 @@ __global__ __launch_bounds__(256) void k_orient(const OrientLaunch L) {
                 uint8_t bin = 0xff;
                 float val = 0.0f;
                 if (yy > 0 && yy < H - 1 && xx > 0 && xx < W - 1) {
-                    const float* rw = img + (size_t)yy * pitch;
+                    const gfloat* rw = as_global(img) + (size_t)yy * pitch;
                     const float dx = rw[xx + 1] - rw[xx - 1];
                     const float dy = rw[xx - pitch] - rw[xx + pitch];
                     const float wexp = (float)(yp * yp + xp * xp) * gws;

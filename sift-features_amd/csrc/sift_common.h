@@ -97,6 +97,13 @@ __host__ __device__ __forceinline__ int reflect101(int p, int len) {
     return p;
 }
 
+// Global-address-space view of a pointer that the compiler only knows as
+// generic (e.g. loaded from a device array of plane pointers): its loads
+// become global_load (vmcnt only) instead of flat_load, which also counts
+// against lgkmcnt and serialises with the kernel's LDS traffic.
+typedef __attribute__((address_space(1))) const float gfloat;
+__device__ __forceinline__ const gfloat* as_global(const float* p) { return (const gfloat*)p; }
+
 // XCD-aware tile order for (tx, ty, frames) grids.  The dispatcher deals
 // workgroups round-robin over the 8 XCDs (each with a private 4 MB L2), so
 // neighbouring tiles of a plain grid land on different XCDs and every halo
