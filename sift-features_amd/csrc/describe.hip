@@ -70,6 +70,60 @@ __device__ __forceinline__ float row_hi(float hi0, float kk, bool row_only, floa
     return row_only ? (row_in(fy, k, c) ? 1e9f : -1e9f) : hi0 + kk * fy;
 }
 
+// Per-row column intervals of the rotated 4x4 region (window rows
+// -radius..radius, n <= 79: lanes own rows lane and lane + 64), widened by one
+// column on each side -- the reference's f32 predicate decides membership per
+// sample -- and their exclusive prefix sums (the compacted sample index of
+// each row's first sample), built with wave scans.
+__device__ __forceinline__ void build_row_table(int* rowlo, int* rowpre, int radius, float cos_s, float sin_s,
+                                                int lane) {
+    const int n = 2 * radius + 1;
+    const double c = cos_s, s = sin_s;
+    const bool cz = !(fabs(c) > 1e-30), sz = !(fabs(s) > 1e-30);
+    const double rc = cz ? 0.0 : 1.0 / c, rs = sz ? 0.0 : 1.0 / s;
+    int cnt[2] = {0, 0};
+#pragma unroll
+    for (int h = 0; h < 2; h++) {
+        const int row = lane + 64 * h;
+        if (row < n) {
+            const double yi = (double)(row - radius);
+            double lo = -radius, hi = radius;
+            bool empty = false;
+            if (!cz) {
+                const double a = (yi * s - 2.5) * rc, b = (yi * s + 2.5) * rc;
+                lo = fmax(lo, fmin(a, b) - 1.0);
+                hi = fmin(hi, fmax(a, b) + 1.0);
+            } else {
+                empty = !(fabs(yi * s) < 2.5 + 1e-3);
+            }
+            if (!sz) {
+                const double a = (-yi * c - 2.5) * rs, b = (-yi * c + 2.5) * rs;
+                lo = fmax(lo, fmin(a, b) - 1.0);
+                hi = fmin(hi, fmax(a, b) + 1.0);
+            } else {
+                empty = empty || !(fabs(yi * c) < 2.5 + 1e-3);
+            }
+            const int ilo = (int)floor(lo), ihi = (int)ceil(hi);
+            rowlo[row] = ilo;
+            cnt[h] = (empty || ihi < ilo) ? 0 : ihi - ilo + 1;
+        }
+    }
+    int s0 = cnt[0], s1 = cnt[1];
+#pragma unroll
+    for (int o = 1; o < 64; o <<= 1) {
+        const int a = __shfl_up(s0, o), b = __shfl_up(s1, o);
+        if (lane >= o) {
+            s0 += a;
+            s1 += b;
+        }
+    }
+    const int t0 = __shfl(s0, 63);
+    if (lane < n) rowpre[lane + 1] = s0;
+    if (lane + 64 < n) rowpre[lane + 65] = s1 + t0;
+    if (lane == 0) rowpre[0] = 0;
+    wave_sync();
+}
+
 // Normalisation (src/lib.rs:951-989) of the 128 interior bins held two per
 // lane (lane l: flat[2l], flat[2l+1]); chunk j = flat[4j..4j+4) = lanes 2j,
 // 2j+1, summed in the reference's exact chunk-of-4 order.
@@ -132,39 +186,7 @@ __device__ __forceinline__ void describe_wave_exact(const float* __restrict__ im
     const float sin_s = sin_ori / hist_width, cos_s = cos_ori / hist_width;
     const int n = 2 * radius + 1;
     // 1. per-row candidate column interval of the whole 4x4 region
-    for (int row = lane; row < n; row += 64) {
-        const double yi = (double)(row - radius);
-        const double c = cos_s, s = sin_s;
-        double lo = -radius, hi = radius;
-        bool empty = false;
-        if (fabs(c) > 1e-30) {
-            const double a = (yi * s - 2.5) / c, b = (yi * s + 2.5) / c;
-            lo = fmax(lo, fmin(a, b) - 1.0);
-            hi = fmin(hi, fmax(a, b) + 1.0);
-        } else {
-            empty = !(fabs(yi * s) < 2.5 + 1e-3);
-        }
-        if (fabs(s) > 1e-30) {
-            const double a = (-yi * c - 2.5) / s, b = (-yi * c + 2.5) / s;
-            lo = fmax(lo, fmin(a, b) - 1.0);
-            hi = fmin(hi, fmax(a, b) + 1.0);
-        } else {
-            empty = empty || !(fabs(yi * c) < 2.5 + 1e-3);
-        }
-        const int ilo = (int)floor(lo), ihi = (int)ceil(hi);
-        sc.rowlo[row] = ilo;
-        sc.rowpre[row + 1] = (empty || ihi < ilo) ? 0 : ihi - ilo + 1;
-    }
-    wave_sync();
-    if (lane == 0) {
-        int acc = 0;
-        sc.rowpre[0] = 0;
-        for (int r = 1; r <= n; r++) {
-            acc += sc.rowpre[r];
-            sc.rowpre[r] = acc;
-        }
-    }
-    wave_sync();
+    build_row_table(sc.rowlo, sc.rowpre, radius, cos_s, sin_s, lane);
     // lane role: interior cell (cr, cc) in 1..4, orientation bins b0, b0 + 1
     const int ci = lane >> 2;
     const int cr = 1 + (ci >> 2), cc = 1 + (ci & 3);
@@ -328,39 +350,7 @@ __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img
 #pragma unroll
     for (int i = 0; i < PRIV_STRIDE * NS / 4; i += 64)
         if (i + lane < PRIV_STRIDE * NS / 4) reinterpret_cast<float4*>(sc.h)[i + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
-    for (int row = lane; row < n; row += 64) {
-        const double yi = (double)(row - radius);
-        const double c = cos_s, s = sin_s;
-        double lo = -radius, hi = radius;
-        bool empty = false;
-        if (fabs(c) > 1e-30) {
-            const double a = (yi * s - 2.5) / c, b = (yi * s + 2.5) / c;
-            lo = fmax(lo, fmin(a, b) - 1.0);
-            hi = fmin(hi, fmax(a, b) + 1.0);
-        } else {
-            empty = !(fabs(yi * s) < 2.5 + 1e-3);
-        }
-        if (fabs(s) > 1e-30) {
-            const double a = (-yi * c - 2.5) / s, b = (-yi * c + 2.5) / s;
-            lo = fmax(lo, fmin(a, b) - 1.0);
-            hi = fmin(hi, fmax(a, b) + 1.0);
-        } else {
-            empty = empty || !(fabs(yi * c) < 2.5 + 1e-3);
-        }
-        const int ilo = (int)floor(lo), ihi = (int)ceil(hi);
-        sc.rowlo[row] = ilo;
-        sc.rowpre[row + 1] = (empty || ihi < ilo) ? 0 : ihi - ilo + 1;
-    }
-    wave_sync();
-    if (lane == 0) {
-        int acc = 0;
-        sc.rowpre[0] = 0;
-        for (int r = 1; r <= n; r++) {
-            acc += sc.rowpre[r];
-            sc.rowpre[r] = acc;
-        }
-    }
-    wave_sync();
+    build_row_table(sc.rowlo, sc.rowpre, radius, cos_s, sin_s, lane);
     const int total = sc.rowpre[n];
     // lane-strided samples: one load instruction touches ~64 neighbouring
     // pixels (2-3 cache lines) instead of 64 scattered ones
