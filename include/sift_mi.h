@@ -39,8 +39,10 @@ typedef struct {
 /* src/lib.rs:86-90 `trait Processing`: which blur / resize arithmetic the
  * pyramid uses.  OPENCV = `OpenCVProcessing` (src/opencv_processing.rs:38-74,
  * the backend the reference's golden snapshots pin).  IMAGEPROC =
- * `ImageprocProcessing` (src/lib.rs:993-1007) -- not implemented yet, the
- * calls return SIFT_MI_EUNSUPPORTED. */
+ * `ImageprocProcessing` (src/lib.rs:993-1007), the crate's default for
+ * `sift()`: imageproc 0.25 gaussian_blur_f32 + image 0.25 resize arithmetic,
+ * restated (those crates are not in the reference tree and no reference test
+ * runs this profile: parity unpinned). */
 typedef enum { SIFT_MI_PROFILE_OPENCV = 0, SIFT_MI_PROFILE_IMAGEPROC = 1 } sift_mi_profile;
 
 typedef enum {

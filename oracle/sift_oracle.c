@@ -311,18 +311,142 @@ static void cv_resize_nearest(const float* src, int sw, int sh, int dw, int dh, 
     free(xo);
 }
 
+/* ------------------------------------------------------------------ */
+/* PROFILE_IMAGEPROC: ImageprocProcessing (src/lib.rs:993-1007)         */
+/* Third-party code absent from /root/reference, restated from the      */
+/* published crates: imageproc 0.25.0 filter::gaussian_blur_f32 and     */
+/* image 0.25.2 imageops::resize (Triangle, Nearest).  No reference     */
+/* test runs this profile: PARITY UNPINNED.                 */
+/* ------------------------------------------------------------------ */
+
+/* imageproc gaussian_kernel_f32: radius ceil(2 sigma), taps
+ * (sqrt(2 pi) r)^-1 * exp(-x^2 / (2 r^2)) in f32, normalised by their f32 sum
+ * (summed in index order). */
+int oracle_ip_kernel(float sigma, float* k) {
+    const int r = (int)ceilf(2.0f * sigma);
+    const int n = 2 * r + 1;
+    const float norm = 1.0f / (sqrtf(2.0f * 3.14159265358979323846f) * sigma);
+    for (int i = 0; i <= r; i++) {
+        const float x = (float)i;
+        const float v = norm * expf(-(x * x) / (2.0f * (sigma * sigma)));
+        k[r + i] = v;
+        k[r - i] = v;
+    }
+    float sum = 0.0f;
+    for (int i = 0; i < n; i++) sum += k[i];
+    for (int i = 0; i < n; i++) k[i] = k[i] / sum;
+    return n;
+}
+
+static inline int clampi(int v, int lo, int hi) { return v < lo ? lo : (v > hi ? hi : v); }
+
+/* separable_filter_equal: horizontal then vertical, acc = acc + p * k from the
+ * first tap (unfused), clamp-to-edge borders; f32 output is not clamped. */
+static void ip_blur(const float* src, int w, int h, float sigma, float* dst) {
+    float k[64];
+    const int n = oracle_ip_kernel(sigma, k), r = n / 2;
+    float* tmp = (float*)malloc(sizeof(float) * (size_t)w * h);
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            float acc = 0.0f;
+            for (int i = 0; i < n; i++) acc = acc + src[(size_t)y * w + clampi(x + i - r, 0, w - 1)] * k[i];
+            tmp[(size_t)y * w + x] = acc;
+        }
+    for (int y = 0; y < h; y++)
+        for (int x = 0; x < w; x++) {
+            float acc = 0.0f;
+            for (int i = 0; i < n; i++) acc = acc + tmp[(size_t)clampi(y + i - r, 0, h - 1) * w + x] * k[i];
+            dst[(size_t)y * w + x] = acc;
+        }
+    free(tmp);
+}
+
+/* image::imageops::sample weights for one axis (vertical_sample /
+ * horizontal_sample): taps [left, right) with f32 weights normalised by their
+ * f32 sum.  support 1 = Triangle, 0 = Nearest (box). */
+int oracle_ip_axis(int src, int dst, int out, float support, int* left, float* wts) {
+    const float ratio = (float)src / (float)dst;
+    const float sratio = ratio < 1.0f ? 1.0f : ratio;
+    const float src_support = support * sratio;
+    float in = ((float)out + 0.5f) * ratio;
+    long l = (long)floorf(in - src_support);
+    l = l < 0 ? 0 : (l > src - 1 ? src - 1 : l);
+    long rt = (long)ceilf(in + src_support);
+    rt = rt < l + 1 ? l + 1 : (rt > src ? src : rt);
+    in = in - 0.5f;
+    float sum = 0.0f;
+    int n = 0;
+    for (long i = l; i < rt; i++) {
+        float wv;
+        if (support > 0.0f) {
+            const float t = fabsf(((float)i - in) / sratio);
+            wv = t < 1.0f ? 1.0f - t : 0.0f;
+        } else {
+            wv = 1.0f; /* box_kernel */
+        }
+        wts[n++] = wv;
+        sum += wv;
+    }
+    for (int i = 0; i < n; i++) wts[i] = wts[i] / sum;
+    *left = (int)l;
+    return n;
+}
+
+/* image::imageops::resize: vertical_sample into an f32 intermediate, then
+ * horizontal_sample, t = t + p * w (unfused) from the first tap; the result
+ * is clamped to [0, 1] (f32 DEFAULT_MIN/MAX_VALUE). */
+static void ip_resize(const float* src, int sw, int sh, int dw, int dh, float support, float* dst) {
+    if (sw == dw && sh == dh) {
+        memcpy(dst, src, sizeof(float) * (size_t)sw * sh);
+        return;
+    }
+    float* tmp = (float*)malloc(sizeof(float) * (size_t)sw * dh);
+    float wts[4096];
+    for (int y = 0; y < dh; y++) {
+        int l;
+        const int n = oracle_ip_axis(sh, dh, y, support, &l, wts);
+        for (int x = 0; x < sw; x++) {
+            float t = 0.0f;
+            for (int i = 0; i < n; i++) t = t + src[(size_t)(l + i) * sw + x] * wts[i];
+            tmp[(size_t)y * sw + x] = t;
+        }
+    }
+    for (int x = 0; x < dw; x++) {
+        int l;
+        const int n = oracle_ip_axis(sw, dw, x, support, &l, wts);
+        for (int y = 0; y < dh; y++) {
+            float t = 0.0f;
+            for (int i = 0; i < n; i++) t = t + tmp[(size_t)y * sw + l + i] * wts[i];
+            dst[(size_t)y * dw + x] = t < 0.0f ? 0.0f : (t > 1.0f ? 1.0f : t);
+        }
+    }
+    free(tmp);
+}
+
 /* Processing trait (src/lib.rs:86-90) dispatch. */
 int oracle_gaussian_blur(const float* src, int w, int h, double sigma, int profile, float* dst) {
+    if (profile == PROFILE_IMAGEPROC) {
+        ip_blur(src, w, h, (float)sigma, dst);
+        return 0;
+    }
     if (profile != PROFILE_OPENCV) return -1;
     cv_blur(src, w, h, sigma, dst);
     return 0;
 }
 int oracle_resize_linear(const float* src, int sw, int sh, int dw, int dh, int profile, float* dst) {
+    if (profile == PROFILE_IMAGEPROC) {
+        ip_resize(src, sw, sh, dw, dh, 1.0f, dst);
+        return 0;
+    }
     if (profile != PROFILE_OPENCV) return -1;
     cv_resize_linear(src, sw, sh, dw, dh, dst);
     return 0;
 }
 int oracle_resize_nearest(const float* src, int sw, int sh, int dw, int dh, int profile, float* dst) {
+    if (profile == PROFILE_IMAGEPROC) {
+        ip_resize(src, sw, sh, dw, dh, 0.0f, dst);
+        return 0;
+    }
     if (profile != PROFILE_OPENCV) return -1;
     cv_resize_nearest(src, sw, sh, dw, dh, dst);
     return 0;
@@ -364,14 +488,14 @@ void oracle_pyramid_free(opyr_t* p) {
 }
 
 opyr_t* oracle_precompute(const uint8_t* img, int w, int h, int stride, int profile) {
-    if (profile != PROFILE_OPENCV || w < 1 || h < 1) return NULL;
+    if ((profile != PROFILE_OPENCV && profile != PROFILE_IMAGEPROC) || w < 1 || h < 1) return NULL;
     /* create_seed_image (src/lib.rs:196-210) */
     float* f = (float*)malloc(sizeof(float) * (size_t)w * h);
     for (int y = 0; y < h; y++)
         for (int x = 0; x < w; x++) f[(size_t)y * w + x] = (float)img[(size_t)y * stride + x] / 255.0f;
     const int W0 = 2 * w, H0 = 2 * h;
     float* up = (float*)malloc(sizeof(float) * (size_t)W0 * H0);
-    cv_resize_linear(f, w, h, W0, H0, up);
+    oracle_resize_linear(f, w, h, W0, H0, profile, up);
     free(f);
     opyr_t* p = (opyr_t*)calloc(1, sizeof(opyr_t));
     p->n_octaves = oracle_n_octaves(w, h);
@@ -391,12 +515,13 @@ opyr_t* oracle_precompute(const uint8_t* img, int w, int h, int stride, int prof
         p->dog[o] = (float*)malloc(sizeof(float) * P * N_DOG_PER_OCTAVE);
         float* G = p->gauss[o];
         if (o == 0) {
-            cv_blur(up, ow, oh, oracle_seed_sigma(), G);
+            oracle_gaussian_blur(up, ow, oh, oracle_seed_sigma(), profile, G);
         } else {
             const float* prev = p->gauss[o - 1] + (size_t)3 * p->w[o - 1] * p->h[o - 1];
-            cv_resize_nearest(prev, p->w[o - 1], p->h[o - 1], ow, oh, G);
+            oracle_resize_nearest(prev, p->w[o - 1], p->h[o - 1], ow, oh, profile, G);
         }
-        for (int s = 1; s < N_IMAGES_PER_OCTAVE; s++) cv_blur(G + (s - 1) * P, ow, oh, sig[s], G + s * P);
+        for (int s = 1; s < N_IMAGES_PER_OCTAVE; s++)
+            oracle_gaussian_blur(G + (s - 1) * P, ow, oh, sig[s], profile, G + s * P);
         /* build_dog (src/lib.rs:271-279) */
         for (int s = 0; s < N_DOG_PER_OCTAVE; s++)
             for (size_t i = 0; i < P; i++) p->dog[o][s * P + i] = G[(s + 1) * P + i] - G[s * P + i];

@@ -159,10 +159,13 @@ __global__ __launch_bounds__(256) void k_detect(const DetectLaunch L) {
     }
     // threshold = floor(0.5 * 0.04 / 3) = 0 (src/lib.rs:460)
     const float threshold = floorf(0.5f * kContrastThreshold / (float)kScalesPerOctave);
+    // branch-free tests of the DT_RPT x 3 (row, scale) candidates of this
+    // thread: bit rr * 3 + (s_in - 1)
+    uint32_t okmask = 0;
 #pragma unroll
     for (int rr = 0; rr < DT_RPT; rr++) {
         const int y = y0 + ly0 + rr;
-        if (!xin || y < kImageBorder || y >= H - kImageBorder) continue;
+        const bool yin = xin && y >= kImageBorder && y < H - kImageBorder;
         // point_is_local_extremum (src/lib.rs:437-506): non-strict vs all 26
         // neighbours; per plane the 3x3 max / min (centre excluded on the
         // middle plane), then one compare per sign.
@@ -179,19 +182,24 @@ __global__ __launch_bounds__(256) void k_detect(const DetectLaunch L) {
             const float n8 = fminf(fminf(hmin[s_in][rr], hmin[s_in][rr + 2]), lr_min[s_in][rr]);
             const float mx = fmaxf(fmaxf(pmax[s_in - 1], pmax[s_in + 1]), m8);
             const float mn = fminf(fminf(pmin[s_in - 1], pmin[s_in + 1]), n8);
-            const bool ok = fabsf(val) > threshold && (val > 0.0f ? val >= mx : val <= mn);
-            if (!ok) continue;
-            // candidate -> refinement kernel (dense, so its dependent global
-            // loads overlap across many threads instead of stalling this tile)
-            const uint64_t key =
-                make_key((uint32_t)(L.img_base + b), (uint32_t)L.octave, (uint32_t)s_in, (uint32_t)y, (uint32_t)x);
-            const uint32_t li = atomicAdd(&lcount, 1u);
-            if (li < DT_LCAP) {
-                lcand[li] = key;
-            } else {
-                const uint32_t slot = atomicAdd(L.counter, 1u);
-                if (slot < L.cap) L.cand[slot] = key;
-            }
+            const bool ok = yin && fabsf(val) > threshold && (val > 0.0f ? val >= mx : val <= mn);
+            okmask |= (uint32_t)ok << (rr * kScalesPerOctave + s_in - 1);
+        }
+    }
+    // candidates -> refinement kernel (dense, so its dependent global loads
+    // overlap across many threads instead of stalling this tile)
+    while (okmask) {
+        const int bit = __builtin_ctz(okmask);
+        okmask &= okmask - 1;
+        const int rr = bit / kScalesPerOctave, s_in = bit - rr * kScalesPerOctave + 1;
+        const uint64_t key = make_key((uint32_t)(L.img_base + b), (uint32_t)L.octave, (uint32_t)s_in,
+                                      (uint32_t)(y0 + ly0 + rr), (uint32_t)x);
+        const uint32_t li = atomicAdd(&lcount, 1u);
+        if (li < DT_LCAP) {
+            lcand[li] = key;
+        } else {
+            const uint32_t slot = atomicAdd(L.counter, 1u);
+            if (slot < L.cap) L.cand[slot] = key;
         }
     }
     // one global atomic per block (a single hot counter serialises at the

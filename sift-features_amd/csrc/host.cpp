@@ -190,6 +190,102 @@ void cv_nearest_ofs(int ssz, int dsz, std::vector<int>& ofs) {
     }
 }
 
+// ---- ImageprocProcessing profile (src/lib.rs:993-1007) ---------------------
+// imageproc 0.25.0 gaussian_kernel_f32 and image 0.25.2 imageops::resize
+// sampling weights, restated (third-party code absent from /root/reference;
+// parity unpinned -- DESIGN.md).  Same f32 arithmetic as oracle/sift_oracle.c.
+int ip_blur_taps(float sigma, BlurTaps* t) {
+    const int r = (int)std::ceil(2.0f * sigma);
+    if (r < 1 || r > 24) return -1;
+    const int n = 2 * r + 1;
+    float k[64];
+    const float norm = 1.0f / (std::sqrt(2.0f * 3.14159265358979323846f) * sigma);
+    for (int i = 0; i <= r; i++) {
+        const float x = (float)i;
+        const float v = norm * std::exp(-(x * x) / (2.0f * (sigma * sigma)));
+        k[r + i] = v;
+        k[r - i] = v;
+    }
+    float sum = 0.0f;
+    for (int i = 0; i < n; i++) sum += k[i];
+    std::memset(t, 0, sizeof(*t));
+    for (int i = 0; i <= r; i++) t->k[i] = k[r + i] / sum;
+    return r;
+}
+
+// One axis of image's vertical_sample / horizontal_sample: taps [left, left+n)
+// with normalised f32 weights; support 1 = Triangle, 0 = Nearest.
+int ip_axis(int src, int dst, int out, float support, int* left, float* w) {
+    const float ratio = (float)src / (float)dst;
+    const float sratio = ratio < 1.0f ? 1.0f : ratio;
+    const float src_support = support * sratio;
+    float in = ((float)out + 0.5f) * ratio;
+    long l = (long)std::floor(in - src_support);
+    l = l < 0 ? 0 : (l > src - 1 ? src - 1 : l);
+    long rt = (long)std::ceil(in + src_support);
+    rt = rt < l + 1 ? l + 1 : (rt > src ? src : rt);
+    in = in - 0.5f;
+    float sum = 0.0f;
+    int n = 0;
+    for (long i = l; i < rt; i++) {
+        float v = 1.0f;  // box_kernel
+        if (support > 0.0f) {
+            const float a = std::fabs(((float)i - in) / sratio);
+            v = a < 1.0f ? 1.0f - a : 0.0f;
+        }
+        w[n++] = v;
+        sum += v;
+    }
+    for (int i = 0; i < n; i++) w[i] = w[i] / sum;
+    *left = (int)l;
+    return n;
+}
+
+// Device tables of one resize (both axes), taps padded with zero weights.
+struct IpTabDev {
+    DevBuf<int> xl, yl;
+    DevBuf<float> xw, yw;
+    int xtaps = 0, ytaps = 0;
+    int upload(int sw, int sh, int dw, int dh, float support, int min_taps, hipStream_t st) {
+        auto axis = [&](int src, int dst, std::vector<int>& L, std::vector<float>& Wt, int& taps) {
+            std::vector<std::vector<float>> ws(dst);
+            L.resize(dst);
+            taps = min_taps;
+            std::vector<float> w(4096);
+            for (int o = 0; o < dst; o++) {
+                const int n = ip_axis(src, dst, o, support, &L[o], w.data());
+                ws[o].assign(w.begin(), w.begin() + n);
+                taps = std::max(taps, n);
+            }
+            Wt.assign((size_t)dst * taps, 0.0f);
+            for (int o = 0; o < dst; o++)
+                for (size_t k = 0; k < ws[o].size(); k++) Wt[(size_t)o * taps + k] = ws[o][k];
+        };
+        std::vector<int> lx, ly;
+        std::vector<float> wx, wy;
+        axis(sw, dw, lx, wx, xtaps);
+        axis(sh, dh, ly, wy, ytaps);
+        if (xtaps > 64 || ytaps > 64) return fail(SIFT_MI_EUNSUPPORTED, "resize ratio too large (> 64 taps)");
+        CHK(xl.ensure(dw));
+        CHK(yl.ensure(dh));
+        CHK(xw.ensure(wx.size()));
+        CHK(yw.ensure(wy.size()));
+        HIPCHK(hipMemcpyAsync(xl.p, lx.data(), dw * sizeof(int), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(yl.p, ly.data(), dh * sizeof(int), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(xw.p, wx.data(), wx.size() * sizeof(float), hipMemcpyHostToDevice, st));
+        HIPCHK(hipMemcpyAsync(yw.p, wy.data(), wy.size() * sizeof(float), hipMemcpyHostToDevice, st));
+        HIPCHK(hipStreamSynchronize(st));
+        return 0;
+    }
+    IpResizeTab tab() const { return IpResizeTab{xl.p, xw.p, yl.p, yw.p}; }
+    void release() {
+        xl.release();
+        yl.release();
+        xw.release();
+        yw.release();
+    }
+};
+
 struct ResizeTabDev {
     DevBuf<int> xofs, yofs;
     DevBuf<float> xa0, xa1, ya0, ya1;
@@ -241,7 +337,9 @@ struct Plan {
     std::vector<size_t> px;          // real pixels per octave image (W * H)
     std::vector<size_t> goff, doff;  // float offsets of octave arenas
     DevBuf<float> arena;             // [G_0 | D_0 | G_1 | D_1 ...], each chunk-major
-    ResizeTabDev seed_tab;
+    int profile = SIFT_MI_PROFILE_OPENCV;
+    ResizeTabDev seed_tab;  // OpenCV profile
+    IpTabDev seed_iptab;    // Imageproc profile
     DevBuf<const float*> d_gauss, d_dog;
     DevBuf<size_t> d_gstride, d_dstride;
     DevBuf<int> d_ow, d_oh, d_opitch;
@@ -259,6 +357,7 @@ struct Plan {
     void release() {
         arena.release();
         seed_tab.release();
+        seed_iptab.release();
         d_gauss.release();
         d_gstride.release();
         d_dog.release();
@@ -352,8 +451,10 @@ uint32_t auto_chunk(const Plan& p_probe_w_h, uint32_t w, uint32_t h, uint32_t n)
 
 int ensure_plan(sift_mi_ctx* c, uint32_t w, uint32_t h, uint32_t chunk) {
     Plan& p = c->plan;
-    if (p.w == w && p.h == h && p.chunk >= chunk && p.arena.p) return 0;
-    if (!(p.w == w && p.h == h)) p.release();
+    if (p.w == w && p.h == h && p.chunk >= chunk && p.arena.p && p.profile == (int)c->profile) return 0;
+    if (!(p.w == w && p.h == h && p.profile == (int)c->profile)) p.release();
+    p.profile = (int)c->profile;
+    const bool ip = c->profile == SIFT_MI_PROFILE_IMAGEPROC;
     p.w = w;
     p.h = h;
     p.chunk = chunk;
@@ -382,14 +483,25 @@ int ensure_plan(sift_mi_ctx* c, uint32_t w, uint32_t h, uint32_t chunk) {
         total += (size_t)chunk * kDogPerOctave * p.P[o];
         total = (total + 63) & ~(size_t)63;  // 256-B aligned octave arenas
         if (o + 1 < p.n_oct) {
-            // nearest 1/2 must be source pixel (2x, 2y) for the fused epilogue
-            std::vector<int> xo, yo;
-            cv_nearest_ofs(ow, ow / 2, xo);
-            cv_nearest_ofs(oh, oh / 2, yo);
-            for (int i = 0; i < (int)xo.size(); i++)
-                if (xo[i] != 2 * i) return fail(SIFT_MI_EUNSUPPORTED, "nearest offset != 2x");
-            for (int i = 0; i < (int)yo.size(); i++)
-                if (yo[i] != 2 * i) return fail(SIFT_MI_EUNSUPPORTED, "nearest offset != 2y");
+            // nearest 1/2 must be source pixel (2x, 2y) (OpenCV INTER_NEAREST)
+            // or (2x + 1, 2y + 1) (image Nearest) for the fused epilogue
+            const int par = ip ? 1 : 0;
+            for (int axis = 0; axis < 2; axis++) {
+                const int src = axis ? oh : ow, dst = src / 2;
+                std::vector<int> xo;
+                if (ip) {
+                    xo.resize(dst);
+                    float wt[8];
+                    for (int i = 0; i < dst; i++) {
+                        const int n = ip_axis(src, dst, i, 0.0f, &xo[i], wt);
+                        if (n != 1) return fail(SIFT_MI_EUNSUPPORTED, "nearest 1/2 with more than one tap");
+                    }
+                } else {
+                    cv_nearest_ofs(src, dst, xo);
+                }
+                for (int i = 0; i < dst; i++)
+                    if (xo[i] != 2 * i + par) return fail(SIFT_MI_EUNSUPPORTED, "nearest 1/2 offset is not 2x (+1)");
+            }
         }
         ow /= 2;
         oh /= 2;
@@ -397,7 +509,12 @@ int ensure_plan(sift_mi_ctx* c, uint32_t w, uint32_t h, uint32_t chunk) {
     p.algo_bytes_per_frame = (uint64_t)w * h + 44ull * sum_p;
     CHK(p.arena.ensure(total));
     hipStream_t st = c->stream;
-    CHK(p.seed_tab.upload((int)w, (int)h, 2 * (int)w, 2 * (int)h, st));
+    if (ip)
+        CHK(p.seed_iptab.upload((int)w, (int)h, 2 * (int)w, 2 * (int)h, 1.0f, kIpTaps, st));
+    else
+        CHK(p.seed_tab.upload((int)w, (int)h, 2 * (int)w, 2 * (int)h, st));
+    if (ip && (p.seed_iptab.xtaps > kIpTaps || p.seed_iptab.ytaps > kIpTaps))
+        return fail(SIFT_MI_EUNSUPPORTED, "2x Triangle upsample with more than 3 taps");
     std::vector<const float*> gp(p.n_oct), dp(p.n_oct);
     std::vector<size_t> gs(p.n_oct), ds(p.n_oct);
     for (int o = 0; o < p.n_oct; o++) {
@@ -421,10 +538,12 @@ int ensure_plan(sift_mi_ctx* c, uint32_t w, uint32_t h, uint32_t chunk) {
     HIPCHK(hipMemcpyAsync(p.d_oh.p, p.oh.data(), p.n_oct * sizeof(int), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(p.d_opitch.p, p.opitch.data(), p.n_oct * sizeof(int), hipMemcpyHostToDevice, st));
     HIPCHK(hipStreamSynchronize(st));
-    p.seed_r = cv_blur_taps(seed_sigma(), &p.seed_taps);
+    // P::gaussian_blur(img, sigma: f64); ImageprocProcessing passes sigma as f32
+    p.seed_r = ip ? ip_blur_taps((float)seed_sigma(), &p.seed_taps) : cv_blur_taps(seed_sigma(), &p.seed_taps);
     double sig[kImagesPerOctave];
     octave_sigmas(sig);
-    for (int s = 1; s < kImagesPerOctave; s++) p.oct_r[s] = cv_blur_taps(sig[s], &p.oct_taps[s]);
+    for (int s = 1; s < kImagesPerOctave; s++)
+        p.oct_r[s] = ip ? ip_blur_taps((float)sig[s], &p.oct_taps[s]) : cv_blur_taps(sig[s], &p.oct_taps[s]);
     return 0;
 }
 
@@ -442,6 +561,8 @@ int run_pyramid(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, siz
     S.sh = (int)p.h;
     S.sw = (int)p.w;
     S.tab = p.seed_tab.tab;
+    S.iptab = p.seed_iptab.tab();
+    S.profile = p.profile;
     S.dst = p.gauss(0);
     S.dst_img_stride = p.gstride(0);
     S.W = p.ow[0];
@@ -475,6 +596,7 @@ int run_pyramid(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, siz
             B.pitch = p.opitch[o];
             B.n_img = (int)n;
             B.taps = p.oct_taps[s];
+            B.profile = p.profile;
             if (launch_blur(p.oct_r[s], B, st)) return fail(SIFT_MI_EUNSUPPORTED, "octave blur radius");
             launches++;
         }
@@ -787,8 +909,6 @@ int check_frame_args(uint32_t w, uint32_t h, size_t stride) {
 int extract_device(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, uint32_t n, uint32_t w, uint32_t h,
                    size_t stride, int64_t limit, size_t* offsets) {
     CHK(check_frame_args(w, h, stride));
-    if (c->profile != SIFT_MI_PROFILE_OPENCV)
-        return fail(SIFT_MI_EUNSUPPORTED, "IMAGEPROC profile not implemented (parity unpinned)");
     const uint32_t chunk =
         std::min(kMaxChunk, c->chunk_override ? std::min(c->chunk_override, n) : auto_chunk(c->plan, w, h, n));
     CHK(ensure_plan(c, w, h, chunk));
@@ -820,6 +940,37 @@ int extract_device(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, 
     if (offsets) offsets[n] = c->n_result;
     c->have_result = true;
     return 0;
+}
+
+// image::imageops::resize on a host f32 image (Imageproc profile ops).
+int ip_resize_op(sift_mi_ctx* c, const float* src, uint32_t w, uint32_t h, uint32_t dw, uint32_t dh, float support,
+                 float* dst) {
+    if (w == dw && h == dh) {  // image's resize copies when the size is unchanged
+        std::memcpy(dst, src, sizeof(float) * (size_t)w * h);
+        return 0;
+    }
+    IpTabDev tab;
+    int rc = tab.upload((int)w, (int)h, (int)dw, (int)dh, support, 1, c->stream);
+    DevBuf<float> a, t, b;
+    if (!rc) rc = a.ensure((size_t)w * h);
+    if (!rc) rc = t.ensure((size_t)w * dh);
+    if (!rc) rc = b.ensure((size_t)dw * dh);
+    if (!rc) {
+        if (hipMemcpyAsync(a.p, src, (size_t)w * h * 4, hipMemcpyHostToDevice, c->stream) != hipSuccess)
+            rc = fail(SIFT_MI_EHIP, "H2D failed");
+    }
+    if (!rc) {
+        launch_ip_resize_f32(a.p, (int)w, (int)h, tab.xl.p, tab.xw.p, tab.xtaps, tab.yl.p, tab.yw.p, tab.ytaps, t.p,
+                             b.p, (int)dw, (int)dh, c->stream);
+        if (hipMemcpyAsync(dst, b.p, (size_t)dw * dh * 4, hipMemcpyDeviceToHost, c->stream) != hipSuccess ||
+            hipStreamSynchronize(c->stream) != hipSuccess)
+            rc = fail(SIFT_MI_EHIP, "resize failed");
+    }
+    a.release();
+    t.release();
+    b.release();
+    tab.release();
+    return rc;
 }
 
 int upload_frames(sift_mi_ctx* c, const uint8_t* const* frames, uint32_t n, uint32_t w, uint32_t h, size_t stride) {
@@ -1030,7 +1181,6 @@ int sift_mi_precompute(sift_mi_ctx* c, const uint8_t* pixels, uint32_t w, uint32
                        size_t* n_octaves) {
     if (!c || !pixels) return fail(SIFT_MI_EINVAL, "bad arguments");
     CHK(check_frame_args(w, h, stride));
-    if (c->profile != SIFT_MI_PROFILE_OPENCV) return fail(SIFT_MI_EUNSUPPORTED, "IMAGEPROC profile not implemented");
     CHK(set_device(c));
     const uint8_t* frames[1] = {pixels};
     CHK(upload_frames(c, frames, 1, w, h, stride));
@@ -1117,10 +1267,10 @@ int sift_mi_compute_descriptor(sift_mi_ctx* c, const float* img, uint32_t w, uin
 // ---- Processing ops ------------------------------------------------------
 int sift_mi_gaussian_blur(sift_mi_ctx* c, const float* src, uint32_t w, uint32_t h, double sigma, float* dst) {
     if (!c || !src || !dst || w < 2 || h < 2 || !(sigma > 0)) return fail(SIFT_MI_EINVAL, "bad arguments");
-    if (c->profile != SIFT_MI_PROFILE_OPENCV) return fail(SIFT_MI_EUNSUPPORTED, "IMAGEPROC profile not implemented");
     CHK(set_device(c));
     BlurTaps taps;
-    const int r = cv_blur_taps(sigma, &taps);
+    const bool ip = c->profile == SIFT_MI_PROFILE_IMAGEPROC;
+    const int r = ip ? ip_blur_taps((float)sigma, &taps) : cv_blur_taps(sigma, &taps);
     if (r < 1) return fail(SIFT_MI_EUNSUPPORTED, "blur radius outside 1..24");
     DevBuf<float> a, b;
     const size_t pitch = ((size_t)w + 63) & ~(size_t)63;  // same row alignment as the pyramid
@@ -1135,6 +1285,7 @@ int sift_mi_gaussian_blur(sift_mi_ctx* c, const float* src, uint32_t w, uint32_t
     L.pitch = (int)pitch;
     L.n_img = 1;
     L.taps = taps;
+    L.profile = ip ? kProfileImageproc : kProfileOpenCV;
     if (hipMemcpy2DAsync(a.p, pitch * 4, src, (size_t)w * 4, (size_t)w * 4, h, hipMemcpyHostToDevice, c->stream) !=
             hipSuccess ||
         launch_blur(r, L, c->stream) != 0 ||
@@ -1150,8 +1301,8 @@ int sift_mi_gaussian_blur(sift_mi_ctx* c, const float* src, uint32_t w, uint32_t
 int sift_mi_resize_linear(sift_mi_ctx* c, const float* src, uint32_t w, uint32_t h, uint32_t dw, uint32_t dh,
                           float* dst) {
     if (!c || !src || !dst || !w || !h || !dw || !dh) return fail(SIFT_MI_EINVAL, "bad arguments");
-    if (c->profile != SIFT_MI_PROFILE_OPENCV) return fail(SIFT_MI_EUNSUPPORTED, "IMAGEPROC profile not implemented");
     CHK(set_device(c));
+    if (c->profile == SIFT_MI_PROFILE_IMAGEPROC) return ip_resize_op(c, src, w, h, dw, dh, 1.0f, dst);
     ResizeTabDev tab;
     CHK(tab.upload((int)w, (int)h, (int)dw, (int)dh, c->stream));
     DevBuf<float> a, b;
@@ -1172,8 +1323,8 @@ int sift_mi_resize_linear(sift_mi_ctx* c, const float* src, uint32_t w, uint32_t
 int sift_mi_resize_nearest(sift_mi_ctx* c, const float* src, uint32_t w, uint32_t h, uint32_t dw, uint32_t dh,
                            float* dst) {
     if (!c || !src || !dst || !w || !h || !dw || !dh) return fail(SIFT_MI_EINVAL, "bad arguments");
-    if (c->profile != SIFT_MI_PROFILE_OPENCV) return fail(SIFT_MI_EUNSUPPORTED, "IMAGEPROC profile not implemented");
     CHK(set_device(c));
+    if (c->profile == SIFT_MI_PROFILE_IMAGEPROC) return ip_resize_op(c, src, w, h, dw, dh, 0.0f, dst);
     std::vector<int> xo, yo;
     cv_nearest_ofs((int)w, (int)dw, xo);
     cv_nearest_ofs((int)h, (int)dh, yo);

@@ -72,7 +72,11 @@ typedef __attribute__((address_space(3))) volatile f4v lds_f4v;
 // pair them into ds_read2_b64, which runs at half that rate)
 typedef __attribute__((address_space(3))) volatile f2v lds_f2v;
 
-template <int R, int TH>
+// P = kProfileOpenCV: OpenCV's RowFilter (fma chain) + SymmColumnFilter
+// (centre product, fma of pair sums).  P = kProfileImageproc: imageproc's
+// separable_filter -- acc = acc + p * k from the first tap (unfused) in both
+// passes -- and the nearest 1/2 at pixel (2x + 1, 2y + 1) (image's Nearest).
+template <int R, int TH, int P = kProfileOpenCV>
 __device__ __forceinline__ void blur_tile_compute(const float* __restrict__ tin, float* __restrict__ th,
                                                   const BlurTaps& taps, int x0, int y0, int W, int H, int pitch,
                                                   float* __restrict__ dst, float* __restrict__ dog,
@@ -126,7 +130,9 @@ __device__ __forceinline__ void blur_tile_compute(const float* __restrict__ tin,
         for (int t = 1; t <= 2 * R; t++) {
             const float kt = taps.k[t > R ? t - R : R - t];
 #pragma unroll
-            for (int o = 0; o < G::QW; o++) acc[o] = __builtin_fmaf(v[G::OFF + o + t], kt, acc[o]);
+            for (int o = 0; o < G::QW; o++)
+                acc[o] = P == kProfileOpenCV ? __builtin_fmaf(v[G::OFF + o + t], kt, acc[o])
+                                             : acc[o] + v[G::OFF + o + t] * kt;
         }
         // all lanes of this row have their window in registers (in-order LDS)
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
@@ -151,11 +157,23 @@ __device__ __forceinline__ void blur_tile_compute(const float* __restrict__ tin,
     for (int o = 0; o < VB2; o++) {
         const int gy = y0 + band * VB2 + o;
         if (!full && gy >= H) break;
-        f2v acc = v[o + R] * k0;
+        f2v acc;
+        if constexpr (P == kProfileOpenCV) {
+            acc = v[o + R] * k0;
 #pragma unroll
-        for (int t = 1; t <= R; t++) {
-            const f2v kt = {taps.k[t], taps.k[t]};
-            acc = __builtin_elementwise_fma(v[o + R + t] + v[o + R - t], kt, acc);
+            for (int t = 1; t <= R; t++) {
+                const f2v kt = {taps.k[t], taps.k[t]};
+                acc = __builtin_elementwise_fma(v[o + R + t] + v[o + R - t], kt, acc);
+            }
+        } else {
+            const f2v kr = {taps.k[R], taps.k[R]};
+            acc = v[o] * kr;
+#pragma unroll
+            for (int t = 1; t <= 2 * R; t++) {
+                const float k = taps.k[t > R ? t - R : R - t];
+                const f2v kt = {k, k};
+                acc = acc + v[o + t] * kt;
+            }
         }
         const size_t off = (size_t)gy * pitch + gx;
         if (pair) {
@@ -165,13 +183,19 @@ __device__ __forceinline__ void blur_tile_compute(const float* __restrict__ tin,
             dst[off] = acc.x;
             if (dog) dog[off] = acc.x - centre[o].x;
         }
-        // nearest 1/2 (cv::resize INTER_NEAREST): pixel (2x, 2y); gy parity == o parity
-        if ((o & 1) == 0 && nxt && (gx >> 1) < wn && (gy >> 1) < hn)
-            nxt[(size_t)(gy >> 1) * pitch_n + (gx >> 1)] = acc.x;
+        // nearest 1/2: pixel (2x, 2y) for cv::resize INTER_NEAREST, (2x + 1,
+        // 2y + 1) for image's Nearest; gy parity == o parity
+        if constexpr (P == kProfileOpenCV) {
+            if ((o & 1) == 0 && nxt && (gx >> 1) < wn && (gy >> 1) < hn)
+                nxt[(size_t)(gy >> 1) * pitch_n + (gx >> 1)] = acc.x;
+        } else {
+            if ((o & 1) == 1 && nxt && pair && (gx >> 1) < wn && (gy >> 1) < hn)
+                nxt[(size_t)(gy >> 1) * pitch_n + (gx >> 1)] = acc.y;
+        }
     }
 }
 
-template <int R, int TH>
+template <int R, int TH, int P>
 __global__ __launch_bounds__(256) void k_blur(const float* __restrict__ src, size_t src_img_stride,
                                               float* __restrict__ dst, size_t dst_img_stride,
                                               float* __restrict__ dog, size_t dog_img_stride,
@@ -210,12 +234,14 @@ __global__ __launch_bounds__(256) void k_blur(const float* __restrict__ src, siz
     } else {
         for (int i = tid; i < G::IH * G::IWV; i += 256) {
             const int ly = i / G::IWV, lx = i - ly * G::IWV;
-            const int gy = reflect101(y0 - R + ly, H), gx = reflect101(x0 - G::HWL + lx, W);
+            // BORDER_REFLECT_101 (OpenCV) / clamp to edge (imageproc)
+            const int gy = P == kProfileOpenCV ? reflect101(y0 - R + ly, H) : clamp_idx(y0 - R + ly, H);
+            const int gx = P == kProfileOpenCV ? reflect101(x0 - G::HWL + lx, W) : clamp_idx(x0 - G::HWL + lx, W);
             tin[ly * G::IWP + lx] = src[(size_t)gy * pitch + gx];
         }
     }
     __syncthreads();
-    blur_tile_compute<R, TH>(tin, th, taps, x0, y0, W, H, pitch, dst + b * dst_img_stride,
+    blur_tile_compute<R, TH, P>(tin, th, taps, x0, y0, W, H, pitch, dst + b * dst_img_stride,
                              dog ? dog + b * dog_img_stride : nullptr, nxt ? nxt + b * nxt_img_stride : nullptr,
                              pitch_n, wn, hn);
 }
@@ -358,6 +384,118 @@ __global__ __launch_bounds__(256) void k_seed(const uint8_t* __restrict__ frames
 }
 
 // ---------------------------------------------------------------------------
+// Seed, Imageproc profile: u8 -> f32 (v / 255) -> image::imageops::resize
+// Triangle 2x (vertical_sample into an f32 intermediate, then
+// horizontal_sample; t = t + p * w from the first tap, result clamped to
+// [0, 1]) -> imageproc gaussian_blur_f32 (clamp-to-edge), fused like k_seed.
+// ---------------------------------------------------------------------------
+template <int R, int TH>
+__global__ __launch_bounds__(256) void k_seed_ip(const uint8_t* __restrict__ frames, size_t frame_pitch,
+                                                 size_t row_stride, int sh, int sw, const IpResizeTab tab,
+                                                 float* __restrict__ dst, size_t dst_img_stride, int W, int H,
+                                                 int pitch, const BlurTaps taps) {
+    using G = BlurGeom<R, TH>;
+    constexpr int SR = G::IH / 2 + kIpTaps + 2, SC = G::IWV / 2 + kIpTaps + 2;
+    static_assert(G::IH <= 128 && G::IWV <= 128, "span reduction covers 128 positions per axis");
+    __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
+    __shared__ float srcf[SR * SC];     // u8 -> f32 source window
+    __shared__ float vbuf[G::IH * SC];  // vertical_sample rows of the window
+    __shared__ float lut[256];
+    __shared__ int span[4][2];
+    __shared__ int txl[G::IWV], tyl[G::IH];
+    __shared__ float txw[G::IWV][kIpTaps], tyw[G::IH][kIpTaps];
+    float* tin = lds;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    lut[tid] = (float)tid / 255.0f;
+    const TileId tile = xcd_tile();
+    const int x0 = tile.x * G::TW, y0 = tile.y * G::TH;
+    const size_t b = tile.z;
+    const uint8_t* src = frames + b * frame_pitch;
+    {
+        // window column (threads 0..127) / row (128..255): clamp-to-edge
+        // position, its sampling taps, and the source span they cover
+        const int t = tid & 127;
+        const bool isx = tid < 128;
+        const bool act = isx ? t < G::IWV : t < G::IH;
+        const int g = act ? (isx ? clamp_idx(x0 - G::HWL + t, W) : clamp_idx(y0 - R + t, H)) : 0;
+        int s0 = 0, s1 = 0;
+        if (act) {
+            const int* lp = isx ? tab.xl : tab.yl;
+            const float* wp = isx ? tab.xw : tab.yw;
+            s0 = lp[g];
+            s1 = min(s0 + kIpTaps - 1, (isx ? sw : sh) - 1);
+#pragma unroll
+            for (int k = 0; k < kIpTaps; k++) {
+                if (isx)
+                    txw[t][k] = wp[g * kIpTaps + k];
+                else
+                    tyw[t][k] = wp[g * kIpTaps + k];
+            }
+            if (isx)
+                txl[t] = s0;
+            else
+                tyl[t] = s0;
+        }
+        int mn = act ? s0 : INT_MAX, mx = act ? s1 : INT_MIN;
+#pragma unroll
+        for (int o = 32; o >= 1; o >>= 1) {
+            mn = min(mn, __shfl_xor(mn, o));
+            mx = max(mx, __shfl_xor(mx, o));
+        }
+        if (lane == 0) {
+            span[wv][0] = mn;
+            span[wv][1] = mx;
+        }
+    }
+    __syncthreads();
+    const int sxa = min(span[0][0], span[1][0]), sxb = max(span[0][1], span[1][1]);
+    const int sya = min(span[2][0], span[3][0]), syb = max(span[2][1], span[3][1]);
+    const int nc = sxb - sxa + 1, nr = syb - sya + 1;
+    if (nc <= SC && nr <= SR) {
+        for (int r = wv; r < nr; r += 4)
+            for (int c = lane; c < nc; c += 64) srcf[r * SC + c] = lut[src[(size_t)(sya + r) * row_stride + sxa + c]];
+        __syncthreads();
+        // vertical_sample: window row ly over the source columns
+        for (int i = tid; i < G::IH * nc; i += 256) {
+            const int ly = i / nc, c = i - ly * nc;
+            const int l = tyl[ly] - sya;
+            float acc = 0.0f;
+#pragma unroll
+            for (int k = 0; k < kIpTaps; k++) acc = acc + srcf[min(l + k, nr - 1) * SC + c] * tyw[ly][k];
+            vbuf[ly * SC + c] = acc;
+        }
+        __syncthreads();
+        // horizontal_sample, clamped to [0, 1]
+        for (int i = tid; i < G::IH * G::IWV; i += 256) {
+            const int ly = i / G::IWV, lx = i - ly * G::IWV;
+            const int l = txl[lx] - sxa;
+            float acc = 0.0f;
+#pragma unroll
+            for (int k = 0; k < kIpTaps; k++) acc = acc + vbuf[ly * SC + min(l + k, nc - 1)] * txw[lx][k];
+            tin[ly * G::IWP + lx] = fminf(fmaxf(acc, 0.0f), 1.0f);
+        }
+    } else {  // degenerate shapes: direct gathers
+        for (int i = tid; i < G::IH * G::IWV; i += 256) {
+            const int ly = i / G::IWV, lx = i - ly * G::IWV;
+            float acc = 0.0f;
+#pragma unroll
+            for (int kx = 0; kx < kIpTaps; kx++) {
+                const int cx = min(txl[lx] + kx, sw - 1);
+                float v = 0.0f;
+#pragma unroll
+                for (int ky = 0; ky < kIpTaps; ky++)
+                    v = v + lut[src[(size_t)min(tyl[ly] + ky, sh - 1) * row_stride + cx]] * tyw[ly][ky];
+                acc = acc + v * txw[lx][kx];
+            }
+            tin[ly * G::IWP + lx] = fminf(fmaxf(acc, 0.0f), 1.0f);
+        }
+    }
+    __syncthreads();
+    blur_tile_compute<R, TH, kProfileImageproc>(tin, lds, taps, x0, y0, W, H, pitch, dst + b * dst_img_stride, nullptr,
+                                                nullptr, 0, 0, 0);
+}
+
+// ---------------------------------------------------------------------------
 // launchers
 // ---------------------------------------------------------------------------
 template <int R>
@@ -365,9 +503,14 @@ static void launch_blur_r(const BlurLaunch& L, hipStream_t st) {
     constexpr int TH = R >= 10 ? 64 : 32;  // measured: tools/ubench_kernels.hip blur
     using G = BlurGeom<R, TH>;
     dim3 grid((L.W + G::TW - 1) / G::TW, (L.H + G::TH - 1) / G::TH, L.n_img);
-    hipLaunchKernelGGL((k_blur<R, TH>), grid, dim3(256), 0, st, L.src, L.src_img_stride, L.dst, L.dst_img_stride,
-                       L.dog, L.dog_img_stride, L.nxt, L.nxt_img_stride, L.pitch_n, L.wn, L.hn, L.W, L.H, L.pitch,
-                       L.taps);
+    if (L.profile == kProfileImageproc)
+        hipLaunchKernelGGL((k_blur<R, TH, kProfileImageproc>), grid, dim3(256), 0, st, L.src, L.src_img_stride, L.dst,
+                           L.dst_img_stride, L.dog, L.dog_img_stride, L.nxt, L.nxt_img_stride, L.pitch_n, L.wn, L.hn,
+                           L.W, L.H, L.pitch, L.taps);
+    else
+        hipLaunchKernelGGL((k_blur<R, TH, kProfileOpenCV>), grid, dim3(256), 0, st, L.src, L.src_img_stride, L.dst,
+                           L.dst_img_stride, L.dog, L.dog_img_stride, L.nxt, L.nxt_img_stride, L.pitch_n, L.wn, L.hn,
+                           L.W, L.H, L.pitch, L.taps);
 }
 
 int launch_blur(int R, const BlurLaunch& L, hipStream_t st) {
@@ -392,14 +535,26 @@ static void launch_seed_r(const SeedLaunch& L, hipStream_t st) {
                        L.dst, L.dst_img_stride, L.W, L.H, L.pitch, L.taps);
 }
 
+template <int R>
+static void launch_seed_ip_r(const SeedLaunch& L, hipStream_t st) {
+    constexpr int TH = 32;
+    using G = BlurGeom<R, TH>;
+    dim3 grid((L.W + G::TW - 1) / G::TW, (L.H + G::TH - 1) / G::TH, L.n_img);
+    hipLaunchKernelGGL((k_seed_ip<R, TH>), grid, dim3(256), 0, st, L.frames, L.frame_pitch, L.row_stride, L.sh, L.sw,
+                       L.iptab, L.dst, L.dst_img_stride, L.W, L.H, L.pitch, L.taps);
+}
+
 int launch_seed(int R, const SeedLaunch& L, hipStream_t st) {
-    switch (R) {
-        case 5:
-            launch_seed_r<5>(L, st);
-            return 0;
-        default:
-            return -1;  // seed sigma is a constant: cvRound(1.249 * 8 + 1) | 1 = 11 taps
+    // the seed sigma is a constant: OpenCV cvRound(1.249 * 8 + 1) | 1 = 11
+    // taps (R = 5); imageproc ceil(2 * 1.249) = 3
+    if (L.profile == kProfileImageproc) {
+        if (R != 3) return -1;
+        launch_seed_ip_r<3>(L, st);
+        return 0;
     }
+    if (R != 5) return -1;
+    launch_seed_r<5>(L, st);
+    return 0;
 }
 
 // ---------------------------------------------------------------------------
@@ -441,6 +596,39 @@ void launch_resize_nearest_f32(const float* src, int sw, const int* xofs, const 
                                hipStream_t st) {
     dim3 grid((dw + 63) / 64, (dh + 3) / 4, 1);
     hipLaunchKernelGGL(k_resize_nearest_f32, grid, dim3(256), 0, st, src, sw, xofs, yofs, dst, dw, dh);
+}
+
+// image::imageops::resize (Imageproc profile): vertical_sample into tmp
+// (sw x dh), then horizontal_sample with the final [0, 1] clamp.
+__global__ void k_ip_vsample(const float* __restrict__ src, int sw, int sh, const int* __restrict__ yl,
+                             const float* __restrict__ yw, int ytaps, float* __restrict__ tmp, int dh) {
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (x >= sw || y >= dh) return;
+    const int l = yl[y];
+    float acc = 0.0f;
+    // zero-padded taps (weight 0) may run past the image: clamp the index
+    for (int k = 0; k < ytaps; k++) acc = acc + src[(size_t)min(l + k, sh - 1) * sw + x] * yw[y * ytaps + k];
+    tmp[(size_t)y * sw + x] = acc;
+}
+
+__global__ void k_ip_hsample(const float* __restrict__ tmp, int sw, const int* __restrict__ xl,
+                             const float* __restrict__ xw, int xtaps, float* __restrict__ dst, int dw, int dh) {
+    const int x = blockIdx.x * 64 + (threadIdx.x & 63);
+    const int y = blockIdx.y * 4 + (threadIdx.x >> 6);
+    if (x >= dw || y >= dh) return;
+    const int l = xl[x];
+    float acc = 0.0f;
+    for (int k = 0; k < xtaps; k++) acc = acc + tmp[(size_t)y * sw + min(l + k, sw - 1)] * xw[x * xtaps + k];
+    dst[(size_t)y * dw + x] = fminf(fmaxf(acc, 0.0f), 1.0f);
+}
+
+void launch_ip_resize_f32(const float* src, int sw, int sh, const int* xl, const float* xw, int xtaps, const int* yl,
+                          const float* yw, int ytaps, float* tmp, float* dst, int dw, int dh, hipStream_t st) {
+    hipLaunchKernelGGL(k_ip_vsample, dim3((sw + 63) / 64, (dh + 3) / 4, 1), dim3(256), 0, st, src, sw, sh, yl, yw,
+                       ytaps, tmp, dh);
+    hipLaunchKernelGGL(k_ip_hsample, dim3((dw + 63) / 64, (dh + 3) / 4, 1), dim3(256), 0, st, tmp, sw, xl, xw, xtaps,
+                       dst, dw, dh);
 }
 
 }  // namespace siftmi

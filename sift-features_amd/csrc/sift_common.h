@@ -127,6 +127,8 @@ __device__ __forceinline__ TileId xcd_tile() {
     return {(int)(rem - (rem / tx) * tx), (int)(rem / tx), (int)z};
 }
 
+__host__ __device__ __forceinline__ int clamp_idx(int p, int len) { return p < 0 ? 0 : (p >= len ? len - 1 : p); }
+
 // Correctly rounded f32 transcendentals evaluated in f64 (the reference calls
 // glibc expf/sinf/cosf/powf, which are correctly rounded in all but rare
 // near-midpoint cases).

@@ -20,6 +20,20 @@ struct ResizeTab {
     int xmax;
 };
 
+// image::imageops::resize sampling tables (ImageprocProcessing profile),
+// per destination index: first source tap and up to kIpTaps normalised f32
+// weights (zero-padded; an extra zero-weight tap adds +0 and changes nothing).
+constexpr int kIpTaps = 3;
+struct IpResizeTab {
+    const int* xl;
+    const float* xw;  // [dst_w][kIpTaps]
+    const int* yl;
+    const float* yw;  // [dst_h][kIpTaps]
+};
+
+// Arithmetic profile of the Processing backend (src/lib.rs:86-90).
+enum : int { kProfileOpenCV = 0, kProfileImageproc = 1 };
+
 // Image planes are row-pitched: element (y, x) at plane[y * pitch + x].
 struct BlurLaunch {
     const float* src;
@@ -34,13 +48,16 @@ struct BlurLaunch {
     int W, H, pitch;
     int n_img;
     BlurTaps taps;
+    int profile;  // kProfileOpenCV | kProfileImageproc
 };
 
 struct SeedLaunch {
     const uint8_t* frames;
     size_t frame_pitch, row_stride;
     int sh, sw;      // source height, width
-    ResizeTab tab;   // 2x bilinear tables
+    ResizeTab tab;   // 2x bilinear tables (OpenCV profile)
+    IpResizeTab iptab;  // 2x Triangle tables (Imageproc profile)
+    int profile;
     float* dst;      // octave 0, plane 0
     size_t dst_img_stride;
     int W, H, pitch;  // seed (2x) geometry
@@ -53,6 +70,10 @@ int launch_blur(int radius, const BlurLaunch& L, hipStream_t st);
 int launch_seed(int radius, const SeedLaunch& L, hipStream_t st);
 void launch_resize_linear_f32(const float* src, int sw, int sh, const ResizeTab& tab, float* dst, int dw, int dh,
                               hipStream_t st);
+// image::imageops::resize (Imageproc profile, op level): generic tap tables
+// with up to `taps` entries per index ([n][taps] weights)
+void launch_ip_resize_f32(const float* src, int sw, int sh, const int* xl, const float* xw, int xtaps, const int* yl,
+                          const float* yw, int ytaps, float* tmp, float* dst, int dw, int dh, hipStream_t st);
 void launch_resize_nearest_f32(const float* src, int sw, const int* xofs, const int* yofs, float* dst, int dw, int dh,
                                hipStream_t st);
 

@@ -12,9 +12,11 @@ Reference: /root/reference/src/lib.rs (tnibler/sift-features @ 2024-10-22)
 Names, argument meaning and output layout follow the reference; the
 computation is the HIP path (no CPU fallback).  Differences, all documented
 in DESIGN.md:
-  * `sift()` uses the OpenCV arithmetic profile (the one the reference's own
-    golden snapshots pin); `ImageprocProcessing` raises SiftMiError
-    (EUNSUPPORTED) until its profile is implemented.
+  * `sift()` uses `ImageprocProcessing`, as the crate does (src/lib.rs:71-73);
+    that profile restates imageproc 0.25 / image 0.25 arithmetic, which no
+    reference test pins (parity unpinned).  `sift_with_processing(
+    OpenCVProcessing, ...)` is the profile the reference's golden snapshots
+    pin.
   * with a features_limit, ties in response keep emission order (the
     reference's `sort_unstable_by` leaves their order unspecified).
   * errors raise SiftMiError where the reference panics.
@@ -318,8 +320,10 @@ class OpenCVProcessing(Processing):
 
 
 class ImageprocProcessing(Processing):
-    """imageproc gaussian_blur_f32 / image::resize arithmetic (src/lib.rs:993-1007).
-    Not implemented yet: every call raises SiftMiError(EUNSUPPORTED)."""
+    """imageproc gaussian_blur_f32 / image::imageops::resize arithmetic
+    (src/lib.rs:993-1007): the crate's default backend.  Restated from
+    imageproc 0.25.0 / image 0.25.2 (not in the reference tree); parity
+    against the reference is unpinned (no reference test runs it)."""
     profile = PROFILE_IMAGEPROC
 
 
@@ -327,7 +331,7 @@ _tls = threading.local()
 
 
 def default_context(device=0, processing=None):
-    processing = processing or OpenCVProcessing
+    processing = processing or ImageprocProcessing
     cache = getattr(_tls, "ctx", None)
     if cache is None:
         cache = _tls.ctx = {}
@@ -338,8 +342,8 @@ def default_context(device=0, processing=None):
 
 
 def sift(img, features_limit=None):
-    """src/lib.rs:71 (default backend: see module docstring)."""
-    return default_context().sift(img, features_limit)
+    """src/lib.rs:71: sift_with_processing::<ImageprocProcessing>."""
+    return default_context(processing=ImageprocProcessing).sift(img, features_limit)
 
 
 def sift_with_processing(processing, img, features_limit=None):

@@ -98,15 +98,16 @@ def test_precomputed_split(pkg, ctx, oracle):
 
 
 def test_module_level_api(pkg, oracle):
+    """sift() is sift_with_processing::<ImageprocProcessing> (src/lib.rs:71-73)."""
     img = INPUTS["bird_small"]
     res = pkg.sift(img)
-    res2 = pkg.sift_with_processing(pkg.OpenCVProcessing, img)
-    assert res == res2
-    kp_o, desc_o, ext_o = oracle.sift(img, internal=True)
+    assert res == pkg.sift_with_processing(pkg.ImageprocProcessing, img)
+    kp_o, desc_o, ext_o = oracle.sift(img, profile=1, internal=True)
     assert_parity(pkg, res, kp_o, desc_o, ext_o)
+    res_cv = pkg.sift_with_processing(pkg.OpenCVProcessing, img)
+    kp_o, desc_o, ext_o = oracle.sift(img, internal=True)
+    assert_parity(pkg, res_cv, kp_o, desc_o, ext_o)
     assert len(res.keypoints) == len(res)
-    with pytest.raises(pkg.SiftMiError):
-        pkg.sift_with_processing(pkg.ImageprocProcessing, img)
 
 
 def test_golden_snapshots_gpu(pkg, ctx, oracle):

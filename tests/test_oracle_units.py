@@ -148,3 +148,40 @@ def test_stable_sort_matches_snapshot_order(pkg):
     order = pkg.stable_sort_xy_size(g[perm])
     # same (x, y, size) sequence as the snapshot (rows tied on all three may swap)
     assert np.array_equal(g[perm][order][:, :3], g[:, :3])
+
+
+# ---- ImageprocProcessing profile (restated third-party arithmetic; unpinned) --
+
+def test_ip_kernel_sizes(oracle):
+    import ctypes
+    L = oracle.lib()
+    L.oracle_ip_kernel.argtypes = [ctypes.c_float, ctypes.POINTER(ctypes.c_float)]
+    k = (ctypes.c_float * 64)()
+    sig = [oracle.seed_sigma()] + list(oracle.octave_sigmas()[1:])
+    sizes = []
+    for x in sig:
+        n = L.oracle_ip_kernel(x, k)
+        sizes.append(n)
+        v = np.array(k[:n])
+        assert np.array_equal(v, v[::-1]) and abs(float(v.astype(np.float64).sum()) - 1) < 1e-6
+    assert sizes == [7, 7, 9, 9, 11, 15]  # radius ceil(2 sigma)
+
+
+def test_ip_resize_semantics(oracle):
+    img = np.arange(6 * 8, dtype=np.float32).reshape(6, 8) / 64.0
+    near = oracle.resize_nearest(img, 4, 3, 1)
+    assert np.array_equal(near, img[1::2, 1::2])  # image's Nearest halves at (2x+1, 2y+1)
+    up = oracle.resize_linear(img, 16, 12, 1)
+    # Triangle 2x: interior weights 0.25 / 0.75, clamped borders, vertical pass first
+    col = 0.75 * img[:, 1] + 0.25 * img[:, 2]
+    assert abs(up[0, 3] - np.float32(col[0])) < 1e-6
+    assert up[0, 0] == img[0, 0]
+    assert np.all((up >= 0) & (up <= 1))
+
+
+def test_ip_blur_clamp_border(oracle):
+    img = np.zeros((20, 20), np.float32)
+    img[:, 0] = 1.0
+    out = oracle.gaussian_blur(img, 1.0, 1)
+    # clamp-to-edge: the edge column sees its own value in the outside taps
+    assert out[10, 0] > 0.5 and out[10, 19] == 0.0
