@@ -138,6 +138,21 @@ int sift_mi_resize_linear(sift_mi_ctx* ctx, const float* src, uint32_t width, ui
 int sift_mi_resize_nearest(sift_mi_ctx* ctx, const float* src, uint32_t width, uint32_t height, uint32_t dst_width,
                            uint32_t dst_height, float* dst);
 
+/* ---- examples/sift-match.rs:30-35: cv::BFMatcher(NORM_L2, crossCheck)
+ * .match(query, train) -- the step after the path.
+ * query / train: (n, 128) u8 descriptor rows (SiftResult::descriptors).
+ * distance = sqrt((float) exact integer L2^2); nearest = lowest index among
+ * equal distances; cross_check != 0 keeps query i only when its nearest
+ * train row's nearest query is i.  Matches are written in query order to
+ * out[cap]; *n_matches = their count (SIFT_MI_EINVAL if cap is smaller, with
+ * *n_matches set). */
+typedef struct {
+    int32_t query_idx, train_idx;
+    float distance;
+} sift_mi_match;
+int sift_mi_match_descriptors(sift_mi_ctx* ctx, const uint8_t* query, size_t n_query, const uint8_t* train,
+                              size_t n_train, int cross_check, sift_mi_match* out, size_t cap, size_t* n_matches);
+
 /* ---- measurement ---------------------------------------------------------
  * Cumulative since the last reset, from HIP events on the context stream.
  * pyramid_* covers the seed + octave blur/DoG kernels (the HBM-bound stage);

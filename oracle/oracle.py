@@ -73,6 +73,7 @@ def lib():
         L.oracle_cv_kernel.argtypes = [i32, f64, vp]
         L.oracle_octave_sigmas.argtypes = [vp]
         L.oracle_seed_sigma.restype = f64
+        L.oracle_match.argtypes = [vp, i32, vp, i32, i32, vp, vp]
         _lib = L
     return _lib
 
@@ -213,3 +214,17 @@ def stable_sort_xy_size(kps):
     """The snapshot order of `sift_end2end` (src/lib.rs:1020-1030): stable sort
     by (x, y, size) with f32::total_cmp."""
     return np.lexsort((kps[:, 2], kps[:, 1], kps[:, 0]), axis=0) if len(kps) else np.zeros(0, np.int64)
+
+
+def match(query, train, cross_check=True):
+    """Oracle of cv::BFMatcher(NORM_L2, crossCheck).match (examples/sift-match.rs:30-35).
+    Returns (query_idx, train_idx, distance) arrays of the matches, in query order."""
+    q = np.ascontiguousarray(query, dtype=np.uint8).reshape(-1, 128)
+    t = np.ascontiguousarray(train, dtype=np.uint8).reshape(-1, 128)
+    ti = np.zeros(max(len(q), 1), np.int32)
+    di = np.zeros(max(len(q), 1), np.float32)
+    lib().oracle_match(q.ctypes.data, len(q), t.ctypes.data, len(t), 1 if cross_check else 0, ti.ctypes.data,
+                       di.ctypes.data)
+    ti, di = ti[: len(q)], di[: len(q)]
+    keep = np.nonzero(ti >= 0)[0]
+    return keep.astype(np.int32), ti[keep], di[keep]

@@ -950,3 +950,55 @@ void oracle_result_free(ores_t* r) {
     free(r->desc);
     free(r);
 }
+
+/* ------------------------------------------------------------------ */
+/* Descriptor matching (examples/sift-match.rs:30-35):                  */
+/* cv::BFMatcher(NORM_L2, crossCheck).match(query, train).              */
+/* distance = sqrt((float) exact integer L2^2) (batchDistL2_8u32f);     */
+/* nearest = first minimum (strict <); cross check = mutual nearest     */
+/* (cv::batchDistance crosscheck).  train_idx[i] = -1: no match.        */
+/* ------------------------------------------------------------------ */
+static uint32_t l2sq_u8(const uint8_t* a, const uint8_t* b) {
+    uint32_t s = 0;
+    for (int k = 0; k < DESC_SIZE; k++) {
+        const int d = (int)a[k] - (int)b[k];
+        s += (uint32_t)(d * d);
+    }
+    return s;
+}
+
+void oracle_match(const uint8_t* q, int nq, const uint8_t* t, int nt, int cross_check, int* train_idx,
+                  float* dist) {
+    int* tq = (int*)malloc(sizeof(int) * (size_t)(nt > 0 ? nt : 1));
+    for (int j = 0; j < nt; j++) { /* nearest query of each train row */
+        uint32_t best = 0xffffffffu;
+        int bi = -1;
+        for (int i = 0; i < nq; i++) {
+            const uint32_t d = l2sq_u8(q + (size_t)i * DESC_SIZE, t + (size_t)j * DESC_SIZE);
+            if (d < best) {
+                best = d;
+                bi = i;
+            }
+        }
+        tq[j] = bi;
+    }
+    for (int i = 0; i < nq; i++) {
+        uint32_t best = 0xffffffffu;
+        int bj = -1;
+        for (int j = 0; j < nt; j++) {
+            const uint32_t d = l2sq_u8(q + (size_t)i * DESC_SIZE, t + (size_t)j * DESC_SIZE);
+            if (d < best) {
+                best = d;
+                bj = j;
+            }
+        }
+        if (bj >= 0 && (!cross_check || tq[bj] == i)) {
+            train_idx[i] = bj;
+            dist[i] = sqrtf((float)best);
+        } else {
+            train_idx[i] = -1;
+            dist[i] = 0.0f;
+        }
+    }
+    free(tq);
+}

@@ -17,7 +17,8 @@ EXPORTS = [
     "sift_mi_extract_batch_device", "sift_mi_set_exact_descriptors", "sift_mi_set_keep_on_device", "sift_mi_device_results",
     "sift_mi_precompute", "sift_mi_octave_dims", "sift_mi_read_scale_space", "sift_mi_read_dog",
     "sift_mi_sift_with_precomputed", "sift_mi_compute_descriptor", "sift_mi_gaussian_blur",
-    "sift_mi_resize_linear", "sift_mi_resize_nearest", "sift_mi_get_stats", "sift_mi_reset_stats",
+    "sift_mi_resize_linear", "sift_mi_resize_nearest", "sift_mi_match_descriptors", "sift_mi_get_stats",
+    "sift_mi_reset_stats",
     "sift_mi_version", "sift_mi_last_error",
 ]
 
@@ -28,6 +29,11 @@ class SiftMiError(RuntimeError):
     def __init__(self, code, msg):
         super().__init__(f"sift_mi error {STATUS.get(code, code)}: {msg}")
         self.code = code
+
+
+class Match(ctypes.Structure):
+    """include/sift_mi.h sift_mi_match (cv::DMatch without imgIdx)."""
+    _fields_ = [("query_idx", ctypes.c_int32), ("train_idx", ctypes.c_int32), ("distance", ctypes.c_float)]
 
 
 class Stats(ctypes.Structure):
@@ -86,6 +92,7 @@ def lib():
         "sift_mi_gaussian_blur": [vp, vp, u32, u32, f64, vp],
         "sift_mi_resize_linear": [vp, vp, u32, u32, u32, u32, vp],
         "sift_mi_resize_nearest": [vp, vp, u32, u32, u32, u32, vp],
+        "sift_mi_match_descriptors": [vp, vp, sz, vp, sz, i32, vp, sz, P(sz)],
         "sift_mi_get_stats": [vp, P(Stats)],
         "sift_mi_reset_stats": [vp],
         "sift_mi_version": [],

@@ -1350,6 +1350,62 @@ int sift_mi_resize_nearest(sift_mi_ctx* c, const float* src, uint32_t w, uint32_
     return rc;
 }
 
+// ---- descriptor matching (examples/sift-match.rs:30-35) ---------------------
+int sift_mi_match_descriptors(sift_mi_ctx* c, const uint8_t* query, size_t nq, const uint8_t* train, size_t nt,
+                              int cross_check, sift_mi_match* out, size_t cap, size_t* n_matches) {
+    if (!c || !n_matches || (nq && !query) || (nt && !train)) return fail(SIFT_MI_EINVAL, "bad arguments");
+    if (nq > 0x7fffffff || nt > 0x7fffffff) return fail(SIFT_MI_EINVAL, "descriptor set too large");
+    *n_matches = 0;
+    if (nq == 0) return 0;
+    CHK(set_device(c));
+    DevBuf<uint8_t> dq, dt;
+    DevBuf<float> qn, tn, dist;
+    DevBuf<unsigned long long> rb, cb;
+    DevBuf<int> tix;
+    int rc = 0;
+    if (!rc) rc = dq.ensure(nq * kDescSize);
+    if (!rc) rc = dt.ensure(std::max<size_t>(nt, 1) * kDescSize);
+    if (!rc) rc = qn.ensure(nq);
+    if (!rc) rc = tn.ensure(std::max<size_t>(nt, 1));
+    if (!rc) rc = rb.ensure(nq);
+    if (!rc) rc = cb.ensure(std::max<size_t>(nt, 1));
+    if (!rc) rc = tix.ensure(nq);
+    if (!rc) rc = dist.ensure(nq);
+    std::vector<int> h_t(nq);
+    std::vector<float> h_d(nq);
+    if (!rc) {
+        hipStream_t st = c->stream;
+        if (hipMemcpyAsync(dq.p, query, nq * kDescSize, hipMemcpyHostToDevice, st) != hipSuccess ||
+            (nt && hipMemcpyAsync(dt.p, train, nt * kDescSize, hipMemcpyHostToDevice, st) != hipSuccess))
+            rc = fail(SIFT_MI_EHIP, "H2D failed");
+        if (!rc) {
+            launch_match(dq.p, (int)nq, dt.p, (int)nt, cross_check ? 1 : 0, qn.p, tn.p, rb.p, cb.p, tix.p, dist.p, st);
+            if (hipGetLastError() != hipSuccess ||
+                hipMemcpyAsync(h_t.data(), tix.p, nq * sizeof(int), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipMemcpyAsync(h_d.data(), dist.p, nq * sizeof(float), hipMemcpyDeviceToHost, st) != hipSuccess ||
+                hipStreamSynchronize(st) != hipSuccess)
+                rc = fail(SIFT_MI_EHIP, "match failed");
+        }
+    }
+    dq.release();
+    dt.release();
+    qn.release();
+    tn.release();
+    rb.release();
+    cb.release();
+    tix.release();
+    dist.release();
+    CHK(rc);
+    size_t n = 0;
+    for (size_t i = 0; i < nq; i++) n += h_t[i] >= 0;
+    *n_matches = n;
+    if (cap < n || (n && !out)) return fail(SIFT_MI_EINVAL, "cap < number of matches");
+    size_t k = 0;
+    for (size_t i = 0; i < nq; i++)
+        if (h_t[i] >= 0) out[k++] = sift_mi_match{(int32_t)i, h_t[i], h_d[i]};
+    return 0;
+}
+
 int sift_mi_get_stats(sift_mi_ctx* c, sift_mi_stats* out) {
     if (!c || !out) return fail(SIFT_MI_EINVAL, "bad arguments");
     *out = c->stats;

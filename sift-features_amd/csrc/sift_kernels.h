@@ -150,6 +150,11 @@ void launch_select(const uint32_t* emis_order, const uint32_t* resp_order, const
                    const uint32_t* out_off, const uint8_t* use_resp, int n_img, const uint32_t* n_out, uint32_t bound,
                    uint32_t* final_idx, hipStream_t st);
 
+// match.hip: per query the nearest train row (or -1), its distance
+void launch_match(const uint8_t* q, int nq, const uint8_t* t, int nt, int cross_check, float* qn, float* tn,
+                  unsigned long long* row_best, unsigned long long* col_best, int* train_idx, float* dist,
+                  hipStream_t st);
+
 // describe.hip
 struct DescLaunch {
     const KpRec* kp;

@@ -232,6 +232,21 @@ class Context:
                                                float(y), float(scale), float(orientation), out.ctypes.data))
         return out
 
+    # -- matching (examples/sift-match.rs:30-35) -----------------------------
+    def match_descriptors(self, query, train, cross_check=True):
+        """cv::BFMatcher(NORM_L2, crossCheck).match(query, train) on the GPU.
+        query / train: (n, 128) u8 descriptors.  Returns (query_idx, train_idx,
+        distance) arrays in query order."""
+        q = np.ascontiguousarray(query, dtype=np.uint8).reshape(-1, DESCRIPTOR_SIZE)
+        t = np.ascontiguousarray(train, dtype=np.uint8).reshape(-1, DESCRIPTOR_SIZE)
+        out = (_lib.Match * max(len(q), 1))()
+        n = ctypes.c_size_t()
+        check(lib().sift_mi_match_descriptors(self._h, q.ctypes.data, len(q), t.ctypes.data, len(t),
+                                              1 if cross_check else 0, out, len(q), ctypes.byref(n)))
+        a = np.ctypeslib.as_array(out)[: n.value]
+        return (a["query_idx"].astype(np.int32), a["train_idx"].astype(np.int32),
+                a["distance"].astype(np.float32))
+
     # -- Processing ops (src/lib.rs:86-90) ---------------------------------
     def gaussian_blur(self, img, sigma):
         a = _f32_image(img)
@@ -364,6 +379,11 @@ def sift_with_precomputed(pre, features_limit=None):
 def compute_descriptor(img, x, y, scale, orientation):
     """src/lib.rs:785"""
     return default_context().compute_descriptor(img, x, y, scale, orientation)
+
+
+def match_descriptors(query, train, cross_check=True):
+    """examples/sift-match.rs:30-35: BFMatcher(NORM_L2, crossCheck).match."""
+    return default_context().match_descriptors(query, train, cross_check)
 
 
 def stable_sort_xy_size(keypoints_array):
