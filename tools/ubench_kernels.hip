@@ -64,7 +64,7 @@ float time_blur(const float* src, float* dst, float* dog, size_t stride, int W, 
     const int tx = (W + G::TW - 1) / G::TW, ty = (H + G::TH - 1) / G::TH;
     dim3 grid(tx, ty, nimg);
     auto go = [&]() {
-        hipLaunchKernelGGL((k_blur<R, TH>), grid, dim3(256), 0, 0, src, stride, dst, stride, dog, stride,
+        hipLaunchKernelGGL((k_blur<R, TH, kProfileOpenCV>), grid, dim3(256), 0, 0, src, stride, dst, stride, dog, stride,
                            (float*)nullptr, (size_t)0, 0, 0, 0, W, H, pitch, taps);
     };
     go();
@@ -111,7 +111,7 @@ void bench_blur(int N, bool arena, bool random) {
         const float ms = time_blur<R, TH>(s, d, g, stride, W, H, pitch, N, 5);                           \
         std::printf("  R=%2d TH=%2d %8.3f ms %8.1f GB/s\n", R, TH, ms, bytes / (ms * 1e-3) / 1e9);        \
     }
-    B(5, 32) B(6, 32) B(8, 32) B(10, 32) B(10, 64) B(13, 32) B(13, 64)
+    B(5, 32) B(5, 64) B(6, 32) B(6, 64) B(8, 32) B(8, 64) B(10, 64) B(10, 128) B(13, 64) B(13, 128)
 #undef B
     CK(hipFree(base));
 }
