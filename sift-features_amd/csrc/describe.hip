@@ -314,9 +314,12 @@ __device__ __forceinline__ void describe_wave_exact(const float* __restrict__ im
 // kShare lanes share one slice (64 / kShare slices per wave): their updates
 // are issued group by group (lanes [g*S, (g+1)*S) in step g), so no two lanes
 // of a slice write in the same instruction.  Sharing trades LDS instructions
-// for LDS footprint -- 33.8 KB per wave at kShare = 1 (one wave per SIMD),
-// 16.9 KB at 2, 8.4 KB at 4 -- i.e. for occupancy.
-constexpr int PRIV_STRIDE = 132;  // 128 bins + 4 dummy slots (border-ring contributions)
+// for LDS footprint -- 34.8 KB per wave at kShare = 1 (one wave per SIMD),
+// 17.4 KB at 2, 8.7 KB at 4 -- i.e. for occupancy.
+// 128 bins + 4 x 2 dummy slots: border-ring contributions of the sample's four
+// cells go to distinct dummies, so a sample's 8 addresses never alias and its
+// 8 reads can be issued together before the 8 writes
+constexpr int PRIV_STRIDE = 136;
 
 template <int kShare>
 struct DescScratchFast {
@@ -405,24 +408,29 @@ __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img
         o0 = o0 < 0 ? o0 + kDescBins : (o0 >= kDescBins ? o0 - kDescBins : o0);
         o0 &= kDescBins - 1;
         const int o1 = (o0 + 1) & (kDescBins - 1);
-        // interior slice offset of cell (r, q), or the dummy slots for the border ring
-        auto cell = [](int r, int q) { return (r >= 1 && r <= 4 && q >= 1 && q <= 4) ? ((r - 1) * 4 + (q - 1)) * 8 : 128; };
-        const int b11 = cell(r1, q1), b12 = cell(r1, q1 + 1), b21 = cell(r1 + 1, q1), b22 = cell(r1 + 1, q1 + 1);
-        const int d0 = o0 & (b11 == 128 ? 3 : 7), d1 = o1 & (b11 == 128 ? 3 : 7);
-        const int e0 = o0 & (b12 == 128 ? 3 : 7), e1 = o1 & (b12 == 128 ? 3 : 7);
-        const int f0 = o0 & (b21 == 128 ? 3 : 7), f1 = o1 & (b21 == 128 ? 3 : 7);
-        const int g0 = o0 & (b22 == 128 ? 3 : 7), g1 = o1 & (b22 == 128 ? 3 : 7);
+        // bin of (cell (r, q), orientation o): interior slice offset, or the
+        // corner's own dummy pair (128 + 2 * corner + (o & 1)) for the border ring
+        auto bin = [](int r, int q, int corner, int o) {
+            return (r >= 1 && r <= 4 && q >= 1 && q <= 4) ? ((r - 1) * 4 + (q - 1)) * 8 + o : 128 + 2 * corner + (o & 1);
+        };
+        const int a0 = bin(r1, q1, 0, o0) * NS, a1 = bin(r1, q1, 0, o1) * NS;
+        const int a2 = bin(r1, q1 + 1, 1, o0) * NS, a3 = bin(r1, q1 + 1, 1, o1) * NS;
+        const int a4 = bin(r1 + 1, q1, 2, o0) * NS, a5 = bin(r1 + 1, q1, 2, o1) * NS;
+        const int a6 = bin(r1 + 1, q1 + 1, 3, o0) * NS, a7 = bin(r1 + 1, q1 + 1, 3, o1) * NS;
 #pragma unroll
         for (int g = 0; g < kShare; g++) {
             if (kShare > 1 && !(inside && grp == g)) continue;
-            hp[(b11 + d0) * NS] += c000;
-            hp[(b11 + d1) * NS] += c001;
-            hp[(b12 + e0) * NS] += c010;
-            hp[(b12 + e1) * NS] += c011;
-            hp[(b21 + f0) * NS] += c100;
-            hp[(b21 + f1) * NS] += c101;
-            hp[(b22 + g0) * NS] += c110;
-            hp[(b22 + g1) * NS] += c111;
+            // 8 distinct addresses (o1 = o0 + 1 mod 8): all reads, then all writes
+            const float h0 = hp[a0], h1 = hp[a1], h2 = hp[a2], h3 = hp[a3];
+            const float h4 = hp[a4], h5 = hp[a5], h6 = hp[a6], h7 = hp[a7];
+            hp[a0] = h0 + c000;
+            hp[a1] = h1 + c001;
+            hp[a2] = h2 + c010;
+            hp[a3] = h3 + c011;
+            hp[a4] = h4 + c100;
+            hp[a5] = h5 + c101;
+            hp[a6] = h6 + c110;
+            hp[a7] = h7 + c111;
         }
     }
     wave_sync();
