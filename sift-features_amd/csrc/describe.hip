@@ -356,12 +356,41 @@ __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img
     build_row_table(sc.rowlo, sc.rowpre, radius, cos_s, sin_s, lane);
     const int total = sc.rowpre[n];
     // lane-strided samples: one load instruction touches ~64 neighbouring
-    // pixels (2-3 cache lines) instead of 64 scattered ones
+    // pixels (2-3 cache lines) instead of 64 scattered ones.  Software
+    // pipelined: the gradient loads of a lane's next sample are issued before
+    // the current sample is processed (a wave spends ~2 us per load round trip
+    // otherwise, with only ~2 waves per SIMD to cover it).
     int row = 0;
-    for (int k = lane; k < total; k += 64) {
+    const gfloat* gimg = as_global(img);
+    auto locate = [&](int k, int& xi, int& yi) {
         while (sc.rowpre[row + 1] <= k) row++;
-        const int yi = row - radius;
-        const int xi = sc.rowlo[row] + (k - sc.rowpre[row]);
+        yi = row - radius;
+        xi = sc.rowlo[row] + (k - sc.rowpre[row]);
+    };
+    // the four neighbours of sample k; positions outside the image (rejected
+    // samples) are clamped so every load stays inside the plane
+    auto fetch = [&](int xi, int yi, float& l, float& r, float& u, float& d) {
+        const int ay = min(max(y + yi, 1), height - 2), ax = min(max(x + xi, 1), width - 2);
+        const gfloat* rw = gimg + (size_t)ay * pitch + ax;
+        r = rw[1];
+        l = rw[-1];
+        u = rw[-pitch];
+        d = rw[pitch];
+    };
+    int nxi = 0, nyi = 0;
+    float nl = 0.f, nr = 0.f, nu = 0.f, nd = 0.f;
+    if (lane < total) {
+        locate(lane, nxi, nyi);
+        if (!(kAblate & 8)) fetch(nxi, nyi, nl, nr, nu, nd);
+    }
+    for (int k = lane; k < total; k += 64) {
+        const int xi = nxi, yi = nyi;
+        const float gl = nl, gr = nr, gu = nu, gd = nd;
+        {
+            const int k2 = min(k + 64, total - 1);  // the last lap refetches its own sample
+            locate(k2, nxi, nyi);
+            if (!(kAblate & 8)) fetch(nxi, nyi, nl, nr, nu, nd);
+        }
         const float col_rot = (float)xi * cos_s - (float)yi * sin_s;
         const float row_rot = (float)xi * sin_s + (float)yi * cos_s;
         float row_bin = row_rot + (float)(kDescHist / 2);
@@ -376,19 +405,24 @@ __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img
             dx = (float)xi * 0.01f + 0.001f;
             dy = (float)yi * 0.01f - 0.002f;
         } else {
-            const gfloat* rw = as_global(img) + (size_t)ay * pitch;
-            dx = rw[ax + 1] - rw[ax - 1];
-            dy = rw[ax - pitch] - rw[ax + pitch];
+            dx = gr - gl;
+            dy = gu - gd;
         }
         const float wsq = col_rot * col_rot + row_rot * row_rot;
         const float earg = wsq * (-2.f / (float)(kDescHist * kDescHist));
         const float weight = (kAblate & 4) ? 1.0f + wsq * (-0.125f) : ((kAblate & 16) ? expf(earg) : exp_f32(earg));
-        double deg = ((kAblate & 2)    ? (double)(dy * 50.0f + dx)
-                      : (kAblate & 16) ? (double)(atan2f(dy, dx) * (180.0f / 3.14159265358979323846f))
-                                       : atan2((double)dy, (double)dx) * (180.0 / 3.14159265358979323846)) +
-                     360.0;
-        deg = deg >= 360.0 ? deg - 360.0 : deg;  // f64 `% 360.0` of a value in [180, 540]
-        const float ori = (float)deg - orientation;
+        float degf;
+        if (kAblate & 18) {
+            // f32 angle v: (float)(((double)v + 360) % 360) == (v < 0 ? v + 360.0f : v)
+            // (the f64 sum is exact, and rounded once either way)
+            const float v = (kAblate & 2) ? dy * 50.0f + dx : atan2f(dy, dx) * (180.0f / 3.14159265358979323846f);
+            degf = v < 0.0f ? v + 360.0f : v;
+        } else {
+            double deg = atan2((double)dy, (double)dx) * (180.0 / 3.14159265358979323846) + 360.0;
+            deg = deg >= 360.0 ? deg - 360.0 : deg;  // f64 `% 360.0` of a value in [180, 540]
+            degf = (float)deg;
+        }
+        const float ori = degf - orientation;
         float mag = sqrtf(dx * dx + dy * dy);
         row_bin = row_bin - 0.5f;
         col_bin = col_bin - 0.5f;
@@ -410,13 +444,15 @@ __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img
         const int o1 = (o0 + 1) & (kDescBins - 1);
         // bin of (cell (r, q), orientation o): interior slice offset, or the
         // corner's own dummy pair (128 + 2 * corner + (o & 1)) for the border ring
-        auto bin = [](int r, int q, int corner, int o) {
-            return (r >= 1 && r <= 4 && q >= 1 && q <= 4) ? ((r - 1) * 4 + (q - 1)) * 8 + o : 128 + 2 * corner + (o & 1);
-        };
-        const int a0 = bin(r1, q1, 0, o0) * NS, a1 = bin(r1, q1, 0, o1) * NS;
-        const int a2 = bin(r1, q1 + 1, 1, o0) * NS, a3 = bin(r1, q1 + 1, 1, o1) * NS;
-        const int a4 = bin(r1 + 1, q1, 2, o0) * NS, a5 = bin(r1 + 1, q1, 2, o1) * NS;
-        const int a6 = bin(r1 + 1, q1 + 1, 3, o0) * NS, a7 = bin(r1 + 1, q1 + 1, 3, o1) * NS;
+        const bool rv1 = (uint32_t)(r1 - 1) < 4u, rv2 = (uint32_t)r1 < 4u;  // rows r1, r1 + 1 interior
+        const bool qv1 = (uint32_t)(q1 - 1) < 4u, qv2 = (uint32_t)q1 < 4u;
+        const int base = ((r1 - 1) * 4 + (q1 - 1)) * 8;
+        const int p0 = o0 & 1, p1 = o1 & 1;
+        const bool v11 = rv1 & qv1, v12 = rv1 & qv2, v21 = rv2 & qv1, v22 = rv2 & qv2;
+        const int a0 = (v11 ? base + o0 : 128 + p0) * NS, a1 = (v11 ? base + o1 : 128 + p1) * NS;
+        const int a2 = (v12 ? base + 8 + o0 : 130 + p0) * NS, a3 = (v12 ? base + 8 + o1 : 130 + p1) * NS;
+        const int a4 = (v21 ? base + 32 + o0 : 132 + p0) * NS, a5 = (v21 ? base + 32 + o1 : 132 + p1) * NS;
+        const int a6 = (v22 ? base + 40 + o0 : 134 + p0) * NS, a7 = (v22 ? base + 40 + o1 : 134 + p1) * NS;
 #pragma unroll
         for (int g = 0; g < kShare; g++) {
             if (kShare > 1 && !(inside && grp == g)) continue;
