@@ -314,12 +314,16 @@ __device__ __forceinline__ void describe_wave_exact(const float* __restrict__ im
 // kShare lanes share one slice (64 / kShare slices per wave): their updates
 // are issued group by group (lanes [g*S, (g+1)*S) in step g), so no two lanes
 // of a slice write in the same instruction.  Sharing trades LDS instructions
-// for LDS footprint -- 34.8 KB per wave at kShare = 1 (one wave per SIMD),
-// 17.4 KB at 2, 8.7 KB at 4 -- i.e. for occupancy.
-// 128 bins + 4 x 2 dummy slots: border-ring contributions of the sample's four
-// cells go to distinct dummies, so a sample's 8 addresses never alias and its
-// 8 reads can be issued together before the 8 writes
-constexpr int PRIV_STRIDE = 136;
+// for LDS footprint -- 38.9 KB per wave at kShare = 1 (one wave per SIMD),
+// 19.5 KB at 2, 9.7 KB at 4 -- i.e. for occupancy.
+//
+// Slice layout: 9 slots per interior cell (slot 8 aliases orientation 0 and is
+// folded into it at the end), so a sample's two orientation bins o0, o0 + 1 of
+// a cell are always adjacent slots -- one ds_read2_b32 / ds_write2_b32 and one
+// v_pk_add_f32 per cell -- plus one dummy pair per footprint corner that takes
+// the border-ring contributions (the reference discards that ring): a
+// sample's 4 slot pairs never alias, so all reads issue before the writes.
+constexpr int PRIV_STRIDE = 16 * 9 + 4 * 2;
 
 template <int kShare>
 struct DescScratchFast {
@@ -441,46 +445,48 @@ __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img
         int o0 = (int)ori_floor;
         o0 = o0 < 0 ? o0 + kDescBins : (o0 >= kDescBins ? o0 - kDescBins : o0);
         o0 &= kDescBins - 1;
-        const int o1 = (o0 + 1) & (kDescBins - 1);
-        // bin of (cell (r, q), orientation o): interior slice offset, or the
-        // corner's own dummy pair (128 + 2 * corner + (o & 1)) for the border ring
+        // slot pair of each footprint corner: (cell, o0 / o0 + 1) of an interior
+        // cell, or the corner's own dummy pair (144 + 2 * corner) on the border ring
         const bool rv1 = (uint32_t)(r1 - 1) < 4u, rv2 = (uint32_t)r1 < 4u;  // rows r1, r1 + 1 interior
         const bool qv1 = (uint32_t)(q1 - 1) < 4u, qv2 = (uint32_t)q1 < 4u;
-        const int base = ((r1 - 1) * 4 + (q1 - 1)) * 8;
-        const int p0 = o0 & 1, p1 = o1 & 1;
         const bool v11 = rv1 & qv1, v12 = rv1 & qv2, v21 = rv2 & qv1, v22 = rv2 & qv2;
-        const int a0 = (v11 ? base + o0 : 128 + p0) * NS, a1 = (v11 ? base + o1 : 128 + p1) * NS;
-        const int a2 = (v12 ? base + 8 + o0 : 130 + p0) * NS, a3 = (v12 ? base + 8 + o1 : 130 + p1) * NS;
-        const int a4 = (v21 ? base + 32 + o0 : 132 + p0) * NS, a5 = (v21 ? base + 32 + o1 : 132 + p1) * NS;
-        const int a6 = (v22 ? base + 40 + o0 : 134 + p0) * NS, a7 = (v22 ? base + 40 + o1 : 134 + p1) * NS;
+        const int base = ((r1 - 1) * 4 + (q1 - 1)) * 9 + o0;  // o0 + 1 <= 8: no wrap
+        const int a0 = (v11 ? base : 144) * NS, a2 = (v12 ? base + 9 : 146) * NS;
+        const int a4 = (v21 ? base + 36 : 148) * NS, a6 = (v22 ? base + 45 : 150) * NS;
+        const f2v w00 = {c000, c001}, w01 = {c010, c011}, w10 = {c100, c101}, w11 = {c110, c111};
 #pragma unroll
         for (int g = 0; g < kShare; g++) {
             if (kShare > 1 && !(inside && grp == g)) continue;
-            // 8 distinct addresses (o1 = o0 + 1 mod 8): all reads, then all writes
-            const float h0 = hp[a0], h1 = hp[a1], h2 = hp[a2], h3 = hp[a3];
-            const float h4 = hp[a4], h5 = hp[a5], h6 = hp[a6], h7 = hp[a7];
-            hp[a0] = h0 + c000;
-            hp[a1] = h1 + c001;
-            hp[a2] = h2 + c010;
-            hp[a3] = h3 + c011;
-            hp[a4] = h4 + c100;
-            hp[a5] = h5 + c101;
-            hp[a6] = h6 + c110;
-            hp[a7] = h7 + c111;
+            const f2v h0 = {hp[a0], hp[a0 + NS]}, h2 = {hp[a2], hp[a2 + NS]};
+            const f2v h4 = {hp[a4], hp[a4 + NS]}, h6 = {hp[a6], hp[a6 + NS]};
+            const f2v s0 = h0 + w00, s2 = h2 + w01, s4 = h4 + w10, s6 = h6 + w11;
+            hp[a0] = s0.x;
+            hp[a0 + NS] = s0.y;
+            hp[a2] = s2.x;
+            hp[a2 + NS] = s2.y;
+            hp[a4] = s4.x;
+            hp[a4 + NS] = s4.y;
+            hp[a6] = s6.x;
+            hp[a6 + NS] = s6.y;
         }
     }
     wave_sync();
     // per-bin sum of the 64 private slices: lane l owns flat bins 2l, 2l+1 and
     // starts at slice l (rotated start: the 32 lanes of a half hit 32 banks)
     float acc0 = 0.0f, acc1 = 0.0f;
-    const float* r0 = sc.h + (2 * lane) * NS;
+    const int fb = (lane >> 2) * 9 + 2 * (lane & 3);  // slot of flat bin 2 * lane
+    const float* r0 = sc.h + fb * NS;
     const float* r1 = r0 + NS;
+    const float* r8 = sc.h + ((lane >> 2) * 9 + 8) * NS;  // orientation-0 alias of the cell
+    float acc8 = 0.0f;
 #pragma unroll 8
     for (int j = 0; j < NS; j++) {
         const int jj = (j + lane) & (NS - 1);
         acc0 += r0[jj];
         acc1 += r1[jj];
+        acc8 += r8[jj];
     }
+    if ((lane & 3) == 0) acc0 += acc8;
     describe_normalize(acc0, acc1, out, lane);
 }
 
@@ -534,8 +540,8 @@ __global__ __launch_bounds__(64) void k_describe(const DescLaunch L) {
 
 void launch_describe(const DescLaunch& L, hipStream_t st) {
     if (L.bound == 0) return;
-    // fast path: 17 KB of LDS per wave -> 9 resident per CU (exact: 14 KB)
-    const dim3 grid(std::min<uint32_t>(L.bound, 256 * 9));
+    // fast path: 20 KB of LDS per wave -> 8 resident per CU (exact: 14 KB)
+    const dim3 grid(std::min<uint32_t>(L.bound, 256 * 8));
     if (L.exact)
         hipLaunchKernelGGL((k_describe<0, 0>), grid, dim3(64), 0, st, L);
     else

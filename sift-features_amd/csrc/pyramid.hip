@@ -63,8 +63,6 @@ struct BlurGeom {
 // independent, individually rounded lanes -- the same results as scalar fma /
 // add): the row pass pairs adjacent outputs of a row, the column pass
 // adjacent columns.
-typedef float f2v __attribute__((ext_vector_type(2)));
-typedef float f4v __attribute__((ext_vector_type(4)));
 // volatile LDS view: keeps each row-window read one ds_read_b128 (the compiler
 // otherwise narrows the unused edge lanes into ds_read2_b32 pairs)
 typedef __attribute__((address_space(3))) volatile f4v lds_f4v;

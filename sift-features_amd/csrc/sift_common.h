@@ -13,6 +13,10 @@
 
 namespace siftmi {
 
+// packed f32 pairs / quads (v_pk_* arithmetic, 8- and 16-byte LDS accesses)
+typedef float f2v __attribute__((ext_vector_type(2)));
+typedef float f4v __attribute__((ext_vector_type(4)));
+
 constexpr int kScalesPerOctave = 3;                  // src/lib.rs:92
 constexpr int kImagesPerOctave = kScalesPerOctave + 3;  // 6 Gaussian images (src/lib.rs:218-221)
 constexpr int kDogPerOctave = kScalesPerOctave + 2;     // 5 DoG images (src/lib.rs:277)

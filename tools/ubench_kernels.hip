@@ -27,7 +27,7 @@ float time_describe(const DescLaunch& L, int reps) {
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
-    dim3 grid(std::min<uint32_t>(L.bound, 2048));
+    dim3 grid(std::min<uint32_t>(L.bound, 256 * 8));
     CK(hipMemset(L.work, 0, 4));
     hipLaunchKernelGGL((k_describe<E, A>), grid, dim3(64), 0, 0, L);
     CK(hipEventRecord(a));
