@@ -358,7 +358,7 @@ __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img
     for (int i = 0; i < PRIV_STRIDE * NS / 4; i += 64)
         if (i + lane < PRIV_STRIDE * NS / 4) reinterpret_cast<float4*>(sc.h)[i + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
     build_row_table(sc.rowlo, sc.rowpre, radius, cos_s, sin_s, lane);
-    const int total = sc.rowpre[n];
+    const int total_samples = sc.rowpre[n];
     // lane-strided samples: one load instruction touches ~64 neighbouring
     // pixels (2-3 cache lines) instead of 64 scattered ones.  Software
     // pipelined: the gradient loads of a lane's next sample are issued before
@@ -383,6 +383,8 @@ __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img
     };
     int nxi = 0, nyi = 0;
     float nl = 0.f, nr = 0.f, nu = 0.f, nd = 0.f;
+    f2v sink = {0.f, 0.f};  // kAblate bit 0: register sink instead of the slice updates
+    const int total = (kAblate & 64) ? 0 : total_samples;  // bit 6: no samples (per-keypoint overhead)
     if (lane < total) {
         locate(lane, nxi, nyi);
         if (!(kAblate & 8)) fetch(nxi, nyi, nl, nr, nu, nd);
@@ -454,6 +456,10 @@ __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img
         const int a0 = (v11 ? base : 144) * NS, a2 = (v12 ? base + 9 : 146) * NS;
         const int a4 = (v21 ? base + 36 : 148) * NS, a6 = (v22 ? base + 45 : 150) * NS;
         const f2v w00 = {c000, c001}, w01 = {c010, c011}, w10 = {c100, c101}, w11 = {c110, c111};
+        if (kAblate & 1) {
+            if (inside) sink += (w00 + w01) * (w10 + w11) + f2v{(float)a0, (float)(a2 + a4 + a6)};
+            continue;
+        }
 #pragma unroll
         for (int g = 0; g < kShare; g++) {
             if (kShare > 1 && !(inside && grp == g)) continue;
@@ -487,6 +493,7 @@ __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img
         acc8 += r8[jj];
     }
     if ((lane & 3) == 0) acc0 += acc8;
+    if (kAblate & 1) acc0 += sink.x + sink.y;
     describe_normalize(acc0, acc1, out, lane);
 }
 
@@ -501,10 +508,28 @@ __global__ __launch_bounds__(64) void k_describe(const DescLaunch L) {
     const uint32_t n = min(*L.n, L.bound);
     // one wave per keypoint, taken from a work counter: window sizes (and
     // costs) vary ~20x, a static stride would leave a long tail
+    // Keypoints come from kDescQueues interleaved queues (queue q holds
+    // keypoints q, q + 8, ...; one wave per keypoint, window costs vary ~20x):
+    // a wave drains its home queue (blockIdx % 8, the XCD the block runs on),
+    // then the others in turn.  kAblate bit 7: static assignment.
+    uint32_t it = 0;
+    int q = blockIdx.x & (kDescQueues - 1), drained = 0;
     for (;;) {
         uint32_t i = 0;
-        if (lane == 0) i = atomicAdd(L.work, 1u);
-        i = __shfl(i, 0);
+        if (kAblate & 128) {
+            i = blockIdx.x + gridDim.x * it++;
+        } else {
+            uint32_t j = 0;
+            if (lane == 0) j = atomicAdd(L.work + q * kDescQueueStride, 1u);
+            j = __builtin_amdgcn_readfirstlane(__shfl(j, 0));
+            i = j * kDescQueues + q;
+            if (i >= n) {
+                if (++drained == kDescQueues) break;
+                q = (q + 1) & (kDescQueues - 1);
+                continue;
+            }
+        }
+        i = __builtin_amdgcn_readfirstlane(i);  // wave-uniform: keeps the per-keypoint control flow scalar
         if (i >= n) break;
         const KpRec kp = L.kp[L.idx ? L.idx[i] : i];
         const int o = kp.octave;

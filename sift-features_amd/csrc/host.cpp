@@ -377,7 +377,7 @@ struct Plan {
 // kernels run while the host waits for chunk k and copies its results out.
 struct Slot {
     // [0] candidates [1] extrema [2] keypoints [3] outputs [4..4+F) frame starts
-    // [4+F..4+2F) per-frame outputs [4+2F..6+2F) work counters
+    // [4+F..4+2F) per-frame outputs [4+2F..4+2F+kDescWorkWords) descriptor work queues
     DevBuf<uint32_t> counters;
     PinBuf<uint32_t> h_counts;
     DevBuf<OutKp> out_kp;
@@ -645,7 +645,7 @@ int reserve_chunk(sift_mi_ctx* c, const Bounds& B, uint32_t frames) {
                       frames > c->seg_off.cap;
     bool grow_out = false;
     for (auto& S : c->slot)
-        grow_out |= B.bk > S.out_kp.cap || 6 + 2 * frames > S.counters.cap;
+        grow_out |= B.bk > S.out_kp.cap || 4 + 2 * frames + kDescWorkWords > S.counters.cap;
     if (grow || grow_out) {
         HIPCHK(hipStreamSynchronize(c->stream));
         HIPCHK(hipStreamSynchronize(c->cstream));
@@ -662,7 +662,7 @@ int reserve_chunk(sift_mi_ctx* c, const Bounds& B, uint32_t frames) {
     CHK(c->out_off.ensure(frames));
     CHK(c->use_resp.ensure(frames));
     for (auto& S : c->slot) {
-        CHK(S.counters.ensure(6 + 2 * frames));
+        CHK(S.counters.ensure(4 + 2 * frames + kDescWorkWords));
         CHK(S.h_counts.ensure(4 + 2 * frames));
         CHK(S.out_kp.ensure(B.bk));
         CHK(S.out_desc.ensure((size_t)B.bk * kDescSize));
@@ -690,9 +690,9 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
     uint32_t* cnt = S.counters.p;
     uint32_t* starts = cnt + 4;
     uint32_t* out_cnt = cnt + 4 + m;
-    uint32_t* work = cnt + 4 + 2 * m;  // [1]: descriptor work counter
+    uint32_t* work = cnt + 4 + 2 * m;  // descriptor work queues
     HIPCHK(hipMemsetAsync(cnt, 0, 4 * sizeof(uint32_t), st));
-    HIPCHK(hipMemsetAsync(work, 0, 2 * sizeof(uint32_t), st));
+    HIPCHK(hipMemsetAsync(work, 0, kDescWorkWords * sizeof(uint32_t), st));
     HIPCHK(hipMemsetAsync(starts, 0xff, m * sizeof(uint32_t), st));
     for (int o = 0; o < p.n_oct; o++) {
         if (p.oh[o] < 2 * kImageBorder || p.ow[o] < 2 * kImageBorder) continue;  // src/lib.rs:315
@@ -784,7 +784,7 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
     DL.idx = order;
     DL.n = cnt + 3;
     DL.bound = B.bk;
-    DL.work = work + 1;
+    DL.work = work;
     DL.key_base = (uint64_t)frame_base << kKeyImgShift;
     DL.gauss = p.d_gauss.p;
     DL.gauss_img_stride = p.d_gstride.p;

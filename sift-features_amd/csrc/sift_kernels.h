@@ -156,12 +156,20 @@ void launch_match(const uint8_t* q, int nq, const uint8_t* t, int nt, int cross_
                   hipStream_t st);
 
 // describe.hip
+// Descriptor work queues: keypoint i belongs to queue i % kDescQueues, which
+// hands out its keypoints in order; 8 counters on separate 128-B lines (one
+// per XCD) keep the same-address atomic rate at an eighth.
+constexpr int kDescQueues = 8;
+constexpr int kDescQueueStride = 32;  // uint32 words
+constexpr int kDescWorkWords = kDescQueues * kDescQueueStride;
+
 struct DescLaunch {
     const KpRec* kp;
     const uint32_t* idx;  // final order -> kp index (may be null = identity)
     const uint32_t* n;    // device count, clamped to bound
     uint32_t bound;
-    uint32_t* work;       // zeroed work counter: waves take keypoints dynamically (costs vary ~20x)
+    uint32_t* work;       // kDescQueues zeroed work counters, kDescQueueStride words apart: waves
+                          // take keypoints dynamically (costs vary ~20x)
     uint64_t key_base;    // added to the emission keys (frame offset of the chunk)
     const float* const* gauss;
     const size_t* gauss_img_stride;

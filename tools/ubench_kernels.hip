@@ -28,11 +28,11 @@ float time_describe(const DescLaunch& L, int reps) {
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
     dim3 grid(std::min<uint32_t>(L.bound, 256 * 8));
-    CK(hipMemset(L.work, 0, 4));
+    CK(hipMemset(L.work, 0, kDescWorkWords * 4));
     hipLaunchKernelGGL((k_describe<E, A>), grid, dim3(64), 0, 0, L);
     CK(hipEventRecord(a));
     for (int i = 0; i < reps; i++) {
-        CK(hipMemsetAsync(L.work, 0, 4, 0));
+        CK(hipMemsetAsync(L.work, 0, kDescWorkWords * 4, 0));
         hipLaunchKernelGGL((k_describe<E, A>), grid, dim3(64), 0, 0, L);
     }
     CK(hipEventRecord(b));
@@ -178,7 +178,7 @@ int main(int argc, char** argv) {
     L.n = d_n;
     L.bound = NKP;
     uint32_t* d_work;
-    CK(hipMalloc(&d_work, 4));
+    CK(hipMalloc(&d_work, kDescWorkWords * 4));
     L.work = d_work;
     L.gauss = d_g;
     L.gauss_img_stride = d_gs;
@@ -196,6 +196,11 @@ int main(int argc, char** argv) {
     std::printf("  fast s1 f32     %8.3f ms\n", time_describe<1, 16>(L, reps));
     std::printf("  fast s2 f32     %8.3f ms\n", time_describe<2, 16>(L, reps));
     std::printf("  fast s4 f32     %8.3f ms\n", time_describe<4, 16>(L, reps));
+    std::printf("  fast s2 f32 -rmw     %8.3f ms\n", time_describe<2, 17>(L, reps));
+    std::printf("  fast s2 f32 nosample %8.3f ms\n", time_describe<2, 80>(L, reps));
+    std::printf("  fast s2 -all -rmw    %8.3f ms\n", time_describe<2, 15>(L, reps));
+    std::printf("  fast s2 f32 static   %8.3f ms\n", time_describe<2, 144>(L, reps));
+    std::printf("  fast s2 f32 nosample static %8.3f ms\n", time_describe<2, 208>(L, reps));
     std::printf("  fast s2 -atan2  %8.3f ms\n", time_describe<2, 2>(L, reps));
     std::printf("  fast s2 -loads  %8.3f ms\n", time_describe<2, 8>(L, reps));
     std::printf("  fast s2 -all    %8.3f ms\n", time_describe<2, 14>(L, reps));
