@@ -18,14 +18,6 @@
 #include "sift_common.h"
 #include "sift_kernels.h"
 
-// Build-time choice of the fast path's per-sample transcendentals: 0 = the
-// reference's (f64 atan2, correctly rounded expf), 16 = f32 ocml atan2f/expf
-// (default: ~10 % faster; measured on MI355X the u8 descriptors stay >= 99.99 %
-// byte-identical to the oracle either way, tools/exp/desc_math_check.py).
-#ifndef SIFT_DESC_MATH
-#define SIFT_DESC_MATH 16
-#endif
-
 namespace siftmi {
 
 
@@ -75,8 +67,11 @@ __device__ __forceinline__ float row_hi(float hi0, float kk, bool row_only, floa
 // column on each side -- the reference's f32 predicate decides membership per
 // sample -- and their exclusive prefix sums (the compacted sample index of
 // each row's first sample), built with wave scans.
+// Optional clip window [xmin, xmax] x [ymin, ymax] (window coordinates): the
+// fast path drops samples outside the image here instead of testing each one.
 __device__ __forceinline__ void build_row_table(int* rowlo, int* rowpre, int radius, float cos_s, float sin_s,
-                                                int lane) {
+                                                int lane, int xmin = INT_MIN, int xmax = INT_MAX,
+                                                int ymin = INT_MIN, int ymax = INT_MAX) {
     const int n = 2 * radius + 1;
     const double c = cos_s, s = sin_s;
     const bool cz = !(fabs(c) > 1e-30), sz = !(fabs(s) > 1e-30);
@@ -87,8 +82,8 @@ __device__ __forceinline__ void build_row_table(int* rowlo, int* rowpre, int rad
         const int row = lane + 64 * h;
         if (row < n) {
             const double yi = (double)(row - radius);
-            double lo = -radius, hi = radius;
-            bool empty = false;
+            double lo = fmax(-radius, (double)xmin), hi = fmin(radius, (double)xmax);
+            bool empty = row - radius < ymin || row - radius > ymax;
             if (!cz) {
                 const double a = (yi * s - 2.5) * rc, b = (yi * s + 2.5) * rc;
                 lo = fmax(lo, fmin(a, b) - 1.0);
@@ -332,9 +327,42 @@ struct DescScratchFast {
     int rowpre[ROWS_MAX + 1];
 };
 
-// kAblate bit 4: f32 atan2 / exp (ocml) instead of the reference's f64 atan2
-// and the correctly rounded f32 exp -- results stay within the fast path's
-// +-1 tolerance (the sample angle moves by < 1e-5 degree).
+// atan2(dy, dx) in degrees for a pair of samples: |t| = min/max in [0, 1]
+// (v_rcp_f32), atan(t) = t + t s P(s) (s = t^2, degree-7 minimax, |error| <
+// 6e-8 on [0, 1] in f32), then the octant / quadrant reflections.  atan2(+0,
+// +0) = 0 and atan2(+0, x < 0) = 180 as the reference's; the gradient
+// differences are never -0.
+__device__ __forceinline__ f2v atan2_deg2(f2v dy, f2v dx) {
+    const f2v ax = __builtin_elementwise_abs(dx), ay = __builtin_elementwise_abs(dy);
+    const f2v mx = __builtin_elementwise_max(ax, ay), mn = __builtin_elementwise_min(ax, ay);
+    f2v t = mn * f2v{__builtin_amdgcn_rcpf(mx.x), __builtin_amdgcn_rcpf(mx.y)};
+    t.x = mx.x > 0.0f ? t.x : 0.0f;
+    t.y = mx.y > 0.0f ? t.y : 0.0f;
+    const f2v sq = t * t;
+    f2v p = f2v{0.0025999427f, 0.0025999427f};
+    p = __builtin_elementwise_fma(p, sq, f2v{-0.015042510f, -0.015042510f});
+    p = __builtin_elementwise_fma(p, sq, f2v{0.040974170f, 0.040974170f});
+    p = __builtin_elementwise_fma(p, sq, f2v{-0.073540933f, -0.073540933f});
+    p = __builtin_elementwise_fma(p, sq, f2v{0.10567977f, 0.10567977f});
+    p = __builtin_elementwise_fma(p, sq, f2v{-0.14184459f, -0.14184459f});
+    p = __builtin_elementwise_fma(p, sq, f2v{0.19990212f, 0.19990212f});
+    p = __builtin_elementwise_fma(p, sq, f2v{-0.33332980f, -0.33332980f});
+    f2v a = __builtin_elementwise_fma(t * sq, p, t);
+    constexpr float kHalfPi = 1.57079632679489662f, kPi = 3.14159265358979324f;
+#pragma unroll
+    for (int j = 0; j < 2; j++) {
+        float v = ay[j] > ax[j] ? kHalfPi - a[j] : a[j];
+        v = dx[j] < 0.0f ? kPi - v : v;
+        a[j] = dy[j] < 0.0f ? -v : v;
+    }
+    return a * (180.0f / kPi);
+}
+
+// Fast path per-sample math: the reference's expressions (same operand order,
+// -ffp-contract=off) in packed f32 on two samples at a time, with hardware
+// transcendentals -- v_sqrt_f32 / v_exp_f32 (1 ulp) and atan2_deg2 -- in place
+// of the correctly rounded ones: the sample angle moves by < 1e-5 degree and
+// the weights by ~1e-7 relative, inside the fast path's +-1 u8 tolerance.
 template <int kShare, int kAblate = 0>
 __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img, int pitch, int width, int height,
                                                    float xf, float yf, float scale, float orientation,
@@ -357,13 +385,15 @@ __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img
 #pragma unroll
     for (int i = 0; i < PRIV_STRIDE * NS / 4; i += 64)
         if (i + lane < PRIV_STRIDE * NS / 4) reinterpret_cast<float4*>(sc.h)[i + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
-    build_row_table(sc.rowlo, sc.rowpre, radius, cos_s, sin_s, lane);
-    const int total_samples = sc.rowpre[n];
-    // lane-strided samples: one load instruction touches ~64 neighbouring
-    // pixels (2-3 cache lines) instead of 64 scattered ones.  Software
-    // pipelined: the gradient loads of a lane's next sample are issued before
-    // the current sample is processed (a wave spends ~2 us per load round trip
-    // otherwise, with only ~2 waves per SIMD to cover it).
+    // samples outside the image (0 < y + yi < height - 1, 0 < x + xi < width - 1
+    // fails) are not enumerated
+    build_row_table(sc.rowlo, sc.rowpre, radius, cos_s, sin_s, lane, 1 - x, width - 2 - x, 1 - y, height - 2 - y);
+    const int total = (kAblate & 64) ? 0 : sc.rowpre[n];  // kAblate bit 6: no samples (per-keypoint overhead)
+    // Lane-strided samples: one load instruction touches ~64 neighbouring
+    // pixels (2-3 cache lines) instead of 64 scattered ones.  Each iteration
+    // takes two samples per lane (k, k + 64) -- packed math, independent
+    // chains for the ~2 waves per SIMD the LDS footprint allows -- and the
+    // gradient loads of the next two are in flight meanwhile.
     int row = 0;
     const gfloat* gimg = as_global(img);
     auto locate = [&](int k, int& xi, int& yi) {
@@ -371,109 +401,125 @@ __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img
         yi = row - radius;
         xi = sc.rowlo[row] + (k - sc.rowpre[row]);
     };
-    // the four neighbours of sample k; positions outside the image (rejected
-    // samples) are clamped so every load stays inside the plane
     auto fetch = [&](int xi, int yi, float& l, float& r, float& u, float& d) {
-        const int ay = min(max(y + yi, 1), height - 2), ax = min(max(x + xi, 1), width - 2);
-        const gfloat* rw = gimg + (size_t)ay * pitch + ax;
+        const gfloat* rw = gimg + (size_t)(y + yi) * pitch + (x + xi);
         r = rw[1];
         l = rw[-1];
         u = rw[-pitch];
         d = rw[pitch];
     };
-    int nxi = 0, nyi = 0;
-    float nl = 0.f, nr = 0.f, nu = 0.f, nd = 0.f;
     f2v sink = {0.f, 0.f};  // kAblate bit 0: register sink instead of the slice updates
-    const int total = (kAblate & 64) ? 0 : total_samples;  // bit 6: no samples (per-keypoint overhead)
-    if (lane < total) {
-        locate(lane, nxi, nyi);
-        if (!(kAblate & 8)) fetch(nxi, nyi, nl, nr, nu, nd);
-    }
-    for (int k = lane; k < total; k += 64) {
-        const int xi = nxi, yi = nyi;
-        const float gl = nl, gr = nr, gu = nu, gd = nd;
-        {
-            const int k2 = min(k + 64, total - 1);  // the last lap refetches its own sample
-            locate(k2, nxi, nyi);
-            if (!(kAblate & 8)) fetch(nxi, nyi, nl, nr, nu, nd);
+    int nxi[2] = {0, 0}, nyi[2] = {0, 0};
+    float nl[2] = {0.f, 0.f}, nr[2] = {0.f, 0.f}, nu[2] = {0.f, 0.f}, nd[2] = {0.f, 0.f};
+    if (total > 0) {
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            locate(min(lane + 64 * u, total - 1), nxi[u], nyi[u]);
+            if (!(kAblate & 8)) fetch(nxi[u], nyi[u], nl[u], nr[u], nu[u], nd[u]);
         }
-        const float col_rot = (float)xi * cos_s - (float)yi * sin_s;
-        const float row_rot = (float)xi * sin_s + (float)yi * cos_s;
-        float row_bin = row_rot + (float)(kDescHist / 2);
-        float col_bin = col_rot + (float)(kDescHist / 2);
-        const int32_t ay = y + yi, ax = x + xi;
-        const bool inside = row_bin > -0.5f && row_bin < (float)kDescHist + 0.5f && col_bin > -0.5f &&
-                            col_bin < (float)kDescHist + 0.5f && ay > 0 && ay < height - 1 && ax > 0 &&
-                            ax < width - 1;
-        if (kShare == 1 && !inside) continue;
-        float dx, dy;
+    }
+    for (int k = lane; k - lane < total; k += 128) {
+        const int xi[2] = {nxi[0], nxi[1]}, yi[2] = {nyi[0], nyi[1]};
+        const f2v gl = {nl[0], nl[1]}, gr = {nr[0], nr[1]}, gu = {nu[0], nu[1]}, gd = {nd[0], nd[1]};
+        if (k - lane + 128 < total) {
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                locate(min(k + 128 + 64 * u, total - 1), nxi[u], nyi[u]);
+                if (!(kAblate & 8)) fetch(nxi[u], nyi[u], nl[u], nr[u], nu[u], nd[u]);
+            }
+        }
+        const f2v fx = {(float)xi[0], (float)xi[1]}, fy = {(float)yi[0], (float)yi[1]};
+        const f2v cs = {cos_s, cos_s}, sn = {sin_s, sin_s};
+        const f2v col_rot = fx * cs - fy * sn;
+        const f2v row_rot = fx * sn + fy * cs;
+        f2v row_bin = row_rot + (float)(kDescHist / 2);
+        f2v col_bin = col_rot + (float)(kDescHist / 2);
+        bool inside[2];
+#pragma unroll
+        for (int u = 0; u < 2; u++)
+            inside[u] = k + 64 * u < total && row_bin[u] > -0.5f && row_bin[u] < (float)kDescHist + 0.5f &&
+                        col_bin[u] > -0.5f && col_bin[u] < (float)kDescHist + 0.5f;
+        f2v dx, dy;
         if (kAblate & 8) {
-            dx = (float)xi * 0.01f + 0.001f;
-            dy = (float)yi * 0.01f - 0.002f;
+            dx = fx * 0.01f + 0.001f;
+            dy = fy * 0.01f - 0.002f;
         } else {
             dx = gr - gl;
             dy = gu - gd;
         }
-        const float wsq = col_rot * col_rot + row_rot * row_rot;
-        const float earg = wsq * (-2.f / (float)(kDescHist * kDescHist));
-        const float weight = (kAblate & 4) ? 1.0f + wsq * (-0.125f) : ((kAblate & 16) ? expf(earg) : exp_f32(earg));
-        float degf;
-        if (kAblate & 18) {
-            // f32 angle v: (float)(((double)v + 360) % 360) == (v < 0 ? v + 360.0f : v)
-            // (the f64 sum is exact, and rounded once either way)
-            const float v = (kAblate & 2) ? dy * 50.0f + dx : atan2f(dy, dx) * (180.0f / 3.14159265358979323846f);
-            degf = v < 0.0f ? v + 360.0f : v;
+        const f2v wsq = col_rot * col_rot + row_rot * row_rot;
+        f2v weight;
+        if (kAblate & 4) {
+            weight = wsq * (-0.125f) + 1.0f;
         } else {
-            double deg = atan2((double)dy, (double)dx) * (180.0 / 3.14159265358979323846) + 360.0;
-            deg = deg >= 360.0 ? deg - 360.0 : deg;  // f64 `% 360.0` of a value in [180, 540]
-            degf = (float)deg;
+            const f2v e2 = wsq * (-2.f / (float)(kDescHist * kDescHist)) * 1.44269504088896341f;
+            weight = f2v{__builtin_amdgcn_exp2f(e2.x), __builtin_amdgcn_exp2f(e2.y)};
         }
-        const float ori = degf - orientation;
-        float mag = sqrtf(dx * dx + dy * dy);
+        f2v degf = (kAblate & 2) ? dy * 50.0f + dx : atan2_deg2(dy, dx);
+        // (float)(((double)v + 360) % 360) == (v < 0 ? v + 360.0f : v): the f64
+        // sum is exact and rounded once either way
+#pragma unroll
+        for (int u = 0; u < 2; u++) degf[u] = degf[u] < 0.0f ? degf[u] + 360.0f : degf[u];
+        const f2v ori = degf - orientation;
+        f2v mag = dx * dx + dy * dy;
+        mag = f2v{__builtin_amdgcn_sqrtf(mag.x), __builtin_amdgcn_sqrtf(mag.y)};
         row_bin = row_bin - 0.5f;
         col_bin = col_bin - 0.5f;
         mag = mag * weight;
-        const float obin = ori * BIN_ANGLE_STEP;
-        const float row_floor = floorf(row_bin), col_floor = floorf(col_bin), ori_floor = floorf(obin);
-        const float row_frac = row_bin - row_floor, col_frac = col_bin - col_floor, ori_frac = obin - ori_floor;
-        const float c1 = mag * row_frac, c0 = mag - c1;
-        const float c11 = c1 * col_frac, c10 = c1 - c11;
-        const float c01 = c0 * col_frac, c00 = c0 - c01;
-        const float c111 = c11 * ori_frac, c110 = c11 - c111;
-        const float c101 = c10 * ori_frac, c100 = c10 - c101;
-        const float c011 = c01 * ori_frac, c010 = c01 - c011;
-        const float c001 = c00 * ori_frac, c000 = c00 - c001;
-        const int r1 = (int)row_floor + 1, q1 = (int)col_floor + 1;  // 0..4
-        int o0 = (int)ori_floor;
-        o0 = o0 < 0 ? o0 + kDescBins : (o0 >= kDescBins ? o0 - kDescBins : o0);
-        o0 &= kDescBins - 1;
-        // slot pair of each footprint corner: (cell, o0 / o0 + 1) of an interior
-        // cell, or the corner's own dummy pair (144 + 2 * corner) on the border ring
-        const bool rv1 = (uint32_t)(r1 - 1) < 4u, rv2 = (uint32_t)r1 < 4u;  // rows r1, r1 + 1 interior
-        const bool qv1 = (uint32_t)(q1 - 1) < 4u, qv2 = (uint32_t)q1 < 4u;
-        const bool v11 = rv1 & qv1, v12 = rv1 & qv2, v21 = rv2 & qv1, v22 = rv2 & qv2;
-        const int base = ((r1 - 1) * 4 + (q1 - 1)) * 9 + o0;  // o0 + 1 <= 8: no wrap
-        const int a0 = (v11 ? base : 144) * NS, a2 = (v12 ? base + 9 : 146) * NS;
-        const int a4 = (v21 ? base + 36 : 148) * NS, a6 = (v22 ? base + 45 : 150) * NS;
-        const f2v w00 = {c000, c001}, w01 = {c010, c011}, w10 = {c100, c101}, w11 = {c110, c111};
+        const f2v obin = ori * BIN_ANGLE_STEP;
+        const f2v row_floor = __builtin_elementwise_floor(row_bin), col_floor = __builtin_elementwise_floor(col_bin);
+        const f2v ori_floor = __builtin_elementwise_floor(obin);
+        const f2v row_frac = row_bin - row_floor, col_frac = col_bin - col_floor, ori_frac = obin - ori_floor;
+        const f2v c1 = mag * row_frac, c0 = mag - c1;
+        const f2v c11 = c1 * col_frac, c10 = c1 - c11;
+        const f2v c01 = c0 * col_frac, c00 = c0 - c01;
+        const f2v c111 = c11 * ori_frac, c110 = c11 - c111;
+        const f2v c101 = c10 * ori_frac, c100 = c10 - c101;
+        const f2v c011 = c01 * ori_frac, c010 = c01 - c011;
+        const f2v c001 = c00 * ori_frac, c000 = c00 - c001;
+        int a[2][4];
+#pragma unroll
+        for (int u = 0; u < 2; u++) {
+            const int r1 = (int)row_floor[u] + 1, q1 = (int)col_floor[u] + 1;  // 0..4
+            int o0 = (int)ori_floor[u];
+            o0 = o0 < 0 ? o0 + kDescBins : (o0 >= kDescBins ? o0 - kDescBins : o0);
+            o0 &= kDescBins - 1;
+            // slot pair of each footprint corner: (cell, o0 / o0 + 1) of an interior
+            // cell, or the corner's own dummy pair (144 + 2 * corner) on the border ring
+            const bool rv1 = (uint32_t)(r1 - 1) < 4u, rv2 = (uint32_t)r1 < 4u;  // rows r1, r1 + 1 interior
+            const bool qv1 = (uint32_t)(q1 - 1) < 4u, qv2 = (uint32_t)q1 < 4u;
+            const int base = ((r1 - 1) * 4 + (q1 - 1)) * 9 + o0;  // o0 + 1 <= 8: no wrap
+            a[u][0] = ((rv1 && qv1) ? base : 144) * NS;
+            a[u][1] = ((rv1 && qv2) ? base + 9 : 146) * NS;
+            a[u][2] = ((rv2 && qv1) ? base + 36 : 148) * NS;
+            a[u][3] = ((rv2 && qv2) ? base + 45 : 150) * NS;
+        }
+        const f2v w[2][4] = {{f2v{c000.x, c001.x}, f2v{c010.x, c011.x}, f2v{c100.x, c101.x}, f2v{c110.x, c111.x}},
+                             {f2v{c000.y, c001.y}, f2v{c010.y, c011.y}, f2v{c100.y, c101.y}, f2v{c110.y, c111.y}}};
         if (kAblate & 1) {
-            if (inside) sink += (w00 + w01) * (w10 + w11) + f2v{(float)a0, (float)(a2 + a4 + a6)};
+#pragma unroll
+            for (int u = 0; u < 2; u++)
+                if (inside[u])
+                    sink += (w[u][0] + w[u][1]) * (w[u][2] + w[u][3]) +
+                            f2v{(float)a[u][0], (float)(a[u][1] + a[u][2] + a[u][3])};
             continue;
         }
 #pragma unroll
         for (int g = 0; g < kShare; g++) {
-            if (kShare > 1 && !(inside && grp == g)) continue;
-            const f2v h0 = {hp[a0], hp[a0 + NS]}, h2 = {hp[a2], hp[a2 + NS]};
-            const f2v h4 = {hp[a4], hp[a4 + NS]}, h6 = {hp[a6], hp[a6 + NS]};
-            const f2v s0 = h0 + w00, s2 = h2 + w01, s4 = h4 + w10, s6 = h6 + w11;
-            hp[a0] = s0.x;
-            hp[a0 + NS] = s0.y;
-            hp[a2] = s2.x;
-            hp[a2 + NS] = s2.y;
-            hp[a4] = s4.x;
-            hp[a4 + NS] = s4.y;
-            hp[a6] = s6.x;
-            hp[a6 + NS] = s6.y;
+#pragma unroll
+            for (int u = 0; u < 2; u++) {
+                if (!(inside[u] && grp == g)) continue;
+                // 4 distinct slot pairs: all reads, then all writes
+                f2v h[4];
+#pragma unroll
+                for (int j = 0; j < 4; j++) h[j] = f2v{hp[a[u][j]], hp[a[u][j] + NS]};
+#pragma unroll
+                for (int j = 0; j < 4; j++) {
+                    const f2v sum = h[j] + w[u][j];
+                    hp[a[u][j]] = sum.x;
+                    hp[a[u][j] + NS] = sum.y;
+                }
+            }
         }
     }
     wave_sync();
@@ -511,14 +557,11 @@ __global__ __launch_bounds__(64) void k_describe(const DescLaunch L) {
     // Keypoints come from kDescQueues interleaved queues (queue q holds
     // keypoints q, q + 8, ...; one wave per keypoint, window costs vary ~20x):
     // a wave drains its home queue (blockIdx % 8, the XCD the block runs on),
-    // then the others in turn.  kAblate bit 7: static assignment.
-    uint32_t it = 0;
+    // then the others in turn.
     int q = blockIdx.x & (kDescQueues - 1), drained = 0;
     for (;;) {
         uint32_t i = 0;
-        if (kAblate & 128) {
-            i = blockIdx.x + gridDim.x * it++;
-        } else {
+        {
             uint32_t j = 0;
             if (lane == 0) j = atomicAdd(L.work + q * kDescQueueStride, 1u);
             j = __builtin_amdgcn_readfirstlane(__shfl(j, 0));
@@ -570,7 +613,7 @@ void launch_describe(const DescLaunch& L, hipStream_t st) {
     if (L.exact)
         hipLaunchKernelGGL((k_describe<0, 0>), grid, dim3(64), 0, st, L);
     else
-        hipLaunchKernelGGL((k_describe<2, SIFT_DESC_MATH>), grid, dim3(64), 0, st, L);
+        hipLaunchKernelGGL((k_describe<2, 0>), grid, dim3(64), 0, st, L);
 }
 
 __global__ __launch_bounds__(64) void k_describe_one(const float* img, int w, int h, float x, float y, float scale,

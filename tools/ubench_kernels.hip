@@ -193,16 +193,12 @@ int main(int argc, char** argv) {
     std::printf("  fast s1         %8.3f ms\n", time_describe<1, 0>(L, reps));
     std::printf("  fast s2         %8.3f ms\n", time_describe<2, 0>(L, reps));
     std::printf("  fast s4         %8.3f ms\n", time_describe<4, 0>(L, reps));
-    std::printf("  fast s1 f32     %8.3f ms\n", time_describe<1, 16>(L, reps));
-    std::printf("  fast s2 f32     %8.3f ms\n", time_describe<2, 16>(L, reps));
-    std::printf("  fast s4 f32     %8.3f ms\n", time_describe<4, 16>(L, reps));
-    std::printf("  fast s2 f32 -rmw     %8.3f ms\n", time_describe<2, 17>(L, reps));
-    std::printf("  fast s2 f32 nosample %8.3f ms\n", time_describe<2, 80>(L, reps));
-    std::printf("  fast s2 -all -rmw    %8.3f ms\n", time_describe<2, 15>(L, reps));
-    std::printf("  fast s2 f32 static   %8.3f ms\n", time_describe<2, 144>(L, reps));
-    std::printf("  fast s2 f32 nosample static %8.3f ms\n", time_describe<2, 208>(L, reps));
+    std::printf("  fast s2 -rmw    %8.3f ms\n", time_describe<2, 1>(L, reps));
+    std::printf("  fast s2 nosample %8.3f ms\n", time_describe<2, 64>(L, reps));
     std::printf("  fast s2 -atan2  %8.3f ms\n", time_describe<2, 2>(L, reps));
+    std::printf("  fast s2 -exp    %8.3f ms\n", time_describe<2, 4>(L, reps));
     std::printf("  fast s2 -loads  %8.3f ms\n", time_describe<2, 8>(L, reps));
     std::printf("  fast s2 -all    %8.3f ms\n", time_describe<2, 14>(L, reps));
+    std::printf("  fast s2 -all -rmw %8.3f ms\n", time_describe<2, 15>(L, reps));
     return 0;
 }
