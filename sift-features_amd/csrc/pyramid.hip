@@ -269,96 +269,129 @@ __device__ __forceinline__ float upsample_at(const uint8_t* __restrict__ src, si
     return h0 * tab.ya0[dy] + h1 * tab.ya1[dy];
 }
 
+// Index range [lo, hi] of the reflect-101 positions p0 .. p0 + n - 1 of an
+// axis of length L (one reflection per side: n <= L).
+__device__ __forceinline__ void reflect_range(int p0, int n, int L, int& lo, int& hi) {
+    lo = max(p0, 0);
+    hi = min(p0 + n - 1, L - 1);
+    if (p0 < 0) hi = max(hi, min(-p0, L - 1));                    // left reflections 1 .. -p0
+    if (p0 + n > L) lo = min(lo, max(2 * L - 1 - (p0 + n), 0));  // right ones down to 2L - 1 - (p0 + n)
+}
+
 template <int R, int TH>
 __global__ __launch_bounds__(256) void k_seed(const uint8_t* __restrict__ frames, size_t frame_pitch,
                                               size_t row_stride, int sh, int sw, const ResizeTab tab,
                                               float* __restrict__ dst, size_t dst_img_stride, int W, int H,
                                               int pitch, const BlurTaps taps) {
     using G = BlurGeom<R, TH>;
-    // source window: a span of D upsampled pixels needs <= D/2 + 2 source pixels
-    constexpr int SR = G::IH / 2 + 3, SC = G::IWV / 2 + 3;
-    static_assert(G::IH <= 128 && G::IWV <= 128, "span reduction covers 128 positions per axis");
+    // Source window of an exact 2x upsample: destination g reads source
+    // floor(g / 2 - 0.25) and the next one, so the window's destination range
+    // [glo, ghi] needs source [glo / 2 - 1, ghi / 2 + 1] (clamped): computed
+    // here, no table reads before the source loads.
+    constexpr int SR = G::IH / 2 + 4, SC = G::IWV / 2 + 4;
+    constexpr int NW = (SC + 3) / 4 + 1;  // dwords per source row (unaligned start)
+    constexpr int NLD = (SR * NW + 255) / 256;
     __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
     __shared__ float srcf[SR * SC];         // u8 -> f32 source window
     __shared__ __attribute__((aligned(16))) float hbuf[SR * G::IWV];  // HResizeLinear per source row
     __shared__ float lut[256];
-    __shared__ int span[4][4];              // per wave: min/max upsampled x (waves 0,1) / y (waves 2,3)
     // per window column / row: source index and coefficients (resize tables)
     __shared__ __attribute__((aligned(16))) int txo[G::IWV];
     __shared__ __attribute__((aligned(16))) float txa0[G::IWV], txa1[G::IWV];
     __shared__ int tyo[G::IH];
     __shared__ float tya0[G::IH], tya1[G::IH];
-    static_assert(G::IWV % 4 == 0, "float4 passes");
+    static_assert(G::IWV % 4 == 0 && G::IWV <= 128 && G::IH <= 128, "table threads: columns 0..127, rows 128..255");
     float* tin = lds;
     float* th = lds;
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const int tid = threadIdx.x;
     lut[tid] = (float)tid / 255.0f;
     const TileId tile = xcd_tile();
     const int x0 = tile.x * G::TW, y0 = tile.y * G::TH;
     const size_t b = tile.z;
     const uint8_t* src = frames + b * frame_pitch;
-    // per window column (threads 0..127) / row (128..255): reflect-101 position,
-    // its resize table entries (all loads in flight together), and the span of
-    // source columns / rows the window needs
+    // the exact-2x window math needs single reflections and a 2x geometry
+    const bool fast = W == 2 * sw && H == 2 * sh && W >= G::IWV && H >= G::IH;
+    int sxa = 0, sya = 0, sxb = -1, syb = -1;
+    if (fast) {
+        int glo, ghi;
+        reflect_range(x0 - G::HWL, G::IWV, W, glo, ghi);
+        sxa = max(glo / 2 - 1, 0);
+        sxb = min(ghi / 2 + 1, sw - 1);
+        reflect_range(y0 - R, G::IH, H, glo, ghi);
+        sya = max(glo / 2 - 1, 0);
+        syb = min(ghi / 2 + 1, sh - 1);
+    }
+    // 1. in flight together: the window's source dwords and its resize table
+    //    entries (threads 0..127: columns, 128..255: rows)
+    const int a0 = sxa & ~3;  // first source dword (4-B aligned frame rows)
+    const int nwr = (sxb - a0) / 4 + 1, nr = syb - sya + 1;
+    uint32_t wv[NLD];
+#pragma unroll
+    for (int j = 0; j < NLD; j++) {
+        const int i = tid + 256 * j;
+        const int r = i / NW, w = i - r * NW;
+        wv[j] = 0;
+        if (fast && r < nr && w < nwr) {
+            const int c = a0 + 4 * w;
+            const uint8_t* p = src + (size_t)(sya + r) * row_stride + c;
+            if (c + 3 < sw) {
+                wv[j] = *reinterpret_cast<const uint32_t*>(p);
+            } else {  // row end: bytes only (the dword could run past the frame)
+                for (int q = 0; q < 4 && c + q < sw; q++) wv[j] |= (uint32_t)p[q] << (8 * q);
+            }
+        }
+    }
     {
         const int t = tid & 127;
-        const bool isx = tid < 128;
-        const bool act = isx ? t < G::IWV : t < G::IH;
-        const int g = act ? (isx ? reflect101(x0 - G::HWL + t, W) : reflect101(y0 - R + t, H)) : 0;
-        int s0 = 0, s1 = 0;
-        if (act && isx) {
-            s0 = tab.xofs[g];
-            s1 = min(s0 + 1, sw - 1);
+        if (tid < 128 && t < G::IWV) {
+            const int g = reflect101(x0 - G::HWL + t, W);
+            const int s0 = tab.xofs[g];
             txo[t] = g < tab.xmax ? s0 : -1 - s0;  // < 0: single-tap right border
             txa0[t] = tab.xa0[g];
             txa1[t] = tab.xa1[g];
-        } else if (act) {
-            s0 = tab.yofs[g];
-            s1 = min(s0 + 1, sh - 1);
-            tyo[t] = s0;
+        } else if (tid >= 128 && t < G::IH) {
+            const int g = reflect101(y0 - R + t, H);
+            tyo[t] = tab.yofs[g];
             tya0[t] = tab.ya0[g];
             tya1[t] = tab.ya1[g];
         }
-        int mn = act ? s0 : INT_MAX, mx = act ? s1 : INT_MIN;
-#pragma unroll
-        for (int o = 32; o >= 1; o >>= 1) {
-            mn = min(mn, __shfl_xor(mn, o));
-            mx = max(mx, __shfl_xor(mx, o));
-        }
-        if (lane == 0) {
-            span[wv][0] = mn;
-            span[wv][1] = mx;
-        }
     }
-    __syncthreads();
-    const int sxa = min(span[0][0], span[1][0]), sxb = max(span[0][1], span[1][1]);
-    const int sya = min(span[2][0], span[3][0]), syb = max(span[2][1], span[3][1]);
-    const int nc = sxb - sxa + 1, nr = syb - sya + 1;
-    if (nc <= SC && nr <= SR) {
-        for (int r = wv; r < nr; r += 4)
-            for (int c = lane; c < nc; c += 64)
-                srcf[r * SC + c] = lut[src[(size_t)(sya + r) * row_stride + sxa + c]];
+    __syncthreads();  // lut
+    if (fast) {
+        // 2. u8 -> f32 (v / 255) into the source window
+#pragma unroll
+        for (int j = 0; j < NLD; j++) {
+            const int i = tid + 256 * j;
+            const int r = i / NW, w = i - r * NW;
+            if (r < nr && w < nwr) {
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int c = a0 + 4 * w + q - sxa;
+                    if (c >= 0 && c < SC) srcf[r * SC + c] = lut[(wv[j] >> (8 * q)) & 0xff];
+                }
+            }
+        }
         __syncthreads();
-        // HResizeLinear: t = S[sx]*a0 + S[sx+1]*a1 (two roundings + add); 4 columns per item
+        // 3. HResizeLinear: t = S[sx]*a0 + S[sx+1]*a1 (two roundings + add); 4 columns per item
         constexpr int Q = G::IWV / 4;
         for (int i = tid; i < nr * Q; i += 256) {
             const int r = i / Q, c = (i - r * Q) * 4;
             const int4 xo = *reinterpret_cast<const int4*>(txo + c);
-            const float4 a0 = *reinterpret_cast<const float4*>(txa0 + c);
-            const float4 a1 = *reinterpret_cast<const float4*>(txa1 + c);
+            const float4 w0 = *reinterpret_cast<const float4*>(txa0 + c);
+            const float4 w1 = *reinterpret_cast<const float4*>(txa1 + c);
             const float* sr = srcf + r * SC - sxa;
-            auto hres = [&](int o, float w0, float w1) {
+            auto hres = [&](int o, float u0, float u1) {
                 const bool two = o >= 0;
                 const int sx = two ? o : -1 - o;
                 const float p0 = sr[sx];
-                return two ? p0 * w0 + sr[sx + 1] * w1 : p0;
+                return two ? p0 * u0 + sr[sx + 1] * u1 : p0;
             };
             *reinterpret_cast<float4*>(hbuf + r * G::IWV + c) =
-                make_float4(hres(xo.x, a0.x, a1.x), hres(xo.y, a0.y, a1.y), hres(xo.z, a0.z, a1.z),
-                            hres(xo.w, a0.w, a1.w));
+                make_float4(hres(xo.x, w0.x, w1.x), hres(xo.y, w0.y, w1.y), hres(xo.z, w0.z, w1.z),
+                            hres(xo.w, w0.w, w1.w));
         }
         __syncthreads();
-        // VResizeLinear: S0*b0 + S1*b1; 4 columns per item
+        // 4. VResizeLinear: S0*b0 + S1*b1; 4 columns per item
         for (int i = tid; i < G::IH * Q; i += 256) {
             const int ly = i / Q, c = (i - ly * Q) * 4;
             const int s0 = tyo[ly];
@@ -369,7 +402,7 @@ __global__ __launch_bounds__(256) void k_seed(const uint8_t* __restrict__ frames
             *reinterpret_cast<float4*>(tin + ly * G::IWP + c) =
                 make_float4(u.x * b0 + v.x * b1, u.y * b0 + v.y * b1, u.z * b0 + v.z * b1, u.w * b0 + v.w * b1);
         }
-    } else {  // not reached for a 2x seed; kept for safety on degenerate shapes
+    } else {  // small or non-2x frames: per pixel from the tables
         for (int i = tid; i < G::IH * G::IWV; i += 256) {
             const int ly = i / G::IWV, lx = i - ly * G::IWV;
             const int gy = reflect101(y0 - R + ly, H), gx = reflect101(x0 - G::HWL + lx, W);
