@@ -110,7 +110,9 @@ int sift_mi_set_exact_descriptors(sift_mi_ctx* ctx, int exact);
  * device memory; see sift_mi_device_results).  Default 0 = copy. */
 int sift_mi_set_keep_on_device(sift_mi_ctx* ctx, int keep);
 
-/* Device pointers of the last (single-chunk) result; valid until the next call. */
+/* Device pointers of the last batch's results (keep_on_device = 1): the
+ * keypoints and descriptors of every frame, concatenated in frame order
+ * (frame i at offsets[i] .. offsets[i+1]); valid until the next call. */
 int sift_mi_device_results(sift_mi_ctx* ctx, const sift_mi_keypoint** d_kps, const uint8_t** d_desc, size_t* n);
 
 /* ---- src/lib.rs:123-143 `precompute_images` / `PrecomputedImages` ------- */

@@ -67,6 +67,23 @@ struct DevBuf {
     }
 };
 
+// Grows d to at least n elements keeping its first `used` elements (device copy
+// on stream st, synchronised).
+template <class T>
+int grow_keep(DevBuf<T>& d, size_t n, size_t used, hipStream_t st) {
+    if (n <= d.cap && d.p) return 0;
+    DevBuf<T> nd;
+    CHK(nd.ensure(std::max(n, 2 * d.cap)));
+    if (used && d.p) HIPCHK(hipMemcpyAsync(nd.p, d.p, used * sizeof(T), hipMemcpyDeviceToDevice, st));
+    HIPCHK(hipStreamSynchronize(st));
+    d.release();
+    d.p = nd.p;
+    d.cap = nd.cap;
+    nd.p = nullptr;
+    nd.cap = 0;
+    return 0;
+}
+
 template <class T>
 struct PinBuf {
     T* p = nullptr;
@@ -414,6 +431,10 @@ struct sift_mi_ctx {
     int last_slot = 0;
     // per-frame high-water marks that size the next chunk's bounds
     double pf_cand = 0, pf_ext = 0, pf_kp = 0;
+    // device results of a whole batch (keep_on_device), concatenated in frame order
+    DevBuf<OutKp> r_kp;
+    DevBuf<uint8_t> r_desc;
+    DevBuf<uint64_t> r_key;
     // host results (pinned)
     PinBuf<OutKp> h_kp;
     PinBuf<uint8_t> h_desc;
@@ -851,6 +872,25 @@ int finalize_chunk(sift_mi_ctx* c, int si, size_t* offsets) {
     }
     c->dev_result_n = n_out;
     c->last_slot = si;
+    if (c->keep_on_device && n_out) {
+        // whole-batch device arena: device-to-device copies on the copy stream
+        const size_t need = base + n_out;
+        if (need > c->r_kp.cap || need * kDescSize > c->r_desc.cap || need > c->r_key.cap) {
+            HIPCHK(hipStreamSynchronize(c->cstream));
+            CHK(grow_keep(c->r_kp, need, base, c->cstream));
+            CHK(grow_keep(c->r_desc, need * kDescSize, base * kDescSize, c->cstream));
+            CHK(grow_keep(c->r_key, need, base, c->cstream));
+        }
+        HIPCHK(hipStreamWaitEvent(c->cstream, S.ev[6], 0));
+        HIPCHK(hipMemcpyAsync(c->r_kp.p + base, S.out_kp.p, n_out * sizeof(OutKp), hipMemcpyDeviceToDevice,
+                              c->cstream));
+        HIPCHK(hipMemcpyAsync(c->r_desc.p + base * kDescSize, S.out_desc.p, (size_t)n_out * kDescSize,
+                              hipMemcpyDeviceToDevice, c->cstream));
+        HIPCHK(hipMemcpyAsync(c->r_key.p + base, S.out_key.p, n_out * sizeof(uint64_t), hipMemcpyDeviceToDevice,
+                              c->cstream));
+        HIPCHK(hipEventRecord(S.copied, c->cstream));
+        S.pending_copy = true;
+    }
     if (!c->keep_on_device) {
         const size_t need = base + n_out;
         if (need > c->h_kp.cap || need * kDescSize > c->h_desc.cap || need > c->h_key.cap) {
@@ -1057,6 +1097,9 @@ void sift_mi_destroy(sift_mi_ctx* c) {
             if (e) (void)hipEventDestroy(e);
         if (S.copied) (void)hipEventDestroy(S.copied);
     }
+    c->r_kp.release();
+    c->r_desc.release();
+    c->r_key.release();
     c->h_kp.release();
     c->h_desc.release();
     c->h_key.release();
@@ -1169,10 +1212,10 @@ int sift_mi_fetch_keys(sift_mi_ctx* c, uint64_t* keys, size_t cap) {
 int sift_mi_device_results(sift_mi_ctx* c, const sift_mi_keypoint** d_kps, const uint8_t** d_desc, size_t* n) {
     if (!c) return fail(SIFT_MI_EINVAL, "ctx is null");
     if (!c->have_result) return fail(SIFT_MI_ESTATE, "no result");
-    const Slot& S = c->slot[c->last_slot];
-    if (d_kps) *d_kps = reinterpret_cast<const sift_mi_keypoint*>(S.out_kp.p);
-    if (d_desc) *d_desc = S.out_desc.p;
-    if (n) *n = c->dev_result_n;
+    if (!c->keep_on_device) return fail(SIFT_MI_ESTATE, "results were copied to the host (keep_on_device is 0)");
+    if (d_kps) *d_kps = reinterpret_cast<const sift_mi_keypoint*>(c->r_kp.p);
+    if (d_desc) *d_desc = c->r_desc.p;
+    if (n) *n = c->n_result;
     return 0;
 }
 

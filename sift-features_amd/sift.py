@@ -209,6 +209,14 @@ class Context:
             return offsets, None
         return offsets, SiftResult(*self._fetch(int(offsets[-1]), out=out))
 
+    def device_results(self):
+        """(keypoints device pointer, descriptors device pointer, n) of the last
+        sift_batch_device(..., fetch=False): every frame's results, concatenated
+        in frame order, in HBM."""
+        kp, desc, n = ctypes.c_void_p(), ctypes.c_void_p(), ctypes.c_size_t()
+        check(lib().sift_mi_device_results(self._h, ctypes.byref(kp), ctypes.byref(desc), ctypes.byref(n)))
+        return kp.value, desc.value, n.value
+
     # -- precompute_images / sift_with_precomputed (src/lib.rs:123-177) ------
     def precompute_images(self, img):
         a = _u8_image(img)

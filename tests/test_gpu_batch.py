@@ -81,3 +81,34 @@ def test_random_noise(pkg, ctx, oracle):
     kp_o, desc_o, ext_o = oracle.sift(img, internal=True)
     res = ctx.sift(img)
     assert_parity(pkg, res, kp_o, desc_o, ext_o)
+
+
+@pytest.mark.parametrize("chunk", [0, 2])
+def test_device_resident_results(pkg, ctx, chunk):
+    """fetch=False keeps every frame's results in HBM (the bench's `value`
+    path); copied back they equal the host-fetched batch, chunked or not."""
+    import torch
+    fr = _frames()
+    t = torch.from_numpy(fr).cuda()
+    c2 = pkg.Context(0)
+    if chunk:
+        c2.set_chunk(chunk)
+    offs, res = c2.sift_batch_device(t.data_ptr(), t.shape[0], t.shape[2], t.shape[1], t.stride(1), t.stride(0),
+                                     fetch=False)
+    assert res is None
+    kp_ptr, desc_ptr, n = c2.device_results()
+    assert n == int(offs[-1]) > 0
+    # copy the device arrays back with hipMemcpy
+    kp = np.empty((n, 5), np.float32)
+    desc = np.empty((n, 128), np.uint8)
+    import ctypes
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    assert hip.hipMemcpy(kp.ctypes.data, kp_ptr, kp.nbytes, 2) == 0      # hipMemcpyDeviceToHost
+    assert hip.hipMemcpy(desc.ctypes.data, desc_ptr, desc.nbytes, 2) == 0
+    ref = ctx.sift_batch(fr)
+    for i in range(len(fr)):
+        a, b = int(offs[i]), int(offs[i + 1])
+        assert np.array_equal(kp[a:b], ref[i].keypoints_array), i
+        assert np.array_equal(desc[a:b], ref[i].descriptors), i
+    c2.close()
