@@ -21,7 +21,9 @@ for 1080p), not the "5 octaves" wording of configs[1].
 second, max-over-ranks wall time between barriers.
 `roofline` = the pyramid stage (seed + blur/DoG kernels; HBM-bound): its
 algorithmic bytes W*H + 44*sum(P_o) per frame / its HIP-event time on the
-kernels' stream, vs 8 TB/s.  `cpu_baseline` = the CPU oracle (a C port of
+kernels' stream, vs 8 TB/s, from a second pass of the same steps with the
+chunks serialised (one pipeline lane) so the stage runs alone;
+`stage_ms_per_step` comes from that pass too.  `cpu_baseline` = the CPU oracle (a C port of
 src/lib.rs, 1 thread) on a bounded sample of the same frames, rank 0 at N=1.
 """
 import argparse
@@ -108,7 +110,22 @@ def main():
     torch.cuda.synchronize()
     barrier()
     dt = time.perf_counter() - t0
+
+    # Stage timing pass: the same steps with the chunks run one after another
+    # (one pipeline lane), so the HIP-event time of each stage -- and the
+    # pyramid roofline below -- is its kernels' own, not shared with the
+    # overlapped neighbour chunk of the two-lane run that `value` measures.
+    ctx.set_pipeline_lanes(1)
+    step()
+    torch.cuda.synchronize()
+    ctx.reset_stats()
+    t1 = time.perf_counter()
+    for _ in range(args.steps):
+        step()
+    torch.cuda.synchronize()
+    serial_ms = 1e3 * (time.perf_counter() - t1) / args.steps
     st = ctx.stats()
+    ctx.set_pipeline_lanes(2)
 
     dt_max, total_kp, total_frames = shard.reduce_run(dt, n_kp, B * args.steps, dist if world > 1 else None)
 
@@ -161,9 +178,8 @@ def main():
     try:
         with open(os.path.join(ROOT, "profiles", "pmc_traffic.json")) as f:
             t = json.load(f)
-        if t["frame"] == f"{W}x{H}" and st["pyramid_launches"]:
-            frames_done = st["frames"]
-            traffic = t["pyramid_hbm_bytes_per_frame"] * frames_done / st["pyramid_launches"]
+        if t["frame"] == f"{W}x{H}":
+            traffic = t["pyramid_hbm_bytes_per_launch"]
             traffic_src = t["source"]
     except (OSError, KeyError, ValueError):
         pass
@@ -190,6 +206,7 @@ def main():
             "keypoints_per_frame": total_kp / max(1.0, total_frames),
             "stage_ms_per_step": {k: st[k] / args.steps for k in
                                   ("pyramid_ms", "detect_ms", "orient_ms", "order_ms", "descriptor_ms", "total_ms")},
+            "serial_lane_ms_per_step": serial_ms,
             "latency_1frame_ms": latency_ms,
             "host_fetch": host_fetch,
             "roofline": {"bound": "hbm", "achieved": pyr_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",

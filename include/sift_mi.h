@@ -106,6 +106,12 @@ int sift_mi_extract_batch_device(sift_mi_ctx* ctx, const uint8_t* d_frames, size
  * descriptors, slower.  Keypoints are identical in both modes. */
 int sift_mi_set_exact_descriptors(sift_mi_ctx* ctx, int exact);
 
+/* Batch pipeline lanes: 2 (default) runs consecutive chunks on two streams
+ * with their own pyramid arenas, so one chunk's kernels overlap the other's;
+ * 1 runs the chunks one after another on the context's stream (half the
+ * device memory; used to time kernels in isolation). */
+int sift_mi_set_pipeline_lanes(sift_mi_ctx* ctx, int lanes);
+
 /* Skip the device->host copy of results in batch calls (results stay in
  * device memory; see sift_mi_device_results).  Default 0 = copy. */
 int sift_mi_set_keep_on_device(sift_mi_ctx* ctx, int keep);

@@ -353,11 +353,12 @@ struct Plan {
     std::vector<size_t> P;           // floats per octave image plane (pitch * H)
     std::vector<size_t> px;          // real pixels per octave image (W * H)
     std::vector<size_t> goff, doff;  // float offsets of octave arenas
-    DevBuf<float> arena;             // [G_0 | D_0 | G_1 | D_1 ...], each chunk-major
+    DevBuf<float> arena[2];          // per lane: [G_0 | D_0 | G_1 | D_1 ...], each chunk-major
+    size_t arena_floats = 0;
     int profile = SIFT_MI_PROFILE_OPENCV;
     ResizeTabDev seed_tab;  // OpenCV profile
     IpTabDev seed_iptab;    // Imageproc profile
-    DevBuf<const float*> d_gauss, d_dog;
+    DevBuf<const float*> d_gauss[2], d_dog[2];  // per lane
     DevBuf<size_t> d_gstride, d_dstride;
     DevBuf<int> d_ow, d_oh, d_opitch;
     BlurTaps seed_taps{};
@@ -366,18 +367,21 @@ struct Plan {
     int oct_r[kImagesPerOctave]{};
     uint64_t algo_bytes_per_frame = 0;
 
-    float* gauss(int o) { return arena.p + goff[o]; }
-    float* dog(int o) { return arena.p + doff[o]; }
+    float* gauss(int o, int lane = 0) { return arena[lane].p + goff[o]; }
+    float* dog(int o, int lane = 0) { return arena[lane].p + doff[o]; }
     size_t gstride(int o) const { return (size_t)kImagesPerOctave * P[o]; }
     size_t dstride(int o) const { return (size_t)kDogPerOctave * P[o]; }
 
     void release() {
-        arena.release();
+        for (int l = 0; l < 2; l++) {
+            arena[l].release();
+            d_gauss[l].release();
+            d_dog[l].release();
+        }
+        arena_floats = 0;
         seed_tab.release();
         seed_iptab.release();
-        d_gauss.release();
         d_gstride.release();
-        d_dog.release();
         d_dstride.release();
         d_ow.release();
         d_oh.release();
@@ -405,20 +409,8 @@ struct Slot {
     bool pending_copy = false;
     uint32_t m = 0, frame_base = 0, cap_frames = 0;
     uint32_t bc = 0, be = 0, bk = 0;  // candidate / extremum / keypoint bounds used by this chunk
-};
-
-struct sift_mi_ctx {
-    int device = 0;
-    sift_mi_profile profile = SIFT_MI_PROFILE_OPENCV;
-    hipStream_t own = nullptr;
-    hipStream_t stream = nullptr;  // compute stream (own or the caller's)
-    hipStream_t cstream = nullptr; // device->host result copies
-    uint32_t chunk_override = 0;
-    int keep_on_device = 0;
-    int exact_descriptors = 0;
-    Plan plan;
-    DevBuf<uint8_t> staging;  // host-sourced frames
-    // detection / description buffers (shared by the slots: chunks run in stream order)
+    // detection / description buffers of this slot's lane (the slot's chunks
+    // run in its lane's stream order)
     DevBuf<uint64_t> cand;
     DevBuf<ExtRec> ext;
     DevBuf<KpRec> kp;
@@ -427,7 +419,37 @@ struct sift_mi_ctx {
     DevBuf<uint8_t> sort_tmp;
     DevBuf<uint32_t> seg_off, out_off;
     DevBuf<uint8_t> use_resp;
-    Slot slot[2];
+    void release_bufs() {
+        cand.release();
+        ext.release();
+        kp.release();
+        keys_a.release();
+        keys_b.release();
+        vals_a.release();
+        vals_b.release();
+        fin.release();
+        sort_tmp.release();
+        seg_off.release();
+        out_off.release();
+        use_resp.release();
+    }
+};
+
+struct sift_mi_ctx {
+    int device = 0;
+    sift_mi_profile profile = SIFT_MI_PROFILE_OPENCV;
+    hipStream_t own = nullptr;
+    hipStream_t stream = nullptr;  // compute stream (own or the caller's)
+    hipStream_t cstream = nullptr; // device->host result copies
+    hipStream_t own2 = nullptr;    // compute stream of pipeline lane 1 (lane 0 runs on `stream`)
+    hipEvent_t fork = nullptr;     // orders lane 1 after / before the caller's stream
+    int lanes = 2;                 // pipeline lanes (sift_mi_set_pipeline_lanes)
+    uint32_t chunk_override = 0;
+    int keep_on_device = 0;
+    int exact_descriptors = 0;
+    Plan plan;
+    DevBuf<uint8_t> staging;  // host-sourced frames
+    Slot slot[2];  // slot = pipeline lane: chunk k runs on lane k & 1
     int last_slot = 0;
     // per-frame high-water marks that size the next chunk's bounds
     double pf_cand = 0, pf_ext = 0, pf_kp = 0;
@@ -447,6 +469,16 @@ struct sift_mi_ctx {
 };
 
 namespace {
+
+// slot si's stream and pyramid arena: its own lane with two lanes, else lane 0
+hipStream_t lane_stream(sift_mi_ctx* c, int si) { return (si == 1 && c->lanes == 2) ? c->own2 : c->stream; }
+int arena_of(const sift_mi_ctx* c, int si) { return c->lanes == 2 ? si : 0; }
+
+int sync_lanes(sift_mi_ctx* c) {
+    HIPCHK(hipStreamSynchronize(c->stream));
+    HIPCHK(hipStreamSynchronize(c->own2));
+    return 0;
+}
 
 int set_device(sift_mi_ctx* c) {
     HIPCHK(hipSetDevice(c->device));
@@ -470,9 +502,28 @@ uint32_t auto_chunk(const Plan& p_probe_w_h, uint32_t w, uint32_t h, uint32_t n)
     return std::max<uint32_t>(1, std::min(c, n));
 }
 
+// Pyramid arena of one pipeline lane (chunks alternate between two lanes so
+// that one chunk's kernels overlap the other's) and its device pointer tables.
+int ensure_lane(sift_mi_ctx* c, int lane) {
+    Plan& p = c->plan;
+    if (p.arena[lane].p && p.d_gauss[lane].p) return 0;
+    CHK(p.arena[lane].ensure(p.arena_floats));
+    std::vector<const float*> gp(p.n_oct), dp(p.n_oct);
+    for (int o = 0; o < p.n_oct; o++) {
+        gp[o] = p.gauss(o, lane);
+        dp[o] = p.dog(o, lane);
+    }
+    CHK(p.d_gauss[lane].ensure(p.n_oct));
+    CHK(p.d_dog[lane].ensure(p.n_oct));
+    HIPCHK(hipMemcpyAsync(p.d_gauss[lane].p, gp.data(), p.n_oct * sizeof(float*), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipMemcpyAsync(p.d_dog[lane].p, dp.data(), p.n_oct * sizeof(float*), hipMemcpyHostToDevice, c->stream));
+    HIPCHK(hipStreamSynchronize(c->stream));
+    return 0;
+}
+
 int ensure_plan(sift_mi_ctx* c, uint32_t w, uint32_t h, uint32_t chunk) {
     Plan& p = c->plan;
-    if (p.w == w && p.h == h && p.chunk >= chunk && p.arena.p && p.profile == (int)c->profile) return 0;
+    if (p.w == w && p.h == h && p.chunk >= chunk && p.arena[0].p && p.profile == (int)c->profile) return 0;
     if (!(p.w == w && p.h == h && p.profile == (int)c->profile)) p.release();
     p.profile = (int)c->profile;
     const bool ip = c->profile == SIFT_MI_PROFILE_IMAGEPROC;
@@ -528,7 +579,12 @@ int ensure_plan(sift_mi_ctx* c, uint32_t w, uint32_t h, uint32_t chunk) {
         oh /= 2;
     }
     p.algo_bytes_per_frame = (uint64_t)w * h + 44ull * sum_p;
-    CHK(p.arena.ensure(total));
+    p.arena_floats = total;
+    for (int l = 0; l < 2; l++) {  // a larger chunk re-sizes both lanes
+        p.arena[l].release();
+        p.d_gauss[l].release();
+        p.d_dog[l].release();
+    }
     hipStream_t st = c->stream;
     if (ip)
         CHK(p.seed_iptab.upload((int)w, (int)h, 2 * (int)w, 2 * (int)h, 1.0f, kIpTaps, st));
@@ -536,24 +592,17 @@ int ensure_plan(sift_mi_ctx* c, uint32_t w, uint32_t h, uint32_t chunk) {
         CHK(p.seed_tab.upload((int)w, (int)h, 2 * (int)w, 2 * (int)h, st));
     if (ip && (p.seed_iptab.xtaps > kIpTaps || p.seed_iptab.ytaps > kIpTaps))
         return fail(SIFT_MI_EUNSUPPORTED, "2x Triangle upsample with more than 3 taps");
-    std::vector<const float*> gp(p.n_oct), dp(p.n_oct);
     std::vector<size_t> gs(p.n_oct), ds(p.n_oct);
     for (int o = 0; o < p.n_oct; o++) {
-        gp[o] = p.gauss(o);
         gs[o] = p.gstride(o);
-        dp[o] = p.dog(o);
         ds[o] = p.dstride(o);
     }
-    CHK(p.d_gauss.ensure(p.n_oct));
     CHK(p.d_gstride.ensure(p.n_oct));
-    CHK(p.d_dog.ensure(p.n_oct));
     CHK(p.d_dstride.ensure(p.n_oct));
-    HIPCHK(hipMemcpyAsync(p.d_dog.p, dp.data(), p.n_oct * sizeof(float*), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(p.d_dstride.p, ds.data(), p.n_oct * sizeof(size_t), hipMemcpyHostToDevice, st));
     CHK(p.d_ow.ensure(p.n_oct));
     CHK(p.d_oh.ensure(p.n_oct));
     CHK(p.d_opitch.ensure(p.n_oct));
-    HIPCHK(hipMemcpyAsync(p.d_gauss.p, gp.data(), p.n_oct * sizeof(float*), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(p.d_gstride.p, gs.data(), p.n_oct * sizeof(size_t), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(p.d_ow.p, p.ow.data(), p.n_oct * sizeof(int), hipMemcpyHostToDevice, st));
     HIPCHK(hipMemcpyAsync(p.d_oh.p, p.oh.data(), p.n_oct * sizeof(int), hipMemcpyHostToDevice, st));
@@ -565,15 +614,17 @@ int ensure_plan(sift_mi_ctx* c, uint32_t w, uint32_t h, uint32_t chunk) {
     octave_sigmas(sig);
     for (int s = 1; s < kImagesPerOctave; s++)
         p.oct_r[s] = ip ? ip_blur_taps((float)sig[s], &p.oct_taps[s]) : cv_blur_taps(sig[s], &p.oct_taps[s]);
-    return 0;
+    return ensure_lane(c, 0);
 }
 
 // ---------------------------------------------------------------------------
 // Stage 1: Gaussian scale space + DoG for n frames (device-resident u8)
 // ---------------------------------------------------------------------------
-int run_pyramid(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, size_t row_stride, uint32_t n) {
+int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_pitch, size_t row_stride,
+                uint32_t n) {
     Plan& p = c->plan;
-    hipStream_t st = c->stream;
+    hipStream_t st = lane_stream(c, lane);
+    lane = arena_of(c, lane);
     // seed: u8 -> 2x bilinear -> blur, fused, -> plane 0 of octave 0
     SeedLaunch S{};
     S.frames = d_frames;
@@ -584,7 +635,7 @@ int run_pyramid(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, siz
     S.tab = p.seed_tab.tab;
     S.iptab = p.seed_iptab.tab();
     S.profile = p.profile;
-    S.dst = p.gauss(0);
+    S.dst = p.gauss(0, lane);
     S.dst_img_stride = p.gstride(0);
     S.W = p.ow[0];
     S.H = p.oh[0];
@@ -594,8 +645,8 @@ int run_pyramid(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, siz
     if (launch_seed(p.seed_r, S, st)) return fail(SIFT_MI_EUNSUPPORTED, "seed blur radius");
     uint64_t launches = 1;
     for (int o = 0; o < p.n_oct; o++) {
-        float* G = p.gauss(o);
-        float* D = p.dog(o);
+        float* G = p.gauss(o, lane);
+        float* D = p.dog(o, lane);
         const size_t P = p.P[o];
         for (int s = 1; s < kImagesPerOctave; s++) {
             BlurLaunch B{};
@@ -606,7 +657,7 @@ int run_pyramid(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, siz
             B.dog = D + (size_t)(s - 1) * P;
             B.dog_img_stride = p.dstride(o);
             if (s == 3 && o + 1 < p.n_oct) {
-                B.nxt = p.gauss(o + 1);
+                B.nxt = p.gauss(o + 1, lane);
                 B.nxt_img_stride = p.gstride(o + 1);
                 B.pitch_n = p.opitch[o + 1];
                 B.wn = p.ow[o + 1];
@@ -661,34 +712,30 @@ Bounds chunk_bounds(sift_mi_ctx* c, uint32_t m) {
 
 // Grows the shared buffers for bounds B (waits for in-flight work first when a
 // buffer has to be reallocated).
-int reserve_chunk(sift_mi_ctx* c, const Bounds& B, uint32_t frames) {
-    const bool grow = B.bc > c->cand.cap || B.be > c->ext.cap || B.bk > c->kp.cap || B.bk > c->keys_a.cap ||
-                      frames > c->seg_off.cap;
-    bool grow_out = false;
-    for (auto& S : c->slot)
-        grow_out |= B.bk > S.out_kp.cap || 4 + 2 * frames + kDescWorkWords > S.counters.cap;
-    if (grow || grow_out) {
-        HIPCHK(hipStreamSynchronize(c->stream));
+int reserve_chunk(sift_mi_ctx* c, int si, const Bounds& B, uint32_t frames) {
+    Slot& S = c->slot[si];
+    const bool grow = B.bc > S.cand.cap || B.be > S.ext.cap || B.bk > S.kp.cap || B.bk > S.keys_a.cap ||
+                      frames > S.seg_off.cap || B.bk > S.out_kp.cap || 4 + 2 * frames + kDescWorkWords > S.counters.cap;
+    if (grow) {
+        HIPCHK(hipStreamSynchronize(lane_stream(c, si)));
         HIPCHK(hipStreamSynchronize(c->cstream));
     }
-    CHK(c->cand.ensure(B.bc));
-    CHK(c->ext.ensure(B.be));
-    CHK(c->kp.ensure(B.bk));
-    CHK(c->keys_a.ensure(B.bk));
-    CHK(c->keys_b.ensure(B.bk));
-    CHK(c->vals_a.ensure(B.bk));
-    CHK(c->vals_b.ensure(B.bk));
-    CHK(c->fin.ensure(B.bk));
-    CHK(c->seg_off.ensure(frames));
-    CHK(c->out_off.ensure(frames));
-    CHK(c->use_resp.ensure(frames));
-    for (auto& S : c->slot) {
-        CHK(S.counters.ensure(4 + 2 * frames + kDescWorkWords));
-        CHK(S.h_counts.ensure(4 + 2 * frames));
-        CHK(S.out_kp.ensure(B.bk));
-        CHK(S.out_desc.ensure((size_t)B.bk * kDescSize));
-        CHK(S.out_key.ensure(B.bk));
-    }
+    CHK(S.cand.ensure(B.bc));
+    CHK(S.ext.ensure(B.be));
+    CHK(S.kp.ensure(B.bk));
+    CHK(S.keys_a.ensure(B.bk));
+    CHK(S.keys_b.ensure(B.bk));
+    CHK(S.vals_a.ensure(B.bk));
+    CHK(S.vals_b.ensure(B.bk));
+    CHK(S.fin.ensure(B.bk));
+    CHK(S.seg_off.ensure(frames));
+    CHK(S.out_off.ensure(frames));
+    CHK(S.use_resp.ensure(frames));
+    CHK(S.counters.ensure(4 + 2 * frames + kDescWorkWords));
+    CHK(S.h_counts.ensure(4 + 2 * frames));
+    CHK(S.out_kp.ensure(B.bk));
+    CHK(S.out_desc.ensure((size_t)B.bk * kDescSize));
+    CHK(S.out_key.ensure(B.bk));
     return 0;
 }
 
@@ -701,7 +748,7 @@ int img_bits_for(uint32_t m) {
 int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_t frame_base, const Bounds& B) {
     Plan& p = c->plan;
     Slot& S = c->slot[si];
-    hipStream_t st = c->stream;
+    hipStream_t st = lane_stream(c, si);
     S.m = m;
     S.frame_base = frame_base;
     S.cap_frames = m;
@@ -718,7 +765,7 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
     for (int o = 0; o < p.n_oct; o++) {
         if (p.oh[o] < 2 * kImageBorder || p.ow[o] < 2 * kImageBorder) continue;  // src/lib.rs:315
         DetectLaunch D{};
-        D.dog = p.dog(o);
+        D.dog = p.dog(o, arena_of(c, si));
         D.img_stride = p.dstride(o);
         D.W = p.ow[o];
         D.H = p.oh[o];
@@ -726,37 +773,37 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
         D.octave = o;
         D.n_img = (int)m;
         D.img_base = 0;
-        D.cand = c->cand.p;
+        D.cand = S.cand.p;
         D.counter = cnt + 0;
         D.cap = B.bc;
         launch_detect(D, st);
     }
     RefineLaunch R{};
-    R.cand = c->cand.p;
+    R.cand = S.cand.p;
     R.n_cand = cnt + 0;
     R.cand_cap = B.bc;
-    R.dog = p.d_dog.p;
+    R.dog = p.d_dog[arena_of(c, si)].p;
     R.dog_img_stride = p.d_dstride.p;
     R.ow = p.d_ow.p;
     R.oh = p.d_oh.p;
     R.opitch = p.d_opitch.p;
     R.img_base = 0;
-    R.out = c->ext.p;
+    R.out = S.ext.p;
     R.counter = cnt + 1;
     R.cap = B.be;
     launch_refine(R, st);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(S.ev[2], st));
     OrientLaunch O{};
-    O.ext = c->ext.p;
+    O.ext = S.ext.p;
     O.n_ext = cnt + 1;
     O.ext_cap = B.be;
-    O.gauss = p.d_gauss.p;
+    O.gauss = p.d_gauss[arena_of(c, si)].p;
     O.gauss_img_stride = p.d_gstride.p;
     O.ow = p.d_ow.p;
     O.oh = p.d_oh.p;
     O.opitch = p.d_opitch.p;
-    O.out = c->kp.p;
+    O.out = S.kp.p;
     O.counter = cnt + 2;
     O.img_base = 0;
     O.cap = B.bk;
@@ -767,47 +814,47 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
     const int img_bits = img_bits_for(m);
     const int end_bit = kKeyImgShift + img_bits;
     const uint64_t pad = (end_bit >= 64) ? ~0ull : ((1ull << end_bit) - 1);
-    size_t tmp = sort_pairs_u64(nullptr, 0, c->keys_a.p, c->keys_b.p, c->vals_a.p, c->vals_b.p, B.bk, end_bit, st);
+    size_t tmp = sort_pairs_u64(nullptr, 0, S.keys_a.p, S.keys_b.p, S.vals_a.p, S.vals_b.p, B.bk, end_bit, st);
     const int rb = 32 + img_bits;
     const uint64_t rpad = (1ull << rb) - 1;
     if (limit >= 0)
-        tmp = std::max(tmp, sort_pairs_u64(nullptr, 0, c->keys_a.p, c->keys_b.p, c->vals_a.p, c->fin.p, B.bk, rb, st));
+        tmp = std::max(tmp, sort_pairs_u64(nullptr, 0, S.keys_a.p, S.keys_b.p, S.vals_a.p, S.fin.p, B.bk, rb, st));
     if (!tmp) return fail(SIFT_MI_EHIP, "radix sort sizing failed");
-    if (tmp > c->sort_tmp.cap) {
+    if (tmp > S.sort_tmp.cap) {
         HIPCHK(hipStreamSynchronize(st));
-        CHK(c->sort_tmp.ensure(tmp));
+        CHK(S.sort_tmp.ensure(tmp));
     }
-    launch_make_sort_keys(c->kp.p, cnt + 2, B.bk, pad, c->keys_a.p, c->vals_a.p, st);
-    if (!sort_pairs_u64(c->sort_tmp.p, c->sort_tmp.cap, c->keys_a.p, c->keys_b.p, c->vals_a.p, c->vals_b.p, B.bk,
+    launch_make_sort_keys(S.kp.p, cnt + 2, B.bk, pad, S.keys_a.p, S.vals_a.p, st);
+    if (!sort_pairs_u64(S.sort_tmp.p, S.sort_tmp.cap, S.keys_a.p, S.keys_b.p, S.vals_a.p, S.vals_b.p, B.bk,
                         end_bit, st))
         return fail(SIFT_MI_EHIP, "radix sort failed");
-    const uint32_t* order = c->vals_b.p;  // emission order -> kp index
-    launch_frame_starts(c->keys_b.p, cnt + 2, B.bk, starts, st);
+    const uint32_t* order = S.vals_b.p;  // emission order -> kp index
+    launch_frame_starts(S.keys_b.p, cnt + 2, B.bk, starts, st);
     // features_limit (src/lib.rs:156-161): per-frame plan on the device
-    launch_limit_plan(starts, cnt + 2, B.bk, (int)m, limit, out_cnt, c->seg_off.p, c->out_off.p, c->use_resp.p,
+    launch_limit_plan(starts, cnt + 2, B.bk, (int)m, limit, out_cnt, S.seg_off.p, S.out_off.p, S.use_resp.p,
                       cnt + 3, st);
     if (limit >= 0) {
         // stable sort: response-descending within each frame, emission order on ties
-        launch_make_resp_keys(c->kp.p, order, cnt + 2, B.bk, 0, rpad, c->keys_a.p, c->vals_a.p, st);
-        if (!sort_pairs_u64(c->sort_tmp.p, c->sort_tmp.cap, c->keys_a.p, c->keys_b.p, c->vals_a.p, c->fin.p, B.bk, rb,
+        launch_make_resp_keys(S.kp.p, order, cnt + 2, B.bk, 0, rpad, S.keys_a.p, S.vals_a.p, st);
+        if (!sort_pairs_u64(S.sort_tmp.p, S.sort_tmp.cap, S.keys_a.p, S.keys_b.p, S.vals_a.p, S.fin.p, B.bk, rb,
                             st))
             return fail(SIFT_MI_EHIP, "response sort failed");
-        launch_select(order, c->fin.p, c->seg_off.p, c->out_off.p, c->use_resp.p, (int)m, cnt + 3, B.bk, c->vals_a.p,
+        launch_select(order, S.fin.p, S.seg_off.p, S.out_off.p, S.use_resp.p, (int)m, cnt + 3, B.bk, S.vals_a.p,
                       st);
-        order = c->vals_a.p;
+        order = S.vals_a.p;
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(S.ev[4], st));
     // descriptors into this slot's outputs, once its previous copy-out is done
     if (S.pending_copy) HIPCHK(hipStreamWaitEvent(st, S.copied, 0));
     DescLaunch DL{};
-    DL.kp = c->kp.p;
+    DL.kp = S.kp.p;
     DL.idx = order;
     DL.n = cnt + 3;
     DL.bound = B.bk;
     DL.work = work;
     DL.key_base = (uint64_t)frame_base << kKeyImgShift;
-    DL.gauss = p.d_gauss.p;
+    DL.gauss = p.d_gauss[arena_of(c, si)].p;
     DL.gauss_img_stride = p.d_gstride.p;
     DL.ow = p.d_ow.p;
     DL.oh = p.d_oh.p;
@@ -840,10 +887,12 @@ int enqueue_chunk(sift_mi_ctx* c, int si, const uint8_t* d_frames, size_t frame_
                   int64_t limit, uint32_t frame_base, bool pyramid) {
     Slot& S = c->slot[si];
     const Bounds B = chunk_bounds(c, m);
-    CHK(reserve_chunk(c, B, c->plan.chunk));
-    HIPCHK(hipEventRecord(S.ev[0], c->stream));
-    if (pyramid) CHK(run_pyramid(c, d_frames, frame_pitch, stride, m));
-    HIPCHK(hipEventRecord(S.ev[1], c->stream));
+    CHK(ensure_lane(c, arena_of(c, si)));
+    CHK(reserve_chunk(c, si, B, c->plan.chunk));
+    hipStream_t st = lane_stream(c, si);
+    HIPCHK(hipEventRecord(S.ev[0], st));
+    if (pyramid) CHK(run_pyramid(c, si, d_frames, frame_pitch, stride, m));
+    HIPCHK(hipEventRecord(S.ev[1], st));
     return enqueue_keypoints(c, si, m, limit, frame_base, B);
 }
 
@@ -942,10 +991,11 @@ int check_frame_args(uint32_t w, uint32_t h, size_t stride) {
     return 0;
 }
 
-// Device-resident batch pipeline: chunks alternate between the two slots;
-// chunk k+1 is enqueued before the host waits for chunk k, so the GPU never
-// idles on host round trips, and chunk k's results travel to the host on the
-// copy stream while chunk k+1 computes.
+// Device-resident batch pipeline: chunks alternate between two lanes (slot,
+// stream, pyramid arena and stage buffers each), so chunk k+1's kernels run
+// beside chunk k's -- the small octaves, sorts and kernel tails of one chunk
+// leave CUs idle that the other fills -- and chunk k+2 is enqueued as soon as
+// chunk k has been finalised.  Results travel on the copy stream.
 int extract_device(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, uint32_t n, uint32_t w, uint32_t h,
                    size_t stride, int64_t limit, size_t* offsets) {
     CHK(check_frame_args(w, h, stride));
@@ -961,20 +1011,32 @@ int extract_device(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, 
         return enqueue_chunk(c, (int)(k & 1), d_frames + (size_t)k * chunk * frame_pitch, frame_pitch, stride,
                              frames_of(k), limit, k * chunk, true);
     };
+    // lane 1 starts after the caller's stream (frames produced there); the
+    // caller's stream resumes after lane 1's last chunk
+    const bool two = n_chunks > 1 && c->lanes == 2;
+    if (two) {
+        HIPCHK(hipEventRecord(c->fork, c->stream));
+        HIPCHK(hipStreamWaitEvent(c->own2, c->fork, 0));
+    }
     CHK(enqueue(0));
+    if (n_chunks > 1) CHK(enqueue(1));
     for (uint32_t k = 0; k < n_chunks; k++) {
-        if (k + 1 < n_chunks) CHK(enqueue(k + 1));
         int rc = finalize_chunk(c, (int)(k & 1), offsets);
         if (rc < 0) return rc;
         for (int attempt = 0; rc == 1; attempt++) {
-            // a stage overflowed its bound: drain (the already enqueued chunk
-            // k+1 completes first, its results are unaffected), then re-run k
+            // a stage overflowed its bound: drain both lanes (the other lane's
+            // chunk is unaffected), then re-run k on its lane
             if (attempt == 3) return fail(SIFT_MI_ENOMEM, "stage count kept exceeding its buffer bound");
-            HIPCHK(hipStreamSynchronize(c->stream));
+            CHK(sync_lanes(c));
             CHK(enqueue(k));
             rc = finalize_chunk(c, (int)(k & 1), offsets);
             if (rc < 0) return rc;
         }
+        if (k + 2 < n_chunks) CHK(enqueue(k + 2));
+    }
+    if (two) {
+        HIPCHK(hipEventRecord(c->fork, c->own2));
+        HIPCHK(hipStreamWaitEvent(c->stream, c->fork, 0));
     }
     HIPCHK(hipStreamSynchronize(c->cstream));
     if (offsets) offsets[n] = c->n_result;
@@ -1055,7 +1117,9 @@ int sift_mi_create(int device_ordinal, sift_mi_profile profile, sift_mi_ctx** ou
         return fail(SIFT_MI_EHIP, "hipStreamCreate failed");
     }
     c->stream = c->own;
-    bool ok = hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking) == hipSuccess;
+    bool ok = hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking) == hipSuccess &&
+              hipStreamCreateWithFlags(&c->own2, hipStreamNonBlocking) == hipSuccess;
+    ok = ok && hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) == hipSuccess;
     for (auto& S : c->slot) {
         for (auto& e : S.ev) ok = ok && hipEventCreate(&e) == hipSuccess;
         ok = ok && hipEventCreateWithFlags(&S.copied, hipEventDisableTiming) == hipSuccess;
@@ -1072,21 +1136,11 @@ void sift_mi_destroy(sift_mi_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
     if (c->stream) (void)hipStreamSynchronize(c->stream);
+    if (c->own2) (void)hipStreamSynchronize(c->own2);
     if (c->cstream) (void)hipStreamSynchronize(c->cstream);
     c->plan.release();
     c->staging.release();
-    c->cand.release();
-    c->ext.release();
-    c->kp.release();
-    c->keys_a.release();
-    c->keys_b.release();
-    c->vals_a.release();
-    c->vals_b.release();
-    c->fin.release();
-    c->sort_tmp.release();
-    c->seg_off.release();
-    c->out_off.release();
-    c->use_resp.release();
+    for (auto& S : c->slot) S.release_bufs();
     for (auto& S : c->slot) {
         S.counters.release();
         S.h_counts.release();
@@ -1097,6 +1151,7 @@ void sift_mi_destroy(sift_mi_ctx* c) {
             if (e) (void)hipEventDestroy(e);
         if (S.copied) (void)hipEventDestroy(S.copied);
     }
+    if (c->fork) (void)hipEventDestroy(c->fork);
     c->r_kp.release();
     c->r_desc.release();
     c->r_key.release();
@@ -1104,6 +1159,7 @@ void sift_mi_destroy(sift_mi_ctx* c) {
     c->h_desc.release();
     c->h_key.release();
     if (c->cstream) (void)hipStreamDestroy(c->cstream);
+    if (c->own2) (void)hipStreamDestroy(c->own2);
     if (c->own) (void)hipStreamDestroy(c->own);
     delete c;
 }
@@ -1123,6 +1179,14 @@ int sift_mi_set_chunk(sift_mi_ctx* c, uint32_t k) {
 int sift_mi_set_exact_descriptors(sift_mi_ctx* c, int exact) {
     if (!c) return fail(SIFT_MI_EINVAL, "ctx is null");
     c->exact_descriptors = exact ? 1 : 0;
+    return 0;
+}
+
+int sift_mi_set_pipeline_lanes(sift_mi_ctx* c, int lanes) {
+    if (!c || (lanes != 1 && lanes != 2)) return fail(SIFT_MI_EINVAL, "lanes must be 1 or 2");
+    CHK(set_device(c));
+    CHK(sync_lanes(c));
+    c->lanes = lanes;
     return 0;
 }
 
@@ -1228,7 +1292,7 @@ int sift_mi_precompute(sift_mi_ctx* c, const uint8_t* pixels, uint32_t w, uint32
     const uint8_t* frames[1] = {pixels};
     CHK(upload_frames(c, frames, 1, w, h, stride));
     CHK(ensure_plan(c, w, h, 1));
-    CHK(run_pyramid(c, c->staging.p, (size_t)w * h, w, 1));
+    CHK(run_pyramid(c, 0, c->staging.p, (size_t)w * h, w, 1));
     HIPCHK(hipStreamSynchronize(c->stream));
     c->have_pyramid = true;
     c->have_result = false;

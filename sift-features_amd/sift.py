@@ -209,6 +209,10 @@ class Context:
             return offsets, None
         return offsets, SiftResult(*self._fetch(int(offsets[-1]), out=out))
 
+    def set_pipeline_lanes(self, lanes):
+        """2 (default): consecutive batch chunks overlap on two streams; 1: serial."""
+        check(lib().sift_mi_set_pipeline_lanes(self._h, int(lanes)))
+
     def device_results(self):
         """(keypoints device pointer, descriptors device pointer, n) of the last
         sift_batch_device(..., fetch=False): every frame's results, concatenated

@@ -112,3 +112,17 @@ def test_device_resident_results(pkg, ctx, chunk):
         assert np.array_equal(kp[a:b], ref[i].keypoints_array), i
         assert np.array_equal(desc[a:b], ref[i].descriptors), i
     c2.close()
+
+
+def test_pipeline_lanes_equal(pkg, ctx):
+    """Two-lane (overlapped chunks) and one-lane batches give identical results."""
+    fr = _frames()
+    out = []
+    for lanes in (1, 2):
+        c2 = pkg.Context(0)
+        c2.set_chunk(2)
+        c2.set_pipeline_lanes(lanes)
+        out.append(c2.sift_batch(fr))
+        c2.close()
+    assert all(a == b for a, b in zip(out[0], out[1]))
+    assert all(a == b for a, b in zip(out[0], ctx.sift_batch(fr)))

@@ -47,31 +47,50 @@ trace = one("trace/**/run_kernel_trace.csv")
 stats = one("trace/**/run_kernel_stats.csv")
 shutil.copy(stats, os.path.join(PROF, f"{ROUND}_kernel_stats.csv"))
 b = bench_line(os.path.join(OUT, "bench_trace.log"))
-steps_total = b["steps"] + b["warmup"] if b else 4
 
 agg = defaultdict(lambda: [0, 0.0])
-for r in csv.DictReader(open(trace)):
+rows = list(csv.DictReader(open(trace)))
+for r in rows:
     k = short(r["Kernel_Name"])
     agg[k][0] += 1
     agg[k][1] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
 tot = sum(v[1] for k, v in agg.items() if "siftmi" in k or k.startswith("k_"))
 pyr_us = sum(v[1] for k, v in agg.items() if k.startswith(PYR))
 pyr_n = sum(v[0] for k, v in agg.items() if k.startswith(PYR))
+n_chunks = agg["k_seed<5, 32>"][0] if "k_seed<5, 32>" in agg else max(1, sum(v[0] for k, v in agg.items() if k.startswith("k_seed")))
+
+# Pyramid launches that ran alone (no kernel of another stream overlapping):
+# the serialised stage-timing pass of bench.py, whose HIP-event launch
+# average is the roofline's denominator.  The two-lane passes overlap chunks.
+ivs = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Stream_Id"], short(r["Kernel_Name"])) for r in rows)
+iso_us, iso_n = 0.0, 0
+for i, (s0, e0, st, k) in enumerate(ivs):
+    if not k.startswith(PYR):
+        continue
+    alone = True
+    for j in range(max(0, i - 64), min(len(ivs), i + 64)):
+        s1, e1, st1, _ = ivs[j]
+        if j != i and st1 != st and s1 < e0 and e1 > s0:
+            alone = False
+            break
+    if alone:
+        iso_us += (e0 - s0) / 1e3
+        iso_n += 1
 
 
 def pmc(kind, name):
     f = one(f"{kind}/**/run_counter_collection.csv")
-    v = 0.0
+    v, n = 0.0, 0
     for r in csv.DictReader(open(f)):
         if r["Counter_Name"] == name and short(r["Kernel_Name"]).startswith(PYR):
             v += float(r["Counter_Value"])
-    return v * 1024.0  # KiB -> bytes
+            n += 1
+    return v * 1024.0, n  # KiB -> bytes
 
 
-fetch = 2.0 * pmc("fetch", "FETCH_SIZE")  # gfx950: half of 16-B streaming reads counted
-write = pmc("write", "WRITE_SIZE")
-frames_total = FRAMES * steps_total  # the PMC passes run the same command (warmup + steps)
-traffic_pf = (fetch + write) / frames_total
+fetch, n_f = pmc("fetch", "FETCH_SIZE")
+fetch *= 2.0  # gfx950: half of 16-B streaming reads counted
+write, n_w = pmc("write", "WRITE_SIZE")
 W, H = 1920, 1080
 sum_p, ow, oh = 0, 2 * W, 2 * H
 for _ in range(int(round(__import__("math").log2(min(2 * W, 2 * H)) - 2)) + 1):
@@ -79,9 +98,14 @@ for _ in range(int(round(__import__("math").log2(min(2 * W, 2 * H)) - 2)) + 1):
     ow //= 2
     oh //= 2
 algo_pf = W * H + 44 * sum_p
-json.dump({"round": ROUND, "frame": f"{W}x{H}", "frames_per_call": FRAMES,
-           "pyramid_hbm_bytes_per_frame": traffic_pf, "fetch_bytes_per_frame": fetch / frames_total,
-           "write_bytes_per_frame": write / frames_total, "algorithmic_bytes_per_frame": algo_pf,
+chunk = min(64, max(1, int(16e9 // (44.0 * sum_p))), FRAMES)  # host auto_chunk
+launches_per_chunk = pyr_n / max(1, n_chunks)
+traffic_pl = fetch / max(1, n_f) + write / max(1, n_w)  # HBM bytes per pyramid launch
+traffic_pf = traffic_pl * launches_per_chunk / chunk
+json.dump({"round": ROUND, "frame": f"{W}x{H}", "frames_per_call": FRAMES, "frames_per_chunk": chunk,
+           "pyramid_hbm_bytes_per_launch": traffic_pl, "pyramid_hbm_bytes_per_frame": traffic_pf,
+           "fetch_bytes_per_launch": fetch / max(1, n_f), "write_bytes_per_launch": write / max(1, n_w),
+           "algorithmic_bytes_per_frame": algo_pf,
            "source": f"profiles/{ROUND}_summary.md (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)"},
           open(os.path.join(PROF, "pmc_traffic.json"), "w"), indent=1)
 
@@ -93,14 +117,18 @@ with open(os.path.join(PROF, f"{ROUND}_summary.md"), "w") as f:
         f.write(f"bench line (traced run): value = {b['value']:.4g} keypoints/s, ms_per_step = "
                 f"{b['ms_per_step']:.2f}, stage_ms_per_step = {json.dumps(b['stage_ms_per_step'])}\n\n")
     f.write("## Pyramid stage (the roofline kernel group: k_seed + k_blur<R>)\n\n")
-    f.write(f"* trace: {pyr_n} launches over {steps_total} calls, {pyr_us / 1e3:.3f} ms total -> "
-            f"{pyr_us / 1e3 / steps_total:.3f} ms per call, {pyr_us / max(1, pyr_n):.1f} us per launch\n")
+    f.write(f"* trace, all passes: {pyr_n} launches, {pyr_us / 1e3:.3f} ms total, {pyr_us / max(1, pyr_n):.1f} us "
+            f"per launch (two-lane passes overlap two chunks, which stretches each launch)\n")
+    f.write(f"* trace, launches that ran alone (the serialised stage-timing pass): {iso_n} launches, "
+            f"{iso_us / max(1, iso_n):.1f} us per launch\n")
     if b:
-        f.write(f"* bench.py (HIP events on the compute stream, timed steps only): pyramid_ms per step = "
+        f.write(f"* bench.py (HIP events on the compute stream, serialised pass): pyramid_ms per step = "
                 f"{b['stage_ms_per_step']['pyramid_ms']:.3f}, avg launch = {b['roofline']['avg_launch_ms'] * 1e3:.1f} us\n")
-    f.write(f"* algorithmic bytes per frame (W*H + 44*sum P_o) = {algo_pf / 1e6:.1f} MB\n")
-    f.write(f"* HBM traffic per frame (PMC, FETCH_SIZE x2 + WRITE_SIZE) = {traffic_pf / 1e6:.1f} MB "
-            f"(read {fetch / frames_total / 1e6:.1f} MB, write {write / frames_total / 1e6:.1f} MB); "
+    f.write(f"* algorithmic bytes per frame (W*H + 44*sum P_o) = {algo_pf / 1e6:.1f} MB; per launch "
+            f"{algo_pf * chunk / launches_per_chunk / 1e6:.1f} MB ({launches_per_chunk:.0f} launches per chunk of {chunk} frames)\n")
+    f.write(f"* HBM traffic (PMC, FETCH_SIZE x2 + WRITE_SIZE, mean over {n_f} pyramid dispatches) = "
+            f"{traffic_pl / 1e6:.1f} MB per launch = {traffic_pf / 1e6:.1f} MB per frame "
+            f"(read {fetch / max(1, n_f) / 1e6:.1f} MB, write {write / max(1, n_w) / 1e6:.1f} MB per launch); "
             f"traffic / algorithmic = {traffic_pf / algo_pf:.2f}\n\n")
     f.write("## Kernels (trace, all calls)\n\n| kernel | launches | total ms | avg us | share |\n|---|---|---|---|---|\n")
     for k, (n, us) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
