@@ -122,13 +122,29 @@ __global__ __launch_bounds__(256) void k_detect(const DetectLaunch L) {
             }
         }
     } else {
-        for (int i = tid; i < kDogPerOctave * DT_LH * DT_LWV; i += 256) {
-            const int pl = i / (DT_LH * DT_LWV), r = i - pl * (DT_LH * DT_LWV);
-            const int ly = r / DT_LWV, lx = r - ly * DT_LWV;
-            int gy = y0 - 1 + ly, gx = x0 - 4 + lx;
-            gy = gy < 0 ? 0 : (gy >= H ? H - 1 : gy);
-            gx = gx < 0 ? 0 : (gx >= W ? W - 1 : gx);
-            t[(pl * DT_LH + ly) * DT_LP + lx] = dog[(size_t)pl * P + (size_t)gy * pitch + gx];
+        // border tiles: clamped indices, 8 independent loads in flight per thread
+        constexpr int N = kDogPerOctave * DT_LH * DT_LWV, KB = 8;
+        for (int i0 = tid; i0 < N; i0 += 256 * KB) {
+            float v[KB];
+#pragma unroll
+            for (int k = 0; k < KB; k++) {
+                const int i = min(i0 + 256 * k, N - 1);
+                const int pl = i / (DT_LH * DT_LWV), r = i - pl * (DT_LH * DT_LWV);
+                const int ly = r / DT_LWV, lx = r - ly * DT_LWV;
+                int gy = y0 - 1 + ly, gx = x0 - 4 + lx;
+                gy = gy < 0 ? 0 : (gy >= H ? H - 1 : gy);
+                gx = gx < 0 ? 0 : (gx >= W ? W - 1 : gx);
+                v[k] = dog[(size_t)pl * P + (size_t)gy * pitch + gx];
+            }
+#pragma unroll
+            for (int k = 0; k < KB; k++) {
+                const int i = i0 + 256 * k;
+                if (i < N) {
+                    const int pl = i / (DT_LH * DT_LWV), r = i - pl * (DT_LH * DT_LWV);
+                    const int ly = r / DT_LWV, lx = r - ly * DT_LWV;
+                    t[(pl * DT_LH + ly) * DT_LP + lx] = v[k];
+                }
+            }
         }
     }
     __syncthreads();
