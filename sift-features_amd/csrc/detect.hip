@@ -1,5 +1,5 @@
 // Keypoint detection on MI355X: DoG extrema + sub-pixel refinement + contrast
-// and edge rejection (k_detect), then 36-bin orientation histograms and
+// and edge rejection (k_detect_rows, k_refine), then 36-bin orientation histograms and
 // reference orientations (k_orient).
 //
 // Reference: find_keypoints / find_extrema_in_dog_img / point_is_local_extremum
@@ -76,163 +76,160 @@ __device__ __forceinline__ bool interpolate(const gfloat* __restrict__ dog, int 
 }
 
 // ---------------------------------------------------------------------------
-// k_detect: thread = (column, 4 consecutive rows) of a 64x16 tile, all three
-// scale triples of the octave.  The 5 DoG planes of the tile (+1 px halo)
-// are staged in LDS with 16-B loads on interior tiles.  Extrema are appended
-// as packed emission keys for k_refine.
+// k_detect_rows: point_is_local_extremum (src/lib.rs:437-506) over all three
+// scale triples of an octave, with no LDS staging.  A wave owns a strip of 64
+// columns (62 outputs: lanes 1..62, the edge lanes are halo) and DR_SH rows;
+// it walks down the strip, loading one row of the 5 DoG planes per step (one
+// coalesced 256-B load per plane), forming the 3-wide row max / min with DPP
+// wave shifts and keeping the last 3 rows in registers.  Every DoG byte is
+// read ~1.1x, there are no barriers, and the loads of the next row are in
+// flight while a row is tested.  (A 64x16-tile kernel staging the 5 planes
+// in LDS ran 1.8x longer: latency-bound, 62% of wave cycles waiting.)
+// Extrema are appended as packed emission keys for k_refine.
 // ---------------------------------------------------------------------------
-constexpr int DT_W = 64, DT_H = 16, DT_RPT = 4;     // rows per thread
-constexpr int DT_LH = DT_H + 2, DT_LWV = DT_W + 8;  // loaded window [x0-4, x0+68)
-constexpr int DT_LP = DT_LWV + 4;                    // LDS pitch
-constexpr int DT_NLOAD4 = kDogPerOctave * DT_LH * (DT_LWV / 4);
-constexpr int DT_LPT = (DT_NLOAD4 + 255) / 256;
+constexpr int DR_SH = 32;       // rows per strip
+constexpr int DR_COLS = 62;     // output columns per wave
+constexpr int DR_LCAP = 256;    // per-block LDS candidate list
 
-constexpr int DT_LCAP = 512;  // per-block LDS candidate list (overflow goes straight to global)
+__device__ __forceinline__ float dpp_from_left(float v) {  // lane i <- lane i - 1 (wave_shr:1)
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
+}
+__device__ __forceinline__ float dpp_from_right(float v) {  // lane i <- lane i + 1 (wave_shl:1)
+    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
+}
 
-__global__ __launch_bounds__(256) void k_detect(const DetectLaunch L) {
-    __shared__ __attribute__((aligned(16))) float t[kDogPerOctave * DT_LH * DT_LP];
-    __shared__ uint64_t lcand[DT_LCAP];
+__global__ __launch_bounds__(256) void k_detect_rows(const DetectLaunch L) {
+    __shared__ uint64_t lcand[DR_LCAP];
     __shared__ uint32_t lcount, gbase;
     const int W = L.W, H = L.H, pitch = L.pitch;
-    const TileId tile = xcd_tile();
-    const int x0 = tile.x * DT_W, y0 = tile.y * DT_H;
-    const int b = tile.z;
-    const float* dog = L.dog + (size_t)b * L.img_stride;
-    const size_t P = (size_t)pitch * H;
-    const int tid = threadIdx.x;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int nsx = (W + DR_COLS - 1) / DR_COLS, nsy = (H + DR_SH - 1) / DR_SH;
+    const uint32_t g = blockIdx.x * 4 + wave;  // strip index: frame-major, then row band, then column
+    const uint32_t per = (uint32_t)(nsx * nsy);
+    const int b = (int)(g / per);
+    const uint32_t rem = g - (uint32_t)b * per;
+    const int sy = (int)(rem / nsx), sx = (int)(rem % nsx);
     if (tid == 0) lcount = 0;
-    const bool interior = x0 >= 4 && x0 + DT_W + 4 <= pitch && y0 >= 1 && y0 + DT_H + 1 <= H;
-    if (interior) {
-        float4 tmp[DT_LPT];
+    __syncthreads();
+    if (b < L.n_img) {
+        const float* dog = L.dog + (size_t)b * L.img_stride;
+        const size_t P = (size_t)pitch * H;
+        const int x = sx * DR_COLS - 1 + lane;  // this lane's column
+        const int xc = min(max(x, 0), W - 1);
+        const bool xout = lane >= 1 && lane <= DR_COLS && x >= kImageBorder && x < W - kImageBorder;
+        const int y0 = sy * DR_SH, y1 = min(y0 + DR_SH, H);
+        // rolling state per plane: row max / min of rows y - 1, y, y + 1
+        float hmx[kDogPerOctave][3], hmn[kDogPerOctave][3];
+        float lrx[kDogPerOctave], lrn[kDogPerOctave], ctr[kDogPerOctave];  // row y (middle planes used)
+        float nv[kDogPerOctave], nlx[kDogPerOctave], nln[kDogPerOctave];
+        auto load_row = [&](int yy, float (&v)[kDogPerOctave]) {
+            const gfloat* rp = as_global(dog) + (size_t)min(max(yy, 0), H - 1) * pitch + xc;
 #pragma unroll
-        for (int j = 0; j < DT_LPT; j++) {  // unconditional (index-clamped) loads, see pyramid.hip
-            const int i = min(tid + 256 * j, DT_NLOAD4 - 1);
-            const int pl = i / (DT_LH * (DT_LWV / 4)), r = i - pl * (DT_LH * (DT_LWV / 4));
-            const int ly = r / (DT_LWV / 4), c4 = r - ly * (DT_LWV / 4);
-            tmp[j] = *reinterpret_cast<const float4*>(dog + (size_t)pl * P + (size_t)(y0 - 1 + ly) * pitch +
-                                                      (x0 - 4 + 4 * c4));
-        }
+            for (int p = 0; p < kDogPerOctave; p++) v[p] = rp[(size_t)p * P];
+        };
+        auto row_stats = [&](const float (&v)[kDogPerOctave], float (&mx)[kDogPerOctave], float (&mn)[kDogPerOctave],
+                             float (&lx)[kDogPerOctave], float (&ln)[kDogPerOctave]) {
 #pragma unroll
-        for (int j = 0; j < DT_LPT; j++) {
-            const int i = tid + 256 * j;
-            if (i < DT_NLOAD4) {
-                const int pl = i / (DT_LH * (DT_LWV / 4)), r = i - pl * (DT_LH * (DT_LWV / 4));
-                const int ly = r / (DT_LWV / 4), c4 = r - ly * (DT_LWV / 4);
-                *reinterpret_cast<float4*>(t + (pl * DT_LH + ly) * DT_LP + 4 * c4) = tmp[j];
+            for (int p = 0; p < kDogPerOctave; p++) {
+                const float l = dpp_from_left(v[p]), r = dpp_from_right(v[p]);
+                lx[p] = fmaxf(l, r);
+                ln[p] = fminf(l, r);
+                mx[p] = fmaxf(lx[p], v[p]);
+                mn[p] = fminf(ln[p], v[p]);
             }
+        };
+        float v[kDogPerOctave], m0[kDogPerOctave], n0[kDogPerOctave];
+        // rows y0 - 1 and y0
+        load_row(y0 - 1, v);
+        row_stats(v, m0, n0, nlx, nln);
+#pragma unroll
+        for (int p = 0; p < kDogPerOctave; p++) {
+            hmx[p][0] = m0[p];
+            hmn[p][0] = n0[p];
         }
-    } else {
-        // border tiles: clamped indices, 8 independent loads in flight per thread
-        constexpr int N = kDogPerOctave * DT_LH * DT_LWV, KB = 8;
-        for (int i0 = tid; i0 < N; i0 += 256 * KB) {
-            float v[KB];
+        load_row(y0, v);
+        row_stats(v, m0, n0, lrx, lrn);
 #pragma unroll
-            for (int k = 0; k < KB; k++) {
-                const int i = min(i0 + 256 * k, N - 1);
-                const int pl = i / (DT_LH * DT_LWV), r = i - pl * (DT_LH * DT_LWV);
-                const int ly = r / DT_LWV, lx = r - ly * DT_LWV;
-                int gy = y0 - 1 + ly, gx = x0 - 4 + lx;
-                gy = gy < 0 ? 0 : (gy >= H ? H - 1 : gy);
-                gx = gx < 0 ? 0 : (gx >= W ? W - 1 : gx);
-                v[k] = dog[(size_t)pl * P + (size_t)gy * pitch + gx];
+        for (int p = 0; p < kDogPerOctave; p++) {
+            hmx[p][1] = m0[p];
+            hmn[p][1] = n0[p];
+            ctr[p] = v[p];
+        }
+        load_row(y0 + 1, nv);
+        const float threshold = floorf(0.5f * kContrastThreshold / (float)kScalesPerOctave);
+        for (int y = y0; y < y1; y++) {
+            // row y + 1 arrived; row y + 2 goes in flight
+            float cur[kDogPerOctave];
+#pragma unroll
+            for (int p = 0; p < kDogPerOctave; p++) cur[p] = nv[p];
+            if (y + 1 < y1) load_row(y + 2, nv);
+            row_stats(cur, m0, n0, nlx, nln);
+#pragma unroll
+            for (int p = 0; p < kDogPerOctave; p++) {
+                hmx[p][2] = m0[p];
+                hmn[p][2] = n0[p];
             }
+            // point_is_local_extremum for row y, scales 1..3
+            const bool yin = xout && y >= kImageBorder && y < H - kImageBorder;
+            float pmx[kDogPerOctave], pmn[kDogPerOctave];
 #pragma unroll
-            for (int k = 0; k < KB; k++) {
-                const int i = i0 + 256 * k;
-                if (i < N) {
-                    const int pl = i / (DT_LH * DT_LWV), r = i - pl * (DT_LH * DT_LWV);
-                    const int ly = r / DT_LWV, lx = r - ly * DT_LWV;
-                    t[(pl * DT_LH + ly) * DT_LP + lx] = v[k];
+            for (int p = 0; p < kDogPerOctave; p++) {
+                pmx[p] = fmaxf(fmaxf(hmx[p][0], hmx[p][1]), hmx[p][2]);
+                pmn[p] = fminf(fminf(hmn[p][0], hmn[p][1]), hmn[p][2]);
+            }
+            uint32_t ok3 = 0;
+#pragma unroll
+            for (int s_in = 1; s_in <= kScalesPerOctave; s_in++) {
+                const float val = ctr[s_in];
+                const float m8 = fmaxf(fmaxf(hmx[s_in][0], hmx[s_in][2]), lrx[s_in]);
+                const float n8 = fminf(fminf(hmn[s_in][0], hmn[s_in][2]), lrn[s_in]);
+                const float mx = fmaxf(fmaxf(pmx[s_in - 1], pmx[s_in + 1]), m8);
+                const float mn = fminf(fminf(pmn[s_in - 1], pmn[s_in + 1]), n8);
+                const bool ok = yin && fabsf(val) > threshold && (val > 0.0f ? val >= mx : val <= mn);
+                ok3 |= (uint32_t)ok << (s_in - 1);
+            }
+            if (__ballot(ok3 != 0)) {  // wave-uniform: rare
+                while (ok3) {
+                    const int bit = __builtin_ctz(ok3);
+                    ok3 &= ok3 - 1;
+                    const uint64_t key = make_key((uint32_t)(L.img_base + b), (uint32_t)L.octave, (uint32_t)(bit + 1),
+                                                  (uint32_t)y, (uint32_t)x);
+                    const uint32_t li = atomicAdd(&lcount, 1u);
+                    if (li < DR_LCAP) {
+                        lcand[li] = key;
+                    } else {
+                        const uint32_t slot = atomicAdd(L.counter, 1u);
+                        if (slot < L.cap) L.cand[slot] = key;
+                    }
                 }
             }
-        }
-    }
-    __syncthreads();
-    const int lx = (tid & 63) + 4;  // LDS column of this thread's pixel
-    const int x = x0 + (tid & 63);
-    const bool xin = x >= kImageBorder && x < W - kImageBorder;
-#define T(pl, yy, xx) t[((pl) * DT_LH + (yy)) * DT_LP + (xx)]
-    // Per plane, the 3-wide row max / min of the DT_RPT + 2 rows this thread
-    // touches are formed once (6 rows x 3 reads instead of 4 x 9), then the
-    // 3x3 maxima of each output row are combined from them.
-    const int ly0 = (tid >> 6) * DT_RPT;  // first LDS row of the window (output row ly0 + 1)
-    float hmax[kDogPerOctave][DT_RPT + 2], hmin[kDogPerOctave][DT_RPT + 2];
-    float lr_max[kDogPerOctave][DT_RPT], lr_min[kDogPerOctave][DT_RPT], ctr[kDogPerOctave][DT_RPT];
+            // shift rows: y + 1 becomes the centre row
 #pragma unroll
-    for (int pl = 0; pl < kDogPerOctave; pl++) {
-#pragma unroll
-        for (int r = 0; r < DT_RPT + 2; r++) {
-            const float l = T(pl, ly0 + r, lx - 1), c = T(pl, ly0 + r, lx), rt = T(pl, ly0 + r, lx + 1);
-            const float m2 = fmaxf(l, rt), n2 = fminf(l, rt);
-            hmax[pl][r] = fmaxf(m2, c);
-            hmin[pl][r] = fminf(n2, c);
-            if (r >= 1 && r <= DT_RPT) {
-                lr_max[pl][r - 1] = m2;
-                lr_min[pl][r - 1] = n2;
-                ctr[pl][r - 1] = c;
+            for (int p = 0; p < kDogPerOctave; p++) {
+                hmx[p][0] = hmx[p][1];
+                hmn[p][0] = hmn[p][1];
+                hmx[p][1] = hmx[p][2];
+                hmn[p][1] = hmn[p][2];
+                lrx[p] = nlx[p];
+                lrn[p] = nln[p];
+                ctr[p] = cur[p];
             }
         }
     }
-    // threshold = floor(0.5 * 0.04 / 3) = 0 (src/lib.rs:460)
-    const float threshold = floorf(0.5f * kContrastThreshold / (float)kScalesPerOctave);
-    // branch-free tests of the DT_RPT x 3 (row, scale) candidates of this
-    // thread: bit rr * 3 + (s_in - 1)
-    uint32_t okmask = 0;
-#pragma unroll
-    for (int rr = 0; rr < DT_RPT; rr++) {
-        const int y = y0 + ly0 + rr;
-        const bool yin = xin && y >= kImageBorder && y < H - kImageBorder;
-        // point_is_local_extremum (src/lib.rs:437-506): non-strict vs all 26
-        // neighbours; per plane the 3x3 max / min (centre excluded on the
-        // middle plane), then one compare per sign.
-        float pmax[kDogPerOctave], pmin[kDogPerOctave];
-#pragma unroll
-        for (int pl = 0; pl < kDogPerOctave; pl++) {
-            pmax[pl] = fmaxf(fmaxf(hmax[pl][rr], hmax[pl][rr + 1]), hmax[pl][rr + 2]);
-            pmin[pl] = fminf(fminf(hmin[pl][rr], hmin[pl][rr + 1]), hmin[pl][rr + 2]);
-        }
-#pragma unroll
-        for (int s_in = 1; s_in <= kScalesPerOctave; s_in++) {
-            const float val = ctr[s_in][rr];
-            const float m8 = fmaxf(fmaxf(hmax[s_in][rr], hmax[s_in][rr + 2]), lr_max[s_in][rr]);
-            const float n8 = fminf(fminf(hmin[s_in][rr], hmin[s_in][rr + 2]), lr_min[s_in][rr]);
-            const float mx = fmaxf(fmaxf(pmax[s_in - 1], pmax[s_in + 1]), m8);
-            const float mn = fminf(fminf(pmin[s_in - 1], pmin[s_in + 1]), n8);
-            const bool ok = yin && fabsf(val) > threshold && (val > 0.0f ? val >= mx : val <= mn);
-            okmask |= (uint32_t)ok << (rr * kScalesPerOctave + s_in - 1);
-        }
-    }
-    // candidates -> refinement kernel (dense, so its dependent global loads
-    // overlap across many threads instead of stalling this tile)
-    while (okmask) {
-        const int bit = __builtin_ctz(okmask);
-        okmask &= okmask - 1;
-        const int rr = bit / kScalesPerOctave, s_in = bit - rr * kScalesPerOctave + 1;
-        const uint64_t key = make_key((uint32_t)(L.img_base + b), (uint32_t)L.octave, (uint32_t)s_in,
-                                      (uint32_t)(y0 + ly0 + rr), (uint32_t)x);
-        const uint32_t li = atomicAdd(&lcount, 1u);
-        if (li < DT_LCAP) {
-            lcand[li] = key;
-        } else {
-            const uint32_t slot = atomicAdd(L.counter, 1u);
-            if (slot < L.cap) L.cand[slot] = key;
-        }
-    }
-    // one global atomic per block (a single hot counter serialises at the
-    // memory side), then a coalesced copy of the block's list
+    // one global atomic per block, then a coalesced copy of the block's list
     __syncthreads();
-    const uint32_t nl = lcount < DT_LCAP ? lcount : DT_LCAP;
+    const uint32_t nl = lcount < DR_LCAP ? lcount : DR_LCAP;
     if (nl == 0) return;
     if (tid == 0) gbase = atomicAdd(L.counter, nl);
     __syncthreads();
     for (uint32_t i = tid; i < nl; i += 256)
         if (gbase + i < L.cap) L.cand[gbase + i] = lcand[i];
-#undef T
 }
 
 void launch_detect(const DetectLaunch& L, hipStream_t st) {
-    dim3 grid((L.W + DT_W - 1) / DT_W, (L.H + DT_H - 1) / DT_H, L.n_img);
-    hipLaunchKernelGGL(k_detect, grid, dim3(256), 0, st, L);
+    const uint32_t strips = (uint32_t)((L.W + DR_COLS - 1) / DR_COLS) * ((L.H + DR_SH - 1) / DR_SH) * L.n_img;
+    if (strips == 0) return;
+    hipLaunchKernelGGL(k_detect_rows, dim3((strips + 3) / 4), dim3(256), 0, st, L);
 }
 
 // ---------------------------------------------------------------------------
