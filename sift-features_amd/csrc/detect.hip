@@ -365,7 +365,14 @@ __global__ __launch_bounds__(256) void k_orient(const OrientLaunch L) {
                     const float wexp = (float)(yp * yp + xp * xp) * gws;
                     const float weight = exp_f32(wexp);
                     const float mag = sqrtf(dx * dx + dy * dy);
-                    const float ori = (float)atan2((double)dy, (double)dx);
+                    // The sample only needs its bin, round(bin_step * atan2f): a fast
+                    // f32 atan2 (|error| <= 2.4e-7 rad -> the product moves by
+                    // < 2e-6) decides it unless the product lies within 2e-5 of a
+                    // rounding boundary; those rare lanes (~4e-5 of samples)
+                    // recompute the correctly rounded angle in f64.
+                    float ori = atan2_fast(dy, dx);
+                    const float tf = bin_step * ori;
+                    if (fabsf(tf - floorf(tf) - 0.5f) < 2e-5f) ori = (float)atan2((double)dy, (double)dx);
                     int bi = sat_i32(roundf(bin_step * ori));
                     if (bi >= kOriBins)
                         bi -= kOriBins;
