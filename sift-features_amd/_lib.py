@@ -8,7 +8,9 @@ import ctypes
 import os
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(HERE, "libsift_mi.so")
+# SIFT_MI_LIB: an alternative build of the same library (performance
+# experiments, tools/exp/variants.sh); the product loads the in-tree build.
+LIB_PATH = os.environ.get("SIFT_MI_LIB") or os.path.join(HERE, "libsift_mi.so")
 
 # every symbol declared in include/sift_mi.h
 EXPORTS = [

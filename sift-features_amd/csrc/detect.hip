@@ -314,10 +314,12 @@ void launch_refine(const RefineLaunch& L, hipStream_t st) {
 // sequentially over the list (bit-identical to `raw_hist[bin + 2] += w*mag`).
 // ---------------------------------------------------------------------------
 constexpr int OR_LDS = 1092;
+constexpr int OR_WT = 17 * 18 / 2;  // weight table entries at the largest radius (16)
 
 __global__ __launch_bounds__(256) void k_orient(const OrientLaunch L) {
     __shared__ __attribute__((aligned(16))) float sval[4][OR_LDS];
     __shared__ __attribute__((aligned(16))) uint8_t sbin[4][OR_LDS];
+    __shared__ float swt[4][OR_WT];  // per-wave Gaussian weight table
     __shared__ uint32_t wcount[4], wbase;
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t n_ext = min(*L.n_ext, L.ext_cap);
@@ -352,18 +354,49 @@ __global__ __launch_bounds__(256) void k_orient(const OrientLaunch L) {
             const float gws = -1.0f / (2.0f * sigma * sigma);
             const float bin_step = (float)kOriBins / (3.14159265358979323846f * 2.f);
             const int x = e.x, y = e.y;
+            // Gaussian weights: exp_f32((yp^2 + xp^2) * gws) depends on the
+            // sample only through (max(|xp|,|yp|), min(|xp|,|yp|)): one
+            // correctly rounded exp per triangle entry (<= 153) instead of one
+            // per sample (<= 1089), looked up bit-identically below.
+            const int T = (radius + 1) * (radius + 2) / 2;
+            for (int t = lane; t < T; t += 64) {
+                int a = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
+                a = (a + 1) * (a + 2) / 2 <= t ? a + 1 : (a * (a + 1) / 2 > t ? a - 1 : a);
+                const int bb = t - a * (a + 1) / 2;
+                swt[wave][t] = exp_f32((float)(a * a + bb * bb) * gws);
+            }
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            // The four neighbours of a sample, at clamped positions (samples
+            // outside the image are dropped below); the loads of the lane's
+            // next sample are in flight while the current one is evaluated.
+            const gfloat* gimg = as_global(img);
+            auto fetch = [&](int idx, float& l, float& r, float& u, float& d) {
+                const int iy = idx / n;
+                const int yy = min(max(y + iy - radius, 1), H - 2), xx = min(max(x + idx - iy * n - radius, 1), W - 2);
+                const gfloat* rw = gimg + (size_t)yy * pitch + xx;
+                r = rw[1];
+                l = rw[-1];
+                u = rw[-pitch];
+                d = rw[pitch];
+            };
+            float nl = 0.f, nr = 0.f, nu = 0.f, nd = 0.f;
+            if (lane < N && H > 2 && W > 2) fetch(lane, nl, nr, nu, nd);
             for (int idx = lane; idx < N; idx += 64) {
+                const float gl = nl, gr = nr, gu = nu, gd = nd;
+                if (idx + 64 < N && H > 2 && W > 2) fetch(idx + 64, nl, nr, nu, nd);
                 const int iy = idx / n;
                 const int yp = iy - radius, xp = idx - iy * n - radius;
                 const int yy = y + yp, xx = x + xp;
                 uint8_t bin = 0xff;
                 float val = 0.0f;
                 if (yy > 0 && yy < H - 1 && xx > 0 && xx < W - 1) {
-                    const gfloat* rw = as_global(img) + (size_t)yy * pitch;
-                    const float dx = rw[xx + 1] - rw[xx - 1];
-                    const float dy = rw[xx - pitch] - rw[xx + pitch];
-                    const float wexp = (float)(yp * yp + xp * xp) * gws;
-                    const float weight = exp_f32(wexp);
+                    const float dx = gr - gl;
+                    const float dy = gu - gd;
+                    const int ax = abs(xp), ay = abs(yp);
+                    const int hi = max(ax, ay), lo = min(ax, ay);
+                    const float weight = swt[wave][hi * (hi + 1) / 2 + lo];
                     const float mag = sqrtf(dx * dx + dy * dy);
                     // The sample only needs its bin, round(bin_step * atan2f): a fast
                     // f32 atan2 (|error| <= 2.4e-7 rad -> the product moves by
