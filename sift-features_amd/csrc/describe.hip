@@ -363,10 +363,17 @@ __device__ __forceinline__ f2v atan2_deg2(f2v dy, f2v dx) {
 // transcendentals -- v_sqrt_f32 / v_exp_f32 (1 ulp) and atan2_deg2 -- in place
 // of the correctly rounded ones: the sample angle moves by < 1e-5 degree and
 // the weights by ~1e-7 relative, inside the fast path's +-1 u8 tolerance.
-template <int kShare, int kAblate = 0>
+struct NoHook {
+    __device__ void operator()() const {}
+};
+
+// `mid` runs between the sample loop and the final reduction (the caller
+// issues its next keypoint's loads there, hidden behind the reduction).
+template <int kShare, int kAblate = 0, class Mid = NoHook>
 __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img, int pitch, int width, int height,
                                                    float xf, float yf, float scale, float orientation,
-                                                   DescScratchFast<kShare>& sc, uint8_t* __restrict__ out, int lane) {
+                                                   DescScratchFast<kShare>& sc, uint8_t* __restrict__ out, int lane,
+                                                   Mid mid = Mid()) {
     constexpr int NS = 64 / kShare;  // slices
     const int32_t x = (int32_t)sat_u32(roundf(xf));
     const int32_t y = (int32_t)sat_u32(roundf(yf));
@@ -522,6 +529,7 @@ __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img
             }
         }
     }
+    mid();
     wave_sync();
     // per-bin sum of the 64 private slices: lane l owns flat bins 2l, 2l+1 and
     // starts at slice l (rotated start: the 32 lanes of a half hit 32 banks)
@@ -558,38 +566,58 @@ __global__ __launch_bounds__(64) void k_describe(const DescLaunch L) {
     // keypoints q, q + 8, ...; one wave per keypoint, window costs vary ~20x):
     // a wave drains its home queue (blockIdx % 8, the XCD the block runs on),
     // then the others in turn.
+    // The next keypoint is claimed while the current one is processed, and its
+    // record is loaded between the current sample loop and its reduction, so
+    // neither the queue atomic nor the record load stalls the wave.
     int q = blockIdx.x & (kDescQueues - 1), drained = 0;
-    for (;;) {
-        uint32_t i = 0;
-        {
-            uint32_t j = 0;
-            if (lane == 0) j = atomicAdd(L.work + q * kDescQueueStride, 1u);
-            j = __builtin_amdgcn_readfirstlane(__shfl(j, 0));
-            i = j * kDescQueues + q;
-            if (i >= n) {
-                if (++drained == kDescQueues) break;
-                q = (q + 1) & (kDescQueues - 1);
-                continue;
-            }
+    uint32_t pend = 0;
+    auto issue = [&]() {
+        if (lane == 0) pend = atomicAdd(L.work + q * kDescQueueStride, 1u);
+    };
+    auto take = [&]() -> uint32_t {  // resolves the claim in flight: keypoint index, or n when all queues are empty
+        for (;;) {
+            const uint32_t j = __builtin_amdgcn_readfirstlane(__shfl(pend, 0));
+            const uint32_t i = j * kDescQueues + q;
+            if (i < n) return __builtin_amdgcn_readfirstlane(i);
+            if (++drained == kDescQueues) return n;
+            q = (q + 1) & (kDescQueues - 1);
+            issue();
         }
-        i = __builtin_amdgcn_readfirstlane(i);  // wave-uniform: keeps the per-keypoint control flow scalar
-        if (i >= n) break;
-        const KpRec kp = L.kp[L.idx ? L.idx[i] : i];
-        const int o = kp.octave;
+    };
+    auto record = [&](uint32_t i) {
+        KpRec r{};
+        if (i < n) r = L.kp[L.idx ? L.idx[i] : i];
+        return r;
+    };
+    issue();
+    uint32_t i = take();
+    KpRec kp = record(i);
+    while (i < n) {
+        if (drained < kDescQueues) issue();
+        const int o = __builtin_amdgcn_readfirstlane(kp.octave);
         const int W = L.ow[o], H = L.oh[o];
         const int pitch = L.opitch[o];
-        const float* img =
-            L.gauss[o] + (size_t)(kp.img - L.img_base) * L.gauss_img_stride[o] + (size_t)kp.scale * pitch * H;
+        const float* img = L.gauss[o] + (size_t)(__builtin_amdgcn_readfirstlane(kp.img) - L.img_base) *
+                                            L.gauss_img_stride[o] +
+                           (size_t)__builtin_amdgcn_readfirstlane(kp.scale) * pitch * H;
         // compute_descriptors (src/lib.rs:759-782)
         const float angle = 360.0f - kp.angle;
         const float osf = 1.0f / (float)(1u << o);  // 2_f32.powi(-octave)
         const float kp_size = kp.size * osf;
         uint8_t* out = L.out_desc + (size_t)i * kDescSize;
-        if constexpr (kExact)
+        uint32_t ni = n;
+        KpRec nkp{};
+        auto next = [&]() {
+            ni = drained < kDescQueues ? take() : n;
+            nkp = record(ni);
+        };
+        if constexpr (kExact) {
             describe_wave_exact<kAblate>(img, pitch, W, H, kp.x * osf, kp.y * osf, kp_size, angle, scr, out, lane);
-        else
+            next();
+        } else {
             describe_wave_fast<kExact ? 1 : kMode, kAblate>(img, pitch, W, H, kp.x * osf, kp.y * osf, kp_size, angle,
-                                                            scr, out, lane);
+                                                            scr, out, lane, next);
+        }
         if (lane == 0) {
             if (L.out_kp) {
                 OutKp k;
@@ -603,6 +631,8 @@ __global__ __launch_bounds__(64) void k_describe(const DescLaunch L) {
             if (L.out_key) L.out_key[i] = kp.key + L.key_base;
         }
         wave_sync();  // the scratch is reused by the next keypoint
+        i = ni;
+        kp = nkp;
     }
 }
 
