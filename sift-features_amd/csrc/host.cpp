@@ -578,7 +578,10 @@ int ensure_plan(sift_mi_ctx* c, uint32_t w, uint32_t h, uint32_t chunk) {
         ow /= 2;
         oh /= 2;
     }
-    p.algo_bytes_per_frame = (uint64_t)w * h + 44ull * sum_p;
+    // compulsory traffic of the batch path: the u8 frame read once, G_0..G_4 and
+    // D_0..D_4 written once (G_5 is dead after D_4; precompute_images, which
+    // materialises all of PrecomputedImages, moves 44 B per octave pixel)
+    p.algo_bytes_per_frame = (uint64_t)w * h + 40ull * sum_p;
     p.arena_floats = total;
     for (int l = 0; l < 2; l++) {  // a larger chunk re-sizes both lanes
         p.arena[l].release();
@@ -620,8 +623,10 @@ int ensure_plan(sift_mi_ctx* c, uint32_t w, uint32_t h, uint32_t chunk) {
 // ---------------------------------------------------------------------------
 // Stage 1: Gaussian scale space + DoG for n frames (device-resident u8)
 // ---------------------------------------------------------------------------
+// full: materialise every Gaussian (precompute_images / read_gauss); the batch
+// path skips G_5, which nothing reads after its DoG (D_4) is formed.
 int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_pitch, size_t row_stride,
-                uint32_t n) {
+                uint32_t n, bool full) {
     Plan& p = c->plan;
     hipStream_t st = lane_stream(c, lane);
     lane = arena_of(c, lane);
@@ -652,7 +657,7 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
             BlurLaunch B{};
             B.src = G + (size_t)(s - 1) * P;
             B.src_img_stride = p.gstride(o);
-            B.dst = G + (size_t)s * P;
+            B.dst = (full || s + 1 < kImagesPerOctave) ? G + (size_t)s * P : nullptr;
             B.dst_img_stride = p.gstride(o);
             B.dog = D + (size_t)(s - 1) * P;
             B.dog_img_stride = p.dstride(o);
@@ -891,7 +896,7 @@ int enqueue_chunk(sift_mi_ctx* c, int si, const uint8_t* d_frames, size_t frame_
     CHK(reserve_chunk(c, si, B, c->plan.chunk));
     hipStream_t st = lane_stream(c, si);
     HIPCHK(hipEventRecord(S.ev[0], st));
-    if (pyramid) CHK(run_pyramid(c, si, d_frames, frame_pitch, stride, m));
+    if (pyramid) CHK(run_pyramid(c, si, d_frames, frame_pitch, stride, m, false));
     HIPCHK(hipEventRecord(S.ev[1], st));
     return enqueue_keypoints(c, si, m, limit, frame_base, B);
 }
@@ -1292,7 +1297,7 @@ int sift_mi_precompute(sift_mi_ctx* c, const uint8_t* pixels, uint32_t w, uint32
     const uint8_t* frames[1] = {pixels};
     CHK(upload_frames(c, frames, 1, w, h, stride));
     CHK(ensure_plan(c, w, h, 1));
-    CHK(run_pyramid(c, 0, c->staging.p, (size_t)w * h, w, 1));
+    CHK(run_pyramid(c, 0, c->staging.p, (size_t)w * h, w, 1, true));
     HIPCHK(hipStreamSynchronize(c->stream));
     c->have_pyramid = true;
     c->have_result = false;

@@ -174,11 +174,13 @@ __device__ __forceinline__ void blur_tile_compute(const float* __restrict__ tin,
             }
         }
         const size_t off = (size_t)gy * pitch + gx;
+        // dst == nullptr: G_s is not materialised (the batch path's G_5, only
+        // its DoG is used downstream)
         if (pair) {
-            *reinterpret_cast<f2v*>(dst + off) = acc;
+            if (dst) *reinterpret_cast<f2v*>(dst + off) = acc;
             if (dog) *reinterpret_cast<f2v*>(dog + off) = acc - centre[o];
         } else {
-            dst[off] = acc.x;
+            if (dst) dst[off] = acc.x;
             if (dog) dog[off] = acc.x - centre[o].x;
         }
         // nearest 1/2: pixel (2x, 2y) for cv::resize INTER_NEAREST, (2x + 1,
@@ -261,7 +263,7 @@ __global__ __launch_bounds__(256) void k_blur(const float* __restrict__ src, siz
         load_window_border<R, TH, P>(tin, src, x0, y0, W, H, pitch);  // BORDER_REFLECT_101 / clamp to edge
     }
     __syncthreads();
-    blur_tile_compute<R, TH, P>(tin, th, taps, x0, y0, W, H, pitch, dst + b * dst_img_stride,
+    blur_tile_compute<R, TH, P>(tin, th, taps, x0, y0, W, H, pitch, dst ? dst + b * dst_img_stride : nullptr,
                              dog ? dog + b * dog_img_stride : nullptr, nxt ? nxt + b * nxt_img_stride : nullptr,
                              pitch_n, wn, hn);
 }
