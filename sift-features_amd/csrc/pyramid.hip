@@ -274,8 +274,18 @@ __global__ __launch_bounds__(256) void k_blur(const float* __restrict__ src, siz
 // (src/lib.rs:207-209), fused.  Coefficient tables are built on the host
 // with OpenCV's formulas (resizeGeneric_).
 // ---------------------------------------------------------------------------
+// v / 255 (image::ConvertBuffer), correctly rounded, without a divide or an
+// LDS table (data-dependent table reads bank-conflict): q = v * (1/255) is
+// within an ulp, and one fma residual step rounds it correctly -- checked
+// for all 256 inputs against IEEE division (tests/test_gpu_ops.py).
+__device__ __forceinline__ float u8_unit(uint32_t v) {
+    const float fv = (float)v, c = 1.0f / 255.0f;
+    const float q = fv * c;
+    return __builtin_fmaf(__builtin_fmaf(-q, 255.0f, fv), c, q);
+}
+
 __device__ __forceinline__ float upsample_at(const uint8_t* __restrict__ src, size_t row_stride, int sh,
-                                             const ResizeTab& tab, const float* __restrict__ lut, int dx, int dy) {
+                                             const ResizeTab& tab, int dx, int dy) {
     const int sx = tab.xofs[dx];
     const bool two = dx < tab.xmax;
     const int sx1 = two ? sx + 1 : sx;
@@ -283,8 +293,8 @@ __device__ __forceinline__ float upsample_at(const uint8_t* __restrict__ src, si
     const int sy1 = sy0 + 1 < sh ? sy0 + 1 : sh - 1;
     const uint8_t* r0 = src + (size_t)sy0 * row_stride;
     const uint8_t* r1 = src + (size_t)sy1 * row_stride;
-    const float p00 = lut[r0[sx]], p01 = lut[r0[sx1]];
-    const float p10 = lut[r1[sx]], p11 = lut[r1[sx1]];
+    const float p00 = u8_unit(r0[sx]), p01 = u8_unit(r0[sx1]);
+    const float p10 = u8_unit(r1[sx]), p11 = u8_unit(r1[sx1]);
     const float a0 = tab.xa0[dx], a1 = tab.xa1[dx];
     // HResizeLinear: t = S[sx]*a0 + S[sx+1]*a1 (two roundings + add)
     const float h0 = two ? p00 * a0 + p01 * a1 : p00;
@@ -318,7 +328,6 @@ __global__ __launch_bounds__(256) void k_seed(const uint8_t* __restrict__ frames
     __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
     __shared__ float srcf[SR * SC];         // u8 -> f32 source window
     __shared__ __attribute__((aligned(16))) float hbuf[SR * G::IWV];  // HResizeLinear per source row
-    __shared__ float lut[256];
     // per window column / row: source index and coefficients (resize tables)
     __shared__ __attribute__((aligned(16))) int txo[G::IWV];
     __shared__ __attribute__((aligned(16))) float txa0[G::IWV], txa1[G::IWV];
@@ -328,7 +337,6 @@ __global__ __launch_bounds__(256) void k_seed(const uint8_t* __restrict__ frames
     float* tin = lds;
     float* th = lds;
     const int tid = threadIdx.x;
-    lut[tid] = (float)tid / 255.0f;
     const TileId tile = xcd_tile();
     const int x0 = tile.x * G::TW, y0 = tile.y * G::TH;
     const size_t b = tile.z;
@@ -380,7 +388,6 @@ __global__ __launch_bounds__(256) void k_seed(const uint8_t* __restrict__ frames
             tya1[t] = tab.ya1[g];
         }
     }
-    __syncthreads();  // lut
     if (fast) {
         // 2. u8 -> f32 (v / 255) into the source window
 #pragma unroll
@@ -391,7 +398,7 @@ __global__ __launch_bounds__(256) void k_seed(const uint8_t* __restrict__ frames
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     const int c = a0 + 4 * w + q - sxa;
-                    if (c >= 0 && c < SC) srcf[r * SC + c] = lut[(wv[j] >> (8 * q)) & 0xff];
+                    if (c >= 0 && c < SC) srcf[r * SC + c] = u8_unit((wv[j] >> (8 * q)) & 0xff);
                 }
             }
         }
@@ -430,7 +437,7 @@ __global__ __launch_bounds__(256) void k_seed(const uint8_t* __restrict__ frames
         for (int i = tid; i < G::IH * G::IWV; i += 256) {
             const int ly = i / G::IWV, lx = i - ly * G::IWV;
             const int gy = reflect101(y0 - R + ly, H), gx = reflect101(x0 - G::HWL + lx, W);
-            tin[ly * G::IWP + lx] = upsample_at(src, row_stride, sh, tab, lut, gx, gy);
+            tin[ly * G::IWP + lx] = upsample_at(src, row_stride, sh, tab, gx, gy);
         }
     }
     __syncthreads();
@@ -455,13 +462,11 @@ __global__ __launch_bounds__(256) void k_seed_ip(const uint8_t* __restrict__ fra
     __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
     __shared__ float srcf[SR * SC];     // u8 -> f32 source window
     __shared__ float vbuf[G::IH * SC];  // vertical_sample rows of the window
-    __shared__ float lut[256];
     __shared__ int span[4][2];
     __shared__ int txl[G::IWV], tyl[G::IH];
     __shared__ float txw[G::IWV][kIpTaps], tyw[G::IH][kIpTaps];
     float* tin = lds;
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    lut[tid] = (float)tid / 255.0f;
     const TileId tile = xcd_tile();
     const int x0 = tile.x * G::TW, y0 = tile.y * G::TH;
     const size_t b = tile.z;
@@ -508,7 +513,7 @@ __global__ __launch_bounds__(256) void k_seed_ip(const uint8_t* __restrict__ fra
     const int nc = sxb - sxa + 1, nr = syb - sya + 1;
     if (nc <= SC && nr <= SR) {
         for (int r = wv; r < nr; r += 4)
-            for (int c = lane; c < nc; c += 64) srcf[r * SC + c] = lut[src[(size_t)(sya + r) * row_stride + sxa + c]];
+            for (int c = lane; c < nc; c += 64) srcf[r * SC + c] = u8_unit(src[(size_t)(sya + r) * row_stride + sxa + c]);
         __syncthreads();
         // vertical_sample: window row ly over the source columns
         for (int i = tid; i < G::IH * nc; i += 256) {
@@ -539,7 +544,7 @@ __global__ __launch_bounds__(256) void k_seed_ip(const uint8_t* __restrict__ fra
                 float v = 0.0f;
 #pragma unroll
                 for (int ky = 0; ky < kIpTaps; ky++)
-                    v = v + lut[src[(size_t)min(tyl[ly] + ky, sh - 1) * row_stride + cx]] * tyw[ly][ky];
+                    v = v + u8_unit(src[(size_t)min(tyl[ly] + ky, sh - 1) * row_stride + cx]) * tyw[ly][ky];
                 acc = acc + v * txw[lx][kx];
             }
             tin[ly * G::IWP + lx] = fminf(fmaxf(acc, 0.0f), 1.0f);

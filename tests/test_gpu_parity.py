@@ -140,3 +140,17 @@ def test_exact_descriptors_bit_identical(pkg, oracle, name):
     # rounds differently from glibc's f32 routine (1 ulp, rare)
     neq = res.keypoints_array != kp_o
     assert neq.sum() <= max(2, len(kp_o) // 200), (neq.sum(0), np.argwhere(neq)[:5])
+
+
+@pytest.mark.parametrize("profile", [0, 1])
+def test_seed_all_byte_values(pkg, oracle, profile):
+    """Every u8 value goes through the seed's v / 255 (fma-corrected
+    reciprocal, no table) and the 2x upsample: the first Gaussian of octave 0
+    is bit-identical to the oracle's (which divides)."""
+    img = np.arange(256 * 3, dtype=np.uint32).reshape(24, 32)
+    img = ((img * 97 + 13) % 256).astype(np.uint8)  # all 256 values, scrambled
+    c = pkg.Context(0, pkg.OpenCVProcessing if profile == 0 else pkg.ImageprocProcessing)
+    pre = c.precompute_images(img)
+    opy = oracle.Pyramid(img, profile)
+    assert np.array_equal(pre.scale_space_octave(0), opy.scale_space(0))
+    c.close()
