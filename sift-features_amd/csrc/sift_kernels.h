@@ -65,6 +65,25 @@ struct SeedLaunch {
     BlurTaps taps;
 };
 
+// octave.hip: fused five-blur + DoG streaming kernel (OpenCV profile)
+struct OctaveArgs {
+    float* gauss;  // octave G stack of image 0 (plane s at + s * plane)
+    size_t g_img_stride, plane;
+    float* dog;  // octave D stack of image 0
+    size_t dog_img_stride;
+    float* nxt;  // next octave base (nearest 1/2 of G_3), may be null
+    size_t nxt_img_stride;
+    int pitch_n, wn, hn;
+    int W, H, pitch;
+    int seg_rows;  // rows per workgroup segment
+    int write_g5;  // materialise G_5 (precompute_images); the batch path skips it
+    BlurTaps taps[6];  // taps[s] for s = 1..5
+};
+int launch_octave(const OctaveArgs& a, int n_img, hipStream_t st);
+int octave_strip_width();
+int octave_min_width();
+bool octave_radii_supported(const int* r);  // r[1..5]
+
 // pyramid.hip
 int launch_blur(int radius, const BlurLaunch& L, hipStream_t st);
 int launch_seed(int radius, const SeedLaunch& L, hipStream_t st);

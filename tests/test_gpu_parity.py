@@ -78,6 +78,38 @@ def test_pyramid_bit_exact(ctx, oracle, name):
         assert np.array_equal(d, do), (o, np.abs(d - do).max())
 
 
+@pytest.mark.parametrize("name,seg", [("synth_640x480", None), ("synth_640x480", 37), ("synth_640x480", 200),
+                                      ("synth_301x207", 64), ("synth_97x61", 9), ("synth_1000x333", None),
+                                      ("synth_1000x333", 101), ("unfused:synth_301x207", None)])
+def test_pyramid_fused_octave(ctx, oracle, monkeypatch, name, seg):
+    """octave.hip (one streaming kernel per octave: a loader wave + two waves
+    per blur level, row segments of `seg` rows, 180-column strips with
+    reflect-101 mirrors at the image borders) against
+    the oracle's blur chain, bit for bit; "unfused:" runs the per-blur kernels."""
+    if name.startswith("unfused:"):
+        name = name.split(":", 1)[1]
+        monkeypatch.setenv("SIFT_MI_FUSED_OCTAVE", "0")
+    else:
+        monkeypatch.setenv("SIFT_MI_FUSED_OCTAVE", "1")
+    if seg is not None:
+        monkeypatch.setenv("SIFT_MI_OCT_SEG", str(seg))
+    img = INPUTS[name] if name in INPUTS else _extra(name)
+    pre = ctx.precompute_images(img)
+    opy = oracle.Pyramid(img)
+    assert pre.n_octaves == opy.n_octaves
+    for o in range(opy.n_octaves):
+        g, go = pre.scale_space_octave(o), opy.scale_space(o)
+        assert np.array_equal(g, go), (o, np.argwhere(g != go)[:5])
+        d, do = pre.dog_octave(o), opy.dog(o)
+        assert np.array_equal(d, do), (o, np.argwhere(d != do)[:5])
+
+
+def _extra(name):
+    import synth
+    w, h = map(int, name.split("_")[1].split("x"))
+    return synth.frame(w, h, 7)
+
+
 @pytest.mark.parametrize("limit", [0, 1, 50, 100000])
 def test_features_limit(pkg, ctx, oracle, limit):
     img = INPUTS["tree_small"]
