@@ -58,14 +58,18 @@ constexpr int kV0 = sum_r(1, kL);                      // vertical halo of the w
 constexpr int hp(int s) { return s >= kL ? 0 : ((hp(s + 1) + kR[s + 1] + 1) & ~1); }
 constexpr int kWavesPerLevel = 2;
 constexpr int kPairs = 64 * kWavesPerLevel;            // lanes per level
-constexpr int kTW = 2 * (kPairs - hp(1));              // owned columns per strip (level 1 fills its lanes)
+// owned columns per strip: a multiple of 32 floats (128-B lines), so with
+// strip-aligned x0 every row of every plane is stored as whole lines (partial
+// lines shared by two strips cost the write path dearly); level 1's width
+// (kTW + 2 hp(1)) must fit its 2 x 64 lanes
+constexpr int kTW = (2 * (kPairs - hp(1))) / 32 * 32;
 constexpr int kLoaderWave = kWavesPerLevel * kL;       // the last wave streams G_0 rows into LDS
 constexpr int kThreads = 64 * (kLoaderWave + 1);
 constexpr int width(int s) { return kTW + 2 * hp(s); }  // level s output columns; s = 0: level 1 input
 constexpr int dH(int s) { return hp(s - 1) - hp(s); }
 constexpr int pad(int s) { return (dH(s) - kR[s]) & 1; }  // makes each lane's row window 8-B aligned
 constexpr int pitch(int s) { return (width(s - 1) + pad(s) + 1) & ~1; }
-static_assert(kTW > 0 && kTW % 2 == 0, "strip width");
+static_assert(kTW > 0 && kTW % 32 == 0 && kTW + 2 * hp(1) <= 2 * kPairs, "strip width");
 static_assert(width(0) % 2 == 0 && width(0) / 2 >= 64, "loader: a 64-lane load spans at most two rows");
 static_assert(dH(1) >= kR[1] && dH(2) >= kR[2] && dH(3) >= kR[3] && dH(4) >= kR[4] && dH(5) >= kR[5], "halos");
 
@@ -211,13 +215,14 @@ __device__ __forceinline__ void run_level(const OctaveArgs& a, float* __restrict
     constexpr int RING = Plan<B>::ring_rows(S);
     constexpr int RING_OFF = Plan<B>::ring_off(S);
     static_assert(B % 2 == 0, "rows are filtered two at a time");
-    const bool active = p < NP;
-    const int pp = active ? p : NP - 1;
-#ifdef SIFT_OCT_EXP_NOG4
-    float* __restrict__ gS = (S < 4 || a.write_g5) ? a.gauss + img * a.g_img_stride + (size_t)S * a.plane : nullptr;
-#else
-    float* __restrict__ gS = (S < kL || a.write_g5) ? a.gauss + img * a.g_img_stride + (size_t)S * a.plane : nullptr;
-#endif
+    // lane -> pair, rotated so that the first wave of the level holds the
+    // strip's first 64 owned pairs (its stores are whole 512-B row segments)
+    const int pr = (p + HPS / 2) & (kPairs - 1);
+    const bool active = pr < NP;
+    const int pp = active ? pr : NP - 1;
+    // G_4 and G_5 only when every Gaussian is materialised (precompute_images):
+    // downstream stages read G_1..G_3, and the chain keeps G_4 on chip
+    float* __restrict__ gS = (S < 4 || a.write_all) ? a.gauss + img * a.g_img_stride + (size_t)S * a.plane : nullptr;
     float* __restrict__ dS = a.dog + img * a.dog_img_stride + (size_t)(S - 1) * a.plane;
     float* __restrict__ nxt = (S == 3 && a.nxt) ? a.nxt + img * a.nxt_img_stride : nullptr;
     const int W = a.W, pg = a.pitch;
@@ -261,6 +266,27 @@ __device__ __forceinline__ void run_level(const OctaveArgs& a, float* __restrict
     int wslot = 0;  // ring slot of this step's first input row
     int ibuf = 0;   // input stage buffer of this step: t % 3 for level 1 (the loader's ring), t & 1 otherwise
     const int r1_0 = y0 - kV0;  // first G_0 row fed to level 1
+    // the previous step's output rows, stored during this step
+    f2v pout[B], pdog[B];
+#pragma unroll
+    for (int j = 0; j < B; j++) pout[j] = pdog[j] = f2v{0.f, 0.f};
+    int prow0 = INT_MIN / 2;
+    auto put = [&](int row, f2v g, f2v dv) {
+        if (owned && row >= y0 && row < y1) {
+            const size_t off = (size_t)row * pg + xc;
+            if (!odd_edge || pair2) {
+                if (gS) *reinterpret_cast<f2v*>(gS + off) = g;
+                *reinterpret_cast<f2v*>(dS + off) = dv;
+            } else {
+                if (gS) gS[off] = g.x;
+                dS[off] = dv.x;
+            }
+            if constexpr (S == 3) {
+                if (nxt && (row & 1) == 0 && (row >> 1) < a.hn && (xc >> 1) < a.wn)
+                    nxt[(size_t)(row >> 1) * a.pitch_n + (xc >> 1)] = g.x;
+            }
+        }
+    };
     step_barrier();  // the loader has staged step 0's rows
     OCT_STAMP_DECL;
     OCT_STAMP(st_t0);
@@ -270,6 +296,8 @@ __device__ __forceinline__ void run_level(const OctaveArgs& a, float* __restrict
         const float* in = lds + OFF_IN + ibuf * B * PS + PADS + 2 * pp + DHS - R;
 #pragma unroll
         for (int b = 0; b < B; b += 2) {
+            put(prow0 + b, pout[b], pdog[b]);
+            put(prow0 + b + 1, pout[b + 1], pdog[b + 1]);
             const lds_f2v* rp0 = (const lds_f2v*)(in + b * PS);
             const lds_f2v* rp1 = (const lds_f2v*)(in + (b + 1) * PS);
             f2v w0[R + 1], w1[R + 1];
@@ -316,38 +344,18 @@ __device__ __forceinline__ void run_level(const OctaveArgs& a, float* __restrict
         }
         OCT_STAMP(st_t1);
         OCT_STAMP_ADD(1);
-#ifndef SIFT_OCT_EXP_NOSTORE  // (experiment switch: no global stores)
-        if (owned) {
-#else
-        if (false) {
-#endif
+        // DoG of this step's rows (their ring slots are rewritten next step);
+        // the G / D stores themselves are issued during the next step's row
+        // filter (put below): a burst of them at the end of the step stalled
+        // the waves on the CU's write path while the VALU idled
 #pragma unroll
-            for (int j = 0; j < B; j++) {
-                const int row = orow0 + j;
-                if (row >= y0 && row < y1) {
-                    const size_t off = (size_t)row * pg + xc;
-                    int sl = wslot - R + j;  // in [-R, RING + B - R - 2]
-                    sl = sl < 0 ? sl + RING : (sl >= RING ? sl - RING : sl);
-                    const f2v d = out[j] - *(const lds_f2v*)(ring + sl * kTW);
-                    if (!odd_edge || pair2) {
-#ifdef SIFT_OCT_EXP_NT
-                        if (gS) __builtin_nontemporal_store(out[j], reinterpret_cast<f2v*>(gS + off));
-                        __builtin_nontemporal_store(d, reinterpret_cast<f2v*>(dS + off));
-#else
-                        if (gS) *reinterpret_cast<f2v*>(gS + off) = out[j];
-                        *reinterpret_cast<f2v*>(dS + off) = d;
-#endif
-                    } else {
-                        if (gS) gS[off] = out[j].x;
-                        dS[off] = d.x;
-                    }
-                    if constexpr (S == 3) {
-                        if (nxt && (row & 1) == 0 && (row >> 1) < a.hn && (xc >> 1) < a.wn)
-                            nxt[(size_t)(row >> 1) * a.pitch_n + (xc >> 1)] = out[j].x;
-                    }
-                }
-            }
+        for (int j = 0; j < B; j++) {
+            int sl = wslot - R + j;  // in [-R, RING + B - R - 2]
+            sl = sl < 0 ? sl + RING : (sl >= RING ? sl - RING : sl);
+            pout[j] = out[j];
+            pdog[j] = out[j] - *(const lds_f2v*)(ring + sl * kTW);
         }
+        prow0 = orow0;
         if constexpr (S < kL) {
             float* o = lds + OFF_OUT + ((t + 1) & 1) * B * PN + PADN;
             if (!border) {
@@ -379,6 +387,8 @@ __device__ __forceinline__ void run_level(const OctaveArgs& a, float* __restrict
         OCT_STAMP(st_t1);
         OCT_STAMP_ADD(3);
     }
+#pragma unroll
+    for (int j = 0; j < B; j++) put(prow0 + j, pout[j], pdog[j]);
     OCT_STAMP_FLUSH(S);
 }
 

@@ -76,7 +76,7 @@ struct OctaveArgs {
     int pitch_n, wn, hn;
     int W, H, pitch;
     int seg_rows;  // rows per workgroup segment
-    int write_g5;  // materialise G_5 (precompute_images); the batch path skips it
+    int write_all;  // materialise G_4 and G_5 too (precompute_images); the batch path keeps them on chip
     BlurTaps taps[6];  // taps[s] for s = 1..5
 };
 int launch_octave(const OctaveArgs& a, int n_img, hipStream_t st);
