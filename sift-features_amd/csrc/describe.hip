@@ -638,12 +638,18 @@ __global__ __launch_bounds__(64) void k_describe(const DescLaunch L) {
 
 void launch_describe(const DescLaunch& L, hipStream_t st) {
     if (L.bound == 0) return;
-    // fast path: 20 KB of LDS per wave -> 8 resident per CU (exact: 14 KB)
-    const dim3 grid(std::min<uint32_t>(L.bound, 256 * 8));
+    // fast path at kShare 4: ~10 KB of LDS per wave -> 16 resident per CU (exact: 14 KB)
+#ifndef SIFT_DESC_SHARE
+#define SIFT_DESC_SHARE 4  // lanes per private histogram slice: 9.7 KB of LDS per wave (bench: 4 beats 2 and 8)
+#endif
+#ifndef SIFT_DESC_WAVES_PER_CU
+#define SIFT_DESC_WAVES_PER_CU 16
+#endif
+    const dim3 grid(std::min<uint32_t>(L.bound, 256 * SIFT_DESC_WAVES_PER_CU));
     if (L.exact)
         hipLaunchKernelGGL((k_describe<0, 0>), grid, dim3(64), 0, st, L);
     else
-        hipLaunchKernelGGL((k_describe<2, 0>), grid, dim3(64), 0, st, L);
+        hipLaunchKernelGGL((k_describe<SIFT_DESC_SHARE, 0>), grid, dim3(64), 0, st, L);
 }
 
 __global__ __launch_bounds__(64) void k_describe_one(const float* img, int w, int h, float x, float y, float scale,
