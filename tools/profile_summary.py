@@ -100,7 +100,11 @@ for _ in range(int(round(__import__("math").log2(min(2 * W, 2 * H)) - 2)) + 1):
     ow //= 2
     oh //= 2
 algo_pf = W * H + 40 * sum_p  # batch path: G_0..G_4 + D_0..D_4 written once (G_5 dead)
-chunk = min(64, max(1, int(16e9 // (44.0 * sum_p))), FRAMES)  # host auto_chunk
+# host auto_chunk (host.cpp): <= 64 frames and ~32 GB of pyramid per chunk,
+# balanced, at least two chunks per call
+cmax = min(64, max(1, int(32e9 // (44.0 * sum_p))))
+nck = max(-(-FRAMES // cmax), 2 if FRAMES >= 2 else 1)
+chunk = -(-FRAMES // nck)
 launches_per_chunk = pyr_n / max(1, n_chunks)
 traffic_pl = fetch / max(1, n_f) + write / max(1, n_w)  # HBM bytes per pyramid launch
 traffic_pf = traffic_pl * launches_per_chunk / chunk

@@ -3,10 +3,10 @@
 # --kernel-trace --stats, then two separate PMC passes (FETCH_SIZE, WRITE_SIZE;
 # no trace domains mixed with --pmc) over the same command, summarised into
 # profiles/<round>_* by tools/profile_summary.py.
-#   bash tools/round_profile.sh r01 [frames]
+#   bash tools/round_profile.sh r01 [frames]   (default: bench.py's 128 frames per call)
 cd "$GRAFT_REPO_ROOT" || exit 2
 ROUND=${1:-r01}
-FRAMES=${2:-32}
+FRAMES=${2:-128}
 OUT=gpurun_out/rp_$ROUND
 rm -rf "$OUT"
 mkdir -p "$OUT"
