@@ -27,7 +27,7 @@ float time_describe(const DescLaunch& L, int reps) {
     hipEvent_t a, b;
     CK(hipEventCreate(&a));
     CK(hipEventCreate(&b));
-    dim3 grid(std::min<uint32_t>(L.bound, 256 * 8));
+    dim3 grid(std::min<uint32_t>(L.bound, 256 * (E == 4 ? 16 : 8)));  // as launch_describe: 16 waves / CU at kShare 4
     CK(hipMemset(L.work, 0, kDescWorkWords * 4));
     hipLaunchKernelGGL((k_describe<E, A>), grid, dim3(64), 0, 0, L);
     CK(hipEventRecord(a));
@@ -193,6 +193,13 @@ int main(int argc, char** argv) {
     std::printf("  fast s1         %8.3f ms\n", time_describe<1, 0>(L, reps));
     std::printf("  fast s2         %8.3f ms\n", time_describe<2, 0>(L, reps));
     std::printf("  fast s4         %8.3f ms\n", time_describe<4, 0>(L, reps));
+    std::printf("  fast s4 -rmw    %8.3f ms\n", time_describe<4, 1>(L, reps));
+    std::printf("  fast s4 nosample %8.3f ms\n", time_describe<4, 64>(L, reps));
+    std::printf("  fast s4 -atan2  %8.3f ms\n", time_describe<4, 2>(L, reps));
+    std::printf("  fast s4 -exp    %8.3f ms\n", time_describe<4, 4>(L, reps));
+    std::printf("  fast s4 -loads  %8.3f ms\n", time_describe<4, 8>(L, reps));
+    std::printf("  fast s4 -all    %8.3f ms\n", time_describe<4, 14>(L, reps));
+    std::printf("  fast s4 -all -rmw %8.3f ms\n", time_describe<4, 15>(L, reps));
     std::printf("  fast s2 -rmw    %8.3f ms\n", time_describe<2, 1>(L, reps));
     std::printf("  fast s2 nosample %8.3f ms\n", time_describe<2, 64>(L, reps));
     std::printf("  fast s2 -atan2  %8.3f ms\n", time_describe<2, 2>(L, reps));
