@@ -161,6 +161,19 @@ typedef struct {
 int sift_mi_match_descriptors(sift_mi_ctx* ctx, const uint8_t* query, size_t n_query, const uint8_t* train,
                               size_t n_train, int cross_check, sift_mi_match* out, size_t cap, size_t* n_matches);
 
+/* ---- the input step before the path ---------------
+ * Baseline (SOF0/SOF1) Huffman JPEG, 1 or 3 components -> 8-bit luma, with
+ * the arithmetic of the reference's decode: image 0.25.2 `image::open` /
+ * `load_from_memory` (zune-jpeg) then `.grayscale()` (examples/run-sift.rs:8,
+ * src/lib.rs:1012).  Host entropy decoding, GPU IDCT / upsampling / colour.
+ * sift_mi_jpeg_dims: frame size from the headers (host only, no device).
+ * sift_mi_decode_jpeg: luma into out (row stride out_stride), a host buffer,
+ * or device memory when out_on_device != 0 (ordered on the context stream;
+ * the call returns once the frame is written). */
+int sift_mi_jpeg_dims(const uint8_t* data, size_t len, uint32_t* width, uint32_t* height);
+int sift_mi_decode_jpeg(sift_mi_ctx* ctx, const uint8_t* data, size_t len, uint8_t* out, size_t out_stride,
+                        int out_on_device);
+
 /* ---- measurement ---------------------------------------------------------
  * Cumulative since the last reset, from HIP events on the context stream.
  * pyramid_* covers the seed + octave blur/DoG kernels (the HBM-bound stage);

@@ -7,7 +7,8 @@ from ._lib import SiftMiError, lib  # noqa: F401
 from .sift import (  # noqa: F401
     DESCRIPTOR_SIZE, Context, ImageprocProcessing, KeyPoint, OpenCVProcessing, PrecomputedImages, Processing,
     ResultBuffers,
-    SiftResult, compute_descriptor, default_context, key_fields, match_descriptors, precompute_images, sift,
+    SiftResult, compute_descriptor, decode_jpeg, default_context, jpeg_dims, key_fields, match_descriptors,
+    precompute_images, sift,
     sift_with_precomputed,
     sift_with_processing, stable_sort_xy_size)
 

@@ -1570,6 +1570,26 @@ int sift_mi_match_descriptors(sift_mi_ctx* c, const uint8_t* query, size_t nq, c
     return 0;
 }
 
+int sift_mi_jpeg_dims(const uint8_t* data, size_t len, uint32_t* width, uint32_t* height) {
+    if (!data || !width || !height) return fail(SIFT_MI_EINVAL, "bad arguments");
+    std::string err;
+    const int rc = jpeg_dims(data, len, width, height, err);
+    return rc ? fail(rc, err) : 0;
+}
+
+int sift_mi_decode_jpeg(sift_mi_ctx* c, const uint8_t* data, size_t len, uint8_t* out, size_t out_stride,
+                        int out_on_device) {
+    if (!c || !data || !out) return fail(SIFT_MI_EINVAL, "bad arguments");
+    uint32_t w = 0, h = 0;
+    std::string err;
+    int rc = jpeg_dims(data, len, &w, &h, err);
+    if (rc) return fail(rc, err);
+    if (out_stride < w) return fail(SIFT_MI_EINVAL, "out_stride < width");
+    CHK(set_device(c));
+    rc = jpeg_decode_luma(data, len, out, out_stride, out_on_device != 0, c->stream, err);
+    return rc ? fail(rc, err) : 0;
+}
+
 int sift_mi_get_stats(sift_mi_ctx* c, sift_mi_stats* out) {
     if (!c || !out) return fail(SIFT_MI_EINVAL, "bad arguments");
     *out = c->stats;

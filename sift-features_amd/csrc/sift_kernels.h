@@ -1,6 +1,8 @@
 // Host-side launch interface of the HIP kernels (internal to libsift_mi.so).
 #pragma once
 
+#include <string>
+
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
@@ -80,6 +82,11 @@ struct OctaveArgs {
     BlurTaps taps[6];  // taps[s] for s = 1..5
 };
 int launch_octave(const OctaveArgs& a, int n_img, hipStream_t st);
+
+// jpeg.hip: baseline JPEG -> 8-bit luma (zune-jpeg + image::grayscale arithmetic)
+int jpeg_dims(const uint8_t* data, size_t len, uint32_t* w, uint32_t* h, std::string& err);
+int jpeg_decode_luma(const uint8_t* data, size_t len, uint8_t* out, size_t out_stride, bool out_on_device,
+                     hipStream_t st, std::string& err);
 int octave_strip_width();
 int octave_min_width();
 bool octave_radii_supported(const int* r);  // r[1..5]

@@ -259,6 +259,29 @@ class Context:
         return (a["query_idx"].astype(np.int32), a["train_idx"].astype(np.int32),
                 a["distance"].astype(np.float32))
 
+    # -- the input step ------------------------------
+    def decode_jpeg(self, data):
+        """Baseline JPEG bytes -> (h, w) u8 luma, as the reference makes its
+        inputs: `image::open(..)` (zune-jpeg) then `.grayscale()`
+        (examples/run-sift.rs:8, src/lib.rs:1012).  Entropy decoding on the
+        host, IDCT / upsampling / colour on the GPU."""
+        buf = np.frombuffer(bytes(data), dtype=np.uint8)
+        w, h = jpeg_dims(buf)
+        out = np.empty((h, w), np.uint8)
+        check(lib().sift_mi_decode_jpeg(self._h, buf.ctypes.data, len(buf), out.ctypes.data, w, 0))
+        return out
+
+    def decode_jpeg_device(self, data, out_ptr, out_stride):
+        """The same into device memory (e.g. a torch.uint8 CUDA tensor's
+        data_ptr(), row stride in bytes), ordered on the context stream."""
+        buf = np.frombuffer(bytes(data), dtype=np.uint8)
+        check(lib().sift_mi_decode_jpeg(self._h, buf.ctypes.data, len(buf), out_ptr, out_stride, 1))
+
+    def sift_jpeg(self, data, features_limit=None):
+        """`sift(image::open(path)?.grayscale())` of examples/run-sift.rs on
+        JPEG bytes."""
+        return self.sift(self.decode_jpeg(data), features_limit)
+
     # -- Processing ops (src/lib.rs:86-90) ---------------------------------
     def gaussian_blur(self, img, sigma):
         a = _f32_image(img)
@@ -391,6 +414,18 @@ def sift_with_precomputed(pre, features_limit=None):
 def compute_descriptor(img, x, y, scale, orientation):
     """src/lib.rs:785"""
     return default_context().compute_descriptor(img, x, y, scale, orientation)
+
+
+def jpeg_dims(data):
+    """(width, height) of a baseline JPEG from its headers (host only)."""
+    buf = np.frombuffer(bytes(data), dtype=np.uint8) if not isinstance(data, np.ndarray) else data
+    w, h = ctypes.c_uint32(), ctypes.c_uint32()
+    check(lib().sift_mi_jpeg_dims(buf.ctypes.data, len(buf), ctypes.byref(w), ctypes.byref(h)))
+    return w.value, h.value
+
+
+def decode_jpeg(data):
+    return default_context().decode_jpeg(data)
 
 
 def match_descriptors(query, train, cross_check=True):
