@@ -173,6 +173,13 @@ int sift_mi_match_descriptors(sift_mi_ctx* ctx, const uint8_t* query, size_t n_q
 int sift_mi_jpeg_dims(const uint8_t* data, size_t len, uint32_t* width, uint32_t* height);
 int sift_mi_decode_jpeg(sift_mi_ctx* ctx, const uint8_t* data, size_t len, uint8_t* out, size_t out_stride,
                         int out_on_device);
+/* n JPEGs of one size and sampling -> device luma frames laid out as
+ * sift_mi_extract_batch_device takes them (frame i at d_frames + i *
+ * frame_pitch, rows row_stride apart).  Entropy decoding runs on `threads`
+ * host threads (<= 0: up to 16), overlapped with the GPU reconstruction of
+ * the previous chunk of frames; returns once every frame is written. */
+int sift_mi_decode_jpeg_batch(sift_mi_ctx* ctx, const uint8_t* const* data, const size_t* len, uint32_t n,
+                              uint8_t* d_frames, size_t frame_pitch, size_t row_stride, int threads);
 
 /* ---- measurement ---------------------------------------------------------
  * Cumulative since the last reset, from HIP events on the context stream.

@@ -21,7 +21,7 @@ EXPORTS = [
     "sift_mi_precompute", "sift_mi_octave_dims", "sift_mi_read_scale_space", "sift_mi_read_dog",
     "sift_mi_sift_with_precomputed", "sift_mi_compute_descriptor", "sift_mi_gaussian_blur",
     "sift_mi_resize_linear", "sift_mi_resize_nearest", "sift_mi_match_descriptors", "sift_mi_jpeg_dims",
-    "sift_mi_decode_jpeg", "sift_mi_get_stats",
+    "sift_mi_decode_jpeg", "sift_mi_decode_jpeg_batch", "sift_mi_get_stats",
     "sift_mi_reset_stats",
     "sift_mi_version", "sift_mi_last_error",
 ]
@@ -100,6 +100,7 @@ def lib():
         "sift_mi_match_descriptors": [vp, vp, sz, vp, sz, i32, vp, sz, P(sz)],
         "sift_mi_jpeg_dims": [vp, sz, P(u32), P(u32)],
         "sift_mi_decode_jpeg": [vp, vp, sz, vp, sz, i32],
+        "sift_mi_decode_jpeg_batch": [vp, P(vp), P(sz), u32, vp, sz, sz, i32],
         "sift_mi_get_stats": [vp, P(Stats)],
         "sift_mi_reset_stats": [vp],
         "sift_mi_version": [],

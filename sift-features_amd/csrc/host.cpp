@@ -1590,6 +1590,18 @@ int sift_mi_decode_jpeg(sift_mi_ctx* c, const uint8_t* data, size_t len, uint8_t
     return rc ? fail(rc, err) : 0;
 }
 
+int sift_mi_decode_jpeg_batch(sift_mi_ctx* c, const uint8_t* const* data, const size_t* len, uint32_t n,
+                              uint8_t* d_frames, size_t frame_pitch, size_t row_stride, int threads) {
+    if (!c || (n && (!data || !len || !d_frames))) return fail(SIFT_MI_EINVAL, "bad arguments");
+    for (uint32_t i = 0; i < n; i++)
+        if (!data[i]) return fail(SIFT_MI_EINVAL, "null JPEG");
+    if (threads <= 0) threads = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
+    CHK(set_device(c));
+    std::string err;
+    const int rc = jpeg_decode_batch(data, len, n, d_frames, frame_pitch, row_stride, threads, c->stream, err);
+    return rc ? fail(rc, err) : 0;
+}
+
 int sift_mi_get_stats(sift_mi_ctx* c, sift_mi_stats* out) {
     if (!c || !out) return fail(SIFT_MI_EINVAL, "bad arguments");
     *out = c->stats;

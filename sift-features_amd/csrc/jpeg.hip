@@ -20,8 +20,11 @@
 // bit for bit (tests/test_gpu_jpeg.py).  Baseline / extended sequential
 // Huffman only (SOF0/SOF1), 1 or 3 components, sampling factors 1 or 2,
 // restart intervals.
+#include <atomic>
 #include <cstring>
+#include <mutex>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "../../include/sift_mi.h"
@@ -261,14 +264,17 @@ Geom geometry(const Header& H) {
 }
 
 // Entropy decoding + dequantisation: coef[block][64], natural order.
-int entropy_decode(const uint8_t* d, size_t n, const Header& H, const Geom& g, std::vector<int32_t>& coef,
-                   std::string& err) {
+// Quantised coefficients (natural order, int16: AC magnitudes are < 2^10 by
+// construction; a DC predictor leaving the int16 range is rejected), the GPU
+// dequantises.  Every block of every plane is coded (MCU order), so `coef` is
+// written in full: each block is assembled in a zeroed local array and stored
+// whole.
+int entropy_decode(const uint8_t* d, size_t n, const Header& H, const Geom& g, int16_t* coef, std::string& err) {
     for (int k = 0; k < H.nc; k++) {
         if (!H.qset[H.c[k].tq]) return err = "JPEG: missing quantisation table", SIFT_MI_EINVAL;
         if (!H.dc[H.c[k].td].present || !H.ac[H.c[k].ta].present)
             return err = "JPEG: missing Huffman table", SIFT_MI_EINVAL;
     }
-    coef.assign(g.total * 64, 0);
     Bits bs(d, n, H.scan);
     int pred[3] = {0, 0, 0};
     long long mcu = 0;
@@ -283,15 +289,18 @@ int entropy_decode(const uint8_t* d, size_t n, const Header& H, const Geom& g, s
                 const Comp& c = H.c[ci];
                 const Huff& dct = H.dc[c.td];
                 const Huff& act = H.ac[c.ta];
-                const int32_t* q = H.q[c.tq];
                 for (int by = 0; by < c.v; by++) {
                     for (int bx = 0; bx < c.h; bx++) {
-                        int32_t* blk = coef.data() +
-                                       64 * (g.off[ci] + (size_t)(my * c.v + by) * g.bw[ci] + (size_t)(mx * c.h + bx));
+                        int16_t* dst =
+                            coef + 64 * (g.off[ci] + (size_t)(my * c.v + by) * g.bw[ci] + (size_t)(mx * c.h + bx));
+                        int16_t blk[64];
+                        std::memset(blk, 0, sizeof(blk));
                         const int t = decode_sym(bs, dct);
                         if (t < 0 || t > 16) return err = "JPEG: bad Huffman code", SIFT_MI_EINVAL;
                         pred[ci] += extend(bs.bits(t), t);
-                        blk[0] = pred[ci] * q[0];
+                        if (pred[ci] < -32768 || pred[ci] > 32767)
+                            return err = "JPEG: DC coefficient out of range", SIFT_MI_EUNSUPPORTED;
+                        blk[0] = (int16_t)pred[ci];
                         for (int k = 1; k < 64;) {
                             const int rs = decode_sym(bs, act);
                             if (rs < 0) return err = "JPEG: bad Huffman code", SIFT_MI_EINVAL;
@@ -303,9 +312,10 @@ int entropy_decode(const uint8_t* d, size_t n, const Header& H, const Geom& g, s
                             }
                             k += r;
                             if (k > 63) return err = "JPEG: coefficient index out of range", SIFT_MI_EINVAL;
-                            blk[kZigzag[k]] = extend(bs.bits(s), s) * q[kZigzag[k]];
+                            blk[kZigzag[k]] = (int16_t)extend(bs.bits(s), s);
                             k++;
                         }
+                        std::memcpy(dst, blk, sizeof(blk));
                     }
                 }
             }
@@ -366,32 +376,38 @@ __device__ __forceinline__ Idct1 idct1d(int64_t s0, int64_t s1, int64_t s2, int6
 __device__ __forceinline__ uint8_t clamp_u8(int64_t v) { return (uint8_t)(v < 0 ? 0 : (v > 255 ? 255 : v)); }
 
 struct Planes {
-    uint8_t* p[3];
-    int pitch[3];  // = bw * 8
+    uint8_t* p[3];  // frame 0's planes; frame f's at + f * frame_bytes
+    int pitch[3];   // = bw * 8
     int bw[3];
-    size_t off[3];
+    size_t off[3];  // first block of each component in a frame's coefficients
+    size_t frame_blocks, frame_bytes;
+    const int32_t* qtab;  // per frame: 3 x 64 quantisation tables (components' order, natural order)
     int nc;
 };
 
 // one thread per 8x8 block: zune-jpeg's IDCT (see the file comment)
-__global__ __launch_bounds__(256) void k_jpeg_idct(const int32_t* __restrict__ coef, size_t nblk, const Planes P) {
+__global__ __launch_bounds__(256) void k_jpeg_idct(const int16_t* __restrict__ coef, size_t nblk, const Planes P) {
     constexpr int64_t kRowBias = 512 + 65536 + (128 << 17);
-    const size_t b = (size_t)blockIdx.x * 256 + threadIdx.x;
+    const size_t b = (size_t)blockIdx.x * 256 + threadIdx.x;  // over all frames
     if (b >= nblk) return;
+    const size_t f = b / P.frame_blocks, fb = b - f * P.frame_blocks;
     int ci = 0;
-    while (ci + 1 < P.nc && b >= P.off[ci + 1]) ci++;
-    const size_t lb = b - P.off[ci];
+    while (ci + 1 < P.nc && fb >= P.off[ci + 1]) ci++;
+    const size_t lb = fb - P.off[ci];
     const int by = (int)(lb / P.bw[ci]), bx = (int)(lb - (size_t)by * P.bw[ci]);
-    uint8_t* out = P.p[ci] + (size_t)by * 8 * P.pitch[ci] + bx * 8;
-    int32_t c[64];
+    uint8_t* out = P.p[ci] + f * P.frame_bytes + (size_t)by * 8 * P.pitch[ci] + bx * 8;
+    const int32_t* q = P.qtab + (f * 3 + ci) * 64;
+    int32_t c[64];  // dequantised (T.81 F.2.1.4: coefficient x table entry)
     const int4* src = reinterpret_cast<const int4*>(coef + b * 64);
 #pragma unroll
-    for (int i = 0; i < 16; i++) {
+    for (int i = 0; i < 8; i++) {
         const int4 v = src[i];
-        c[4 * i] = v.x;
-        c[4 * i + 1] = v.y;
-        c[4 * i + 2] = v.z;
-        c[4 * i + 3] = v.w;
+        const int32_t w[4] = {v.x, v.y, v.z, v.w};
+#pragma unroll
+        for (int j = 0; j < 4; j++) {
+            c[8 * i + 2 * j] = (int32_t)(int16_t)(w[j] & 0xffff) * q[8 * i + 2 * j];
+            c[8 * i + 2 * j + 1] = (int32_t)(int16_t)((uint32_t)w[j] >> 16) * q[8 * i + 2 * j + 1];
+        }
     }
     bool ac0 = true;
 #pragma unroll
@@ -451,15 +467,15 @@ struct LumaArgs {
     int w, h;
     int fh[3], fv[3];  // upsampling factors hmax / h_c, vmax / v_c (1 or 2)
     int ph[3], pw[3];  // padded plane size (rows, columns)
-    uint8_t* out;
-    size_t out_stride;
+    uint8_t* out;  // frame f at out + f * out_pitch
+    size_t out_stride, out_pitch;
 };
 
 // full-resolution sample (y, x) of component ci: two-pass 3:1 triangle
 // upsampling ((3a + b + 2) >> 2, vertical then horizontal, neighbours
 // clamped to the padded plane)
-__device__ __forceinline__ int sample(const LumaArgs& A, int ci, int y, int x) {
-    const uint8_t* p = A.P.p[ci];
+__device__ __forceinline__ int sample(const LumaArgs& A, int ci, int y, int x, size_t fo) {
+    const uint8_t* p = A.P.p[ci] + fo;
     const int pitch = A.P.pitch[ci];
     if (A.fv[ci] == 1 && A.fh[ci] == 1) return p[(size_t)y * pitch + x];
     auto vrow = [&](int c) -> int {  // vertical pass at plane column c for output row y
@@ -477,11 +493,12 @@ __device__ __forceinline__ int sample(const LumaArgs& A, int ci, int y, int x) {
 __global__ __launch_bounds__(256) void k_jpeg_luma(const LumaArgs A) {
     const int x = blockIdx.x * 64 + (threadIdx.x & 63), y = blockIdx.y * 4 + (threadIdx.x >> 6);
     if (x >= A.w || y >= A.h) return;
+    const size_t fo = (size_t)blockIdx.z * A.P.frame_bytes;  // frame blockIdx.z
     uint8_t v;
     if (A.P.nc == 1) {
-        v = A.P.p[0][(size_t)y * A.P.pitch[0] + x];
+        v = A.P.p[0][fo + (size_t)y * A.P.pitch[0] + x];
     } else {
-        const int yy = sample(A, 0, y, x), cb = sample(A, 1, y, x) - 128, cr = sample(A, 2, y, x) - 128;
+        const int yy = sample(A, 0, y, x, fo), cb = sample(A, 1, y, x, fo) - 128, cr = sample(A, 2, y, x, fo) - 128;
         // zune-jpeg's 6-bit fixed-point YCbCr -> RGB (arithmetic shifts)
         const int r = min(max(yy + ((45 * cr) >> 5), 0), 255);
         const int g = min(max(yy - ((11 * cb + 23 * cr) >> 5), 0), 255);
@@ -489,7 +506,7 @@ __global__ __launch_bounds__(256) void k_jpeg_luma(const LumaArgs A) {
         // image 0.25 grayscale(): (2126 R + 7152 G + 722 B) / 10000
         v = (uint8_t)min((2126 * r + 7152 * g + 722 * b) / 10000, 255);
     }
-    A.out[(size_t)y * A.out_stride + x] = v;
+    A.out[(size_t)blockIdx.z * A.out_pitch + (size_t)y * A.out_stride + x] = v;
 }
 
 }  // namespace jpg
@@ -503,39 +520,23 @@ int jpeg_dims(const uint8_t* data, size_t len, uint32_t* w, uint32_t* h, std::st
     return 0;
 }
 
-int jpeg_decode_luma(const uint8_t* data, size_t len, uint8_t* out, size_t out_stride, bool out_on_device,
-                     hipStream_t st, std::string& err) {
-    jpg::Header H;
-    int rc = jpg::parse(data, len, H, err);
-    if (rc) return rc;
-    const jpg::Geom g = jpg::geometry(H);
-    for (int k = 0; k < H.nc; k++)  // h2v1, h2v2 and full-size chroma (the restatement's cases)
-        if (H.nc == 3 && g.hmax / H.c[k].h == 1 && g.vmax / H.c[k].v == 2)
-            return err = "JPEG: vertical-only chroma subsampling", SIFT_MI_EUNSUPPORTED;
-    std::vector<int32_t> coef;
-    rc = jpg::entropy_decode(data, len, H, g, coef, err);
-    if (rc) return rc;
-    size_t plane_bytes = 0;
-    for (int k = 0; k < H.nc; k++) plane_bytes += (size_t)g.bw[k] * g.bh[k] * 64;
-    const size_t out_bytes = out_on_device ? 0 : (size_t)H.w * H.h;
-    // one device allocation: coefficients, padded planes, (host output staging)
-    const size_t coef_bytes = coef.size() * sizeof(int32_t);
-    uint8_t* dev = nullptr;
-    if (hipMallocAsync((void**)&dev, coef_bytes + plane_bytes + out_bytes + 64, st) != hipSuccess)
-        return err = "JPEG: device allocation failed", SIFT_MI_ENOMEM;
-    int32_t* d_coef = reinterpret_cast<int32_t*>(dev);
-    uint8_t* d_pl = dev + coef_bytes;
-    jpg::Planes P{};
+namespace jpg {
+// device views of n frames' coefficients / planes / output for one geometry
+void views(const Header& H, const Geom& g, uint8_t* d_planes, uint8_t* out, size_t out_stride, size_t out_pitch,
+           Planes& P, LumaArgs& A) {
+    P = Planes{};
     P.nc = H.nc;
     size_t po = 0;
     for (int k = 0; k < H.nc; k++) {
-        P.p[k] = d_pl + po;
+        P.p[k] = d_planes + po;
         P.pitch[k] = g.bw[k] * 8;
         P.bw[k] = g.bw[k];
         P.off[k] = g.off[k];
         po += (size_t)g.bw[k] * g.bh[k] * 64;
     }
-    jpg::LumaArgs A{};
+    P.frame_blocks = g.total;
+    P.frame_bytes = po;
+    A = LumaArgs{};
     A.P = P;
     A.w = H.w;
     A.h = H.h;
@@ -545,22 +546,181 @@ int jpeg_decode_luma(const uint8_t* data, size_t len, uint8_t* out, size_t out_s
         A.ph[k] = g.bh[k] * 8;
         A.pw[k] = g.bw[k] * 8;
     }
-    A.out = out_on_device ? out : d_pl + plane_bytes;
-    A.out_stride = out_on_device ? out_stride : (size_t)H.w;
-    bool ok = hipMemcpyAsync(d_coef, coef.data(), coef_bytes, hipMemcpyHostToDevice, st) == hipSuccess;
+    A.out = out;
+    A.out_stride = out_stride;
+    A.out_pitch = out_pitch;
+}
+
+void qtables(const Header& H, int32_t* q) {  // 3 x 64, components' order
+    for (int k = 0; k < H.nc; k++) std::memcpy(q + 64 * k, H.q[H.c[k].tq], 64 * sizeof(int32_t));
+}
+
+int check_support(const Header& H, const Geom& g, std::string& err) {
+    for (int k = 0; k < H.nc; k++)  // h2v1, h2v2 and full-size chroma (the restatement's cases)
+        if (H.nc == 3 && g.hmax / H.c[k].h == 1 && g.vmax / H.c[k].v == 2)
+            return err = "JPEG: vertical-only chroma subsampling", SIFT_MI_EUNSUPPORTED;
+    return 0;
+}
+
+void launch(const int16_t* d_coef, uint32_t n, const Geom& g, const Header& H, const Planes& P, const LumaArgs& A,
+            hipStream_t st) {
+    const size_t nblk = g.total * n;
+    hipLaunchKernelGGL(k_jpeg_idct, dim3((unsigned)((nblk + 255) / 256)), dim3(256), 0, st, d_coef, nblk, P);
+    hipLaunchKernelGGL(k_jpeg_luma, dim3((H.w + 63) / 64, (H.h + 3) / 4, n), dim3(256), 0, st, A);
+}
+}  // namespace jpg
+
+int jpeg_decode_luma(const uint8_t* data, size_t len, uint8_t* out, size_t out_stride, bool out_on_device,
+                     hipStream_t st, std::string& err) {
+    jpg::Header H;
+    int rc = jpg::parse(data, len, H, err);
+    if (rc) return rc;
+    const jpg::Geom g = jpg::geometry(H);
+    if ((rc = jpg::check_support(H, g, err))) return rc;
+    std::vector<int16_t> coef(g.total * 64);
+    rc = jpg::entropy_decode(data, len, H, g, coef.data(), err);
+    if (rc) return rc;
+    const size_t coef_bytes = coef.size() * sizeof(int16_t);
+    jpg::Planes P;
+    jpg::LumaArgs A;
+    jpg::views(H, g, nullptr, nullptr, 0, 0, P, A);
+    const size_t plane_bytes = P.frame_bytes;
+    const size_t out_bytes = out_on_device ? 0 : (size_t)H.w * H.h;
+    const size_t q_bytes = 3 * 64 * sizeof(int32_t);
+    std::vector<int32_t> qt(3 * 64, 0);
+    jpg::qtables(H, qt.data());
+    // one device allocation: quantisation tables, coefficients, padded planes, (host output staging)
+    uint8_t* dev = nullptr;
+    if (hipMallocAsync((void**)&dev, q_bytes + coef_bytes + plane_bytes + out_bytes + 64, st) != hipSuccess)
+        return err = "JPEG: device allocation failed", SIFT_MI_ENOMEM;
+    uint8_t* d_cf = dev + q_bytes;
+    uint8_t* d_pl = d_cf + coef_bytes;
+    uint8_t* d_out = out_on_device ? out : d_pl + plane_bytes;
+    jpg::views(H, g, d_pl, d_out, out_on_device ? out_stride : (size_t)H.w, 0, P, A);
+    P.qtab = A.P.qtab = reinterpret_cast<const int32_t*>(dev);
+    bool ok = hipMemcpyAsync(dev, qt.data(), q_bytes, hipMemcpyHostToDevice, st) == hipSuccess &&
+              hipMemcpyAsync(d_cf, coef.data(), coef_bytes, hipMemcpyHostToDevice, st) == hipSuccess;
     if (ok) {
-        hipLaunchKernelGGL(jpg::k_jpeg_idct, dim3((unsigned)((g.total + 255) / 256)), dim3(256), 0, st, d_coef,
-                           g.total, P);
-        hipLaunchKernelGGL(jpg::k_jpeg_luma, dim3((H.w + 63) / 64, (H.h + 3) / 4), dim3(256), 0, st, A);
+        jpg::launch(reinterpret_cast<int16_t*>(d_cf), 1, g, H, P, A, st);
         ok = hipGetLastError() == hipSuccess;
     }
     if (ok && !out_on_device)
-        ok = hipMemcpy2DAsync(out, out_stride, A.out, (size_t)H.w, (size_t)H.w, (size_t)H.h, hipMemcpyDeviceToHost,
+        ok = hipMemcpy2DAsync(out, out_stride, d_out, (size_t)H.w, (size_t)H.w, (size_t)H.h, hipMemcpyDeviceToHost,
                               st) == hipSuccess;
     ok = (hipFreeAsync(dev, st) == hipSuccess) && ok;
     // the coefficient upload reads pageable host memory that is freed on return
     ok = (hipStreamSynchronize(st) == hipSuccess) && ok;
     if (!ok) return err = "JPEG: HIP error", SIFT_MI_EHIP;
+    return 0;
+}
+
+// n equal-geometry JPEGs -> device luma frames (frame i at d_out + i *
+// frame_pitch).  Entropy decoding of a chunk of frames runs on `threads` host
+// threads into pinned buffers (two, alternating) while the previous chunk's
+// upload and reconstruction kernels run on the stream.
+int jpeg_decode_batch(const uint8_t* const* data, const size_t* len, uint32_t n, uint8_t* d_out,
+                      size_t frame_pitch, size_t stride, int threads, hipStream_t st, std::string& err) {
+    if (n == 0) return 0;
+    jpg::Header H0;
+    int rc = jpg::parse(data[0], len[0], H0, err);
+    if (rc) return rc;
+    const jpg::Geom g = jpg::geometry(H0);
+    if ((rc = jpg::check_support(H0, g, err))) return rc;
+    if (stride < (size_t)H0.w || frame_pitch < stride * H0.h) return err = "JPEG batch: output too small", SIFT_MI_EINVAL;
+    std::vector<jpg::Header> hdr(n);
+    hdr[0] = H0;
+    for (uint32_t i = 1; i < n; i++) {
+        if ((rc = jpg::parse(data[i], len[i], hdr[i], err))) return rc;
+        const jpg::Header& h = hdr[i];
+        bool same = h.w == H0.w && h.h == H0.h && h.nc == H0.nc;
+        for (int k = 0; same && k < h.nc; k++) same = h.c[k].h == H0.c[k].h && h.c[k].v == H0.c[k].v;
+        if (!same) return err = "JPEG batch: frames differ in size or sampling", SIFT_MI_EINVAL;
+    }
+    const uint32_t C = std::min<uint32_t>(n, 16);  // frames per chunk
+    const size_t fcoef = g.total * 64;              // int16 per frame
+    jpg::Planes P;
+    jpg::LumaArgs A;
+    jpg::views(H0, g, nullptr, nullptr, 0, 0, P, A);
+    const size_t fplane = P.frame_bytes;
+    int16_t* pin[2] = {nullptr, nullptr};
+    hipEvent_t up[2] = {nullptr, nullptr};
+    uint8_t* dev = nullptr;
+    auto cleanup = [&]() {
+        (void)hipStreamSynchronize(st);
+        for (int k = 0; k < 2; k++) {
+            if (pin[k]) (void)hipHostFree(pin[k]);
+            if (up[k]) (void)hipEventDestroy(up[k]);
+        }
+        if (dev) (void)hipFree(dev);
+    };
+    bool ok = true;
+    for (int k = 0; k < 2 && ok; k++)
+        ok = hipHostMalloc((void**)&pin[k], C * fcoef * sizeof(int16_t), hipHostMallocDefault) == hipSuccess &&
+             hipEventCreateWithFlags(&up[k], hipEventDisableTiming) == hipSuccess;
+    const size_t q_bytes = (size_t)n * 3 * 64 * sizeof(int32_t);
+    ok = ok && hipMalloc((void**)&dev, q_bytes + 2 * C * fcoef * sizeof(int16_t) + C * fplane) == hipSuccess;
+    if (!ok) {
+        cleanup();
+        return err = "JPEG batch: allocation failed", SIFT_MI_ENOMEM;
+    }
+    // every frame's quantisation tables (frames may differ in quality)
+    std::vector<int32_t> qt((size_t)n * 3 * 64, 0);
+    for (uint32_t i = 0; i < n; i++) jpg::qtables(hdr[i], qt.data() + (size_t)i * 192);
+    const int32_t* d_q = reinterpret_cast<const int32_t*>(dev);
+    if (hipMemcpyAsync(dev, qt.data(), q_bytes, hipMemcpyHostToDevice, st) != hipSuccess ||
+        hipStreamSynchronize(st) != hipSuccess) {
+        cleanup();
+        return err = "JPEG batch: HIP error", SIFT_MI_EHIP;
+    }
+    uint8_t* d_cf = dev + q_bytes;
+    uint8_t* d_pl = d_cf + 2 * C * fcoef * sizeof(int16_t);
+    const int T = std::max(1, threads);
+    std::string terr;
+    int trc = 0;
+    for (uint32_t c0 = 0, k = 0; c0 < n; c0 += C, k ^= 1) {
+        const uint32_t m = std::min(C, n - c0);
+        // the pinned buffer's previous upload (two chunks back) has finished
+        if (c0 >= 2 * C && hipEventSynchronize(up[k]) != hipSuccess) {
+            cleanup();
+            return err = "JPEG batch: HIP error", SIFT_MI_EHIP;
+        }
+        std::atomic<uint32_t> next{0};
+        std::mutex mu;
+        auto work = [&]() {
+            std::string e;
+            for (uint32_t i; (i = next.fetch_add(1)) < m;) {
+                const uint32_t f = c0 + i;
+                const int r = jpg::entropy_decode(data[f], len[f], hdr[f], g, pin[k] + i * fcoef, e);
+                if (r) {
+                    std::lock_guard<std::mutex> lk(mu);
+                    if (!trc) trc = r, terr = e;
+                    return;
+                }
+            }
+        };
+        std::vector<std::thread> pool;
+        for (int t = 1; t < std::min<int>(T, (int)m); t++) pool.emplace_back(work);
+        work();
+        for (auto& th : pool) th.join();
+        if (trc) {
+            cleanup();
+            return err = terr, trc;
+        }
+        int16_t* d_coef = reinterpret_cast<int16_t*>(d_cf) + k * C * fcoef;
+        jpg::views(H0, g, d_pl, d_out + (size_t)c0 * frame_pitch, stride, frame_pitch, P, A);
+        P.qtab = A.P.qtab = d_q + (size_t)c0 * 192;
+        ok = hipMemcpyAsync(d_coef, pin[k], m * fcoef * sizeof(int16_t), hipMemcpyHostToDevice, st) == hipSuccess &&
+             hipEventRecord(up[k], st) == hipSuccess;
+        if (ok) {
+            jpg::launch(d_coef, m, g, H0, P, A, st);
+            ok = hipGetLastError() == hipSuccess;
+        }
+        if (!ok) {
+            cleanup();
+            return err = "JPEG batch: HIP error", SIFT_MI_EHIP;
+        }
+    }
+    cleanup();
     return 0;
 }
 

@@ -277,6 +277,16 @@ class Context:
         buf = np.frombuffer(bytes(data), dtype=np.uint8)
         check(lib().sift_mi_decode_jpeg(self._h, buf.ctypes.data, len(buf), out_ptr, out_stride, 1))
 
+    def decode_jpeg_batch_device(self, datas, out_ptr, frame_pitch, row_stride, threads=0):
+        """Equal-size JPEGs -> device frames (frame i at out_ptr + i *
+        frame_pitch), ready for sift_batch_device; host threads decode the
+        entropy-coded data."""
+        bufs = [np.frombuffer(bytes(d), dtype=np.uint8) for d in datas]
+        ptrs = (ctypes.c_void_p * max(1, len(bufs)))(*[b.ctypes.data for b in bufs])
+        lens = (ctypes.c_size_t * max(1, len(bufs)))(*[len(b) for b in bufs])
+        check(lib().sift_mi_decode_jpeg_batch(self._h, ptrs, lens, len(bufs), out_ptr, frame_pitch, row_stride,
+                                              int(threads)))
+
     def sift_jpeg(self, data, features_limit=None):
         """`sift(image::open(path)?.grayscale())` of examples/run-sift.rs on
         JPEG bytes."""

@@ -95,3 +95,25 @@ def test_decode_to_device(ctx):
     torch.cuda.synchronize()
     assert np.array_equal(t[:, :w].cpu().numpy(), ref)
     assert int(t[:, w:].sum()) == 0  # the stride padding is untouched
+
+
+def test_batch_decode_to_device(pkg, ctx):
+    """sift_mi_decode_jpeg_batch (threaded entropy decoding, chunked uploads)
+    equals per-frame decoding, in the device layout sift_batch_device reads,
+    and the keypoints of the decoded batch equal per-frame sift()."""
+    import torch
+    datas = [_pil_jpeg((90, 120), 40 + i, quality=80 + i, subsampling=2) for i in range(37)]
+    h, w = 90, 120
+    t = torch.zeros((len(datas), h, w + 8), dtype=torch.uint8, device="cuda")
+    ctx.decode_jpeg_batch_device(datas, t.data_ptr(), t.stride(0), t.stride(1), threads=4)
+    torch.cuda.synchronize()
+    got = t[:, :, :w].cpu().numpy()
+    for i, d in enumerate(datas):
+        assert np.array_equal(got[i], ctx.decode_jpeg(d)), i
+    offs, res = ctx.sift_batch_device(t.data_ptr(), len(datas), w, h, t.stride(1), t.stride(0), fetch=True)
+    for i in (0, 17, 36):
+        single = ctx.sift(got[i])
+        a, b = int(offs[i]), int(offs[i + 1])
+        assert np.array_equal(res.keypoints_array[a:b], single.keypoints_array)
+    with pytest.raises(pkg.SiftMiError):  # frames of different sizes
+        ctx.decode_jpeg_batch_device([datas[0], _pil_jpeg((91, 120), 1)], t.data_ptr(), t.stride(0), t.stride(1))
