@@ -25,7 +25,9 @@ D_0..D_4 written once -- G_5 is dead after its DoG) / its HIP-event time on the
 kernels' stream, vs 8 TB/s, from a second pass of the same steps with the
 chunks serialised (one pipeline lane) so the stage runs alone;
 `stage_ms_per_step` comes from that pass too.  `cpu_baseline` = the CPU oracle (a C port of
-src/lib.rs, 1 thread) on a bounded sample of the same frames, rank 0 at N=1.
+src/lib.rs, 1 thread) on a bounded sample of the same frames, rank 0 at N=1;
+`cpu_baseline_all_cores` the same with one frame per thread on the host's
+CPU share (OMP_NUM_THREADS, 16 per GPU on the GPU pool).
 """
 import argparse
 import json
@@ -158,7 +160,7 @@ def main():
             ts.append(time.perf_counter() - t)
         latency_ms = 1e3 * float(np.median(ts))
 
-    cpu = None
+    cpu, cpu_all = None, None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         sys.path.insert(0, os.path.join(ROOT, "oracle"))
         import oracle
@@ -171,6 +173,21 @@ def main():
         cpu = {"value": kps / el, "unit": "keypoints/s", "cores": 1, "kind": "port",
                "sample": f"{nfr} of the {B} benchmark frames ({W}x{H}), full sift() each, "
                          f"single-threaded C oracle (oracle/sift_oracle.c), {el:.1f} s"}
+        # the host cores this process may use, one frame per thread (the C
+        # oracle releases the GIL; SURVEY.md 8(d) asks for both baselines)
+        from concurrent.futures import ThreadPoolExecutor
+        # the box's CPU share: OMP_NUM_THREADS (16 per GPU on the pool; the
+        # affinity mask shows the whole machine)
+        cores = min(len(os.sched_getaffinity(0)), int(os.environ.get("OMP_NUM_THREADS", "16") or 16))
+        kps, nfr, t = 0, 0, time.perf_counter()
+        with ThreadPoolExecutor(cores) as ex:
+            while nfr < B and (nfr == 0 or time.perf_counter() - t < args.cpu_seconds):
+                batch = range(nfr, min(B, nfr + cores))
+                kps += sum(len(r[0]) for r in ex.map(lambda i: oracle.sift(host[i]), batch))
+                nfr += len(batch)
+        el = time.perf_counter() - t
+        cpu_all = {"value": kps / el, "unit": "keypoints/s", "cores": cores, "kind": "port",
+                   "sample": f"{nfr} of the {B} benchmark frames, one per thread on {cores} threads, {el:.1f} s"}
 
     # HBM traffic of the same launch group from the committed PMC passes
     # (tools/round_profile.sh -> profiles/pmc_traffic.json), scaled to one
@@ -217,6 +234,7 @@ def main():
                          "algorithmic_bytes_per_launch": per_launch_bytes,
                          "avg_launch_ms": per_launch_ms},
             "cpu_baseline": cpu,
+            "cpu_baseline_all_cores": cpu_all,
         }
         print(json.dumps(out), flush=True)
     ctx.close()
