@@ -20,8 +20,10 @@ for 1080p), not the "5 octaves" wording of configs[1].
 `value` = keypoints (each with its descriptor) produced by all ranks per
 second, max-over-ranks wall time between barriers.
 `roofline` = the pyramid stage (seed + blur/DoG kernels; HBM-bound): its
-algorithmic bytes W*H + 40*sum(P_o) per frame (u8 read once; G_0..G_4 and
-D_0..D_4 written once -- G_5 is dead after its DoG) / its HIP-event time on the
+algorithmic bytes W*H + 44*sum(P_o) per frame (u8 read once,
+G_0..G_5 and D_0..D_4 written once; the batch path writes only G_0..G_5 and
+forms D where detection reads it -- its kernels' actual HBM traffic is the
+PMC `traffic` field) / its HIP-event time on the
 kernels' stream, vs 8 TB/s, from a second pass of the same steps with the
 chunks serialised (one pipeline lane) so the stage runs alone;
 `stage_ms_per_step` comes from that pass too.  `cpu_baseline` = the CPU oracle (a C port of

@@ -23,14 +23,23 @@ namespace siftmi {
 // ---------------------------------------------------------------------------
 // interpolate_extremum (src/lib.rs:525-603) on the DoG stack of one frame.
 // ---------------------------------------------------------------------------
-__device__ __forceinline__ bool interpolate(const gfloat* __restrict__ dog, int W, int H, int pitch, int& scale,
-                                            int& x, int& y, float& os, float& ox, float& oy) {
-    const size_t P = (size_t)pitch * H;
+// The batch path does not materialise the DoG planes: D_s = G_{s+1} - G_s is
+// formed where it is read, with the same single f32 subtraction the blur
+// epilogue uses when it does write D (pyramid.hip), so every value is
+// bit-identical to the stored plane.
+struct DogView {
+    const gfloat* g;  // G_0 of one frame's octave
+    size_t P;         // floats per plane
+    __device__ __forceinline__ float operator()(int s, size_t off) const {
+        return g[(size_t)(s + 1) * P + off] - g[(size_t)s * P + off];
+    }
+};
+
+__device__ __forceinline__ bool interpolate(const DogView& dv, int W, int H, int pitch, int& scale, int& x, int& y,
+                                            float& os, float& ox, float& oy) {
     for (int it = 0; it < kMaxInterpSteps; it++) {
-        const gfloat* prev = dog + (size_t)(scale - 1) * P;
-        const gfloat* curr = dog + (size_t)scale * P;
-        const gfloat* next = dog + (size_t)(scale + 1) * P;
-#define AT(a, yy, xx) (a)[(size_t)(yy) * pitch + (xx)]
+        const int prev = scale - 1, curr = scale, next = scale + 1;
+#define AT(a, yy, xx) dv(a, (size_t)(yy) * pitch + (xx))
         const float g1 = (AT(next, y, x) - AT(prev, y, x)) / 2.f;
         const float g2 = (AT(curr, y + 1, x) - AT(curr, y - 1, x)) / 2.f;
         const float g3 = (AT(curr, y, x + 1) - AT(curr, y, x - 1)) / 2.f;
@@ -112,7 +121,7 @@ __global__ __launch_bounds__(256) void k_detect_rows(const DetectLaunch L) {
     if (tid == 0) lcount = 0;
     __syncthreads();
     if (b < L.n_img) {
-        const float* dog = L.dog + (size_t)b * L.img_stride;
+        const float* gb = L.gauss + (size_t)b * L.img_stride;
         const size_t P = (size_t)pitch * H;
         const int x = sx * DR_COLS - 1 + lane;  // this lane's column
         const int xc = min(max(x, 0), W - 1);
@@ -121,11 +130,17 @@ __global__ __launch_bounds__(256) void k_detect_rows(const DetectLaunch L) {
         // rolling state per plane: row max / min of rows y - 1, y, y + 1
         float hmx[kDogPerOctave][3], hmn[kDogPerOctave][3];
         float lrx[kDogPerOctave], lrn[kDogPerOctave], ctr[kDogPerOctave];  // row y (middle planes used)
-        float nv[kDogPerOctave], nlx[kDogPerOctave], nln[kDogPerOctave];
-        auto load_row = [&](int yy, float (&v)[kDogPerOctave]) {
-            const gfloat* rp = as_global(dog) + (size_t)min(max(yy, 0), H - 1) * pitch + xc;
+        float nv[kImagesPerOctave], nlx[kDogPerOctave], nln[kDogPerOctave];
+        // one row of G_0..G_5; the loads of row y + 2 stay in flight as raw
+        // Gaussians and become D values (to_dog) when the row is consumed
+        auto load_row = [&](int yy, float (&g)[kImagesPerOctave]) {
+            const gfloat* rp = as_global(gb) + (size_t)min(max(yy, 0), H - 1) * pitch + xc;
 #pragma unroll
-            for (int p = 0; p < kDogPerOctave; p++) v[p] = rp[(size_t)p * P];
+            for (int p = 0; p < kImagesPerOctave; p++) g[p] = rp[(size_t)p * P];
+        };
+        auto to_dog = [&](const float (&g)[kImagesPerOctave], float (&v)[kDogPerOctave]) {
+#pragma unroll
+            for (int p = 0; p < kDogPerOctave; p++) v[p] = g[p + 1] - g[p];
         };
         auto row_stats = [&](const float (&v)[kDogPerOctave], float (&mx)[kDogPerOctave], float (&mn)[kDogPerOctave],
                              float (&lx)[kDogPerOctave], float (&ln)[kDogPerOctave]) {
@@ -140,14 +155,16 @@ __global__ __launch_bounds__(256) void k_detect_rows(const DetectLaunch L) {
         };
         float v[kDogPerOctave], m0[kDogPerOctave], n0[kDogPerOctave];
         // rows y0 - 1 and y0
-        load_row(y0 - 1, v);
+        load_row(y0 - 1, nv);
+        to_dog(nv, v);
         row_stats(v, m0, n0, nlx, nln);
 #pragma unroll
         for (int p = 0; p < kDogPerOctave; p++) {
             hmx[p][0] = m0[p];
             hmn[p][0] = n0[p];
         }
-        load_row(y0, v);
+        load_row(y0, nv);
+        to_dog(nv, v);
         row_stats(v, m0, n0, lrx, lrn);
 #pragma unroll
         for (int p = 0; p < kDogPerOctave; p++) {
@@ -160,8 +177,7 @@ __global__ __launch_bounds__(256) void k_detect_rows(const DetectLaunch L) {
         for (int y = y0; y < y1; y++) {
             // row y + 1 arrived; row y + 2 goes in flight
             float cur[kDogPerOctave];
-#pragma unroll
-            for (int p = 0; p < kDogPerOctave; p++) cur[p] = nv[p];
+            to_dog(nv, cur);
             if (y + 1 < y1) load_row(y + 2, nv);
             row_stats(cur, m0, n0, nlx, nln);
 #pragma unroll
@@ -244,27 +260,26 @@ __device__ __forceinline__ bool refine_one(const RefineLaunch& L, uint64_t key, 
     const int y = (int)((key >> kKeyYShift) & 0x3fff);
     const int x = (int)((key >> kKeyXShift) & 0x3fff);
     const int W = L.ow[o], H = L.oh[o], pitch = L.opitch[o];
-    const gfloat* dog = as_global(L.dog[o]) + (size_t)(b - L.img_base) * L.dog_img_stride[o];
-    const size_t P = (size_t)pitch * H;
+    const DogView dv{as_global(L.gauss[o]) + (size_t)(b - L.img_base) * L.g_img_stride[o], (size_t)pitch * H};
     int sc = s_in, xi = x, yi = y;
     float os, ox, oy;
-    if (!interpolate(dog, W, H, pitch, sc, xi, yi, os, ox, oy)) return false;
-    const gfloat* prev = dog + (size_t)(sc - 1) * P;
-    const gfloat* curr = dog + (size_t)sc * P;
-    const gfloat* next = dog + (size_t)(sc + 1) * P;
+    if (!interpolate(dv, W, H, pitch, sc, xi, yi, os, ox, oy)) return false;
     const size_t c = (size_t)yi * pitch + xi;
+    auto prev = [&](size_t off) { return dv(sc - 1, off); };
+    auto curr = [&](size_t off) { return dv(sc, off); };
+    auto next = [&](size_t off) { return dv(sc + 1, off); };
     // extremum_contrast (src/lib.rs:606-626)
-    const float g1 = (next[c] - prev[c]) / 2.f;
-    const float g2 = (curr[c + pitch] - curr[c - pitch]) / 2.f;
-    const float g3 = (curr[c + 1] - curr[c - 1]) / 2.f;
+    const float g1 = (next(c) - prev(c)) / 2.f;
+    const float g2 = (curr(c + pitch) - curr(c - pitch)) / 2.f;
+    const float g3 = (curr(c + 1) - curr(c - 1)) / 2.f;
     const float interp = os * g1 + oy * g2 + ox * g3;
-    const float contrast = fabsf(curr[c] + interp / 2.f);
+    const float contrast = fabsf(curr(c) + interp / 2.f);
     if (contrast * (float)kScalesPerOctave <= kContrastThreshold) return false;
     // extremum_is_on_edge (src/lib.rs:630-653)
-    const float v2 = curr[c] * 2.0f;
-    const float h11 = curr[c + pitch] + curr[c - pitch] - v2;
-    const float d22 = curr[c + 1] + curr[c - 1] - v2;
-    const float h12 = (curr[c + pitch + 1] - curr[c + pitch - 1] - curr[c - pitch + 1] + curr[c - pitch - 1]) / 4.f;
+    const float v2 = curr(c) * 2.0f;
+    const float h11 = curr(c + pitch) + curr(c - pitch) - v2;
+    const float d22 = curr(c + 1) + curr(c - 1) - v2;
+    const float h12 = (curr(c + pitch + 1) - curr(c + pitch - 1) - curr(c - pitch + 1) + curr(c - pitch - 1)) / 4.f;
     const float tr = d22 + h11;
     const float det = d22 * h11 - h12 * h12;
     if (det <= 0.f) return false;

@@ -583,12 +583,13 @@ int ensure_plan(sift_mi_ctx* c, uint32_t w, uint32_t h, uint32_t chunk) {
         ow /= 2;
         oh /= 2;
     }
-    // compulsory traffic of the batch path with the per-blur kernels: the u8
-    // frame read once, G_0..G_4 and D_0..D_4 written once (G_5 is dead after
-    // D_4; precompute_images, which materialises all of PrecomputedImages,
-    // moves 44 B per octave pixel).  run_pyramid counts what the path it takes
-    // writes (the fused octave kernel keeps G_4 on chip too: 36 B).
-    p.algo_bytes_per_frame = (uint64_t)w * h + 40ull * sum_p;
+    // algorithmic bytes: the u8 frame read once and every
+    // image of PrecomputedImages (G_0..G_5, D_0..D_4: 44 B per octave pixel)
+    // written once -- the fixed yardstick for every path.  The batch path
+    // itself writes only G_0..G_5 and forms D where detection reads it, so
+    // its pyramid kernels move ~44 B per octave pixel counting their reads
+    // (DESIGN.md 3.1).
+    p.algo_bytes_per_frame = (uint64_t)w * h + 44ull * sum_p;
     p.arena_floats = total;
     for (int l = 0; l < 2; l++) {  // a larger chunk re-sizes both lanes
         p.arena[l].release();
@@ -633,8 +634,10 @@ int ensure_plan(sift_mi_ctx* c, uint32_t w, uint32_t h, uint32_t chunk) {
 // Fused five-blur octave kernel (octave.hip) by default where it applies.
 constexpr bool kFusedOctaveDefault = false;  // opt-in until it beats the per-blur kernels
 
-// full: materialise every Gaussian (precompute_images / read_gauss); the batch
-// path skips G_5, which nothing reads after its DoG (D_4) is formed.
+// full: materialise every image (precompute_images / read_dog); the batch
+// path writes G_0..G_5 only: detection and refinement form D_s = G_{s+1} - G_s
+// where they read it (detect.hip), 16 B per octave pixel less than writing
+// the DoG planes and reading them back.
 int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_pitch, size_t row_stride,
                 uint32_t n, bool full) {
     Plan& p = c->plan;
@@ -659,7 +662,7 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
     S.taps = p.seed_taps;
     if (launch_seed(p.seed_r, S, st)) return fail(SIFT_MI_EUNSUPPORTED, "seed blur radius");
     uint64_t launches = 1;
-    uint64_t bytes = (uint64_t)p.w * p.h;  // per frame: u8 read + the planes this call writes (batch view)
+    const uint64_t bytes = p.algo_bytes_per_frame;  // per frame, SURVEY.md 8(d)
     // fused five-blur octave kernel (octave.hip) where it applies: OpenCV
     // profile with its constant radii, octaves wide enough for one-reflection
     // column borders; the per-blur kernels otherwise
@@ -697,20 +700,19 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
             int nseg = (512 + strips * (int)n - 1) / (strips * (int)n);
             nseg = std::max(1, std::min(nseg, A.H / 96));
             A.seg_rows = seg_env > 0 ? seg_env : (A.H + nseg - 1) / nseg;
-            A.write_all = full ? 1 : 0;
+            A.write_all = 1;  // detection forms D from G_0..G_5
             for (int s = 1; s < kImagesPerOctave; s++) A.taps[s] = p.oct_taps[s];
             if (launch_octave(A, (int)n, st)) return fail(SIFT_MI_EUNSUPPORTED, "fused octave kernel");
             launches++;
-            bytes += 36ull * p.px[o];
             continue;
         }
         for (int s = 1; s < kImagesPerOctave; s++) {
             BlurLaunch B{};
             B.src = G + (size_t)(s - 1) * P;
             B.src_img_stride = p.gstride(o);
-            B.dst = (full || s + 1 < kImagesPerOctave) ? G + (size_t)s * P : nullptr;
+            B.dst = G + (size_t)s * P;
             B.dst_img_stride = p.gstride(o);
-            B.dog = D + (size_t)(s - 1) * P;
+            B.dog = full ? D + (size_t)(s - 1) * P : nullptr;
             B.dog_img_stride = p.dstride(o);
             if (s == 3 && o + 1 < p.n_oct) {
                 B.nxt = p.gauss(o + 1, lane);
@@ -728,7 +730,6 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
             if (launch_blur(p.oct_r[s], B, st)) return fail(SIFT_MI_EUNSUPPORTED, "octave blur radius");
             launches++;
         }
-        bytes += 40ull * p.px[o];
     }
     HIPCHK(hipGetLastError());
     c->stats.pyramid_launches += launches;
@@ -822,8 +823,8 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
     for (int o = 0; o < p.n_oct; o++) {
         if (p.oh[o] < 2 * kImageBorder || p.ow[o] < 2 * kImageBorder) continue;  // src/lib.rs:315
         DetectLaunch D{};
-        D.dog = p.dog(o, arena_of(c, si));
-        D.img_stride = p.dstride(o);
+        D.gauss = p.gauss(o, arena_of(c, si));
+        D.img_stride = p.gstride(o);
         D.W = p.ow[o];
         D.H = p.oh[o];
         D.pitch = p.opitch[o];
@@ -839,8 +840,8 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
     R.cand = S.cand.p;
     R.n_cand = cnt + 0;
     R.cand_cap = B.bc;
-    R.dog = p.d_dog[arena_of(c, si)].p;
-    R.dog_img_stride = p.d_dstride.p;
+    R.gauss = p.d_gauss[arena_of(c, si)].p;
+    R.g_img_stride = p.d_gstride.p;
     R.ow = p.d_ow.p;
     R.oh = p.d_oh.p;
     R.opitch = p.d_opitch.p;

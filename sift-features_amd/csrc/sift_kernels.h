@@ -107,8 +107,8 @@ void launch_resize_nearest_f32(const float* src, int sw, const int* xofs, const 
 
 // detect.hip
 struct DetectLaunch {
-    const float* dog;  // octave DoG base, image b at dog + b*img_stride, plane s at + s*W*H
-    size_t img_stride;
+    const float* gauss;  // octave G_0 base, image b at gauss + b*img_stride, plane s at + s*pitch*H
+    size_t img_stride;   // (the DoG planes are formed from G_0..G_5 as they are read)
     int W, H, pitch, octave, n_img, img_base;
     uint64_t* cand;  // packed candidate keys (frame, octave, scale, y, x)
     uint32_t* counter;
@@ -123,8 +123,8 @@ struct RefineLaunch {
     const uint64_t* cand;
     const uint32_t* n_cand;  // device count (may exceed cand_cap: overflow, clamped)
     uint32_t cand_cap;
-    const float* const* dog;       // device array [n_octaves] of octave D bases
-    const size_t* dog_img_stride;  // device array [n_octaves]
+    const float* const* gauss;   // device array [n_octaves] of octave G_0 bases (D formed from G)
+    const size_t* g_img_stride;  // device array [n_octaves]
     const int* ow;
     const int* oh;
     const int* opitch;

@@ -99,7 +99,7 @@ for _ in range(int(round(__import__("math").log2(min(2 * W, 2 * H)) - 2)) + 1):
     sum_p += ow * oh
     ow //= 2
     oh //= 2
-algo_pf = W * H + 40 * sum_p  # batch path: G_0..G_4 + D_0..D_4 written once (G_5 dead)
+algo_pf = W * H + 44 * sum_p  # G_0..G_5 + D_0..D_4 written once (the batch path writes G only)
 # host auto_chunk (host.cpp): <= 64 frames and ~32 GB of pyramid per chunk,
 # balanced, at least two chunks per call
 cmax = min(64, max(1, int(32e9 // (44.0 * sum_p))))
@@ -130,7 +130,7 @@ with open(os.path.join(PROF, f"{ROUND}_summary.md"), "w") as f:
     if b:
         f.write(f"* bench.py (HIP events on the compute stream, serialised pass): pyramid_ms per step = "
                 f"{b['stage_ms_per_step']['pyramid_ms']:.3f}, avg launch = {b['roofline']['avg_launch_ms'] * 1e3:.1f} us\n")
-    f.write(f"* algorithmic bytes per frame (W*H + 40*sum P_o) = {algo_pf / 1e6:.1f} MB; per launch "
+    f.write(f"* algorithmic bytes per frame (W*H + 44*sum P_o) = {algo_pf / 1e6:.1f} MB; per launch "
             f"{algo_pf * chunk / launches_per_chunk / 1e6:.1f} MB ({launches_per_chunk:.0f} launches per chunk of {chunk} frames)\n")
     f.write(f"* HBM traffic (PMC, FETCH_SIZE x2 + WRITE_SIZE, mean over {n_f} pyramid dispatches) = "
             f"{traffic_pl / 1e6:.1f} MB per launch = {traffic_pf / 1e6:.1f} MB per frame "
