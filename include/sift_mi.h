@@ -112,6 +112,19 @@ int sift_mi_set_exact_descriptors(sift_mi_ctx* ctx, int exact);
  * device memory; used to time kernels in isolation). */
 int sift_mi_set_pipeline_lanes(sift_mi_ctx* ctx, int lanes);
 
+/* Row band of the keypoint stages, for splitting ONE large frame across
+ * contexts / GPUs (replaces nothing in the reference,
+ * whose sift() is whole-frame: src/lib.rs:71-81).  With n_bands > 1 the
+ * context still builds the whole frame's pyramid, but detection (and so
+ * refinement, orientation and descriptors) covers only octave rows
+ * [H_o*band/n_bands, H_o*(band+1)/n_bands) of each octave o.  The bands
+ * partition every octave's candidate rows, so the union of the n_bands
+ * results, ordered by emission key (sift_mi_fetch_keys), is exactly the
+ * whole-frame result.  features_limit is rejected (SIFT_MI_EINVAL) while
+ * n_bands > 1: it ranks the whole frame's keypoints, so apply it after the
+ * merge.  Default band 0 of 1 (the whole frame). */
+int sift_mi_set_row_band(sift_mi_ctx* ctx, uint32_t band, uint32_t n_bands);
+
 /* Skip the device->host copy of results in batch calls (results stay in
  * device memory; see sift_mi_device_results).  Default 0 = copy. */
 int sift_mi_set_keep_on_device(sift_mi_ctx* ctx, int keep);

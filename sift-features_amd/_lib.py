@@ -17,7 +17,7 @@ EXPORTS = [
     "sift_mi_create", "sift_mi_destroy", "sift_mi_set_stream", "sift_mi_set_chunk",
     "sift_mi_extract", "sift_mi_fetch", "sift_mi_fetch_keys", "sift_mi_extract_batch",
     "sift_mi_extract_batch_device", "sift_mi_set_exact_descriptors", "sift_mi_set_keep_on_device", "sift_mi_device_results",
-    "sift_mi_set_pipeline_lanes",
+    "sift_mi_set_pipeline_lanes", "sift_mi_set_row_band",
     "sift_mi_precompute", "sift_mi_octave_dims", "sift_mi_read_scale_space", "sift_mi_read_dog",
     "sift_mi_sift_with_precomputed", "sift_mi_compute_descriptor", "sift_mi_gaussian_blur",
     "sift_mi_resize_linear", "sift_mi_resize_nearest", "sift_mi_match_descriptors", "sift_mi_jpeg_dims",
@@ -86,6 +86,7 @@ def lib():
         "sift_mi_extract_batch_device": [vp, vp, sz, u32, u32, u32, sz, i64, P(sz)],
         "sift_mi_set_keep_on_device": [vp, i32],
         "sift_mi_set_pipeline_lanes": [vp, i32],
+        "sift_mi_set_row_band": [vp, ctypes.c_uint32, ctypes.c_uint32],
         "sift_mi_set_exact_descriptors": [vp, i32],
         "sift_mi_device_results": [vp, P(vp), P(vp), P(sz)],
         "sift_mi_precompute": [vp, vp, u32, u32, sz, P(sz)],

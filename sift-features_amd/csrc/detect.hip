@@ -112,7 +112,7 @@ __global__ __launch_bounds__(256) void k_detect_rows(const DetectLaunch L) {
     __shared__ uint32_t lcount, gbase;
     const int W = L.W, H = L.H, pitch = L.pitch;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int nsx = (W + DR_COLS - 1) / DR_COLS, nsy = (H + DR_SH - 1) / DR_SH;
+    const int nsx = (W + DR_COLS - 1) / DR_COLS, nsy = (L.y_hi - L.y_lo + DR_SH - 1) / DR_SH;
     const uint32_t g = blockIdx.x * 4 + wave;  // strip index: frame-major, then row band, then column
     const uint32_t per = (uint32_t)(nsx * nsy);
     const int b = (int)(g / per);
@@ -126,7 +126,7 @@ __global__ __launch_bounds__(256) void k_detect_rows(const DetectLaunch L) {
         const int x = sx * DR_COLS - 1 + lane;  // this lane's column
         const int xc = min(max(x, 0), W - 1);
         const bool xout = lane >= 1 && lane <= DR_COLS && x >= kImageBorder && x < W - kImageBorder;
-        const int y0 = sy * DR_SH, y1 = min(y0 + DR_SH, H);
+        const int y0 = L.y_lo + sy * DR_SH, y1 = min(y0 + DR_SH, L.y_hi);
         // rolling state per plane: row max / min of rows y - 1, y, y + 1
         float hmx[kDogPerOctave][3], hmn[kDogPerOctave][3];
         float lrx[kDogPerOctave], lrn[kDogPerOctave], ctr[kDogPerOctave];  // row y (middle planes used)
@@ -243,7 +243,9 @@ __global__ __launch_bounds__(256) void k_detect_rows(const DetectLaunch L) {
 }
 
 void launch_detect(const DetectLaunch& L, hipStream_t st) {
-    const uint32_t strips = (uint32_t)((L.W + DR_COLS - 1) / DR_COLS) * ((L.H + DR_SH - 1) / DR_SH) * L.n_img;
+    if (L.y_lo < 0 || L.y_hi > L.H || L.y_hi <= L.y_lo) return;
+    const uint32_t strips =
+        (uint32_t)((L.W + DR_COLS - 1) / DR_COLS) * ((L.y_hi - L.y_lo + DR_SH - 1) / DR_SH) * L.n_img;
     if (strips == 0) return;
     hipLaunchKernelGGL(k_detect_rows, dim3((strips + 3) / 4), dim3(256), 0, st, L);
 }

@@ -446,6 +446,7 @@ struct sift_mi_ctx {
     int lanes = 2;                 // pipeline lanes (sift_mi_set_pipeline_lanes)
     uint32_t chunk_override = 0;
     int keep_on_device = 0;
+    uint32_t band_r = 0, band_n = 1;  // row band of the keypoint stages (sift_mi_set_row_band)
     int exact_descriptors = 0;
     Plan plan;
     DevBuf<uint8_t> staging;  // host-sourced frames
@@ -831,6 +832,11 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
         D.octave = o;
         D.n_img = (int)m;
         D.img_base = 0;
+        // row band: octave rows [H*r/n, H*(r+1)/n) -- the bands of one
+        // octave partition its rows, so every candidate (keyed by its
+        // initial octave, scale, y, x) belongs to exactly one band
+        D.y_lo = (int)((uint64_t)p.oh[o] * c->band_r / c->band_n);
+        D.y_hi = (int)((uint64_t)p.oh[o] * (c->band_r + 1) / c->band_n);
         D.cand = S.cand.p;
         D.counter = cnt + 0;
         D.cap = B.bc;
@@ -1029,6 +1035,8 @@ int finalize_chunk(sift_mi_ctx* c, int si, size_t* offsets) {
 int run_chunk_sync(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, size_t stride, uint32_t m,
                    int64_t limit, bool pyramid, size_t* offsets) {
     c->n_result = 0;
+    if (c->band_n > 1 && limit >= 0)
+        return fail(SIFT_MI_EINVAL, "features_limit ranks a whole frame's keypoints: apply it after merging row bands");
     for (int attempt = 0; attempt < 4; attempt++) {
         CHK(enqueue_chunk(c, 0, d_frames, frame_pitch, stride, m, limit, 0, pyramid));
         const int rc = finalize_chunk(c, 0, offsets);
@@ -1057,6 +1065,8 @@ int check_frame_args(uint32_t w, uint32_t h, size_t stride) {
 int extract_device(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, uint32_t n, uint32_t w, uint32_t h,
                    size_t stride, int64_t limit, size_t* offsets) {
     CHK(check_frame_args(w, h, stride));
+    if (c->band_n > 1 && limit >= 0)
+        return fail(SIFT_MI_EINVAL, "features_limit ranks a whole frame's keypoints: apply it after merging row bands");
     const uint32_t chunk =
         std::min(kMaxChunk, c->chunk_override ? std::min(c->chunk_override, n) : auto_chunk(c->plan, w, h, n));
     CHK(ensure_plan(c, w, h, chunk));
@@ -1245,6 +1255,13 @@ int sift_mi_set_pipeline_lanes(sift_mi_ctx* c, int lanes) {
     CHK(set_device(c));
     CHK(sync_lanes(c));
     c->lanes = lanes;
+    return 0;
+}
+
+int sift_mi_set_row_band(sift_mi_ctx* c, uint32_t band, uint32_t n_bands) {
+    if (!c || n_bands == 0 || band >= n_bands) return fail(SIFT_MI_EINVAL, "band must be < n_bands, n_bands >= 1");
+    c->band_r = band;
+    c->band_n = n_bands;
     return 0;
 }
 

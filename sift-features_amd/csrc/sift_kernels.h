@@ -110,6 +110,7 @@ struct DetectLaunch {
     const float* gauss;  // octave G_0 base, image b at gauss + b*img_stride, plane s at + s*pitch*H
     size_t img_stride;   // (the DoG planes are formed from G_0..G_5 as they are read)
     int W, H, pitch, octave, n_img, img_base;
+    int y_lo, y_hi;  // candidate rows [y_lo, y_hi) (a row band; 0, H for the whole octave)
     uint64_t* cand;  // packed candidate keys (frame, octave, scale, y, x)
     uint32_t* counter;
     uint32_t cap;

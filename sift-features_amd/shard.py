@@ -11,6 +11,14 @@ only collectives are
                         in one gather per array).
 Both run unchanged on gloo (CPU tensors; tests/test_shard.py) and RCCL (GPU
 tensors).
+
+One large frame splits by ROW BANDS instead:
+`sift_row_bands` gives each rank band (rank, world) of the keypoint stages
+(Context.set_row_band: every rank builds the frame's pyramid, detection and
+everything after it covers only the rank's octave rows), then all-gathers
+the bands' (emission key, keypoint, descriptor) rows and merges them by
+emission key -- the one exchange step.  The bands partition every octave's
+candidate rows, so the merge is exactly the whole-frame sift() result.
 """
 import numpy as np
 
@@ -94,3 +102,77 @@ def gather_results(keypoints, descriptors, offsets, dist, dst=0):
         base += ns[r]
     return (np.concatenate(k_all).reshape(-1, 5), np.concatenate(d_all).reshape(-1, 128),
             np.asarray(o_all, dtype=np.int64))
+
+
+def merge_bands(parts):
+    """Merge per-band results [(keypoints (n,5) f32, descriptors (n,128) u8,
+    emission keys (n,) u64), ...] into one frame's result in the reference's
+    emission order (ascending key; src/lib.rs:281-294, :397-431).  Keys are
+    unique per keypoint, so the order is total; a key seen twice means two
+    bands overlapped and raises."""
+    kps = np.concatenate([np.asarray(p[0], np.float32).reshape(-1, 5) for p in parts])
+    desc = np.concatenate([np.asarray(p[1], np.uint8).reshape(-1, 128) for p in parts])
+    keys = np.concatenate([np.asarray(p[2], np.uint64).reshape(-1) for p in parts])
+    if not (len(kps) == len(desc) == len(keys)):
+        raise ValueError("keypoints / descriptors / keys disagree")
+    order = np.argsort(keys, kind="stable")
+    keys = keys[order]
+    if len(keys) > 1 and np.any(keys[1:] == keys[:-1]):
+        raise ValueError("duplicate emission key: bands overlap")
+    return kps[order], desc[order], keys
+
+
+def allgather_bands(keypoints, descriptors, keys, dist):
+    """All-gather every rank's band result (sizes first, then one padded
+    all_gather per array, raw bits) and merge them; every rank gets the
+    whole frame's (keypoints, descriptors, keys)."""
+    import torch
+    world = dist.get_world_size()
+    dev = _device(dist)
+    kps = np.ascontiguousarray(keypoints, dtype=np.float32).reshape(-1, 5)
+    desc = np.ascontiguousarray(descriptors, dtype=np.uint8).reshape(-1, 128)
+    key = np.ascontiguousarray(keys, dtype=np.uint64).reshape(-1)
+    n = len(kps)
+    if len(desc) != n or len(key) != n:
+        raise ValueError("keypoints / descriptors / keys disagree")
+    size = torch.tensor([n], dtype=torch.int64, device=dev)
+    sizes = [torch.zeros_like(size) for _ in range(world)]
+    dist.all_gather(sizes, size)
+    ns = [int(s.item()) for s in sizes]
+    n_max = max(max(ns), 1)
+
+    def padded(a, dtype):
+        t = torch.zeros((n_max,) + a.shape[1:], dtype=dtype, device=dev)
+        if len(a):
+            t[: len(a)] = torch.from_numpy(a).to(dev)
+        return t
+
+    gathered = {}
+    for name, t in (("kps", padded(kps.view(np.int32), torch.int32)), ("desc", padded(desc, torch.uint8)),
+                    ("keys", padded(key.view(np.int64), torch.int64))):
+        lst = [torch.zeros_like(t) for _ in range(world)]
+        dist.all_gather(lst, t)
+        gathered[name] = [x.cpu().numpy() for x in lst]
+    parts = [(gathered["kps"][r][: ns[r]].view(np.float32), gathered["desc"][r][: ns[r]],
+              gathered["keys"][r][: ns[r]].view(np.uint64)) for r in range(world)]
+    return merge_bands(parts)
+
+
+def sift_row_bands(ctx, img, dist=None, band=None, n_bands=None):
+    """sift() of ONE frame split across ranks by row bands (see the module
+    docstring).  With `dist` initialised, the band is (rank, world) and the
+    merged whole-frame SiftResult is returned on every rank; without it,
+    `band` / `n_bands` select one band and that band's SiftResult (with keys)
+    is returned for the caller to merge (merge_bands)."""
+    if dist is not None and dist.is_initialized():
+        band, n_bands = dist.get_rank(), dist.get_world_size()
+    elif band is None or n_bands is None:
+        band, n_bands = 0, 1
+    ctx.set_row_band(band, n_bands)
+    try:
+        r = ctx.sift(img)
+    finally:
+        ctx.set_row_band(0, 1)
+    if dist is None or not dist.is_initialized() or n_bands == 1:
+        return r
+    return type(r)(*allgather_bands(r.keypoints_array, r.descriptors, r.keys, dist))  # a SiftResult

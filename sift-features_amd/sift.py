@@ -146,6 +146,12 @@ class Context:
         """Bit-exact descriptor accumulation order (slower); default off."""
         check(lib().sift_mi_set_exact_descriptors(self._h, 1 if exact else 0))
 
+    def set_row_band(self, band, n_bands):
+        """Keypoint stages over octave rows [H_o*band/n_bands, H_o*(band+1)/n_bands)
+        only (include/sift_mi.h); band 0 of 1 = the whole frame.  Merge the
+        bands' results with shard.merge_bands."""
+        check(lib().sift_mi_set_row_band(self._h, int(band), int(n_bands)))
+
     def set_chunk(self, images_per_chunk):
         check(lib().sift_mi_set_chunk(self._h, int(images_per_chunk)))
 

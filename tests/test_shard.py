@@ -96,3 +96,87 @@ def test_shard_range_partition():
             assert max(sizes) - min(sizes) <= 1
     with pytest.raises(ValueError):
         shard.shard_range(4, 2, 2)
+
+
+# ---------------------------------------------------------------------------
+# row bands of one frame (shard.merge_bands / allgather_bands): SURVEY 8(f) row 4
+# ---------------------------------------------------------------------------
+def _shard_mod():
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "sift-features_amd"))
+    import shard
+    return shard
+
+
+def _fake_frame(n=300, seed=5):
+    """A whole frame's result in emission order: unique ascending keys."""
+    rng = np.random.default_rng(seed)
+    keys = np.sort(rng.choice(np.uint64(1) << np.uint64(40), n, replace=False).astype(np.uint64))
+    kps = rng.standard_normal((n, 5)).astype(np.float32)
+    desc = rng.integers(0, 256, (n, 128), dtype=np.uint8)
+    return kps, desc, keys
+
+
+def _split(kps, desc, keys, world, seed=9):
+    """Random disjoint partition into `world` bands (each band keeps its own
+    emission order, as one context's result does)."""
+    owner = np.random.default_rng(seed).integers(0, world, len(keys))
+    return [(kps[owner == r], desc[owner == r], keys[owner == r]) for r in range(world)]
+
+
+def test_merge_bands_restores_emission_order():
+    shard = _shard_mod()
+    kps, desc, keys = _fake_frame()
+    for world in (1, 2, 3, 8):
+        parts = _split(kps, desc, keys, world)
+        k, d, y = shard.merge_bands(parts)
+        assert np.array_equal(y, keys)
+        assert np.array_equal(k.view(np.uint32), kps.view(np.uint32))
+        assert np.array_equal(d, desc)
+    # empty bands and an empty frame
+    k, d, y = shard.merge_bands([(kps[:0], desc[:0], keys[:0])] * 3)
+    assert len(k) == len(d) == len(y) == 0
+    parts = _split(kps, desc, keys, 2)
+    with pytest.raises(ValueError):  # overlapping bands
+        shard.merge_bands(parts + [parts[0]])
+
+
+def _band_worker(rank, world, port, q):
+    import sys
+    import torch.distributed as dist
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "sift-features_amd"))
+    import shard
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        kps, desc, keys = _fake_frame()
+        mine = _split(kps, desc, keys, world)[rank]
+        q.put(("ok", rank, shard.allgather_bands(*mine, dist)))
+    except Exception as e:  # pragma: no cover - surfaced by the assert below
+        q.put(("err", rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_gloo_world2_allgather_bands():
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_band_worker, args=(r, 2, port, q)) for r in range(2)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=100) for _ in range(2)]
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    assert all(r[0] == "ok" for r in res), res
+    kps, desc, keys = _fake_frame()
+    for _, _, (k, d, y) in res:  # every rank holds the whole frame
+        assert np.array_equal(y, keys)
+        assert np.array_equal(k.view(np.uint32), kps.view(np.uint32))
+        assert np.array_equal(d, desc)
