@@ -447,6 +447,7 @@ struct sift_mi_ctx {
     uint32_t chunk_override = 0;
     int keep_on_device = 0;
     uint32_t band_r = 0, band_n = 1;  // row band of the keypoint stages (sift_mi_set_row_band)
+    JpegBatchCache jpeg;              // sift_mi_decode_jpeg_batch buffers
     int exact_descriptors = 0;
     Plan plan;
     DevBuf<uint8_t> staging;  // host-sourced frames
@@ -1208,6 +1209,7 @@ void sift_mi_destroy(sift_mi_ctx* c) {
     if (c->cstream) (void)hipStreamSynchronize(c->cstream);
     c->plan.release();
     c->staging.release();
+    c->jpeg.release();
     for (auto& S : c->slot) S.release_bufs();
     for (auto& S : c->slot) {
         S.counters.release();
@@ -1616,7 +1618,7 @@ int sift_mi_decode_jpeg_batch(sift_mi_ctx* c, const uint8_t* const* data, const 
     if (threads <= 0) threads = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
     CHK(set_device(c));
     std::string err;
-    const int rc = jpeg_decode_batch(data, len, n, d_frames, frame_pitch, row_stride, threads, c->stream, err);
+    const int rc = jpeg_decode_batch(data, len, n, d_frames, frame_pitch, row_stride, threads, c->stream, c->jpeg, err);
     return rc ? fail(rc, err) : 0;
 }
 

@@ -21,6 +21,7 @@
 // Huffman only (SOF0/SOF1), 1 or 3 components, sampling factors 1 or 2,
 // restart intervals.
 #include <atomic>
+#include <condition_variable>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -38,12 +39,20 @@ constexpr int kZigzag[64] = {0,  1,  8,  16, 9,  2,  3,  10, 17, 24, 32, 25, 18,
                              41, 34, 27, 20, 13, 6,  7,  14, 21, 28, 35, 42, 49, 56, 57, 50, 43, 36, 29, 22, 15, 23,
                              30, 37, 44, 51, 58, 59, 52, 45, 38, 31, 39, 46, 53, 60, 61, 54, 47, 55, 62, 63};
 
+#ifndef SIFT_JPEG_FAST_AC
+#define SIFT_JPEG_FAST_AC 11
+#endif
+constexpr int kFastAc = SIFT_JPEG_FAST_AC;
+
 // canonical Huffman decoding tables (T.81 F.2.2.3) plus a 9-bit lookahead
 struct Huff {
     bool present = false;
     int maxcode[17], valptr[17], mincode[17];
     uint8_t sym[256];
     uint16_t fast[512];  // (code length << 8) | symbol for codes of <= 9 bits; 0: walk the lengths
+    // AC run/size symbol and its extra bits in one kFastAc-bit lookup (code
+    // length + size <= kFastAc, size > 0): (coefficient << 16) | (run << 8) | bits used
+    int32_t fast_ac[1 << kFastAc];
 };
 
 struct Comp {
@@ -71,6 +80,19 @@ class Bits {
     Bits(const uint8_t* d_, size_t n_, size_t p_) : d(d_), n(n_), p(p_) {}
     void fill() {
         while (cnt <= 56) {
+            if (p + 8 <= n) {  // 8 bytes at once when none of them is 0xFF
+                uint64_t v;
+                std::memcpy(&v, d + p, 8);
+                v = __builtin_bswap64(v);
+                const uint64_t x = ~v;  // a 0xFF byte of v is a zero byte of x
+                if (((x - 0x0101010101010101ull) & ~x & 0x8080808080808080ull) == 0) {
+                    const int k = (64 - cnt) >> 3;  // 1..8 whole bytes fit
+                    acc = k == 8 ? v : (acc << (8 * k)) | (v >> (64 - 8 * k));
+                    p += k;
+                    cnt += 8 * k;
+                    continue;
+                }
+            }
             uint32_t b = 0;
             if (p < n) {
                 b = d[p];
@@ -88,14 +110,21 @@ class Bits {
             cnt += 8;
         }
     }
+    // at least 32 buffered bits: a Huffman code (<= 16) plus its extra bits (<= 16)
+    void refill() {
+        if (cnt < 32) fill();
+    }
     int peek9() {
-        fill();
+        refill();
         return (int)((acc >> (cnt - 9)) & 511u);
+    }
+    int peek_ac() {  // kFastAc bits, after refill()
+        return (int)((acc >> (cnt - kFastAc)) & ((1u << kFastAc) - 1));
     }
     void skip(int k) { cnt -= k; }
     int bits(int k) {
         if (!k) return 0;
-        fill();
+        refill();
         cnt -= k;
         return (int)((acc >> cnt) & ((1ull << k) - 1));
     }
@@ -128,6 +157,23 @@ bool build_huff(const uint8_t* counts, const uint8_t* syms, int nsym, Huff& t) {
             t.maxcode[ln] = code - 1;
         }
         code <<= 1;
+    }
+    // combined AC lookups: every kFastAc-bit window whose leading code has
+    // length ln <= 10 and whose symbol's extra bits also fit
+    std::memset(t.fast_ac, 0, sizeof(t.fast_ac));
+    for (int x = 0; x < (1 << kFastAc); x++) {
+        for (int ln = 1; ln <= kFastAc; ln++) {
+            const int c = x >> (kFastAc - ln);
+            if (c > t.maxcode[ln]) continue;
+            const int rs = t.sym[t.valptr[ln] + c - t.mincode[ln]];
+            const int r = rs >> 4, sz = rs & 15;
+            if (sz && ln + sz <= kFastAc) {
+                const int raw = (x >> (kFastAc - ln - sz)) & ((1 << sz) - 1);
+                const int v = (raw < (1 << (sz - 1))) ? raw - (1 << sz) + 1 : raw;  // extend()
+                t.fast_ac[x] = (int32_t)((uint32_t)(v & 0xffff) << 16 | (uint32_t)(r << 8) | (uint32_t)(ln + sz));
+            }
+            break;
+        }
     }
     t.present = true;
     return true;
@@ -293,8 +339,8 @@ int entropy_decode(const uint8_t* d, size_t n, const Header& H, const Geom& g, i
                     for (int bx = 0; bx < c.h; bx++) {
                         int16_t* dst =
                             coef + 64 * (g.off[ci] + (size_t)(my * c.v + by) * g.bw[ci] + (size_t)(mx * c.h + bx));
-                        int16_t blk[64];
-                        std::memset(blk, 0, sizeof(blk));
+                        int16_t* __restrict__ blk = dst;  // natural order, written in place
+                        std::memset(blk, 0, 64 * sizeof(int16_t));
                         const int t = decode_sym(bs, dct);
                         if (t < 0 || t > 16) return err = "JPEG: bad Huffman code", SIFT_MI_EINVAL;
                         pred[ci] += extend(bs.bits(t), t);
@@ -302,6 +348,16 @@ int entropy_decode(const uint8_t* d, size_t n, const Header& H, const Geom& g, i
                             return err = "JPEG: DC coefficient out of range", SIFT_MI_EUNSUPPORTED;
                         blk[0] = (int16_t)pred[ci];
                         for (int k = 1; k < 64;) {
+                            bs.refill();
+                            const int32_t fa = act.fast_ac[bs.peek_ac()];
+                            if (fa) {  // run, size and coefficient in one lookup
+                                k += (fa >> 8) & 15;
+                                bs.skip(fa & 255);
+                                if (k > 63) return err = "JPEG: coefficient index out of range", SIFT_MI_EINVAL;
+                                blk[kZigzag[k]] = (int16_t)(fa >> 16);
+                                k++;
+                                continue;
+                            }
                             const int rs = decode_sym(bs, act);
                             if (rs < 0) return err = "JPEG: bad Huffman code", SIFT_MI_EINVAL;
                             const int r = rs >> 4, s = rs & 15;
@@ -315,7 +371,6 @@ int entropy_decode(const uint8_t* d, size_t n, const Header& H, const Geom& g, i
                             blk[kZigzag[k]] = (int16_t)extend(bs.bits(s), s);
                             k++;
                         }
-                        std::memcpy(dst, blk, sizeof(blk));
                     }
                 }
             }
@@ -618,8 +673,26 @@ int jpeg_decode_luma(const uint8_t* data, size_t len, uint8_t* out, size_t out_s
 // frame_pitch).  Entropy decoding of a chunk of frames runs on `threads` host
 // threads into pinned buffers (two, alternating) while the previous chunk's
 // upload and reconstruction kernels run on the stream.
+void JpegBatchCache::release() {
+    for (int k = 0; k < 2; k++) {
+        if (pin[k]) (void)hipHostFree(pin[k]);
+        if (up[k]) (void)hipEventDestroy(up[k]);
+        pin[k] = nullptr;
+        up[k] = nullptr;
+    }
+    if (dev) (void)hipFree(dev);
+    dev = nullptr;
+    pin_bytes = dev_bytes = 0;
+}
+
+// Host threads entropy-decode frames in order (work stealing over the whole
+// batch) into two pinned chunk buffers; the calling thread uploads each chunk
+// as soon as its frames are in and launches the chunk's reconstruction, so
+// decoding chunk k + 1 overlaps the upload and kernels of chunk k.  A buffer
+// is handed back to the workers when its upload has completed.
 int jpeg_decode_batch(const uint8_t* const* data, const size_t* len, uint32_t n, uint8_t* d_out,
-                      size_t frame_pitch, size_t stride, int threads, hipStream_t st, std::string& err) {
+                      size_t frame_pitch, size_t stride, int threads, hipStream_t st, JpegBatchCache& cache,
+                      std::string& err) {
     if (n == 0) return 0;
     jpg::Header H0;
     int rc = jpg::parse(data[0], len[0], H0, err);
@@ -637,90 +710,125 @@ int jpeg_decode_batch(const uint8_t* const* data, const size_t* len, uint32_t n,
         if (!same) return err = "JPEG batch: frames differ in size or sampling", SIFT_MI_EINVAL;
     }
     const uint32_t C = std::min<uint32_t>(n, 16);  // frames per chunk
+    const uint32_t n_chunks = (n + C - 1) / C;
     const size_t fcoef = g.total * 64;              // int16 per frame
     jpg::Planes P;
     jpg::LumaArgs A;
     jpg::views(H0, g, nullptr, nullptr, 0, 0, P, A);
     const size_t fplane = P.frame_bytes;
-    int16_t* pin[2] = {nullptr, nullptr};
-    hipEvent_t up[2] = {nullptr, nullptr};
-    uint8_t* dev = nullptr;
-    auto cleanup = [&]() {
-        (void)hipStreamSynchronize(st);
+    const size_t q_bytes = ((size_t)n * 3 * 64 * sizeof(int32_t) + 255) & ~(size_t)255;
+    const size_t pin_bytes = C * fcoef * sizeof(int16_t);
+    const size_t dev_bytes = q_bytes + 2 * C * fcoef * sizeof(int16_t) + C * fplane;
+    // buffers: grow-only, kept by the context (the previous call has drained:
+    // every call synchronises its stream before returning)
+    if (cache.pin_bytes < pin_bytes) {
         for (int k = 0; k < 2; k++) {
-            if (pin[k]) (void)hipHostFree(pin[k]);
-            if (up[k]) (void)hipEventDestroy(up[k]);
+            if (cache.pin[k]) (void)hipHostFree(cache.pin[k]);
+            cache.pin[k] = nullptr;
         }
-        if (dev) (void)hipFree(dev);
-    };
-    bool ok = true;
-    for (int k = 0; k < 2 && ok; k++)
-        ok = hipHostMalloc((void**)&pin[k], C * fcoef * sizeof(int16_t), hipHostMallocDefault) == hipSuccess &&
-             hipEventCreateWithFlags(&up[k], hipEventDisableTiming) == hipSuccess;
-    const size_t q_bytes = (size_t)n * 3 * 64 * sizeof(int32_t);
-    ok = ok && hipMalloc((void**)&dev, q_bytes + 2 * C * fcoef * sizeof(int16_t) + C * fplane) == hipSuccess;
-    if (!ok) {
-        cleanup();
-        return err = "JPEG batch: allocation failed", SIFT_MI_ENOMEM;
+        cache.pin_bytes = 0;
+        for (int k = 0; k < 2; k++)
+            if (hipHostMalloc((void**)&cache.pin[k], pin_bytes, hipHostMallocDefault) != hipSuccess) {
+                cache.release();
+                return err = "JPEG batch: allocation failed", SIFT_MI_ENOMEM;
+            }
+        cache.pin_bytes = pin_bytes;
     }
+    for (int k = 0; k < 2; k++)
+        if (!cache.up[k] && hipEventCreateWithFlags(&cache.up[k], hipEventDisableTiming) != hipSuccess) {
+            cache.release();
+            return err = "JPEG batch: HIP error", SIFT_MI_EHIP;
+        }
+    if (cache.dev_bytes < dev_bytes) {
+        if (cache.dev) (void)hipFree(cache.dev);
+        cache.dev = nullptr;
+        cache.dev_bytes = 0;
+        if (hipMalloc((void**)&cache.dev, dev_bytes) != hipSuccess) {
+            cache.release();
+            return err = "JPEG batch: allocation failed", SIFT_MI_ENOMEM;
+        }
+        cache.dev_bytes = dev_bytes;
+    }
+    int16_t* const* pin = cache.pin;
+    uint8_t* dev = cache.dev;
     // every frame's quantisation tables (frames may differ in quality)
     std::vector<int32_t> qt((size_t)n * 3 * 64, 0);
     for (uint32_t i = 0; i < n; i++) jpg::qtables(hdr[i], qt.data() + (size_t)i * 192);
     const int32_t* d_q = reinterpret_cast<const int32_t*>(dev);
-    if (hipMemcpyAsync(dev, qt.data(), q_bytes, hipMemcpyHostToDevice, st) != hipSuccess ||
-        hipStreamSynchronize(st) != hipSuccess) {
-        cleanup();
+    if (hipMemcpyAsync(dev, qt.data(), qt.size() * sizeof(int32_t), hipMemcpyHostToDevice, st) != hipSuccess)
         return err = "JPEG batch: HIP error", SIFT_MI_EHIP;
-    }
     uint8_t* d_cf = dev + q_bytes;
     uint8_t* d_pl = d_cf + 2 * C * fcoef * sizeof(int16_t);
-    const int T = std::max(1, threads);
-    std::string terr;
+
+    // worker pool over the whole batch
+    std::mutex mu;
+    std::condition_variable cv;
+    std::vector<uint32_t> done(n_chunks, 0);
+    uint32_t free_upto = 2;  // chunks below this may be decoded (their buffer is free)
+    bool stop = false;
     int trc = 0;
-    for (uint32_t c0 = 0, k = 0; c0 < n; c0 += C, k ^= 1) {
-        const uint32_t m = std::min(C, n - c0);
-        // the pinned buffer's previous upload (two chunks back) has finished
-        if (c0 >= 2 * C && hipEventSynchronize(up[k]) != hipSuccess) {
-            cleanup();
-            return err = "JPEG batch: HIP error", SIFT_MI_EHIP;
-        }
-        std::atomic<uint32_t> next{0};
-        std::mutex mu;
-        auto work = [&]() {
-            std::string e;
-            for (uint32_t i; (i = next.fetch_add(1)) < m;) {
-                const uint32_t f = c0 + i;
-                const int r = jpg::entropy_decode(data[f], len[f], hdr[f], g, pin[k] + i * fcoef, e);
-                if (r) {
-                    std::lock_guard<std::mutex> lk(mu);
-                    if (!trc) trc = r, terr = e;
-                    return;
-                }
+    std::string terr;
+    std::atomic<uint32_t> next{0};
+    auto work = [&]() {
+        std::string e;
+        for (uint32_t i; (i = next.fetch_add(1)) < n;) {
+            const uint32_t ch = i / C;
+            {
+                std::unique_lock<std::mutex> lk(mu);
+                cv.wait(lk, [&] { return ch < free_upto || stop; });
+                if (stop) return;
             }
-        };
-        std::vector<std::thread> pool;
-        for (int t = 1; t < std::min<int>(T, (int)m); t++) pool.emplace_back(work);
-        work();
-        for (auto& th : pool) th.join();
-        if (trc) {
-            cleanup();
-            return err = terr, trc;
+            const int r = jpg::entropy_decode(data[i], len[i], hdr[i], g, pin[ch & 1] + (size_t)(i - ch * C) * fcoef, e);
+            {
+                std::lock_guard<std::mutex> lk(mu);
+                if (r && !trc) trc = r, terr = e, stop = true;
+                done[ch]++;
+            }
+            cv.notify_all();
+            if (r) return;
+        }
+    };
+    const int T = std::max(1, std::min<int>(threads, (int)n));
+    std::vector<std::thread> pool;
+    pool.reserve(T);
+    for (int t = 0; t < T; t++) pool.emplace_back(work);
+    bool ok = true;
+    for (uint32_t ch = 0; ch < n_chunks && ok; ch++) {
+        const uint32_t c0 = ch * C, m = std::min(C, n - c0), k = ch & 1;
+        {
+            std::unique_lock<std::mutex> lk(mu);
+            cv.wait(lk, [&] { return done[ch] == m || stop; });
+            if (stop) break;
         }
         int16_t* d_coef = reinterpret_cast<int16_t*>(d_cf) + k * C * fcoef;
         jpg::views(H0, g, d_pl, d_out + (size_t)c0 * frame_pitch, stride, frame_pitch, P, A);
         P.qtab = A.P.qtab = d_q + (size_t)c0 * 192;
         ok = hipMemcpyAsync(d_coef, pin[k], m * fcoef * sizeof(int16_t), hipMemcpyHostToDevice, st) == hipSuccess &&
-             hipEventRecord(up[k], st) == hipSuccess;
+             hipEventRecord(cache.up[k], st) == hipSuccess;
         if (ok) {
             jpg::launch(d_coef, m, g, H0, P, A, st);
             ok = hipGetLastError() == hipSuccess;
         }
-        if (!ok) {
-            cleanup();
-            return err = "JPEG batch: HIP error", SIFT_MI_EHIP;
+        // pinned buffer k is free for chunk ch + 2 once this upload is done
+        ok = ok && hipEventSynchronize(cache.up[k]) == hipSuccess;
+        {
+            std::lock_guard<std::mutex> lk(mu);
+            if (ok)
+                free_upto = ch + 3;
+            else
+                stop = true;
         }
+        cv.notify_all();
     }
-    cleanup();
+    {
+        std::lock_guard<std::mutex> lk(mu);
+        stop = stop || !ok;
+    }
+    cv.notify_all();
+    for (auto& th : pool) th.join();
+    const bool synced = hipStreamSynchronize(st) == hipSuccess;
+    if (trc) return err = terr, trc;
+    if (!ok || !synced) return err = "JPEG batch: HIP error", SIFT_MI_EHIP;
     return 0;
 }
 

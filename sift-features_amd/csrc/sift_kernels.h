@@ -87,8 +87,18 @@ int launch_octave(const OctaveArgs& a, int n_img, hipStream_t st);
 int jpeg_dims(const uint8_t* data, size_t len, uint32_t* w, uint32_t* h, std::string& err);
 int jpeg_decode_luma(const uint8_t* data, size_t len, uint8_t* out, size_t out_stride, bool out_on_device,
                      hipStream_t st, std::string& err);
+// pinned coefficient buffers and device scratch of the batch decoder, kept by
+// the context across calls (grow-only)
+struct JpegBatchCache {
+    int16_t* pin[2] = {nullptr, nullptr};
+    hipEvent_t up[2] = {nullptr, nullptr};
+    size_t pin_bytes = 0;
+    uint8_t* dev = nullptr;
+    size_t dev_bytes = 0;
+    void release();
+};
 int jpeg_decode_batch(const uint8_t* const* data, const size_t* len, uint32_t n, uint8_t* d_out, size_t frame_pitch,
-                      size_t stride, int threads, hipStream_t st, std::string& err);
+                      size_t stride, int threads, hipStream_t st, JpegBatchCache& cache, std::string& err);
 int octave_strip_width();
 int octave_min_width();
 bool octave_radii_supported(const int* r);  // r[1..5]
