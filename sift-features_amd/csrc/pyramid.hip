@@ -588,7 +588,10 @@ int launch_blur(int R, const BlurLaunch& L, hipStream_t st) {
 
 template <int R>
 static void launch_seed_r(const SeedLaunch& L, hipStream_t st) {
-    constexpr int TH = 32;
+#ifndef SIFT_SEED_TH
+#define SIFT_SEED_TH 32
+#endif
+    constexpr int TH = SIFT_SEED_TH;
     using G = BlurGeom<R, TH>;
     dim3 grid((L.W + G::TW - 1) / G::TW, (L.H + G::TH - 1) / G::TH, L.n_img);
     hipLaunchKernelGGL((k_seed<R, TH>), grid, dim3(256), 0, st, L.frames, L.frame_pitch, L.row_stride, L.sh, L.sw, L.tab,

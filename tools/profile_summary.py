@@ -75,8 +75,17 @@ run = sk[best[0]:best[1]]
 seeds = [i for i, x in enumerate(run) if x[3].startswith("k_seed")]
 steps = b["steps"] if b else 3
 chunks_per_call = max(1, len(seeds) // (steps + 1))
-timed = run[seeds[-steps * chunks_per_call]:] if len(seeds) >= steps * chunks_per_call else run
-iso = [(e - s0) / 1e3 for s0, e, _, k in timed if k.startswith(PYR)]
+# complete chunks of the serialised pass: a seed and every blur after it up to
+# the next seed (a group cut short at the run's end is dropped); the last
+# steps * chunks_per_call complete groups are the timed steps
+groups = []
+for a, z in zip(seeds, seeds[1:] + [len(run)]):
+    g = [x for x in run[a:z] if x[3].startswith(PYR)]
+    groups.append(g)
+full = max((len(g) for g in groups), default=0)
+groups = [g for g in groups if len(g) == full]
+timed = [x for g in groups[-steps * chunks_per_call:] for x in g]
+iso = [(e - s0) / 1e3 for s0, e, _, k in timed]
 iso_us, iso_n = sum(iso), len(iso)
 
 
