@@ -210,6 +210,7 @@ typedef struct {
     uint64_t frames;
     uint64_t extrema;
     uint64_t keypoints;
+    uint64_t band_reruns;  /* row-band calls re-run on the whole-frame pyramid (sift_mi_set_row_band) */
 } sift_mi_stats;
 int sift_mi_get_stats(sift_mi_ctx* ctx, sift_mi_stats* out);
 int sift_mi_reset_stats(sift_mi_ctx* ctx);

@@ -36,8 +36,12 @@ struct DogView {
 };
 
 __device__ __forceinline__ bool interpolate(const DogView& dv, int W, int H, int pitch, int& scale, int& x, int& y,
-                                            float& os, float& ox, float& oy) {
+                                            float& os, float& ox, float& oy, uint32_t* band_flag, int vlo, int vhi) {
     for (int it = 0; it < kMaxInterpSteps; it++) {
+        // row bands with a restricted pyramid (host.cpp run_pyramid): the
+        // rows read here must be computed ones, else the host recomputes the
+        // band on the whole-frame pyramid
+        if (band_flag && (y - 1 < vlo || y + 1 >= vhi)) atomicOr(band_flag, 1u);
         const int prev = scale - 1, curr = scale, next = scale + 1;
 #define AT(a, yy, xx) dv(a, (size_t)(yy) * pitch + (xx))
         const float g1 = (AT(next, y, x) - AT(prev, y, x)) / 2.f;
@@ -265,7 +269,12 @@ __device__ __forceinline__ bool refine_one(const RefineLaunch& L, uint64_t key, 
     const DogView dv{as_global(L.gauss[o]) + (size_t)(b - L.img_base) * L.g_img_stride[o], (size_t)pitch * H};
     int sc = s_in, xi = x, yi = y;
     float os, ox, oy;
-    if (!interpolate(dv, W, H, pitch, sc, xi, yi, os, ox, oy)) return false;
+    int vlo = 0, vhi = H;  // rows of this octave's Gaussians that are exact
+    if (L.band_flag) {
+        vlo = max(0, (int)((uint64_t)H * L.band_r / L.band_n) - 1 - L.band_margin);
+        vhi = min(H, (int)((uint64_t)H * (L.band_r + 1) / L.band_n) + 1 + L.band_margin);
+    }
+    if (!interpolate(dv, W, H, pitch, sc, xi, yi, os, ox, oy, L.band_flag, vlo, vhi)) return false;
     const size_t c = (size_t)yi * pitch + xi;
     auto prev = [&](size_t off) { return dv(sc - 1, off); };
     auto curr = [&](size_t off) { return dv(sc, off); };
@@ -286,6 +295,10 @@ __device__ __forceinline__ bool refine_one(const RefineLaunch& L, uint64_t key, 
     const float det = d22 * h11 - h12 * h12;
     if (det <= 0.f) return false;
     if ((tr * tr * kEdgeThreshold) > (kEdgeThreshold + 1.0f) * (kEdgeThreshold + 1.0f) * det) return false;
+    // an accepted keypoint's orientation / descriptor patch must be exact too
+    // (at the image's own top / bottom rows the patch reads clamp, so no limit)
+    if (L.band_flag && ((vlo > 0 && yi - L.band_patch < vlo) || (vhi < H && yi + L.band_patch >= vhi)))
+        atomicOr(L.band_flag, 1u);
     e.key = key;
     e.img = b;
     e.octave = o;

@@ -448,6 +448,9 @@ struct sift_mi_ctx {
     int keep_on_device = 0;
     uint32_t band_r = 0, band_n = 1;  // row band of the keypoint stages (sift_mi_set_row_band)
     JpegBatchCache jpeg;              // sift_mi_decode_jpeg_batch buffers
+    DevBuf<uint32_t> band_flag;       // a refinement left the restricted rows (row bands)
+    bool band_restricted = false;     // this call computes only the band's pyramid rows
+    bool band_whole = false;          // re-run of a band on the whole-frame pyramid
     int exact_descriptors = 0;
     Plan plan;
     DevBuf<uint8_t> staging;  // host-sourced frames
@@ -630,6 +633,12 @@ int ensure_plan(sift_mi_ctx* c, uint32_t w, uint32_t h, uint32_t chunk) {
     return ensure_lane(c, 0);
 }
 
+// Row bands with a restricted pyramid: rows a refined keypoint may drift from
+// its detection row and still be exact without a re-run, and the rows its
+// orientation / descriptor patch reaches (radius <= 16 / 39, plus the
+// gradient's neighbour row).
+constexpr int kBandDrift = 24, kBandPatch = 41;
+
 // ---------------------------------------------------------------------------
 // Stage 1: Gaussian scale space + DoG for n frames (device-resident u8)
 // ---------------------------------------------------------------------------
@@ -662,6 +671,44 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
     S.pitch = p.opitch[0];
     S.n_img = (int)n;
     S.taps = p.seed_taps;
+    // row bands (sift_mi_set_row_band): the rows of every Gaussian the band's
+    // keypoint stages read, propagated back through the blur chain and the
+    // octave downsampling.  Detection covers octave rows [H*r/n, H*(r+1)/n);
+    // around them a margin of kBandDrift + 1 + kBandPatch rows.  A
+    // refinement that reads, or an accepted keypoint whose patch reaches,
+    // beyond it sets band_flag (k_refine) and the host re-runs the band on
+    // the whole pyramid.
+    std::vector<int> rlo((size_t)p.n_oct * kImagesPerOctave, 0), rhi((size_t)p.n_oct * kImagesPerOctave, 0);
+    c->band_restricted = c->band_n > 1 && !full && !c->band_whole && p.profile == (int)SIFT_MI_PROFILE_OPENCV;
+    if (c->band_restricted) {
+        int need_lo = 0, need_hi = 0;  // octave o + 1's G_0 rows, in octave o + 1 coordinates
+        for (int o = p.n_oct - 1; o >= 0; o--) {
+            const int H = p.oh[o], M = kBandDrift + 1 + kBandPatch;
+            const int blo = (int)((uint64_t)H * c->band_r / c->band_n), bhi = (int)((uint64_t)H * (c->band_r + 1) / c->band_n);
+            int* lo = &rlo[(size_t)o * kImagesPerOctave];
+            int* hi = &rhi[(size_t)o * kImagesPerOctave];
+            for (int s = 0; s < kImagesPerOctave; s++) {
+                lo[s] = blo - 1 - M;
+                hi[s] = bhi + 1 + M;
+            }
+            if (o + 1 < p.n_oct && need_hi > need_lo) {  // nearest 1/2 of G_3: row 2y or 2y + 1
+                lo[3] = std::min(lo[3], 2 * need_lo);
+                hi[3] = std::max(hi[3], 2 * need_hi + 1);
+            }
+            for (int s = kImagesPerOctave - 1; s >= 1; s--) {
+                lo[s - 1] = std::min(lo[s - 1], lo[s] - p.oct_r[s]);
+                hi[s - 1] = std::max(hi[s - 1], hi[s] + p.oct_r[s]);
+            }
+            for (int s = 0; s < kImagesPerOctave; s++) {
+                lo[s] = std::max(lo[s], 0);
+                hi[s] = std::min(hi[s], H);
+            }
+            need_lo = lo[0];
+            need_hi = hi[0];
+        }
+        S.y0 = rlo[0];
+        S.y1 = std::max(rhi[0], rlo[0] + 1);
+    }
     if (launch_seed(p.seed_r, S, st)) return fail(SIFT_MI_EUNSUPPORTED, "seed blur radius");
     uint64_t launches = 1;
     const uint64_t bytes = p.algo_bytes_per_frame;  // per frame, SURVEY.md 8(d)
@@ -678,7 +725,7 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
         float* G = p.gauss(o, lane);
         float* D = p.dog(o, lane);
         const size_t P = p.P[o];
-        if (fused_ok && p.ow[o] >= octave_min_width()) {
+        if (fused_ok && !c->band_restricted && p.ow[o] >= octave_min_width()) {
             OctaveArgs A{};
             A.gauss = G;
             A.g_img_stride = p.gstride(o);
@@ -729,6 +776,10 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
             B.n_img = (int)n;
             B.taps = p.oct_taps[s];
             B.profile = p.profile;
+            if (c->band_restricted) {
+                B.y0 = rlo[(size_t)o * kImagesPerOctave + s];
+                B.y1 = std::max(rhi[(size_t)o * kImagesPerOctave + s], B.y0 + 1);
+            }
             if (launch_blur(p.oct_r[s], B, st)) return fail(SIFT_MI_EUNSUPPORTED, "octave blur radius");
             launches++;
         }
@@ -847,6 +898,15 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
     R.cand = S.cand.p;
     R.n_cand = cnt + 0;
     R.cand_cap = B.bc;
+    R.band_flag = c->band_restricted ? c->band_flag.p : nullptr;
+    R.band_r = (int)c->band_r;
+    R.band_n = (int)c->band_n;
+    R.band_patch = kBandPatch;
+    R.band_margin = kBandDrift + 1 + kBandPatch;
+    // SIFT_MI_BAND_DRIFT narrows the rows the check accepts (down to -kBandPatch:
+    // patches may not cross the band edge; tests force the re-run path)
+    if (const char* e = getenv("SIFT_MI_BAND_DRIFT"))
+        R.band_margin = kBandPatch + 1 + std::min(kBandDrift, std::max(-kBandPatch, atoi(e)));
     R.gauss = p.d_gauss[arena_of(c, si)].p;
     R.g_img_stride = p.d_gstride.p;
     R.ow = p.d_ow.p;
@@ -1074,6 +1134,10 @@ int extract_device(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, 
     c->have_pyramid = false;
     c->n_result = 0;
     c->have_result = false;
+    if (c->band_n > 1) {
+        CHK(c->band_flag.ensure(1));
+        HIPCHK(hipMemsetAsync(c->band_flag.p, 0, sizeof(uint32_t), c->stream));
+    }
     const uint32_t n_chunks = (n + chunk - 1) / chunk;
     auto frames_of = [&](uint32_t k) { return std::min(chunk, n - k * chunk); };
     auto enqueue = [&](uint32_t k) {
@@ -1110,6 +1174,20 @@ int extract_device(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, 
     HIPCHK(hipStreamSynchronize(c->cstream));
     if (offsets) offsets[n] = c->n_result;
     c->have_result = true;
+    if (c->band_restricted) {
+        // a refinement drifted past the computed rows: redo the band on the
+        // whole-frame pyramid (exact; the rare case)
+        c->band_restricted = false;
+        uint32_t flag = 0;
+        HIPCHK(hipMemcpy(&flag, c->band_flag.p, sizeof(flag), hipMemcpyDeviceToHost));
+        if (flag) {
+            c->stats.band_reruns++;
+            c->band_whole = true;
+            const int rc = extract_device(c, d_frames, frame_pitch, n, w, h, stride, limit, offsets);
+            c->band_whole = false;
+            return rc;
+        }
+    }
     return 0;
 }
 
@@ -1210,6 +1288,7 @@ void sift_mi_destroy(sift_mi_ctx* c) {
     c->plan.release();
     c->staging.release();
     c->jpeg.release();
+    c->band_flag.release();
     for (auto& S : c->slot) S.release_bufs();
     for (auto& S : c->slot) {
         S.counters.release();

@@ -228,14 +228,14 @@ __global__ __launch_bounds__(256) void k_blur(const float* __restrict__ src, siz
                                               float* __restrict__ dst, size_t dst_img_stride,
                                               float* __restrict__ dog, size_t dog_img_stride,
                                               float* __restrict__ nxt, size_t nxt_img_stride, int pitch_n, int wn,
-                                              int hn, int W, int H, int pitch, const BlurTaps taps) {
+                                              int hn, int W, int H, int pitch, const BlurTaps taps, int ty0) {
     using G = BlurGeom<R, TH>;
     __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
     float* tin = lds;  // [IH][IWP]  G_{s-1} window, then (in place) the row-pass output
     float* th = lds;
     const int tid = threadIdx.x;
     const TileId tile = xcd_tile();
-    const int x0 = tile.x * G::TW, y0 = tile.y * G::TH;
+    const int x0 = tile.x * G::TW, y0 = (tile.y + ty0) * G::TH;  // ty0: first tile row (row bands)
     const size_t b = tile.z;
     src += b * src_img_stride;
     const bool interior = x0 >= G::HWL && x0 + G::TW + G::HWL <= W && y0 >= R && y0 + G::TH + R <= H;
@@ -316,7 +316,7 @@ template <int R, int TH>
 __global__ __launch_bounds__(256) void k_seed(const uint8_t* __restrict__ frames, size_t frame_pitch,
                                               size_t row_stride, int sh, int sw, const ResizeTab tab,
                                               float* __restrict__ dst, size_t dst_img_stride, int W, int H,
-                                              int pitch, const BlurTaps taps) {
+                                              int pitch, const BlurTaps taps, int ty0) {
     using G = BlurGeom<R, TH>;
     // Source window of an exact 2x upsample: destination g reads source
     // floor(g / 2 - 0.25) and the next one, so the window's destination range
@@ -338,7 +338,7 @@ __global__ __launch_bounds__(256) void k_seed(const uint8_t* __restrict__ frames
     float* th = lds;
     const int tid = threadIdx.x;
     const TileId tile = xcd_tile();
-    const int x0 = tile.x * G::TW, y0 = tile.y * G::TH;
+    const int x0 = tile.x * G::TW, y0 = (tile.y + ty0) * G::TH;  // ty0: first tile row (row bands)
     const size_t b = tile.z;
     const uint8_t* src = frames + b * frame_pitch;
     // the exact-2x window math needs single reflections and a 2x geometry
@@ -562,15 +562,20 @@ template <int R>
 static void launch_blur_r(const BlurLaunch& L, hipStream_t st) {
     constexpr int TH = R >= 10 ? 64 : 32;  // measured: tools/ubench_kernels.hip blur
     using G = BlurGeom<R, TH>;
-    dim3 grid((L.W + G::TW - 1) / G::TW, (L.H + G::TH - 1) / G::TH, L.n_img);
+    const int tiles_y = (L.H + G::TH - 1) / G::TH;
+    // optional row range (row bands): tile rows covering [L.y0, L.y1)
+    const int ty0 = L.y1 > L.y0 ? L.y0 / G::TH : 0;
+    const int ty1 = L.y1 > L.y0 ? std::min(tiles_y, (L.y1 + G::TH - 1) / G::TH) : tiles_y;
+    if (ty1 <= ty0) return;
+    dim3 grid((L.W + G::TW - 1) / G::TW, ty1 - ty0, L.n_img);
     if (L.profile == kProfileImageproc)
         hipLaunchKernelGGL((k_blur<R, TH, kProfileImageproc>), grid, dim3(256), 0, st, L.src, L.src_img_stride, L.dst,
                            L.dst_img_stride, L.dog, L.dog_img_stride, L.nxt, L.nxt_img_stride, L.pitch_n, L.wn, L.hn,
-                           L.W, L.H, L.pitch, L.taps);
+                           L.W, L.H, L.pitch, L.taps, ty0);
     else
         hipLaunchKernelGGL((k_blur<R, TH, kProfileOpenCV>), grid, dim3(256), 0, st, L.src, L.src_img_stride, L.dst,
                            L.dst_img_stride, L.dog, L.dog_img_stride, L.nxt, L.nxt_img_stride, L.pitch_n, L.wn, L.hn,
-                           L.W, L.H, L.pitch, L.taps);
+                           L.W, L.H, L.pitch, L.taps, ty0);
 }
 
 int launch_blur(int R, const BlurLaunch& L, hipStream_t st) {
@@ -593,9 +598,13 @@ static void launch_seed_r(const SeedLaunch& L, hipStream_t st) {
 #endif
     constexpr int TH = SIFT_SEED_TH;
     using G = BlurGeom<R, TH>;
-    dim3 grid((L.W + G::TW - 1) / G::TW, (L.H + G::TH - 1) / G::TH, L.n_img);
+    const int tiles_y = (L.H + G::TH - 1) / G::TH;
+    const int ty0 = L.y1 > L.y0 ? L.y0 / G::TH : 0;
+    const int ty1 = L.y1 > L.y0 ? std::min(tiles_y, (L.y1 + G::TH - 1) / G::TH) : tiles_y;
+    if (ty1 <= ty0) return;
+    dim3 grid((L.W + G::TW - 1) / G::TW, ty1 - ty0, L.n_img);
     hipLaunchKernelGGL((k_seed<R, TH>), grid, dim3(256), 0, st, L.frames, L.frame_pitch, L.row_stride, L.sh, L.sw, L.tab,
-                       L.dst, L.dst_img_stride, L.W, L.H, L.pitch, L.taps);
+                       L.dst, L.dst_img_stride, L.W, L.H, L.pitch, L.taps, ty0);
 }
 
 template <int R>

@@ -49,6 +49,7 @@ struct BlurLaunch {
     int pitch_n, wn, hn;
     int W, H, pitch;
     int n_img;
+    int y0, y1;  // output rows [y0, y1) only (rounded out to tiles); y1 <= y0: all rows
     BlurTaps taps;
     int profile;  // kProfileOpenCV | kProfileImageproc
 };
@@ -64,6 +65,7 @@ struct SeedLaunch {
     size_t dst_img_stride;
     int W, H, pitch;  // seed (2x) geometry
     int n_img;
+    int y0, y1;  // output rows [y0, y1) only (rounded out to tiles); y1 <= y0: all rows
     BlurTaps taps;
 };
 
@@ -134,6 +136,12 @@ struct RefineLaunch {
     const uint64_t* cand;
     const uint32_t* n_cand;  // device count (may exceed cand_cap: overflow, clamped)
     uint32_t cand_cap;
+    // row bands with a restricted pyramid (null flag: no check): octave o's
+    // Gaussians are exact on rows [H_o*r/n - 1 - margin, H_o*(r+1)/n + 1 + margin)
+    // (clipped); the flag is set when a refinement reads outside them or an
+    // accepted keypoint's patch (+-patch rows) leaves them
+    uint32_t* band_flag;
+    int band_r, band_n, band_margin, band_patch;
     const float* const* gauss;   // device array [n_octaves] of octave G_0 bases (D formed from G)
     const size_t* g_img_stride;  // device array [n_octaves]
     const int* ow;

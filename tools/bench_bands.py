@@ -3,7 +3,9 @@
 For n in {1, 2, 4, 8}: time each band's sift() of the same device-resident
 frame on this one GPU (results fetched to host, as a caller needs them).  In
 an n-GPU split every rank runs one band concurrently, so the slowest band is
-the per-rank compute latency; the all-gather of the bands' results (~156 B
+the per-rank compute latency (each band computes only its rows of the
+pyramid plus margins; `reruns` counts calls that fell back to the whole
+pyramid); the all-gather of the bands' results (~156 B
 per keypoint) comes on top.  Frames are the tiled synthetic frames of
 tests/test_gpu_large.py (8192 x 8192 by default, configs #5).
 
@@ -49,6 +51,7 @@ def main():
     run(0, 1)  # warm-up: plan + arenas
     out = {"frame": f"{W}x{H}", "reps": a.reps, "bands": {}}
     for n in (1, 2, 4, 8):
+        ctx.reset_stats()
         per = []
         for b in range(n):
             ts, nk = [], 0
@@ -57,7 +60,8 @@ def main():
                 ts.append(dt)
             per.append((float(np.median(ts)) * 1e3, nk))
         out["bands"][n] = {"band_ms": [round(t, 3) for t, _ in per], "band_keypoints": [k for _, k in per],
-                           "max_band_ms": round(max(t for t, _ in per), 3)}
+                           "max_band_ms": round(max(t for t, _ in per), 3),
+                           "reruns": int(ctx.stats()["band_reruns"]), "calls": n * a.reps}
         print(n, out["bands"][n], flush=True)
     ctx.set_row_band(0, 1)
     print(json.dumps(out))
