@@ -114,10 +114,12 @@ int sift_mi_set_pipeline_lanes(sift_mi_ctx* ctx, int lanes);
 
 /* Row band of the keypoint stages, for splitting ONE large frame across
  * contexts / GPUs (replaces nothing in the reference,
- * whose sift() is whole-frame: src/lib.rs:71-81).  With n_bands > 1 the
- * context still builds the whole frame's pyramid, but detection (and so
- * refinement, orientation and descriptors) covers only octave rows
- * [H_o*band/n_bands, H_o*(band+1)/n_bands) of each octave o.  The bands
+ * whose sift() is whole-frame: src/lib.rs:71-81).  With n_bands > 1,
+ * detection (and so refinement, orientation and descriptors) covers only
+ * octave rows [H_o*band/n_bands, H_o*(band+1)/n_bands) of each octave o,
+ * and the pyramid is computed only on those rows plus the halos they read
+ * (a refinement reaching beyond them re-runs the call on the whole pyramid:
+ * sift_mi_stats.band_reruns; OpenCV profile, else the whole pyramid).  The bands
  * partition every octave's candidate rows, so the union of the n_bands
  * results, ordered by emission key (sift_mi_fetch_keys), is exactly the
  * whole-frame result.  features_limit is rejected (SIFT_MI_EINVAL) while
