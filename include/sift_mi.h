@@ -84,8 +84,9 @@ int sift_mi_extract(sift_mi_ctx* ctx, const uint8_t* pixels, uint32_t width, uin
 int sift_mi_fetch(sift_mi_ctx* ctx, sift_mi_keypoint* kps, uint8_t* desc, size_t cap);
 
 /* Emission keys of the last result, for parity checks: bits
- * [40,64) image, [36,40) octave, [34,36) initial scale, [20,34) initial y,
- * [6,20) initial x, [0,6) orientation peak -- the reference's emission order
+ * [42,64) image, [38,42) octave, [36,38) initial scale, [21,36) initial y,
+ * [6,21) initial x, [0,6) orientation peak (x/y in octave pixels; octave 0
+ * is the 2x seed, so frames up to 16384 px fit the 15-bit fields) -- the reference's emission order
  * (src/lib.rs:281-294, :324-332, :397-431). */
 int sift_mi_fetch_keys(sift_mi_ctx* ctx, uint64_t* keys, size_t cap);
 
@@ -213,6 +214,7 @@ typedef struct {
     uint64_t extrema;
     uint64_t keypoints;
     uint64_t band_reruns;  /* row-band calls re-run on the whole-frame pyramid (sift_mi_set_row_band) */
+    uint64_t stage_reruns; /* chunks re-run because a stage count exceeded its buffer bound */
 } sift_mi_stats;
 int sift_mi_get_stats(sift_mi_ctx* ctx, sift_mi_stats* out);
 int sift_mi_reset_stats(sift_mi_ctx* ctx);

@@ -46,7 +46,8 @@ class Stats(ctypes.Structure):
                 ("descriptor_ms", ctypes.c_double), ("total_ms", ctypes.c_double),
                 ("pyramid_bytes", ctypes.c_uint64), ("pyramid_launches", ctypes.c_uint64),
                 ("frames", ctypes.c_uint64), ("extrema", ctypes.c_uint64),
-                ("keypoints", ctypes.c_uint64), ("band_reruns", ctypes.c_uint64)]
+                ("keypoints", ctypes.c_uint64), ("band_reruns", ctypes.c_uint64),
+                ("stage_reruns", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}

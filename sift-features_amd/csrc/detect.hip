@@ -263,8 +263,8 @@ __device__ __forceinline__ bool refine_one(const RefineLaunch& L, uint64_t key, 
     const int b = (int)(key >> kKeyImgShift);
     const int o = (int)((key >> kKeyOctShift) & 15);
     const int s_in = (int)((key >> kKeyScaleShift) & 3);
-    const int y = (int)((key >> kKeyYShift) & 0x3fff);
-    const int x = (int)((key >> kKeyXShift) & 0x3fff);
+    const int y = (int)((key >> kKeyYShift) & kKeyCoordMask);
+    const int x = (int)((key >> kKeyXShift) & kKeyCoordMask);
     const int W = L.ow[o], H = L.oh[o], pitch = L.opitch[o];
     const DogView dv{as_global(L.gauss[o]) + (size_t)(b - L.img_base) * L.g_img_stride[o], (size_t)pitch * H};
     int sc = s_in, xi = x, yi = y;

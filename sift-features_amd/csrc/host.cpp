@@ -534,7 +534,11 @@ int ensure_lane(sift_mi_ctx* c, int lane) {
 int ensure_plan(sift_mi_ctx* c, uint32_t w, uint32_t h, uint32_t chunk) {
     Plan& p = c->plan;
     if (p.w == w && p.h == h && p.chunk >= chunk && p.arena[0].p && p.profile == (int)c->profile) return 0;
-    if (!(p.w == w && p.h == h && p.profile == (int)c->profile)) p.release();
+    if (!(p.w == w && p.h == h && p.profile == (int)c->profile)) {
+        p.release();
+        // per-frame stage high-water marks belong to a frame size
+        c->pf_cand = c->pf_ext = c->pf_kp = 0;
+    }
     p.profile = (int)c->profile;
     const bool ip = c->profile == SIFT_MI_PROFILE_IMAGEPROC;
     p.w = w;
@@ -711,7 +715,22 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
     }
     if (launch_seed(p.seed_r, S, st)) return fail(SIFT_MI_EUNSUPPORTED, "seed blur radius");
     uint64_t launches = 1;
-    const uint64_t bytes = p.algo_bytes_per_frame;  // per frame, SURVEY.md 8(d)
+    uint64_t bytes = p.algo_bytes_per_frame;  // per frame, SURVEY.md 8(d)
+    if (c->band_restricted) {
+        // the same yardstick over the rows this band computes: 4 B per pixel
+        // of each of its 6 Gaussian rows and 5 DoG rows, plus the input rows
+        // the seed reads
+        double b = (double)p.w * std::min<int>((int)p.h, (S.y1 - S.y0 + 1) / 2 + 2);
+        for (int o = 0; o < p.n_oct; o++) {
+            double rows = 0;
+            for (int s = 0; s < kImagesPerOctave; s++) {
+                const int r = std::max(0, rhi[(size_t)o * kImagesPerOctave + s] - rlo[(size_t)o * kImagesPerOctave + s]);
+                rows += (s < kDogPerOctave ? 2.0 : 1.0) * r;
+            }
+            b += 4.0 * p.ow[o] * rows;
+        }
+        bytes = (uint64_t)b;
+    }
     // fused five-blur octave kernel (octave.hip) where it applies: OpenCV
     // profile with its constant radii, octaves wide enough for one-reflection
     // column borders; the per-blur kernels otherwise
@@ -813,7 +832,18 @@ Bounds chunk_bounds(sift_mi_ctx* c, uint32_t m) {
     };
     Bounds B;
     // first chunk: one candidate per 256 octave pixels; later chunks: 1.3x
-    // the per-frame high-water mark
+    // the per-frame high-water mark.  SIFT_MI_BOUND_SHRINK=k (test knob)
+    // divides the first-chunk estimates by k and drops the slack, so every
+    // chunk enqueued before a high-water mark exists overflows and re-runs.
+    double shrink = 1.0;
+    if (const char* e = getenv("SIFT_MI_BOUND_SHRINK")) shrink = std::max(1.0, atof(e));
+    if (shrink > 1.0 && c->pf_cand == 0) {
+        auto tiny = [&](double per) { return (uint32_t)std::max(1.0, std::ceil(per / shrink * m)); };
+        B.bc = tiny(sum_p / 256.0);
+        B.be = std::min(B.bc, tiny(sum_p / 512.0));
+        B.bk = tiny(sum_p / 384.0);
+        return B;
+    }
     B.bc = est(c->pf_cand, c->pf_cand > 0 ? 64.0 : sum_p / 256.0);
     B.be = est(c->pf_ext, c->pf_ext > 0 ? 64.0 : sum_p / 512.0);
     B.bk = est(c->pf_kp, c->pf_kp > 0 ? 64.0 : sum_p / 384.0);
@@ -1033,7 +1063,10 @@ int finalize_chunk(sift_mi_ctx* c, int si, size_t* offsets) {
     c->pf_cand = std::max(c->pf_cand, h[0] / fm);
     c->pf_ext = std::max(c->pf_ext, h[1] / fm);
     c->pf_kp = std::max(c->pf_kp, h[2] / fm);
-    if (h[0] > S.bc || h[1] > S.be || h[2] > S.bk) return 1;
+    if (h[0] > S.bc || h[1] > S.be || h[2] > S.bk) {
+        c->stats.stage_reruns++;
+        return 1;
+    }
     const uint32_t n_out = h[3];
     accumulate_times(c, S);
     const size_t base = c->n_result;
@@ -1114,7 +1147,7 @@ int run_chunk_sync(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, 
 int check_frame_args(uint32_t w, uint32_t h, size_t stride) {
     if (w < 1 || h < 1) return fail(SIFT_MI_EINVAL, "empty image");
     if (stride < w) return fail(SIFT_MI_EINVAL, "row_stride < width");
-    if (w > 8192 * 2 || h > 8192 * 2) return fail(SIFT_MI_EINVAL, "image larger than 16384 px (key field)");
+    if (w > kMaxFrameSide || h > kMaxFrameSide) return fail(SIFT_MI_EINVAL, "image larger than 16384 px (key field)");
     return 0;
 }
 
@@ -1126,6 +1159,8 @@ int check_frame_args(uint32_t w, uint32_t h, size_t stride) {
 int extract_device(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, uint32_t n, uint32_t w, uint32_t h,
                    size_t stride, int64_t limit, size_t* offsets) {
     CHK(check_frame_args(w, h, stride));
+    if (n > (1u << (64 - kKeyImgShift))) return fail(SIFT_MI_EINVAL, "more than 2^22 frames in one call (key field)");
+    const sift_mi_stats stats0 = c->stats;  // restored if a banded pass is redone on the whole pyramid
     if (c->band_n > 1 && limit >= 0)
         return fail(SIFT_MI_EINVAL, "features_limit ranks a whole frame's keypoints: apply it after merging row bands");
     const uint32_t chunk =
@@ -1181,7 +1216,11 @@ int extract_device(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, 
         uint32_t flag = 0;
         HIPCHK(hipMemcpy(&flag, c->band_flag.p, sizeof(flag), hipMemcpyDeviceToHost));
         if (flag) {
-            c->stats.band_reruns++;
+            // the first pass's work is discarded: report the re-run alone
+            const uint64_t reruns = c->stats.band_reruns + 1, stage_reruns = c->stats.stage_reruns;
+            c->stats = stats0;
+            c->stats.band_reruns = reruns;
+            c->stats.stage_reruns = stage_reruns;
             c->band_whole = true;
             const int rc = extract_device(c, d_frames, frame_pitch, n, w, h, stride, limit, offsets);
             c->band_whole = false;

@@ -264,6 +264,8 @@ int parse(const uint8_t* d, size_t n, Header& H, std::string& err) {
             H.restart = (seg[0] << 8) | seg[1];
         } else if (m == 0xDA) {  // SOS
             if (!frame) return err = "JPEG: SOS before SOF", SIFT_MI_EINVAL;
+            // T.81 B.2.3: Ns, Ns x (Cs, Td/Ta), Ss, Se, Ah/Al
+            if (sl < 1 || sl < 1 + 2 * (size_t)seg[0] + 3) return err = "JPEG: truncated SOS", SIFT_MI_EINVAL;
             const int ns = seg[0];
             if (ns != H.nc) return err = "JPEG: one interleaved scan only", SIFT_MI_EUNSUPPORTED;
             for (int k = 0; k < ns; k++) {

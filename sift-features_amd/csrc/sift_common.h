@@ -33,12 +33,16 @@ constexpr float kOriPeakRatio = 0.8f;                // src/lib.rs:297
 constexpr int kMaxInterpSteps = 5;                   // src/lib.rs:516
 constexpr int kMaxBlurRadius = 31;                   // taps <= 63 per pass
 
-// Emission key layout (see include/sift_mi.h, sift_mi_fetch_keys).
-constexpr int kKeyImgShift = 40;
-constexpr int kKeyOctShift = 36;
-constexpr int kKeyScaleShift = 34;
-constexpr int kKeyYShift = 20;
-constexpr int kKeyXShift = 6;
+// Emission key layout (see include/sift_mi.h, sift_mi_fetch_keys).  x_init
+// and y_init are octave coordinates; octave 0 is the 2x seed, so a 16384-px
+// frame needs 15 bits each (coordinates < 32768).
+constexpr int kKeyImgShift = 42;    // [42,64): frame within the call (4M frames)
+constexpr int kKeyOctShift = 38;    // [38,42)
+constexpr int kKeyScaleShift = 36;  // [36,38)
+constexpr int kKeyYShift = 21;      // [21,36)
+constexpr int kKeyXShift = 6;       // [6,21)
+constexpr uint32_t kKeyCoordMask = 0x7fff;
+constexpr uint32_t kMaxFrameSide = 16384;  // 2*16384 - 5 < 2^15
 
 __host__ __device__ inline uint64_t make_key(uint32_t img, uint32_t o, uint32_t s, uint32_t y, uint32_t x) {
     return ((uint64_t)img << kKeyImgShift) | ((uint64_t)o << kKeyOctShift) | ((uint64_t)s << kKeyScaleShift) |

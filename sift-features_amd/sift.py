@@ -462,5 +462,5 @@ def key_fields(keys):
     """Decode emission keys (include/sift_mi.h sift_mi_fetch_keys)."""
     k = np.asarray(keys, dtype=np.uint64)
     f = lambda s, b: ((k >> np.uint64(s)) & np.uint64((1 << b) - 1)).astype(np.int64)
-    return {"frame": f(40, 24), "octave": f(36, 4), "s_init": f(34, 2), "y_init": f(20, 14),
-            "x_init": f(6, 14), "peak": f(0, 6)}
+    return {"frame": f(42, 22), "octave": f(38, 4), "s_init": f(36, 2), "y_init": f(21, 15),
+            "x_init": f(6, 15), "peak": f(0, 6)}

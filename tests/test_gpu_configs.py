@@ -1,0 +1,129 @@
+"""The BASELINE.json configs on the HIP path, checked against the oracle.
+
+* config #2: one 1920x1080 frame, `sift()` vs the oracle directly;
+* config #3: 256 x 640x480 frames through the device-resident batch path
+  (`sift_batch_device(..., fetch=False)`: 4 chunks of 64 over both pipeline
+  lanes), 6 frames spread over every chunk (the last included) vs the
+  oracle, every frame vs per-frame `sift()`;
+* config #4, one GPU's shard: bench.py's exact call (128 x 1920x1080, auto
+  chunks, results kept in HBM), 2 frames vs the oracle, every frame vs
+  per-frame `sift()`;
+* the stage-bound overflow re-run (host.cpp finalize_chunk rc == 1): with
+  SIFT_MI_BOUND_SHRINK every chunk enqueued before a high-water mark exists
+  overflows; the re-run chunks must equal per-frame results.
+Configs #1 (bird_small) and #5 (8192^2) are covered by test_gpu_parity /
+test_oracle_golden and test_gpu_large.
+"""
+import ctypes
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+
+def _device_results(ctx, n):
+    kp_ptr, desc_ptr, m = ctx.device_results()
+    assert m == n
+    kp = np.empty((n, 5), np.float32)
+    desc = np.empty((n, 128), np.uint8)
+    hip = ctypes.CDLL("libamdhip64.so")
+    hip.hipMemcpy.argtypes = [ctypes.c_void_p, ctypes.c_void_p, ctypes.c_size_t, ctypes.c_int]
+    if n:
+        assert hip.hipMemcpy(kp.ctypes.data, kp_ptr, kp.nbytes, 2) == 0  # hipMemcpyDeviceToHost
+        assert hip.hipMemcpy(desc.ctypes.data, desc_ptr, desc.nbytes, 2) == 0
+    return kp, desc
+
+
+def _parity_rows(kp, desc, kp_o, desc_o):
+    """assert_parity on (keypoints, descriptors) rows without keys."""
+    from test_gpu_parity import TOL_ANGLE, TOL_RESP, TOL_XY
+    assert len(kp) == len(kp_o), (len(kp), len(kp_o))
+    d = np.abs(kp - kp_o)
+    assert d[:, :3].max() <= TOL_XY, d.max(0)
+    dang = np.abs(((kp[:, 3] - kp_o[:, 3]) + 180.0) % 360.0 - 180.0)
+    assert dang.max() <= TOL_ANGLE
+    assert d[:, 4].max() <= TOL_RESP
+    dd = np.abs(desc.astype(np.int32) - desc_o.astype(np.int32))
+    assert dd.max() <= 1 and (dd == 0).mean() >= 0.99
+
+
+def _device_batch(pkg, frames_t, ctx=None):
+    c = ctx or pkg.Context(0, pkg.OpenCVProcessing)
+    n, h, w = frames_t.shape
+    offs, res = c.sift_batch_device(frames_t.data_ptr(), n, w, h, frames_t.stride(1), frames_t.stride(0),
+                                    fetch=False)
+    assert res is None
+    kp, desc = _device_results(c, int(offs[-1]))
+    return c, offs, kp, desc
+
+
+def test_config2_single_1080p(pkg, ctx, oracle):
+    import synth
+    from test_gpu_parity import assert_parity
+    img = synth.frame(1920, 1080, 0)
+    kp_o, desc_o, ext_o = oracle.sift(img, internal=True)
+    res = ctx.sift(img)
+    assert len(res) > 5000
+    assert_parity(pkg, res, kp_o, desc_o, ext_o)
+
+
+def test_config3_vga_256_device(pkg, ctx, oracle):
+    import synth
+    import torch
+    t = synth.frames_torch(256, 640, 480, seed0=0, device="cuda")
+    torch.cuda.synchronize()
+    host = t.cpu().numpy()
+    c, offs, kp, desc = _device_batch(pkg, t)
+    st = c.stats()
+    assert st["frames"] == 256
+    c.close()
+    assert np.all(np.diff(offs) > 0)
+    for i in (0, 63, 64, 130, 200, 255):  # every 64-frame chunk, both lanes, the last frame
+        a, b = int(offs[i]), int(offs[i + 1])
+        kp_o, desc_o = oracle.sift(host[i])
+        _parity_rows(kp[a:b], desc[a:b], kp_o, desc_o)
+    for i in range(256):
+        a, b = int(offs[i]), int(offs[i + 1])
+        r = ctx.sift(host[i])
+        assert np.array_equal(kp[a:b].view(np.uint32), r.keypoints_array.view(np.uint32)), i
+        assert np.array_equal(desc[a:b], r.descriptors), i
+
+
+def test_config4_bench_shard_1080p(pkg, ctx, oracle):
+    """bench.py's step: 128 device-resident 1080p frames, auto chunks (two
+    64-frame chunks, one per lane), results kept in the device arena."""
+    import synth
+    import torch
+    t = synth.frames_torch(128, 1920, 1080, seed0=0, device="cuda")
+    torch.cuda.synchronize()
+    c, offs, kp, desc = _device_batch(pkg, t)
+    c.close()
+    host = t.cpu().numpy()
+    del t
+    for i in (5, 127):
+        a, b = int(offs[i]), int(offs[i + 1])
+        kp_o, desc_o = oracle.sift(host[i])
+        _parity_rows(kp[a:b], desc[a:b], kp_o, desc_o)
+    for i in range(128):
+        a, b = int(offs[i]), int(offs[i + 1])
+        r = ctx.sift(host[i])
+        assert np.array_equal(kp[a:b].view(np.uint32), r.keypoints_array.view(np.uint32)), i
+        assert np.array_equal(desc[a:b], r.descriptors), i
+
+
+@pytest.mark.parametrize("lanes", [1, 2])
+def test_stage_bound_overflow_rerun(pkg, ctx, monkeypatch, lanes):
+    import synth
+    fr = synth.frames(7, 320, 240, seed0=40)
+    ref = [ctx.sift(f) for f in fr]
+    monkeypatch.setenv("SIFT_MI_BOUND_SHRINK", "1000")
+    c = pkg.Context(0, pkg.OpenCVProcessing)  # no high-water marks yet
+    c.set_chunk(2)
+    c.set_pipeline_lanes(lanes)
+    got = c.sift_batch(fr)
+    st = c.stats()
+    c.close()
+    assert st["stage_reruns"] >= (2 if lanes == 2 else 1), st
+    assert st["frames"] == 7 and st["keypoints"] == sum(len(r) for r in ref)
+    assert all(a == b for a, b in zip(got, ref))

@@ -8,6 +8,10 @@
   oracle, so size-independent properties: determinism, emission order
   (keys strictly increasing), descriptor range, the single-frame and the
   batch entry points agreeing, and octave coverage.
+* Over 8192 px on one side (the 2x seed is then wider than 16384, which needs
+  the 15-bit x/y fields of the emission key): narrow strips 8200 x 48,
+  48 x 8400 and 16384 x 24 against the oracle, plus a banded merge of the
+  tall one.
 * Above the 16384-pixel key field: rejected with an error, no launch.
 Frames are tiled from a 2048 x 2048 synthetic frame (synth.frame generates
 the blob field as one dense product, too large to form at 8192^2) plus
@@ -67,6 +71,38 @@ def test_max_8192_properties(pkg, ctx):
     # the batch entry point gives the same result for the same frame
     (c,) = ctx.sift_batch(img[None])
     assert c == a
+
+
+@pytest.mark.parametrize("w,h", [(8200, 48), (48, 8400), (16384, 24)])
+def test_oversize_side_parity(pkg, ctx, oracle, w, h):
+    """Octave-0 coordinates reach 2*side - 6 > 16383: the key's x/y fields
+    must hold them (src/lib.rs:131-143 has no size limit)."""
+    import synth
+    from test_gpu_parity import assert_parity
+    img = synth.frame(w, h, 5 + w % 7)
+    kp_o, desc_o, ext_o = oracle.sift(img, internal=True)
+    res = ctx.sift(img)
+    assert len(res) > 100
+    assert_parity(pkg, res, kp_o, desc_o, ext_o)
+    f = pkg.key_fields(res.keys)
+    big = f["x_init"] if w > h else f["y_init"]
+    assert big.max() > 16383  # the case a 14-bit field could not hold
+    assert _emission_sorted(res.keys)
+
+
+def test_oversize_side_bands(pkg, ctx):
+    import shard
+    import synth
+    img = synth.frame(48, 8400, 6)
+    whole = ctx.sift(img)
+    parts = []
+    for r in range(3):
+        b = shard.sift_row_bands(ctx, img, band=r, n_bands=3)
+        parts.append((b.keypoints_array, b.descriptors, b.keys))
+    k, d, y = shard.merge_bands(parts)
+    assert np.array_equal(y, whole.keys)
+    assert np.array_equal(k.view(np.uint32), whole.keypoints_array.view(np.uint32))
+    assert np.array_equal(d, whole.descriptors)
 
 
 def test_too_large_rejected(pkg, ctx):

@@ -8,8 +8,10 @@ Parity contract:
     (in practice bit-identical: same op order, -ffp-contract=off; the only
     possible deviations are 1-ulp differences of f64-evaluated exp/pow vs glibc);
   * descriptors: max |d| <= 1 per u8 component and >= 99 % of bytes identical
-    (the GPU accumulates the 6x6x8 histogram with LDS float atomics, so bin
-    sums can differ from the sequential CPU order in the last f32 bit).
+    (the default GPU mode sums the 6x6x8 histogram in lane-private LDS
+    slices and uses hardware sqrt/exp and a polynomial atan2, so bin sums can
+    differ from the sequential CPU order in the last f32 bits); the exact
+    descriptor mode is byte-identical.
 """
 import numpy as np
 import pytest
@@ -144,16 +146,25 @@ def test_module_level_api(pkg, oracle):
 
 def test_golden_snapshots_gpu(pkg, ctx, oracle):
     """GPU output vs the reference's snapshots: the oracle's agreement
-    (exact counts, >= 95 % identical positions; tests/test_oracle_golden.py)."""
-    from test_oracle_golden import golden_agreement
+    (tests/test_oracle_golden.py: exact counts, >= 99 % of rows within 1e-3 px,
+    descriptor components within +-1).  The exact descriptor mode reproduces
+    the oracle's identical-row fraction; the default mode adds its own +-1."""
+    from test_oracle_golden import MIN_DESC_EQUAL, MIN_POS_EXACT, MIN_ROWS_CLOSE, golden_agreement
+    ex = pkg.Context(0)
+    ex.set_exact_descriptors(True)
     for name, count in [("tree_small", 1270), ("bird_small", 225)]:
         g = load_golden(name)
-        res = ctx.sift(g["image"])
-        assert len(res) == count
-        order = pkg.stable_sort_xy_size(res.keypoints_array)
-        pos_exact, rows_close, desc_equal = golden_agreement(res.keypoints_array[order], res.descriptors[order], g)
-        assert pos_exact >= 0.95 and rows_close >= 0.97, (pos_exact, rows_close)
-        assert desc_equal >= 0.95, desc_equal  # default (fast) descriptors: +-1 components
+        # default mode: its own +-1 can stack on the oracle's +-1 vs the snapshot
+        for c, min_desc, max_d in ((ctx, 0.95, 2), (ex, MIN_DESC_EQUAL, 1)):
+            res = c.sift(g["image"])
+            assert len(res) == count
+            order = pkg.stable_sort_xy_size(res.keypoints_array)
+            pos_exact, rows_close, desc_equal, desc_maxd = golden_agreement(res.keypoints_array[order],
+                                                                             res.descriptors[order], g)
+            assert pos_exact >= MIN_POS_EXACT and rows_close >= MIN_ROWS_CLOSE, (name, pos_exact, rows_close)
+            assert desc_equal >= min_desc, (name, desc_equal)
+            assert desc_maxd <= max_d, (name, desc_maxd)
+    ex.close()
 
 
 @pytest.mark.parametrize("name", ["bird_small", "tree_small", "synth_640x480", "synth_97x61"])

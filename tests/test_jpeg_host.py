@@ -30,3 +30,16 @@ def test_dims_pil_and_rejections(pkg):
         pkg.jpeg_dims(p.getvalue())
     with pytest.raises(pkg.SiftMiError):
         pkg.jpeg_dims(b"\x89PNG\r\n\x1a\n" + b"\0" * 32)
+
+
+def test_truncated_sos_rejected(pkg):
+    """An SOS segment shorter than its component list (T.81 B.2.3) at the end
+    of the buffer is rejected, not read past."""
+    from PIL import Image
+    b = io.BytesIO()
+    Image.fromarray(np.zeros((16, 16, 3), np.uint8)).save(b, "JPEG")
+    data = b.getvalue()
+    p = data.index(b"\xff\xda")
+    assert pkg.jpeg_dims(data) == (16, 16)
+    with pytest.raises(pkg.SiftMiError):
+        pkg.jpeg_dims(data[:p] + b"\xff\xda\x00\x03\x03")  # Ns = 3, no component specs

@@ -7,7 +7,8 @@ descriptors (src/snapshots/*.snap, converted by tests/golden/make_golden.py).
 The committed u8 inputs are decoded with the reconstruction arithmetic of the
 reference's JPEG decoder (zune-jpeg, via image 0.25.2; tests/golden/
 jpeg_decode.py).  With them the oracle reproduces the snapshots' keypoint
-counts exactly and >= 96 % of the keypoints at identical positions; the
+counts exactly, >= 99 % of the keypoints within 1e-3 px (>= 96 % at
+identical positions) and descriptor components within +-1; the
 remaining keypoints differ at the 1e-4..1e-2 px level, from ULP-level
 arithmetic differences of the OpenCV build that produced the snapshots
 (DESIGN.md, "Oracle").
@@ -44,7 +45,17 @@ def golden_agreement(kp, desc, g):
     pos_exact = float((d < 1e-4).mean())
     rows_close = float((np.abs(kp[:, :2] - gk[:, :2]).max(1) < 1e-3).mean())
     desc_equal = float(np.all(desc == gd, axis=1).mean())
-    return pos_exact, rows_close, desc_equal
+    desc_maxd = int(np.abs(desc.astype(np.int32) - gd.astype(np.int32)).max()) if len(gd) else 0
+    return pos_exact, rows_close, desc_equal, desc_maxd
+
+
+# exact counts, >= 99 % of keypoints within 1e-3 px.  Measured
+# (oracle): tree_small 98.98 % / 99.61 % / 98.35 %, bird_small 96.44 % /
+# 100 % / 97.78 % (identical positions / rows within 1e-3 px / identical
+# descriptor rows), descriptor components within +-1 everywhere.
+MIN_POS_EXACT = 0.96
+MIN_ROWS_CLOSE = 0.99
+MIN_DESC_EQUAL = 0.975
 
 
 @pytest.mark.parametrize("name", ["tree_small", "bird_small"])
@@ -52,10 +63,11 @@ def test_oracle_matches_golden(oracle, name):
     g = load_golden(name)
     kp, desc = oracle.sift(g["image"])
     order = oracle.stable_sort_xy_size(kp)
-    pos_exact, rows_close, desc_equal = golden_agreement(kp[order], desc[order], g)
-    assert pos_exact >= 0.95, pos_exact
-    assert rows_close >= 0.97, rows_close
-    assert desc_equal >= 0.97, desc_equal
+    pos_exact, rows_close, desc_equal, desc_maxd = golden_agreement(kp[order], desc[order], g)
+    assert pos_exact >= MIN_POS_EXACT, pos_exact
+    assert rows_close >= MIN_ROWS_CLOSE, rows_close
+    assert desc_equal >= MIN_DESC_EQUAL, desc_equal
+    assert desc_maxd <= 1, desc_maxd
 
 
 @pytest.mark.skipif(not os.path.isdir("/root/reference/images"), reason="reference images only in the build container")

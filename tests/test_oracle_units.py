@@ -135,7 +135,7 @@ def test_result_buffers_grow(pkg):
 
 def test_key_fields_roundtrip(pkg):
     f, o, s, y, x, p = 37, 9, 2, 12345, 16000, 5
-    key = (f << 40) | (o << 36) | (s << 34) | (y << 20) | (x << 6) | p
+    key = (f << 42) | (o << 38) | (s << 36) | (y << 21) | (x << 6) | p
     d = pkg.key_fields(np.array([key], np.uint64))
     assert (d["frame"][0], d["octave"][0], d["s_init"][0], d["y_init"][0], d["x_init"][0], d["peak"][0]) == \
         (f, o, s, y, x, p)

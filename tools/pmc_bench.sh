@@ -5,12 +5,12 @@
 cd "$GRAFT_REPO_ROOT" || exit 2
 RE=${1:-k_detect}
 FRAMES=${2:-32}
-OUT=gpurun_out/pmcb
+OUT=${PMC_OUT:-gpurun_out/pmcb}
 rm -rf $OUT; mkdir -p $OUT
 export TMPDIR=/tmp
 CMD="python3 bench.py --steps 1 --warmup 0 --frames $FRAMES --no-cpu-baseline --no-latency"
 i=0
-for grp in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU" \
+for grp in "SQ_WAVES SQ_BUSY_CYCLES SQ_WAVE_CYCLES SQ_WAIT_ANY SQ_WAIT_INST_ANY SQ_ACTIVE_INST_ANY SQ_ACTIVE_INST_VALU SQ_INSTS_VALU GRBM_GUI_ACTIVE" \
            "SQ_INSTS_LDS SQ_LDS_BANK_CONFLICT SQ_LDS_IDX_ACTIVE SQ_WAIT_INST_LDS SQ_INSTS_SALU SQ_INSTS_VMEM_RD SQ_INSTS_VMEM_WR SQ_ACTIVE_INST_LDS" \
            "FETCH_SIZE" "WRITE_SIZE"; do
   i=$((i+1))
