@@ -27,6 +27,10 @@
 #include "sift_common.h"
 #include "sift_kernels.h"
 
+#include <algorithm>
+#include <cstdlib>
+#include <cstring>
+
 namespace siftmi {
 
 // ---------------------------------------------------------------------------
@@ -266,6 +270,308 @@ __global__ __launch_bounds__(256) void k_blur(const float* __restrict__ src, siz
     blur_tile_compute<R, TH, P>(tin, th, taps, x0, y0, W, H, pitch, dst ? dst + b * dst_img_stride : nullptr,
                              dog ? dog + b * dog_img_stride : nullptr, nxt ? nxt + b * nxt_img_stride : nullptr,
                              pitch_n, wn, hn);
+}
+
+// ---------------------------------------------------------------------------
+// k_blur_strip: the same blur G_{s-1} -> G_s (same arithmetic as k_blur),
+// streamed down a column strip instead of one tile per workgroup.
+//
+// A workgroup owns 128 output columns (64 lanes x a column pair) of a row
+// segment [ys, ye) and walks down it in chunks of S = 32 rows.  Chunk c holds
+// the row-pass output of window rows [ys - R + cS, ys - R + (c+1)S); the
+// column pass for output rows [ys + kS, ys + (k+1)S) reads chunks k and k+1
+// (S >= 2R), so every row-pass row is computed once per segment instead of
+// (TH + 2R) / TH times per tile, and the global loads of chunk k+2 are in
+// flight (registers) while chunk k+1 is row-filtered and chunk k column-
+// filtered.  Two LDS slots of S x IWP floats hold the chunks; the row pass
+// runs in place (each row's 16 items are one wave's lanes, which read their
+// windows before any of them stores), so a slot is the loaded input and then
+// the row-pass output.
+//
+// Per step (4096 outputs): [barrier] store prefetched chunk k+1 -> slot
+// [(k+1)&1]; issue chunk k+2 loads; [barrier] row pass chunk k+1 in place;
+// [barrier] column pass k.  The column pass code is instantiated per wave
+// (rows w*8 .. w*8+7 of the step) so which slot each of its rows lives in is a
+// compile-time choice and every LDS read is one ds_read_b64 with an immediate
+// offset.
+// ---------------------------------------------------------------------------
+template <int R>
+struct StripGeom {
+    static constexpr int TW = 128;                    // output columns per strip
+    static constexpr int S = 32;                      // rows per chunk
+    static constexpr int NW = 4;                      // waves per workgroup
+    static constexpr int VB = S / NW;                 // column-pass rows per wave per step
+    static constexpr int QW = 8;                      // row-pass outputs per item
+    static constexpr int HWL = (R + 3) & ~3;
+    static constexpr int IWV = TW + 2 * HWL;          // loaded columns per row (multiple of 8)
+    static constexpr int IWP = IWV + 4;               // LDS row pitch: IWP / 4 odd
+    static constexpr int OFF = HWL - R;
+    static constexpr int NV = (HWL + R + QW + 3) / 4;  // float4 reads per row-pass item
+    static constexpr int C4 = IWV / 4;                // float4 per loaded row
+    static constexpr int NLOAD4 = S * C4;
+    static constexpr int LPT = (NLOAD4 + 64 * NW - 1) / (64 * NW);
+    static constexpr int SLOT = S * IWP;
+    static constexpr int LDS_FLOATS = 2 * SLOT;
+    // resident workgroups per CU that the LDS allows (<= 4): the register budget follows
+    static constexpr int MINB = 163840 / (4 * LDS_FLOATS) < 4 ? 163840 / (4 * LDS_FLOATS) : 4;
+    static_assert(2 * R <= S, "the column pass reads two chunks");
+    static_assert((IWP / 4) % 2 == 1, "row-pass lane groups: odd float4 pitch");
+    static_assert(4 * NV <= IWV - TW + QW, "row-pass reads stay inside the loaded row");
+    static_assert(S % 16 == 0 && TW / QW == 16, "row pass: a wave filters 4 rows x 16 items");
+};
+constexpr int kStripMaxR = 16;
+
+typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
+
+// Buffer resource over `bytes` bytes at p (wave-uniform inputs: the halves of
+// the pointer and the size go through readfirstlane so the descriptor lives
+// in SGPRs).  Loads / stores then take a 32-bit per-lane voffset and a
+// uniform soffset: no 64-bit address arithmetic per access.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, uint32_t bytes) {
+    const uint64_t a = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    void* q = (void*)(((uint64_t)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(q, 0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+
+// Single reflection (the strip kernel runs only when W, H > R, so every index
+// an output uses is in range after one reflection), then clamped: rows /
+// columns loaded past what any output uses stay inside the image.
+template <int P>
+__device__ __forceinline__ int strip_index(int p, int n) {
+    if (P == kProfileOpenCV) p = p < 0 ? -p : (p >= n ? 2 * n - 2 - p : p);
+    return p < 0 ? 0 : (p >= n ? n - 1 : p);
+}
+
+// Chunk rows [r0, r0 + S) of the source window into registers.  Interior
+// chunks (all rows and the strip's whole window inside the image) are one
+// 16-B buffer load per item with the row offset in soffset; border chunks
+// load element-wise through strip_index.
+template <int R, int P>
+__device__ __forceinline__ void strip_load(float4 (&pre)[StripGeom<R>::LPT], __amdgpu_buffer_rsrc_t rs,
+                                           const int (&voff)[StripGeom<R>::LPT], bool cols_in, int r0, int x0,
+                                           int W, int H, int pitch) {
+    using G = StripGeom<R>;
+    if (cols_in && r0 >= 0 && r0 + G::S <= H) {
+        const int so = r0 * pitch * 4;
+#pragma unroll
+        for (int j = 0; j < G::LPT; j++)
+            pre[j] = __builtin_bit_cast(float4, __builtin_amdgcn_raw_buffer_load_b128(rs, voff[j], so, 0));
+        return;
+    }
+#pragma unroll
+    for (int j = 0; j < G::LPT; j++) {
+        const int i = min((int)threadIdx.x + 64 * G::NW * j, G::NLOAD4 - 1);
+        const int ly = i / G::C4, gx = x0 - G::HWL + 4 * (i - ly * G::C4);
+        const int ro = strip_index<P>(r0 + ly, H) * pitch;
+        float e[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++)
+            e[q] = __builtin_bit_cast(
+                float, __builtin_amdgcn_raw_buffer_load_b32(rs, 4 * (ro + strip_index<P>(gx + q, W)), 0, 0));
+        pre[j] = make_float4(e[0], e[1], e[2], e[3]);
+    }
+}
+
+template <int R>
+__device__ __forceinline__ void strip_store(const float4 (&pre)[StripGeom<R>::LPT], float* slot) {
+    using G = StripGeom<R>;
+    const int tid = threadIdx.x;
+#pragma unroll
+    for (int j = 0; j < G::LPT; j++) {
+        const int i = tid + 64 * G::NW * j;
+        if (G::NLOAD4 % (64 * G::NW) == 0 || i < G::NLOAD4) {
+            const int ly = i / G::C4, c4 = i - ly * G::C4;
+            *reinterpret_cast<float4*>(slot + ly * G::IWP + 4 * c4) = pre[j];
+        }
+    }
+}
+
+// Row pass of one chunk, in place: item = (row, 8 consecutive outputs), an FMA
+// chain from the leftmost tap (OpenCV RowFilter) / unfused acc + p * k
+// (imageproc).  Lane -> (row, item) follows the ds_read_b128 lane groups: each
+// 16-lane group reads two adjacent rows x 8 items, whose float4 slots are the
+// even / odd slots of a bank row (IWP / 4 odd) -> conflict-free.
+template <int R, int P>
+__device__ __forceinline__ void strip_rowpass(float* slot, const BlurTaps& taps, int prow, int pq) {
+    using G = StripGeom<R>;
+#pragma unroll
+    for (int it = 0; it < G::S / 16; it++) {
+        const int ly = it * 16 + prow;
+        const lds_f4v* rp = (const lds_f4v*)(slot + ly * G::IWP + G::QW * pq);
+        float v[4 * G::NV];
+#pragma unroll
+        for (int j = 0; j < G::NV; j++) {
+            const f4v f = rp[j];
+            v[4 * j + 0] = f.x;
+            v[4 * j + 1] = f.y;
+            v[4 * j + 2] = f.z;
+            v[4 * j + 3] = f.w;
+        }
+        float acc[G::QW];
+#pragma unroll
+        for (int o = 0; o < G::QW; o++) acc[o] = v[G::OFF + o] * taps.k[R];
+#pragma unroll
+        for (int t = 1; t <= 2 * R; t++) {
+            const float kt = taps.k[t > R ? t - R : R - t];
+#pragma unroll
+            for (int o = 0; o < G::QW; o++)
+                acc[o] = P == kProfileOpenCV ? __builtin_fmaf(v[G::OFF + o + t], kt, acc[o])
+                                             : acc[o] + v[G::OFF + o + t] * kt;
+        }
+        // every lane of this row has its window in registers (in-order LDS)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        float* wp = slot + ly * G::IWP + G::QW * pq;
+        *reinterpret_cast<float4*>(wp) = make_float4(acc[0], acc[1], acc[2], acc[3]);
+        *reinterpret_cast<float4*>(wp + 4) = make_float4(acc[4], acc[5], acc[6], acc[7]);
+    }
+}
+
+// Column pass of wave WV for one step: output rows y0 = y + WV*VB .. + VB - 1
+// of the column pair x0 + 2*lane.  Logical chunk row L (chunk k starts at
+// output row y - R) is row L of slot a for L < S, row L - S of slot b
+// otherwise -- a compile-time choice per row.  OpenCV's SymmColumnFilter
+// (centre product, fma of pair sums) / imageproc's unfused chain.
+template <int R, int P, int WV, bool NXT>
+__device__ __forceinline__ void strip_colpass(const float* sa, const float* sb, const BlurTaps& taps, int lane,
+                                              int y, int ye, int x0, int W, int pitch, __amdgpu_buffer_rsrc_t rd,
+                                              __amdgpu_buffer_rsrc_t rn, int pitch_n, int wn, int hn) {
+    using G = StripGeom<R>;
+    constexpr int NR = G::VB + 2 * R;
+    f2v v[NR];
+#pragma unroll
+    for (int j = 0; j < NR; j++) {
+        const int L = WV * G::VB + j;
+        const float* rp = L < G::S ? sa + L * G::IWP : sb + (L - G::S) * G::IWP;
+        v[j] = *(const lds_f2v*)(rp + 2 * lane);
+    }
+    f2v out[G::VB];
+    const f2v k0 = {taps.k[0], taps.k[0]};
+#pragma unroll
+    for (int o = 0; o < G::VB; o++) {
+        f2v acc;
+        if constexpr (P == kProfileOpenCV) {
+            acc = v[o + R] * k0;
+#pragma unroll
+            for (int t = 1; t <= R; t++) {
+                const f2v kt = {taps.k[t], taps.k[t]};
+                acc = __builtin_elementwise_fma(v[o + R + t] + v[o + R - t], kt, acc);
+            }
+        } else {
+            const f2v kr = {taps.k[R], taps.k[R]};
+            acc = v[o] * kr;
+#pragma unroll
+            for (int t = 1; t <= 2 * R; t++) {
+                const float k = taps.k[t > R ? t - R : R - t];
+                const f2v kt = {k, k};
+                acc = acc + v[o + t] * kt;
+            }
+        }
+        out[o] = acc;
+    }
+    const int y0 = y + WV * G::VB;
+    const int nrow = min(G::VB, ye - y0);
+    const int gx = x0 + 2 * lane;
+    const bool cols_full = x0 + G::TW <= W;
+    const bool pair = gx + 1 < W;
+    int so = (y0 * pitch + x0) * 4;
+#pragma unroll
+    for (int o = 0; o < G::VB; o++) {
+        if (o >= nrow) break;
+        if (cols_full || pair) {
+            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, out[o]), rd, 8 * lane, so, 0);
+        } else if (gx < W) {
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, out[o].x), rd, 8 * lane, so, 0);
+        }
+        if constexpr (NXT) {
+            // nearest 1/2: pixel (2x, 2y) (cv::resize INTER_NEAREST) / (2x + 1, 2y + 1) (image's Nearest)
+            const int gy = y0 + o;
+            const bool row = P == kProfileOpenCV ? (gy & 1) == 0 : (gy & 1) == 1;
+            if (row && (gy >> 1) < hn && (gx >> 1) < wn && (P == kProfileOpenCV || pair)) {
+                const float val = P == kProfileOpenCV ? out[o].x : out[o].y;
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, val), rn, 4 * lane,
+                                                      ((gy >> 1) * pitch_n + (x0 >> 1)) * 4, 0);
+            }
+        }
+        so += pitch * 4;
+    }
+}
+
+// grid: (strips, segments, frames); segment sg covers output rows
+// [ya + sg * seg, min(yb, ya + (sg + 1) * seg)).  G_{s-1} / G_s planes are
+// H * pitch floats (< 2^31 bytes: checked by the launcher).
+template <int R, int P, bool NXT>
+__global__ __launch_bounds__(256, StripGeom<R>::MINB) void k_blur_strip(
+    const float* __restrict__ src, size_t src_img_stride, float* __restrict__ dst, size_t dst_img_stride,
+    float* __restrict__ nxt, size_t nxt_img_stride, int pitch_n, int wn, int hn, int W, int H, int pitch,
+    const BlurTaps taps, int ya, int yb, int seg) {
+    using G = StripGeom<R>;
+    __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const TileId tile = xcd_tile();
+    const int x0 = tile.x * G::TW;
+    const int ys = ya + tile.y * seg, ye = min(yb, ys + seg);
+    if (ys >= ye) return;
+    const size_t b = tile.z;
+    const uint32_t plane_bytes = (uint32_t)H * (uint32_t)pitch * 4u;
+    const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(src + b * src_img_stride, plane_bytes);
+    const __amdgpu_buffer_rsrc_t rd = uniform_rsrc(dst + b * dst_img_stride, plane_bytes);
+    __amdgpu_buffer_rsrc_t rn = rd;
+    if constexpr (NXT) rn = uniform_rsrc(nxt + b * nxt_img_stride, (uint32_t)hn * (uint32_t)pitch_n * 4u);
+    // loads: item i = (row i / C4, float4 column i % C4) of the chunk
+    const bool cols_in = x0 - G::HWL >= 0 && x0 + G::TW + G::HWL <= W;
+    int voff[G::LPT];
+#pragma unroll
+    for (int j = 0; j < G::LPT; j++) {
+        const int i = min(tid + 64 * G::NW * j, G::NLOAD4 - 1);
+        const int ly = i / G::C4, c4 = i - ly * G::C4;
+        voff[j] = (ly * pitch + x0 - G::HWL + 4 * c4) * 4;
+    }
+    // row-pass lane map (see strip_rowpass)
+    int prow, pq;
+    {
+        const int l = lane & 31;
+        int g, k;
+        if (l < 4) { g = 0; k = l; }
+        else if (l < 12) { g = 1; k = l - 4; }
+        else if (l < 16) { g = 0; k = l - 8; }
+        else if (l < 20) { g = 1; k = l - 8; }
+        else if (l < 28) { g = 0; k = l - 12; }
+        else { g = 1; k = l - 16; }
+        const int grp = (lane >> 5) * 2 + g;  // rows (grp >> 1) * 2 + (k >> 3), items (grp & 1) * 8 + (k & 7)
+        prow = wv * 4 + (grp >> 1) * 2 + (k >> 3);
+        pq = (grp & 1) * 8 + (k & 7);
+    }
+    const int nsteps = (ye - ys + G::S - 1) / G::S;
+    float4 pre[G::LPT];
+    strip_load<R, P>(pre, rs, voff, cols_in, ys - R, x0, W, H, pitch);
+    strip_store<R>(pre, lds);
+    strip_load<R, P>(pre, rs, voff, cols_in, ys - R + G::S, x0, W, H, pitch);
+    __syncthreads();
+    strip_rowpass<R, P>(lds, taps, prow, pq);
+    for (int k = 0; k < nsteps; k++) {
+        float* sa = lds + (k & 1) * G::SLOT;
+        float* sb = lds + ((k + 1) & 1) * G::SLOT;
+        __syncthreads();  // column pass k - 1 is done with slot b
+        strip_store<R>(pre, sb);
+        if (k + 2 <= nsteps) strip_load<R, P>(pre, rs, voff, cols_in, ys - R + (k + 2) * G::S, x0, W, H, pitch);
+        __syncthreads();
+        strip_rowpass<R, P>(sb, taps, prow, pq);
+        __syncthreads();
+        const int y = ys + k * G::S;
+        switch (wv) {
+#define COLPASS(w)                                                                                      \
+    case w:                                                                                             \
+        strip_colpass<R, P, w, NXT>(sa, sb, taps, lane, y, ye, x0, W, pitch, rd, rn, pitch_n, wn, hn); \
+        break;
+            COLPASS(0) COLPASS(1) COLPASS(2) COLPASS(3)
+#undef COLPASS
+        }
+    }
 }
 
 // ---------------------------------------------------------------------------
@@ -578,7 +884,67 @@ static void launch_blur_r(const BlurLaunch& L, hipStream_t st) {
                            L.W, L.H, L.pitch, L.taps, ty0);
 }
 
+template <int R, int P>
+static void launch_blur_strip_rp(const BlurLaunch& L, dim3 grid, int ya, int yb, int seg, hipStream_t st) {
+    using G = StripGeom<R>;
+    if (L.nxt)
+        hipLaunchKernelGGL((k_blur_strip<R, P, true>), grid, dim3(64 * G::NW), 0, st, L.src, L.src_img_stride, L.dst,
+                           L.dst_img_stride, L.nxt, L.nxt_img_stride, L.pitch_n, L.wn, L.hn, L.W, L.H, L.pitch,
+                           L.taps, ya, yb, seg);
+    else
+        hipLaunchKernelGGL((k_blur_strip<R, P, false>), grid, dim3(64 * G::NW), 0, st, L.src, L.src_img_stride,
+                           L.dst, L.dst_img_stride, L.nxt, L.nxt_img_stride, L.pitch_n, L.wn, L.hn, L.W, L.H,
+                           L.pitch, L.taps, ya, yb, seg);
+}
+
+template <int R>
+static void launch_blur_strip_r(const BlurLaunch& L, hipStream_t st) {
+    using G = StripGeom<R>;
+    const int ya = L.y1 > L.y0 ? std::max(L.y0, 0) : 0;
+    const int yb = L.y1 > L.y0 ? std::min(L.y1, L.H) : L.H;
+    if (yb <= ya) return;
+    const int strips = (L.W + G::TW - 1) / G::TW;
+    // segments: ~12 k workgroups per launch (a few dozen per CU: the last
+    // round of equal-sized workgroups is a small fraction), none shorter than
+    // two chunks (each segment re-filters its 2R halo rows)
+    const int rows = yb - ya;
+    const long per = (long)strips * L.n_img;
+    int nseg = (int)std::min<long>(rows / (2 * G::S) + 1, (12288 + per - 1) / per);
+    nseg = std::max(1, nseg);
+    const int seg = (rows + nseg - 1) / nseg;
+    nseg = (rows + seg - 1) / seg;
+    const dim3 grid(strips, nseg, L.n_img);
+    if (L.profile == kProfileImageproc)
+        launch_blur_strip_rp<R, kProfileImageproc>(L, grid, ya, yb, seg, st);
+    else
+        launch_blur_strip_rp<R, kProfileOpenCV>(L, grid, ya, yb, seg, st);
+}
+
+// SIFT_MI_BLUR_KERNEL=tile forces the one-tile-per-workgroup kernel (A/B knob)
+static bool strip_blur_enabled() {
+    static const bool on = [] {
+        const char* e = getenv("SIFT_MI_BLUR_KERNEL");
+        return !(e && !strcmp(e, "tile"));
+    }();
+    return on;
+}
+
 int launch_blur(int R, const BlurLaunch& L, hipStream_t st) {
+    // the strip kernel: materialised G_s, no DoG plane (the batch path), one
+    // reflection per border (W, H > R), planes addressable by 32-bit offsets
+    if (L.dst && !L.dog && R <= kStripMaxR && L.W > R && L.H > R &&
+        (uint64_t)L.H * (uint64_t)L.pitch * 4 < (1ull << 31) && strip_blur_enabled()) {
+        switch (R) {
+#define CASE(r) \
+    case r:     \
+        launch_blur_strip_r<r>(L, st); return 0;
+            CASE(1) CASE(2) CASE(3) CASE(4) CASE(5) CASE(6) CASE(7) CASE(8) CASE(9) CASE(10) CASE(11) CASE(12)
+            CASE(13) CASE(14) CASE(15) CASE(16)
+#undef CASE
+            default:
+                break;
+        }
+    }
     switch (R) {
 #define CASE(r) \
     case r:     \

@@ -65,7 +65,7 @@ float time_blur(const float* src, float* dst, float* dog, size_t stride, int W, 
     dim3 grid(tx, ty, nimg);
     auto go = [&]() {
         hipLaunchKernelGGL((k_blur<R, TH, kProfileOpenCV>), grid, dim3(256), 0, 0, src, stride, dst, stride, dog, stride,
-                           (float*)nullptr, (size_t)0, 0, 0, 0, W, H, pitch, taps);
+                           (float*)nullptr, (size_t)0, 0, 0, 0, W, H, pitch, taps, 0);
     };
     go();
     hipEvent_t a, b;
@@ -78,6 +78,56 @@ float time_blur(const float* src, float* dst, float* dog, size_t stride, int W, 
     float ms;
     CK(hipEventElapsedTime(&ms, a, b));
     return ms / reps;
+}
+
+// the streaming strip kernel through the product launcher (segments as chosen there)
+template <int R>
+float time_blur_strip(const float* src, float* dst, size_t stride, int W, int H, int pitch, int nimg, int reps) {
+    BlurLaunch L{};
+    L.src = src;
+    L.src_img_stride = stride;
+    L.dst = dst;
+    L.dst_img_stride = stride;
+    L.W = W;
+    L.H = H;
+    L.pitch = pitch;
+    L.n_img = nimg;
+    for (int t = 0; t <= R; t++) L.taps.k[t] = 1.0f / (2 * R + 1);
+    launch_blur(R, L, 0);
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    CK(hipEventRecord(a));
+    for (int i = 0; i < reps; i++) launch_blur(R, L, 0);
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    return ms / reps;
+}
+
+// octave-0 geometry of the bench (64 frames of the 2x 1080p seed, 3840x2160,
+// 6-plane G arena): tile kernel vs strip kernel per radius, 8 B/px
+void bench_blur_strip(int N) {
+    const int W = 3840, H = 2160, pitch = 3840;
+    const size_t plane = (size_t)pitch * H;
+    float* base;
+    CK(hipMalloc(&base, plane * 6 * N * 4));
+    hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, base, plane * 6 * N);
+    CK(hipDeviceSynchronize());
+    const size_t stride = plane * 6;
+    const double bytes = 8.0 * W * H * N;
+    std::printf("blur G_{s-1} -> G_s, %d x %dx%d (arena, random): ms, GB/s at 8 B/px\n", N, W, H);
+#define B(R, TH)                                                                                                  \
+    {                                                                                                             \
+        const float mt = time_blur<R, TH>(base, base + plane, nullptr, stride, W, H, pitch, N, 5);                 \
+        const float ms = time_blur_strip<R>(base, base + plane, stride, W, H, pitch, N, 5);                       \
+        std::printf("  R=%2d tile(TH=%d) %8.3f ms %7.1f GB/s | strip %8.3f ms %7.1f GB/s\n", R, TH, mt,            \
+                    bytes / (mt * 1e-3) / 1e9, ms, bytes / (ms * 1e-3) / 1e9);                                      \
+    }
+    B(5, 32) B(6, 32) B(8, 32) B(10, 64) B(13, 64)
+#undef B
+    CK(hipFree(base));
 }
 
 void bench_blur(int N, bool arena, bool random) {
@@ -118,6 +168,10 @@ void bench_blur(int N, bool arena, bool random) {
 
 int main(int argc, char** argv) {
     const char* mode = argc > 1 ? argv[1] : "all";
+    if (!strcmp(mode, "strip")) {
+        bench_blur_strip(argc > 2 ? atoi(argv[2]) : 64);
+        return 0;
+    }
     if (!strcmp(mode, "all") || !strcmp(mode, "blur")) {
         bench_blur(16, false, false);
         bench_blur(16, false, true);
