@@ -59,7 +59,46 @@ def parse():
     p.add_argument("--cpu-seconds", type=float, default=12.0, help="CPU baseline sample budget")
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-latency", action="store_true")
+    p.add_argument("--no-configs", action="store_true", help="skip the other single-GPU BASELINE configs")
     return p.parse_args()
+
+
+def run_config(pkg, synth, dev, device_index, n, W, H, steps, seed0=1000):
+    """One BASELINE config on one GPU: `n` device-resident W x H frames per
+    call, results left in HBM; keypoints/s from two-lane calls, the pyramid
+    stage's HIP-event time (and its roofline fraction) from a serialised pass."""
+    import torch
+    fr = synth.frames_torch(n, W, H, seed0=seed0, device=dev)
+    torch.cuda.synchronize()
+    c = pkg.Context(device_index, pkg.OpenCVProcessing)
+    call = (fr.data_ptr(), n, W, H, fr.stride(1), fr.stride(0))
+
+    def go():
+        return int(c.sift_batch_device(*call, fetch=False)[0][-1])
+
+    go()
+    torch.cuda.synchronize()
+    t = time.perf_counter()
+    kp = sum(go() for _ in range(steps))
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t) / steps
+    c.set_pipeline_lanes(1)
+    go()
+    torch.cuda.synchronize()
+    c.reset_stats()
+    for _ in range(steps):
+        go()
+    torch.cuda.synchronize()
+    st = c.stats()
+    c.close()
+    del fr
+    torch.cuda.empty_cache()
+    gbs = st["pyramid_bytes"] / (st["pyramid_ms"] * 1e-3) / 1e9 if st["pyramid_ms"] > 0 else 0.0
+    return {"frames_per_call": n, "frame": f"{W}x{H}",
+            "octaves": int(round(np.log2(min(2 * W, 2 * H)) - 2)) + 1,
+            "ms_per_call": 1e3 * dt, "keypoints_per_s": kp / steps / dt, "frames_per_s": n / dt,
+            "keypoints_per_frame": kp / steps / n, "pyramid_ms_per_call": st["pyramid_ms"] / steps,
+            "pyramid_gbs": gbs, "pyramid_frac": gbs / HBM_PEAK_GBS}
 
 
 def main():
@@ -95,8 +134,11 @@ def main():
 
     out = pkg.ResultBuffers()  # streaming caller: host result arrays reused across batches
 
+    last = {}
+
     def step(fetch=False):
         offs, res = ctx.sift_batch_device(ptr, B, W, H, stride, pitch, fetch=fetch, out=out)
+        last["offs"] = offs
         return int(offs[-1])
 
     def barrier():
@@ -134,6 +176,28 @@ def main():
 
     dt_max, total_kp, total_frames = shard.reduce_run(dt, n_kp, B * args.steps, dist if world > 1 else None)
 
+    # N > 1: the keypoint gather of the throughput path -- every rank's
+    # device-resident results of its last step to rank 0 over RCCL
+    # (shard.gather_device_results: sizes, then point-to-point rows into one
+    # concatenated device tensor), timed on its own outside the steps
+    gather = None
+    if world > 1:
+        k_dev, d_dev = shard.device_results(ctx)
+        torch.cuda.synchronize()
+        barrier()
+        t = time.perf_counter()
+        g = shard.gather_device_results(k_dev, d_dev, last["offs"], dist, dst=0)
+        torch.cuda.synchronize()
+        barrier()
+        gms = 1e3 * (time.perf_counter() - t)
+        gms = shard.reduce_run(gms / 1e3, 0, 0, dist)[0] * 1e3
+        if rank == 0:
+            nk = int(g[0].shape[0])
+            gather = {"ms": gms, "keypoints": nk, "bytes": nk * (20 + 128),
+                      "note": "one step's results of all ranks to rank 0 (device to device, RCCL send/recv), "
+                              "max over ranks; not inside ms_per_step"}
+        del g, k_dev, d_dev
+
     pyr_gbs = st["pyramid_bytes"] / (st["pyramid_ms"] * 1e-3) / 1e9 if st["pyramid_ms"] > 0 else 0.0
     per_launch_bytes = st["pyramid_bytes"] / max(1, st["pyramid_launches"])
     per_launch_ms = st["pyramid_ms"] / max(1, st["pyramid_launches"])
@@ -143,7 +207,7 @@ def main():
     if rank == 0 and world == 1:
         step(fetch=True)
         torch.cuda.synchronize()
-        hs = max(1, min(args.steps, 2))
+        hs = max(1, args.steps)
         t = time.perf_counter()
         hk = sum(step(fetch=True) for _ in range(hs))
         he = time.perf_counter() - t
@@ -191,6 +255,23 @@ def main():
         cpu_all = {"value": kps / el, "unit": "keypoints/s", "cores": cores, "kind": "port",
                    "sample": f"{nfr} of the {B} benchmark frames, one per thread on {cores} threads, {el:.1f} s"}
 
+    # the other single-GPU configs of BASELINE.json (extra fields, rank 0 at
+    # N = 1): configs[1] one 1080p frame per call, configs[2] 256 VGA frames
+    # per call, configs[4] one 8192^2 frame per call (the crate's octave
+    # count: 10 / 9 / 13 octaves, not the configs' "5" / "7" wording)
+    configs = None
+    if rank == 0 and world == 1 and not args.no_configs:
+        ctx.close()
+        ctx = None
+        del frames
+        torch.cuda.empty_cache()
+        configs = {
+            "single_1080p": run_config(pkg, synth, dev, local, 1, 1920, 1080, max(10, args.steps)),
+            "vga_256": run_config(pkg, synth, dev, local, 256, 640, 480, max(3, args.steps)),
+            "giant_8192": run_config(pkg, synth, dev, local, 1, 8192, 8192, max(3, args.steps)),
+        }
+        configs["single_1080p"]["latency_host_fetch_ms"] = latency_ms
+
     # HBM traffic of the same launch group from the committed PMC passes
     # (tools/round_profile.sh -> profiles/pmc_traffic.json), scaled to one
     # launch like `achieved`; null when no measurement matches this frame size
@@ -237,9 +318,12 @@ def main():
                          "avg_launch_ms": per_launch_ms},
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_all,
+            "gather": gather,
+            "configs": configs,
         }
         print(json.dumps(out), flush=True)
-    ctx.close()
+    if ctx is not None:
+        ctx.close()
     if world > 1:
         dist.destroy_process_group()
 

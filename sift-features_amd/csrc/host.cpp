@@ -646,9 +646,6 @@ constexpr int kBandDrift = 24, kBandPatch = 41;
 // ---------------------------------------------------------------------------
 // Stage 1: Gaussian scale space + DoG for n frames (device-resident u8)
 // ---------------------------------------------------------------------------
-// Fused five-blur octave kernel (octave.hip) by default where it applies.
-constexpr bool kFusedOctaveDefault = false;  // opt-in until it beats the per-blur kernels
-
 // full: materialise every image (precompute_images / read_dog); the batch
 // path writes G_0..G_5 only: detection and refinement form D_s = G_{s+1} - G_s
 // where they read it (detect.hip), 16 B per octave pixel less than writing
@@ -731,57 +728,16 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
         }
         bytes = (uint64_t)b;
     }
-    // fused five-blur octave kernel (octave.hip) where it applies: OpenCV
-    // profile with its constant radii, octaves wide enough for one-reflection
-    // column borders; the per-blur kernels otherwise
-    // (test / tuning knobs, read per call: SIFT_MI_FUSED_OCTAVE=0|1 overrides
-    // kFusedOctaveDefault, SIFT_MI_OCT_SEG rows per workgroup)
-    const char* fused_env = getenv("SIFT_MI_FUSED_OCTAVE");
-    const bool use_fused = fused_env ? atoi(fused_env) != 0 : kFusedOctaveDefault;
-    const int seg_env = getenv("SIFT_MI_OCT_SEG") ? atoi(getenv("SIFT_MI_OCT_SEG")) : 0;
-    const bool fused_ok = use_fused && p.profile == (int)SIFT_MI_PROFILE_OPENCV && octave_radii_supported(p.oct_r);
     for (int o = 0; o < p.n_oct; o++) {
         float* G = p.gauss(o, lane);
         float* D = p.dog(o, lane);
         const size_t P = p.P[o];
-        if (fused_ok && !c->band_restricted && p.ow[o] >= octave_min_width()) {
-            OctaveArgs A{};
-            A.gauss = G;
-            A.g_img_stride = p.gstride(o);
-            A.plane = P;
-            A.dog = D;
-            A.dog_img_stride = p.dstride(o);
-            if (o + 1 < p.n_oct) {
-                A.nxt = p.gauss(o + 1, lane);
-                A.nxt_img_stride = p.gstride(o + 1);
-                A.pitch_n = p.opitch[o + 1];
-                A.wn = p.ow[o + 1];
-                A.hn = p.oh[o + 1];
-            }
-            A.W = p.ow[o];
-            A.H = p.oh[o];
-            A.pitch = p.opitch[o];
-            // rows per workgroup: enough segments for ~2 workgroups per CU,
-            // none shorter than 96 rows (each segment re-streams a 2 x 42-row
-            // warm-up)
-            const int strips = (A.W + octave_strip_width() - 1) / octave_strip_width();
-            int nseg = (512 + strips * (int)n - 1) / (strips * (int)n);
-            nseg = std::max(1, std::min(nseg, A.H / 96));
-            A.seg_rows = seg_env > 0 ? seg_env : (A.H + nseg - 1) / nseg;
-            A.write_all = 1;  // detection forms D from G_0..G_5
-            for (int s = 1; s < kImagesPerOctave; s++) A.taps[s] = p.oct_taps[s];
-            if (launch_octave(A, (int)n, st)) return fail(SIFT_MI_EUNSUPPORTED, "fused octave kernel");
-            launches++;
-            continue;
-        }
         for (int s = 1; s < kImagesPerOctave; s++) {
             BlurLaunch B{};
             B.src = G + (size_t)(s - 1) * P;
             B.src_img_stride = p.gstride(o);
             B.dst = G + (size_t)s * P;
             B.dst_img_stride = p.gstride(o);
-            B.dog = full ? D + (size_t)(s - 1) * P : nullptr;
-            B.dog_img_stride = p.dstride(o);
             if (s == 3 && o + 1 < p.n_oct) {
                 B.nxt = p.gauss(o + 1, lane);
                 B.nxt_img_stride = p.gstride(o + 1);
@@ -802,6 +758,9 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
             if (launch_blur(p.oct_r[s], B, st)) return fail(SIFT_MI_EUNSUPPORTED, "octave blur radius");
             launches++;
         }
+        // precompute_images: D_s = G_{s+1} - G_s, the same f32 subtraction
+        // the keypoint stages form where they read the DoG
+        if (full) launch_dog(G, P, p.gstride(o), D, p.dstride(o), p.ow[o], p.oh[o], p.opitch[o], (int)n, st);
     }
     HIPCHK(hipGetLastError());
     c->stats.pyramid_launches += launches;

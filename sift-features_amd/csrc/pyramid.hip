@@ -295,10 +295,11 @@ __global__ __launch_bounds__(256) void k_blur(const float* __restrict__ src, siz
 // compile-time choice and every LDS read is one ds_read_b64 with an immediate
 // offset.
 // ---------------------------------------------------------------------------
-template <int R>
+template <int R_, int S_ = 32>
 struct StripGeom {
+    static constexpr int R = R_;                      // blur radius
     static constexpr int TW = 128;                    // output columns per strip
-    static constexpr int S = 32;                      // rows per chunk
+    static constexpr int S = S_;                      // rows per chunk
     static constexpr int NW = 4;                      // waves per workgroup
     static constexpr int VB = S / NW;                 // column-pass rows per wave per step
     static constexpr int QW = 8;                      // row-pass outputs per item
@@ -375,9 +376,8 @@ __device__ __forceinline__ void strip_load(float4 (&pre)[StripGeom<R>::LPT], __a
     }
 }
 
-template <int R>
-__device__ __forceinline__ void strip_store(const float4 (&pre)[StripGeom<R>::LPT], float* slot) {
-    using G = StripGeom<R>;
+template <class G>
+__device__ __forceinline__ void strip_store(const float4 (&pre)[G::LPT], float* slot) {
     const int tid = threadIdx.x;
 #pragma unroll
     for (int j = 0; j < G::LPT; j++) {
@@ -394,9 +394,9 @@ __device__ __forceinline__ void strip_store(const float4 (&pre)[StripGeom<R>::LP
 // (imageproc).  Lane -> (row, item) follows the ds_read_b128 lane groups: each
 // 16-lane group reads two adjacent rows x 8 items, whose float4 slots are the
 // even / odd slots of a bank row (IWP / 4 odd) -> conflict-free.
-template <int R, int P>
+template <class G, int P>
 __device__ __forceinline__ void strip_rowpass(float* slot, const BlurTaps& taps, int prow, int pq) {
-    using G = StripGeom<R>;
+    constexpr int R = G::R;
 #pragma unroll
     for (int it = 0; it < G::S / 16; it++) {
         const int ly = it * 16 + prow;
@@ -435,11 +435,11 @@ __device__ __forceinline__ void strip_rowpass(float* slot, const BlurTaps& taps,
 // output row y - R) is row L of slot a for L < S, row L - S of slot b
 // otherwise -- a compile-time choice per row.  OpenCV's SymmColumnFilter
 // (centre product, fma of pair sums) / imageproc's unfused chain.
-template <int R, int P, int WV, bool NXT>
+template <class G, int P, int WV, bool NXT>
 __device__ __forceinline__ void strip_colpass(const float* sa, const float* sb, const BlurTaps& taps, int lane,
                                               int y, int ye, int x0, int W, int pitch, __amdgpu_buffer_rsrc_t rd,
                                               __amdgpu_buffer_rsrc_t rn, int pitch_n, int wn, int hn) {
-    using G = StripGeom<R>;
+    constexpr int R = G::R;
     constexpr int NR = G::VB + 2 * R;
     f2v v[NR];
 #pragma unroll
@@ -549,24 +549,24 @@ __global__ __launch_bounds__(256, StripGeom<R>::MINB) void k_blur_strip(
     const int nsteps = (ye - ys + G::S - 1) / G::S;
     float4 pre[G::LPT];
     strip_load<R, P>(pre, rs, voff, cols_in, ys - R, x0, W, H, pitch);
-    strip_store<R>(pre, lds);
+    strip_store<G>(pre, lds);
     strip_load<R, P>(pre, rs, voff, cols_in, ys - R + G::S, x0, W, H, pitch);
     __syncthreads();
-    strip_rowpass<R, P>(lds, taps, prow, pq);
+    strip_rowpass<G, P>(lds, taps, prow, pq);
     for (int k = 0; k < nsteps; k++) {
         float* sa = lds + (k & 1) * G::SLOT;
         float* sb = lds + ((k + 1) & 1) * G::SLOT;
         __syncthreads();  // column pass k - 1 is done with slot b
-        strip_store<R>(pre, sb);
+        strip_store<G>(pre, sb);
         if (k + 2 <= nsteps) strip_load<R, P>(pre, rs, voff, cols_in, ys - R + (k + 2) * G::S, x0, W, H, pitch);
         __syncthreads();
-        strip_rowpass<R, P>(sb, taps, prow, pq);
+        strip_rowpass<G, P>(sb, taps, prow, pq);
         __syncthreads();
         const int y = ys + k * G::S;
         switch (wv) {
 #define COLPASS(w)                                                                                      \
     case w:                                                                                             \
-        strip_colpass<R, P, w, NXT>(sa, sb, taps, lane, y, ye, x0, W, pitch, rd, rn, pitch_n, wn, hn); \
+        strip_colpass<G, P, w, NXT>(sa, sb, taps, lane, y, ye, x0, W, pitch, rd, rn, pitch_n, wn, hn); \
         break;
             COLPASS(0) COLPASS(1) COLPASS(2) COLPASS(3)
 #undef COLPASS
@@ -752,6 +752,201 @@ __global__ __launch_bounds__(256) void k_seed(const uint8_t* __restrict__ frames
 }
 
 // ---------------------------------------------------------------------------
+// k_seed_strip: the seed in the strip scheme (StripGeom<5, 16>: 128 columns,
+// 16-row chunks).  Per chunk of 16 window rows, the source bytes it needs
+// (<= 12 rows x 80 columns: an exact 2x upsample reads source floor(g / 2 -
+// 0.25) and the next one) are prefetched one chunk ahead with the chunk's
+// row coefficients; then u8 -> v / 255 into LDS, HResizeLinear per source row
+// (hbuf), VResizeLinear into the chunk slot by the wave that row-filters those
+// rows, and the R = 5 blur exactly as k_blur_strip.  The upsampled image never
+// touches HBM; its bytes are read once per strip.
+// ---------------------------------------------------------------------------
+template <int R>
+struct SeedStrip {
+    using G = StripGeom<R, 16>;
+    static constexpr int SR = G::S / 2 + 4;   // source rows per chunk (<= 11 used)
+    static constexpr int NWD = 20;            // source dwords per row (<= 20 used: 74 columns + alignment)
+    static constexpr int SC = 4 * NWD;
+    static_assert(SR * NWD + G::S <= 256, "one prefetch item per thread: bytes, then the row tables");
+    static_assert(G::IWV <= 2 * SC - 12, "source columns of the window fit the row");
+};
+
+template <int R>
+__global__ __launch_bounds__(256, 4) void k_seed_strip(const uint8_t* __restrict__ frames, size_t frame_pitch,
+                                                       size_t row_stride, int sh, int sw, const ResizeTab tab,
+                                                       float* __restrict__ dst, size_t dst_img_stride, int W, int H,
+                                                       int pitch, const BlurTaps taps, int ya, int yb, int seg) {
+    using Q = SeedStrip<R>;
+    using G = typename Q::G;
+    __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
+    __shared__ __attribute__((aligned(16))) float srcf[Q::SR * Q::SC];     // v / 255, columns from a0
+    __shared__ __attribute__((aligned(16))) float hbuf[Q::SR * G::IWV];    // HResizeLinear per source row
+    __shared__ __attribute__((aligned(16))) int txo[G::IWV];               // source column - a0 (< 0: single tap)
+    __shared__ __attribute__((aligned(16))) float txa0[G::IWV], txa1[G::IWV];
+    __shared__ int tyo0[G::S], tyo1[G::S];                                 // source rows - sya of a window row
+    __shared__ float tya0[G::S], tya1[G::S];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const TileId tile = xcd_tile();
+    const int x0 = tile.x * G::TW;
+    const int ys = ya + tile.y * seg, ye = min(yb, ys + seg);
+    if (ys >= ye) return;
+    const size_t b = tile.z;
+    const uint8_t* src = frames + b * frame_pitch;
+    const __amdgpu_buffer_rsrc_t rd =
+        uniform_rsrc(dst + b * dst_img_stride, (uint32_t)H * (uint32_t)pitch * 4u);
+    // source columns of the strip's window (reflect-101 in the 2x image)
+    int sxa, sxb;
+    {
+        int glo, ghi;
+        reflect_range(x0 - G::HWL, G::IWV, W, glo, ghi);
+        sxa = max(glo / 2 - 1, 0);
+        sxb = min(ghi / 2 + 1, sw - 1);
+    }
+    const int a0 = sxa & ~3;  // first source dword
+    const int nwr = (sxb - a0) / 4 + 1;
+    if (tid < G::IWV) {
+        const int g = strip_index<kProfileOpenCV>(x0 - G::HWL + tid, W);
+        const int s0 = tab.xofs[g];
+        txo[tid] = g < tab.xmax ? s0 - a0 : -1 - (s0 - a0);
+        txa0[tid] = tab.xa0[g];
+        txa1[tid] = tab.xa1[g];
+    }
+    // prefetch item of this thread: a source dword (tid < SR * NWD) or a row's coefficients
+    const int pr = tid / Q::NWD, pw = tid - pr * Q::NWD;
+    const int trow = tid - Q::SR * Q::NWD;  // 0 .. S-1: window row of the chunk (tables)
+    uint32_t pv = 0;                        // bytes
+    int py0 = 0, py1 = 0;                   // source rows (absolute)
+    float pb0 = 0.f, pb1 = 0.f;
+    auto chunk_rows = [&](int g0, int& sya, int& nr) {
+        int glo, ghi;
+        reflect_range(g0, G::S, H, glo, ghi);
+        sya = max(glo / 2 - 1, 0);
+        nr = min(ghi / 2 + 1, sh - 1) - sya + 1;
+    };
+    auto prefetch = [&](int g0) {
+        int sya, nr;
+        chunk_rows(g0, sya, nr);
+        if (tid < Q::SR * Q::NWD) {
+            pv = 0;
+            if (pr < nr && pw < nwr) {
+                const int c = a0 + 4 * pw;
+                const uint8_t* p = src + (size_t)(sya + pr) * row_stride + c;
+                if (c + 3 < sw) {
+                    pv = *reinterpret_cast<const uint32_t*>(p);
+                } else {  // row end: bytes only (the dword could run past the frame)
+                    for (int q = 0; q < 4 && c + q < sw; q++) pv |= (uint32_t)p[q] << (8 * q);
+                }
+            }
+        } else if (trow < G::S) {
+            const int g = strip_index<kProfileOpenCV>(g0 + trow, H);
+            py0 = tab.yofs[g];
+            py1 = min(py0 + 1, sh - 1);
+            pb0 = tab.ya0[g];
+            pb1 = tab.ya1[g];
+        }
+    };
+    auto stage = [&](int g0) {  // prefetched chunk -> srcf / row tables
+        int sya, nr;
+        chunk_rows(g0, sya, nr);
+        if (tid < Q::SR * Q::NWD) {
+            if (pr < nr && pw < nwr)
+                *reinterpret_cast<float4*>(srcf + pr * Q::SC + 4 * pw) =
+                    make_float4(u8_unit(pv & 0xff), u8_unit((pv >> 8) & 0xff), u8_unit((pv >> 16) & 0xff),
+                                u8_unit(pv >> 24));
+        } else if (trow < G::S) {
+            tyo0[trow] = py0 - sya;
+            tyo1[trow] = py1 - sya;
+            tya0[trow] = pb0;
+            tya1[trow] = pb1;
+        }
+    };
+    auto hres = [&](int g0) {  // HResizeLinear: t = S[sx]*a0 + S[sx+1]*a1 (two roundings + add)
+        int sya, nr;
+        chunk_rows(g0, sya, nr);
+        constexpr int Q4 = G::IWV / 4;
+        for (int i = tid; i < nr * Q4; i += 256) {
+            const int r = i / Q4, c = (i - r * Q4) * 4;
+            const int4 xo = *reinterpret_cast<const int4*>(txo + c);
+            const float4 w0 = *reinterpret_cast<const float4*>(txa0 + c);
+            const float4 w1 = *reinterpret_cast<const float4*>(txa1 + c);
+            const float* sr = srcf + r * Q::SC;
+            auto h = [&](int o, float u0, float u1) {
+                const bool two = o >= 0;
+                const int sx = two ? o : -1 - o;
+                const float p0 = sr[sx];
+                return two ? p0 * u0 + sr[sx + 1] * u1 : p0;
+            };
+            *reinterpret_cast<float4*>(hbuf + r * G::IWV + c) =
+                make_float4(h(xo.x, w0.x, w1.x), h(xo.y, w0.y, w1.y), h(xo.z, w0.z, w1.z), h(xo.w, w0.w, w1.w));
+        }
+    };
+    // VResizeLinear (S0*b0 + S1*b1) of this wave's 4 window rows into the slot
+    auto vres = [&](float* slot) {
+        constexpr int Q4 = G::IWV / 4;
+        for (int i = lane; i < 4 * Q4; i += 64) {
+            const int ly = wv * 4 + i / Q4, c = (i % Q4) * 4;
+            const float4 u = *reinterpret_cast<const float4*>(hbuf + tyo0[ly] * G::IWV + c);
+            const float4 v = *reinterpret_cast<const float4*>(hbuf + tyo1[ly] * G::IWV + c);
+            const float b0 = tya0[ly], b1 = tya1[ly];
+            *reinterpret_cast<float4*>(slot + ly * G::IWP + c) =
+                make_float4(u.x * b0 + v.x * b1, u.y * b0 + v.y * b1, u.z * b0 + v.z * b1, u.w * b0 + v.w * b1);
+        }
+        // the wave's row pass reads these rows next (in-order LDS within a wave)
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    };
+    // row-pass lane map (as k_blur_strip; S = 16: one 16-row iteration, wave w rows 4w..4w+3)
+    int prow, pq;
+    {
+        const int l = lane & 31;
+        int g, k;
+        if (l < 4) { g = 0; k = l; }
+        else if (l < 12) { g = 1; k = l - 4; }
+        else if (l < 16) { g = 0; k = l - 8; }
+        else if (l < 20) { g = 1; k = l - 8; }
+        else if (l < 28) { g = 0; k = l - 12; }
+        else { g = 1; k = l - 16; }
+        const int grp = (lane >> 5) * 2 + g;
+        prow = wv * 4 + (grp >> 1) * 2 + (k >> 3);
+        pq = (grp & 1) * 8 + (k & 7);
+    }
+    const int nsteps = (ye - ys + G::S - 1) / G::S;
+    const int gb = ys - R;  // window row of chunk 0
+    prefetch(gb);
+    stage(gb);
+    prefetch(gb + G::S);
+    __syncthreads();
+    hres(gb);
+    __syncthreads();
+    vres(lds);
+    strip_rowpass<G, kProfileOpenCV>(lds, taps, prow, pq);
+    for (int k = 0; k < nsteps; k++) {
+        float* sa = lds + (k & 1) * G::SLOT;
+        float* sb = lds + ((k + 1) & 1) * G::SLOT;
+        const int g1 = gb + (k + 1) * G::S;
+        __syncthreads();  // column pass k - 1 is done with slot b, vres / hres with the tables and hbuf
+        stage(g1);
+        if (k + 2 <= nsteps) prefetch(g1 + G::S);
+        __syncthreads();
+        hres(g1);
+        __syncthreads();
+        vres(sb);
+        strip_rowpass<G, kProfileOpenCV>(sb, taps, prow, pq);
+        __syncthreads();
+        const int y = ys + k * G::S;
+        switch (wv) {
+#define COLPASS(w)                                                                                              \
+    case w:                                                                                                     \
+        strip_colpass<G, kProfileOpenCV, w, false>(sa, sb, taps, lane, y, ye, x0, W, pitch, rd, rd, 0, 0, 0); \
+        break;
+            COLPASS(0) COLPASS(1) COLPASS(2) COLPASS(3)
+#undef COLPASS
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
 // Seed, Imageproc profile: u8 -> f32 (v / 255) -> image::imageops::resize
 // Triangle 2x (vertical_sample into an f32 intermediate, then
 // horizontal_sample; t = t + p * w from the first tap, result clamped to
@@ -920,13 +1115,11 @@ static void launch_blur_strip_r(const BlurLaunch& L, hipStream_t st) {
         launch_blur_strip_rp<R, kProfileOpenCV>(L, grid, ya, yb, seg, st);
 }
 
-// SIFT_MI_BLUR_KERNEL=tile forces the one-tile-per-workgroup kernel (A/B knob)
+// SIFT_MI_BLUR_KERNEL=tile forces the one-tile-per-workgroup kernels (A/B
+// and test knob, read per launch)
 static bool strip_blur_enabled() {
-    static const bool on = [] {
-        const char* e = getenv("SIFT_MI_BLUR_KERNEL");
-        return !(e && !strcmp(e, "tile"));
-    }();
-    return on;
+    const char* e = getenv("SIFT_MI_BLUR_KERNEL");
+    return !(e && !strcmp(e, "tile"));
 }
 
 int launch_blur(int R, const BlurLaunch& L, hipStream_t st) {
@@ -991,8 +1184,52 @@ int launch_seed(int R, const SeedLaunch& L, hipStream_t st) {
         return 0;
     }
     if (R != 5) return -1;
+    // the strip seed: exact 2x geometry, frames wide / tall enough for one
+    // reflection of every window (else the tile kernel)
+    if (L.W == 2 * L.sw && L.H == 2 * L.sh && L.W >= 160 && L.H >= 64 &&
+        (uint64_t)L.H * (uint64_t)L.pitch * 4 < (1ull << 31) && strip_blur_enabled()) {
+        using G = StripGeom<5, 16>;
+        const int ya = L.y1 > L.y0 ? std::max(L.y0, 0) : 0;
+        const int yb = L.y1 > L.y0 ? std::min(L.y1, L.H) : L.H;
+        if (yb <= ya) return 0;
+        const int strips = (L.W + G::TW - 1) / G::TW;
+        const int rows = yb - ya;
+        const long per = (long)strips * L.n_img;
+        int nseg = (int)std::min<long>(rows / (2 * G::S) + 1, (12288 + per - 1) / per);
+        nseg = std::max(1, nseg);
+        const int seg = (rows + nseg - 1) / nseg;
+        nseg = (rows + seg - 1) / seg;
+        hipLaunchKernelGGL((k_seed_strip<5>), dim3(strips, nseg, L.n_img), dim3(256), 0, st, L.frames, L.frame_pitch,
+                           L.row_stride, L.sh, L.sw, L.tab, L.dst, L.dst_img_stride, L.W, L.H, L.pitch, L.taps, ya,
+                           yb, seg);
+        return 0;
+    }
     launch_seed_r<5>(L, st);
     return 0;
+}
+
+// ---------------------------------------------------------------------------
+// DoG planes of precompute_images (build_dog, src/lib.rs:271-279): D_s =
+// G_{s+1} - G_s over whole pitched planes (4 floats per thread; the padding
+// columns are never read back).
+// ---------------------------------------------------------------------------
+__global__ void k_dog(const float* __restrict__ gauss, size_t plane, size_t g_img_stride, float* __restrict__ dog,
+                      size_t dog_img_stride, size_t n4) {
+    const size_t i = (size_t)blockIdx.x * 256 + threadIdx.x;
+    if (i >= n4) return;
+    const float* g = gauss + (size_t)blockIdx.z * g_img_stride + (size_t)blockIdx.y * plane;
+    float* d = dog + (size_t)blockIdx.z * dog_img_stride + (size_t)blockIdx.y * plane;
+    const float4 a = reinterpret_cast<const float4*>(g)[i];
+    const float4 b = reinterpret_cast<const float4*>(g + plane)[i];
+    reinterpret_cast<float4*>(d)[i] = make_float4(b.x - a.x, b.y - a.y, b.z - a.z, b.w - a.w);
+}
+
+void launch_dog(const float* gauss, size_t plane, size_t g_img_stride, float* dog, size_t dog_img_stride, int W, int H,
+                int pitch, int n_img, hipStream_t st) {
+    (void)W;
+    const size_t n4 = (size_t)pitch * H / 4;  // pitch: a multiple of 64 floats
+    hipLaunchKernelGGL(k_dog, dim3((unsigned)((n4 + 255) / 256), kDogPerOctave, n_img), dim3(256), 0, st, gauss,
+                       plane, g_img_stride, dog, dog_img_stride, n4);
 }
 
 // ---------------------------------------------------------------------------

@@ -69,21 +69,6 @@ struct SeedLaunch {
     BlurTaps taps;
 };
 
-// octave.hip: fused five-blur + DoG streaming kernel (OpenCV profile)
-struct OctaveArgs {
-    float* gauss;  // octave G stack of image 0 (plane s at + s * plane)
-    size_t g_img_stride, plane;
-    float* dog;  // octave D stack of image 0
-    size_t dog_img_stride;
-    float* nxt;  // next octave base (nearest 1/2 of G_3), may be null
-    size_t nxt_img_stride;
-    int pitch_n, wn, hn;
-    int W, H, pitch;
-    int seg_rows;  // rows per workgroup segment
-    int write_all;  // materialise G_4 and G_5 too (precompute_images); the batch path keeps them on chip
-    BlurTaps taps[6];  // taps[s] for s = 1..5
-};
-int launch_octave(const OctaveArgs& a, int n_img, hipStream_t st);
 
 // jpeg.hip: baseline JPEG -> 8-bit luma (zune-jpeg + image::grayscale arithmetic)
 int jpeg_dims(const uint8_t* data, size_t len, uint32_t* w, uint32_t* h, std::string& err);
@@ -101,13 +86,13 @@ struct JpegBatchCache {
 };
 int jpeg_decode_batch(const uint8_t* const* data, const size_t* len, uint32_t n, uint8_t* d_out, size_t frame_pitch,
                       size_t stride, int threads, hipStream_t st, JpegBatchCache& cache, std::string& err);
-int octave_strip_width();
-int octave_min_width();
-bool octave_radii_supported(const int* r);  // r[1..5]
 
 // pyramid.hip
 int launch_blur(int radius, const BlurLaunch& L, hipStream_t st);
 int launch_seed(int radius, const SeedLaunch& L, hipStream_t st);
+// D_s = G_{s+1} - G_s (s < 5) of an octave's G stack, for n images
+void launch_dog(const float* gauss, size_t plane, size_t g_img_stride, float* dog, size_t dog_img_stride, int W, int H,
+                int pitch, int n_img, hipStream_t st);
 void launch_resize_linear_f32(const float* src, int sw, int sh, const ResizeTab& tab, float* dst, int dw, int dh,
                               hipStream_t st);
 // image::imageops::resize (Imageproc profile, op level): generic tap tables

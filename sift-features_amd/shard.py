@@ -5,11 +5,17 @@ process per GPU (torch.distributed, RCCL backend on MI355X), with no
 data-path collective: every rank runs the whole path on its own frames.  The
 only collectives are
   * `reduce_run`    -- the benchmark's max-over-ranks time and summed counts;
-  * `gather_results` -- the optional "trivial keypoint gather" of the north
-                        star: per-rank results concatenated on one rank in
-                        global frame order (sizes first, then padded payloads
-                        in one gather per array).
-Both run unchanged on gloo (CPU tensors; tests/test_shard.py) and RCCL (GPU
+  * `gather_device_results` -- the "trivial keypoint gather" of the north
+                        star on the throughput path: every rank's
+                        device-resident results (`device_results`: zero-copy
+                        views of the context's result arena) land in one
+                        concatenated device tensor on rank `dst`, in global
+                        frame order -- sizes all-gathered, then each rank's
+                        exact rows sent point-to-point (RCCL send/recv over
+                        xGMI) into their slice: no padding, no host round trip;
+  * `gather_results` -- the same for host arrays (padded payloads in one
+                        gather per array).
+All run unchanged on gloo (CPU tensors; tests/test_shard.py) and RCCL (GPU
 tensors).
 
 One large frame splits by ROW BANDS instead:
@@ -102,6 +108,96 @@ def gather_results(keypoints, descriptors, offsets, dist, dst=0):
         base += ns[r]
     return (np.concatenate(k_all).reshape(-1, 5), np.concatenate(d_all).reshape(-1, 128),
             np.asarray(o_all, dtype=np.int64))
+
+
+class _DeviceArray:
+    """__cuda_array_interface__ view of raw device memory (torch.as_tensor
+    wraps it without a copy)."""
+
+    def __init__(self, ptr, shape, typestr):
+        self.__cuda_array_interface__ = {"shape": tuple(shape), "typestr": typestr, "data": (int(ptr), False),
+                                         "version": 2, "strides": None}
+
+
+def _wrap_device(ptr, shape, dtype, device):
+    import torch
+    if int(np.prod(shape)) == 0:
+        return torch.empty(shape, dtype=dtype, device=device)
+    typestr = {torch.float32: "<f4", torch.uint8: "|u1", torch.int64: "<i8"}[dtype]
+    return torch.as_tensor(_DeviceArray(ptr, shape, typestr), device=device)
+
+
+def device_results(ctx, device=None):
+    """(keypoints (n, 5) f32, descriptors (n, 128) u8) torch tensors on the
+    context's GPU over the results of its last sift_batch_device(...,
+    fetch=False) call -- every frame's keypoints and descriptors in frame
+    order (sift_mi_device_results), wrapped without a copy; valid until the
+    context's next call."""
+    import torch
+    kp, desc, n = ctx.device_results()
+    dev = torch.device("cuda", torch.cuda.current_device()) if device is None else torch.device(device)
+    return _wrap_device(kp, (n, 5), torch.float32, dev), _wrap_device(desc, (n, 128), torch.uint8, dev)
+
+
+def gather_device_results(keypoints, descriptors, offsets, dist, dst=0):
+    """Gather every rank's results -- (keypoints (n, 5) f32, descriptors
+    (n, 128) u8) tensors, e.g. `device_results(ctx)`, and the per-frame
+    offsets (m + 1,) of its frames -- on rank `dst`, concatenated in rank
+    (= global frame) order.
+
+    Sizes are all-gathered first; then every other rank sends its exact rows
+    (raw bits) and rank `dst` receives them straight into its slice of the
+    concatenated output (one batch of point-to-point ops: RCCL send/recv over
+    xGMI on the nccl backend, device memory end to end; on gloo the tensors
+    travel through host memory).  Returns (keypoints, descriptors, offsets)
+    tensors on `dst` -- on the GPU for nccl -- and None elsewhere.
+    """
+    import torch
+    world, rank = dist.get_world_size(), dist.get_rank()
+    dev = _device(dist)
+    kps = keypoints.reshape(-1, 5).view(torch.int32)
+    desc = descriptors.reshape(-1, 128)
+    offs = torch.as_tensor(np.asarray(offsets, dtype=np.int64))
+    n, m = kps.shape[0], offs.numel() - 1
+    if desc.shape[0] != n or int(offs[-1] - offs[0]) != n:
+        raise ValueError("keypoints / descriptors / offsets disagree")
+    kps, desc, offs = kps.to(dev), desc.to(dev), (offs - offs[0]).to(dev)
+    sizes = torch.tensor([n, m], dtype=torch.int64, device=dev)
+    all_sizes = [torch.zeros_like(sizes) for _ in range(world)]
+    dist.all_gather(all_sizes, sizes)
+    ns = [int(x[0]) for x in all_sizes]
+    ms = [int(x[1]) for x in all_sizes]
+    ops = []
+    if rank == dst:
+        K = torch.empty((sum(ns), 5), dtype=torch.int32, device=dev)
+        D = torch.empty((sum(ns), 128), dtype=torch.uint8, device=dev)
+        O = [torch.empty(ms[r] + 1, dtype=torch.int64, device=dev) for r in range(world)]
+        start = 0
+        for r in range(world):
+            k, d = K[start:start + ns[r]], D[start:start + ns[r]]
+            if r == dst:
+                k.copy_(kps)
+                d.copy_(desc)
+                O[r].copy_(offs)
+            else:
+                ops.append(dist.P2POp(dist.irecv, O[r], r))
+                if ns[r]:
+                    ops += [dist.P2POp(dist.irecv, k, r), dist.P2POp(dist.irecv, d, r)]
+            start += ns[r]
+    else:
+        ops.append(dist.P2POp(dist.isend, offs, dst))
+        if n:
+            ops += [dist.P2POp(dist.isend, kps.contiguous(), dst), dist.P2POp(dist.isend, desc.contiguous(), dst)]
+    if ops:
+        for q in dist.batch_isend_irecv(ops):
+            q.wait()
+    if rank != dst:
+        return None
+    base, parts = 0, [torch.zeros(1, dtype=torch.int64, device=dev)]
+    for r in range(world):
+        parts.append(O[r][1:] + base)
+        base += ns[r]
+    return K.view(torch.float32), D, torch.cat(parts)
 
 
 def merge_bands(parts):

@@ -126,6 +126,7 @@ class Context:
         check(lib().sift_mi_create(device, self.profile, ctypes.byref(h)))
         self._h = h
         self._generation = 0
+        self._keep_dev = False  # sift_mi_set_keep_on_device state
 
     def close(self):
         if getattr(self, "_h", None):
@@ -164,6 +165,13 @@ class Context:
         check(lib().sift_mi_reset_stats(self._h))
 
     # -- results ------------------------------------------------------------
+    def _keep(self, on):
+        """Results to host buffers (False: every host-returning call) or left
+        in HBM (True: sift_batch_device(..., fetch=False))."""
+        if bool(on) != self._keep_dev:
+            check(lib().sift_mi_set_keep_on_device(self._h, 1 if on else 0))
+            self._keep_dev = bool(on)
+
     def _fetch(self, n, with_keys=True, out=None):
         if out is not None:
             kps, desc, keys = out.views(n)
@@ -182,6 +190,7 @@ class Context:
     def sift(self, img, features_limit=None):
         a = _u8_image(img)
         n = ctypes.c_size_t()
+        self._keep(False)
         check(lib().sift_mi_extract(self._h, a.ctypes.data, a.shape[1], a.shape[0], a.strides[0],
                                     _limit(features_limit), ctypes.byref(n)))
         return SiftResult(*self._fetch(n.value))
@@ -194,6 +203,7 @@ class Context:
         n, h, w = f.shape
         ptrs = (ctypes.c_void_p * n)(*[f[i].ctypes.data for i in range(n)])
         offs = (ctypes.c_size_t * (n + 1))()
+        self._keep(False)
         check(lib().sift_mi_extract_batch(self._h, ptrs, n, w, h, w, _limit(features_limit), offs))
         kps, desc, keys = self._fetch(offs[n])
         return [SiftResult(kps[offs[i]:offs[i + 1]], desc[offs[i]:offs[i + 1]], keys[offs[i]:offs[i + 1]])
@@ -207,7 +217,7 @@ class Context:
         the returned SiftResult then holds views into it, valid until the
         buffers are reused."""
         offs = (ctypes.c_size_t * (n + 1))()
-        check(lib().sift_mi_set_keep_on_device(self._h, 0 if fetch else 1))
+        self._keep(not fetch)
         check(lib().sift_mi_extract_batch_device(self._h, ctypes.c_void_p(d_frames_ptr), frame_pitch, n, width,
                                                  height, row_stride, _limit(features_limit), offs))
         offsets = np.array(offs[:], dtype=np.int64)
@@ -239,6 +249,7 @@ class Context:
     def sift_with_precomputed(self, pre, features_limit=None):
         pre._check()
         n = ctypes.c_size_t()
+        self._keep(False)
         check(lib().sift_mi_sift_with_precomputed(self._h, _limit(features_limit), ctypes.byref(n)))
         return SiftResult(*self._fetch(n.value))
 

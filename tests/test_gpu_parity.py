@@ -80,21 +80,17 @@ def test_pyramid_bit_exact(ctx, oracle, name):
         assert np.array_equal(d, do), (o, np.abs(d - do).max())
 
 
-@pytest.mark.parametrize("name,seg", [("synth_640x480", None), ("synth_640x480", 37), ("synth_640x480", 200),
-                                      ("synth_301x207", 64), ("synth_97x61", 9), ("synth_1000x333", None),
-                                      ("synth_1000x333", 101), ("unfused:synth_301x207", None)])
-def test_pyramid_fused_octave(ctx, oracle, monkeypatch, name, seg):
-    """octave.hip (one streaming kernel per octave: a loader wave + two waves
-    per blur level, row segments of `seg` rows, 180-column strips with
-    reflect-101 mirrors at the image borders) against
-    the oracle's blur chain, bit for bit; "unfused:" runs the per-blur kernels."""
-    if name.startswith("unfused:"):
-        name = name.split(":", 1)[1]
-        monkeypatch.setenv("SIFT_MI_FUSED_OCTAVE", "0")
-    else:
-        monkeypatch.setenv("SIFT_MI_FUSED_OCTAVE", "1")
-    if seg is not None:
-        monkeypatch.setenv("SIFT_MI_OCT_SEG", str(seg))
+@pytest.mark.parametrize("kernel", ["strip", "tile"])
+@pytest.mark.parametrize("name", ["synth_640x480", "synth_301x207", "synth_97x61", "synth_1000x333",
+                                  "synth_90x700", "synth_2000x40", "synth_33x17"])
+def test_pyramid_blur_kernels(ctx, oracle, monkeypatch, kernel, name):
+    """Both blur kernel families against the oracle's blur chain, bit for bit:
+    "strip" (k_seed_strip / k_blur_strip: 128-column strips streamed down in
+    row chunks, many row segments per octave at these sizes, partial strips,
+    reflect-101 at every border; the tile kernels where a strip does not
+    apply: tiny octaves, W or H <= R) and "tile" (SIFT_MI_BLUR_KERNEL=tile:
+    one 64-column tile per workgroup everywhere)."""
+    monkeypatch.setenv("SIFT_MI_BLUR_KERNEL", kernel)
     img = INPUTS[name] if name in INPUTS else _extra(name)
     pre = ctx.precompute_images(img)
     opy = oracle.Pyramid(img)

@@ -22,7 +22,8 @@ def _fake_result(rank, frames):
     counts = [3 + f + rank for f in range(frames)]
     n = sum(counts)
     kps = rng.standard_normal((n, 5)).astype(np.float32)
-    kps[0, 0] = np.float32(np.nan) if rank == 1 else kps[0, 0]  # bit-exact transport, NaN included
+    if n and rank % 2 == 1:
+        kps[0, 0] = np.float32(np.nan)  # bit-exact transport, NaN included
     desc = rng.integers(0, 256, (n, 128), dtype=np.uint8)
     offs = np.concatenate([[0], np.cumsum(counts)]).astype(np.int64)
     return kps, desc, offs
@@ -80,6 +81,56 @@ def test_gloo_world2_shard_reduce_gather():
     assert np.array_equal(kps.view(np.uint32), np.concatenate([k0, k1]).view(np.uint32))
     assert np.array_equal(desc, np.concatenate([d0, d1]))
     assert np.array_equal(offs, np.concatenate([o0, o1[1:] + o0[-1]]))
+
+
+def _dev_worker(rank, world, port, q):
+    import sys
+    import torch
+    import torch.distributed as dist
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, os.path.join(root, "sift-features_amd"))
+    import shard
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    dist.init_process_group("gloo", rank=rank, world_size=world)
+    try:
+        frames = [4, 0, 3][rank]  # rank 1 has no frames at all
+        kps, desc, offs = _fake_result(rank, frames)
+        g = shard.gather_device_results(torch.from_numpy(kps), torch.from_numpy(desc), offs, dist, dst=0)
+        q.put(("ok", rank, None if g is None else tuple(t.numpy() for t in g)))
+    except Exception as e:  # pragma: no cover - surfaced by the assert below
+        q.put(("err", rank, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.timeout(120)
+def test_gloo_world3_gather_device_results():
+    """shard.gather_device_results (the bench's N > 1 gather: sizes, then
+    point-to-point rows into rank 0's concatenated output) on gloo with three
+    ranks, one of them empty: exact bits (NaN included) in frame order."""
+    import multiprocessing as mp
+    ctx = mp.get_context("spawn")
+    q = ctx.Queue()
+    port = _free_port()
+    procs = [ctx.Process(target=_dev_worker, args=(r, 3, port, q)) for r in range(3)]
+    for p in procs:
+        p.start()
+    res = [q.get(timeout=100) for _ in range(3)]
+    for p in procs:
+        p.join(timeout=30)
+        assert p.exitcode == 0
+    assert all(r[0] == "ok" for r in res), res
+    kps, desc, offs = next(r[2] for r in res if r[1] == 0)
+    parts = [_fake_result(r, [4, 0, 3][r]) for r in range(3)]
+    assert np.array_equal(kps.view(np.uint32), np.concatenate([p[0] for p in parts]).view(np.uint32))
+    assert np.array_equal(desc, np.concatenate([p[1] for p in parts]))
+    want, base = [0], 0
+    for p in parts:
+        want += (p[2][1:] + base).tolist()
+        base += len(p[0])
+    assert np.array_equal(offs, np.asarray(want))
+    assert all(r[2] is None for r in res if r[1] != 0)
 
 
 def test_shard_range_partition():

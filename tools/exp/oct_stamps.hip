@@ -3,7 +3,7 @@
 // octave-0-sized batch.  Build + run (GPU box):
 //   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -DSIFT_OCT_STAMPS \
 //         tools/exp/oct_stamps.hip -o tools/exp/oct_stamps && tools/exp/oct_stamps [W H n]
-#include "../../sift-features_amd/csrc/octave.hip"
+#include "octave.hip"
 
 #include <cstdio>
 #include <cstdlib>

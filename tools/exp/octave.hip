@@ -1,6 +1,11 @@
 // Fused octave kernel: the five incremental blurs of one octave and its DoG in
 // one streaming pass (OpenCV profile).
 //
+// EXPERIMENT RECORD (not built into libsift_mi.so): measured slower than the
+// per-blur kernels and superseded by the strip blur kernels
+// (pyramid.hip k_blur_strip).  Kept with its harnesses (oct_stamps.hip,
+// oct_trace.sh) for the measurements DESIGN.md cites.
+//
 // Reference: build_gaussian_scale_space / build_dog (src/lib.rs:213-279) with
 // OpenCVProcessing::gaussian_blur (src/opencv_processing.rs:38-49):
 // G_s = blur(G_{s-1}, sigma_s), s = 1..5, D_{s-1} = G_s - G_{s-1}, and the next
@@ -44,10 +49,26 @@
 // next level's stage row (one reflection: needs W > hp(1) + 1).
 // Bit-identical to k_blur (same operations in the same order), checked by
 // tests/test_gpu_parity.py against the C oracle.
-#include "sift_common.h"
-#include "sift_kernels.h"
+#include "../../sift-features_amd/csrc/sift_common.h"
+#include "../../sift-features_amd/csrc/sift_kernels.h"
 
 namespace siftmi {
+
+// launch arguments (formerly in sift_kernels.h)
+struct OctaveArgs {
+    float* gauss;  // octave G stack of image 0 (plane s at + s * plane)
+    size_t g_img_stride, plane;
+    float* dog;  // octave D stack of image 0
+    size_t dog_img_stride;
+    float* nxt;  // next octave base (nearest 1/2 of G_3), may be null
+    size_t nxt_img_stride;
+    int pitch_n, wn, hn;
+    int W, H, pitch;
+    int seg_rows;  // rows per workgroup segment
+    int write_all;  // materialise G_4 and G_5 too (precompute_images); the batch path keeps them on chip
+    BlurTaps taps[6];  // taps[s] for s = 1..5
+};
+
 namespace oct {
 
 constexpr int kL = 5;                                  // blurs per octave (s = 1..5)
