@@ -728,7 +728,16 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
         }
         bytes = (uint64_t)b;
     }
-    for (int o = 0; o < p.n_oct; o++) {
+    // the small octaves from o_tail on: one k_octave_tail launch
+    // (SIFT_MI_TAIL=0: per-blur launches for every octave; A/B and test knob)
+    int o_tail = p.n_oct;
+    {
+        const char* e = getenv("SIFT_MI_TAIL");
+        if (!(e && !strcmp(e, "0")) && p.n_oct <= kTailMaxOct)
+            o_tail = tail_octave_start(p.ow.data(), p.oh.data(), p.n_oct,
+                                       *std::max_element(p.oct_r + 1, p.oct_r + kImagesPerOctave));
+    }
+    for (int o = 0; o < o_tail; o++) {
         float* G = p.gauss(o, lane);
         float* D = p.dog(o, lane);
         const size_t P = p.P[o];
@@ -761,6 +770,32 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
         // precompute_images: D_s = G_{s+1} - G_s, the same f32 subtraction
         // the keypoint stages form where they read the DoG
         if (full) launch_dog(G, P, p.gstride(o), D, p.dstride(o), p.ow[o], p.oh[o], p.opitch[o], (int)n, st);
+    }
+    if (o_tail < p.n_oct) {
+        // whole octaves (a row band's restricted rows are a subset: rows outside
+        // them depend only on rows outside them, so the exact rows stay exact)
+        TailLaunch T{};
+        for (int o = 0; o < p.n_oct; o++) {
+            T.gauss[o] = p.gauss(o, lane);
+            T.gstride[o] = p.gstride(o);
+            T.ow[o] = p.ow[o];
+            T.oh[o] = p.oh[o];
+            T.pitch[o] = p.opitch[o];
+        }
+        T.o0 = o_tail;
+        T.n_oct = p.n_oct;
+        T.n_img = (int)n;
+        T.profile = p.profile;
+        for (int s = 1; s < kImagesPerOctave; s++) {
+            T.r[s] = p.oct_r[s];
+            T.taps[s] = p.oct_taps[s];
+        }
+        launch_octave_tail(T, st);
+        launches++;
+        if (full)
+            for (int o = o_tail; o < p.n_oct; o++)
+                launch_dog(p.gauss(o, lane), p.P[o], p.gstride(o), p.dog(o, lane), p.dstride(o), p.ow[o], p.oh[o],
+                           p.opitch[o], (int)n, st);
     }
     HIPCHK(hipGetLastError());
     c->stats.pyramid_launches += launches;

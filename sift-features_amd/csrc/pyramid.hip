@@ -1209,6 +1209,216 @@ int launch_seed(int R, const SeedLaunch& L, hipStream_t st) {
 }
 
 // ---------------------------------------------------------------------------
+// k_octave_tail: every small octave of a frame in ONE launch.  From octave o0
+// on (the first octave whose planes fit the LDS layout below) a workgroup
+// owns one frame: it reads G_0 of octave o0 into LDS, runs the five
+// incremental blurs of the octave LDS to LDS, stores every G_s, forms the
+// next octave's G_0 (nearest 1/2 of G_3) in LDS while G_3 is written, and
+// carries on to the last octave.  The arithmetic is exactly k_blur's (OpenCV:
+// fma chain from the leftmost tap, then centre product + fma of the (below +
+// above) pair sums; imageproc: unfused chains from the first tap).  This
+// replaces 5 launches per tail octave (a few tiles per frame each, bound by
+// launch and pipeline-fill latency) with one.
+//
+// A tail octave is a few thousand pixels per workgroup, so the passes are
+// bound by LDS latency along each output's tap chain: the borders are
+// materialised instead of evaluated per tap (reflect-101 / clamp-to-edge halo
+// columns of the blur input, halo rows of the row-pass output, filled by a
+// pass of their own), so every tap read is a plain offset, and each thread
+// carries four independent chains (four outputs of a row / of a column).
+// LDS layout (floats), with Rm the largest radius of the octave's blurs:
+//   A, B  G_{s-1} / G_s:     H rows of W + 2 Rm (column halos), x at + Rm
+//   T     row-pass output:   H + 2 Rm rows of W (row halos), y at + Rm
+//   N     next octave G_0:   (H / 2) x (W / 2), dense
+// ---------------------------------------------------------------------------
+template <int P>
+__device__ __forceinline__ int tail_index(int p, int n) {
+    return P == kProfileOpenCV ? reflect101(p, n) : clamp_idx(p, n);
+}
+
+__host__ __device__ inline int tail_lds_floats(int W, int H, int rm) {
+    return 2 * (W + 2 * rm) * H + W * (H + 2 * rm) + (W / 2) * (H / 2);
+}
+
+// halo columns [-R, 0) and [W, W + R) of every row of X (pitch W + 2 Rm)
+template <int P>
+__device__ __forceinline__ void tail_fill_cols(float* X, int W, int H, int Rm, int R) {
+    const int PA = W + 2 * Rm;
+    for (int i = threadIdx.x; i < H * 2 * R; i += 1024) {
+        const int y = i / (2 * R), j = i - y * (2 * R);
+        const int p = j < R ? j - R : W + j - R;
+        float* row = X + y * PA + Rm;
+        row[p] = row[tail_index<P>(p, W)];
+    }
+}
+
+template <int P>
+__device__ __forceinline__ void tail_blur(float* __restrict__ A, float* __restrict__ T, float* __restrict__ B,
+                                          const float* __restrict__ kf, int R, int Rn, int Rm, int W, int H,
+                                          float* __restrict__ g, int pitch, bool nxt, float* __restrict__ N,
+                                          float* __restrict__ gn, int wn, int hn, int pn) {
+    constexpr int Q = 4;
+    const int PA = W + 2 * Rm;
+    // row pass (A's halo columns are in place): fma chain from the leftmost
+    // tap (OpenCV) / unfused chain (imageproc); item = (row, 4 columns).  The
+    // last item of a row may read past its halo (into the next row / buffer:
+    // still LDS) for columns >= W, which are not stored.
+    const int qw = (W + Q - 1) / Q;
+    for (int i = threadIdx.x; i < H * qw; i += 1024) {
+        const int y = i / qw, x0 = (i - y * qw) * Q;
+        const float* p = A + y * PA + Rm + x0 - R;
+        float acc[Q];
+#pragma unroll
+        for (int q = 0; q < Q; q++) acc[q] = p[q] * kf[0];
+#pragma unroll 4
+        for (int t = 1; t <= 2 * R; t++) {
+            const float kt = kf[t];
+#pragma unroll
+            for (int q = 0; q < Q; q++)
+                acc[q] = P == kProfileOpenCV ? __builtin_fmaf(p[q + t], kt, acc[q]) : acc[q] + p[q + t] * kt;
+        }
+        float* o = T + (y + Rm) * W + x0;
+#pragma unroll
+        for (int q = 0; q < Q; q++)
+            if (x0 + q < W) o[q] = acc[q];
+    }
+    __syncthreads();
+    // T's halo rows [-R, 0) and [H, H + R)
+    for (int i = threadIdx.x; i < 2 * R * W; i += 1024) {
+        const int j = i / W, x = i - j * W;
+        const int p = j < R ? j - R : H + j - R;
+        T[(p + Rm) * W + x] = T[(tail_index<P>(p, H) + Rm) * W + x];
+    }
+    __syncthreads();
+    // column pass: centre product + fma of the (below + above) pair sums
+    // (OpenCV) / the unfused chain from the first tap (imageproc); item =
+    // (column, 4 consecutive rows), lanes along the row (coalesced stores)
+    const int qh = (H + Q - 1) / Q;
+    constexpr int par = P == kProfileOpenCV ? 0 : 1;  // nearest 1/2: (2x, 2y) / (2x + 1, 2y + 1)
+    for (int i = threadIdx.x; i < W * qh; i += 1024) {
+        const int yq = i / W, x = i - yq * W, y0 = yq * Q;
+        const float* p = T + (y0 + Rm) * W + x;  // row y0
+        float acc[Q];
+        if constexpr (P == kProfileOpenCV) {
+#pragma unroll
+            for (int q = 0; q < Q; q++) acc[q] = p[q * W] * kf[R];
+#pragma unroll 4
+            for (int t = 1; t <= R; t++) {
+                const float kt = kf[R + t];
+#pragma unroll
+                for (int q = 0; q < Q; q++) acc[q] = __builtin_fmaf(p[(q + t) * W] + p[(q - t) * W], kt, acc[q]);
+            }
+        } else {
+#pragma unroll
+            for (int q = 0; q < Q; q++) acc[q] = p[(q - R) * W] * kf[0];
+#pragma unroll 4
+            for (int t = 1; t <= 2 * R; t++) {
+                const float kt = kf[t];
+#pragma unroll
+                for (int q = 0; q < Q; q++) acc[q] = acc[q] + p[(q - R + t) * W] * kt;
+            }
+        }
+#pragma unroll
+        for (int q = 0; q < Q; q++) {
+            const int y = y0 + q;
+            if (y >= H) break;
+            B[y * PA + Rm + x] = acc[q];
+            g[(size_t)y * pitch + x] = acc[q];
+            if (nxt && (x & 1) == par && (y & 1) == par && (x >> 1) < wn && (y >> 1) < hn) {
+                N[(y >> 1) * wn + (x >> 1)] = acc[q];
+                gn[(size_t)(y >> 1) * pn + (x >> 1)] = acc[q];
+            }
+        }
+    }
+    __syncthreads();
+    if (Rn > 0) {  // B's halo columns for the next blur
+        tail_fill_cols<P>(B, W, H, Rm, Rn);
+        __syncthreads();
+    }
+}
+
+template <int P>
+__global__ __launch_bounds__(1024) void k_octave_tail(const TailLaunch L) {
+    __shared__ float lds[kTailLdsFloats];
+    __shared__ float kf[kImagesPerOctave][2 * kMaxBlurRadius + 1];
+    const int tid = threadIdx.x;
+    const int b = blockIdx.x;
+    if (tid < (kImagesPerOctave - 1) * 64) {
+        const int s = 1 + tid / 64, t = tid % 64, R = L.r[s];
+        if (t <= 2 * R) kf[s][t] = L.taps[s].k[t > R ? t - R : R - t];
+    }
+    int Rm = 0;
+    for (int s = 1; s < kImagesPerOctave; s++) Rm = max(Rm, L.r[s]);
+    for (int o = L.o0; o < L.n_oct; o++) {
+        const int W = L.ow[o], H = L.oh[o], pitch = L.pitch[o], PA = W + 2 * Rm;
+        float* A = lds;                    // G_{s-1}
+        float* B = A + PA * H;             // G_s
+        float* T = B + PA * H;             // row-pass output
+        float* N = T + W * (H + 2 * Rm);   // next octave's G_0
+        float* g = L.gauss[o] + (size_t)b * L.gstride[o];
+        const size_t plane = (size_t)pitch * H;
+        const bool has_next = o + 1 < L.n_oct;
+        const int wn = has_next ? L.ow[o + 1] : 0, hn = has_next ? L.oh[o + 1] : 0;
+        float* gn = has_next ? L.gauss[o + 1] + (size_t)b * L.gstride[o + 1] : nullptr;
+        const int pn = has_next ? L.pitch[o + 1] : 0;
+        // G_0: from HBM (first tail octave) or from the previous octave's N
+        // (which overlaps this octave's A / B: copy through registers)
+        if (o == L.o0) {
+            for (int y = tid >> 6; y < H; y += 16)
+                for (int x = tid & 63; x < W; x += 64) A[y * PA + Rm + x] = g[(size_t)y * pitch + x];
+        } else {
+            const int Wp = L.ow[o - 1], Hp = L.oh[o - 1];
+            const float* Np = lds + 2 * (Wp + 2 * Rm) * Hp + Wp * (Hp + 2 * Rm);
+            float v[4];  // W * H <= 4096 here (checked by tail_octave_start)
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int i = tid + 1024 * k;
+                v[k] = i < W * H ? Np[i] : 0.0f;
+            }
+            __syncthreads();
+#pragma unroll
+            for (int k = 0; k < 4; k++) {
+                const int i = tid + 1024 * k;
+                if (i < W * H) {
+                    const int y = i / W, x = i - y * W;
+                    A[y * PA + Rm + x] = v[k];
+                }
+            }
+        }
+        __syncthreads();
+        tail_fill_cols<P>(A, W, H, Rm, L.r[1]);
+        __syncthreads();
+#pragma unroll 1
+        for (int s = 1; s < kImagesPerOctave; s++) {
+            tail_blur<P>(A, T, B, kf[s], L.r[s], s + 1 < kImagesPerOctave ? L.r[s + 1] : 0, Rm, W, H, g + s * plane,
+                         pitch, s == 3 && has_next, N, gn, wn, hn, pn);
+            float* t = A;
+            A = B;
+            B = t;
+        }
+    }
+}
+
+int tail_octave_start(const int* ow, const int* oh, int n_oct, int rmax) {
+    for (int o = 0; o < n_oct; o++) {
+        // the G_0 hand-over copies <= 4 values per thread: the octave after
+        // the first tail octave must have at most 4096 pixels
+        const bool next_ok = o + 1 >= n_oct || ow[o + 1] * oh[o + 1] <= 4096;
+        // (+ slack: the last row / column items read up to 3 rows / columns past their halo)
+        if (tail_lds_floats(ow[o], oh[o], rmax) + 4 * ow[o] + 64 <= kTailLdsFloats && next_ok) return o;
+    }
+    return n_oct;
+}
+
+void launch_octave_tail(const TailLaunch& L, hipStream_t st) {
+    if (L.o0 >= L.n_oct || L.n_img <= 0) return;
+    if (L.profile == kProfileImageproc)
+        hipLaunchKernelGGL(k_octave_tail<kProfileImageproc>, dim3(L.n_img), dim3(1024), 0, st, L);
+    else
+        hipLaunchKernelGGL(k_octave_tail<kProfileOpenCV>, dim3(L.n_img), dim3(1024), 0, st, L);
+}
+
+// ---------------------------------------------------------------------------
 // DoG planes of precompute_images (build_dog, src/lib.rs:271-279): D_s =
 // G_{s+1} - G_s over whole pitched planes (4 floats per thread; the padding
 // columns are never read back).

@@ -87,6 +87,24 @@ struct JpegBatchCache {
 int jpeg_decode_batch(const uint8_t* const* data, const size_t* len, uint32_t n, uint8_t* d_out, size_t frame_pitch,
                       size_t stride, int threads, hipStream_t st, JpegBatchCache& cache, std::string& err);
 
+// Every octave from o0 on of n_img frames in one launch (k_octave_tail): a
+// workgroup per frame, the octave's planes in LDS.  The octave G bases are
+// the lane arena's; G_0 of octave o0 must be in place.
+constexpr int kTailMaxOct = 16;
+constexpr int kTailLdsFloats = 39680;  // 155 KB: A, B, T with halos + the next G_0 (pyramid.hip)
+struct TailLaunch {
+    float* gauss[kTailMaxOct];
+    size_t gstride[kTailMaxOct];
+    int ow[kTailMaxOct], oh[kTailMaxOct], pitch[kTailMaxOct];
+    int o0, n_oct, n_img, profile;
+    int r[kImagesPerOctave];
+    BlurTaps taps[kImagesPerOctave];
+};
+// first octave that fits the tail kernel (n_oct: none); rmax = the largest
+// blur radius of an octave
+int tail_octave_start(const int* ow, const int* oh, int n_oct, int rmax);
+void launch_octave_tail(const TailLaunch& L, hipStream_t st);
+
 // pyramid.hip
 int launch_blur(int radius, const BlurLaunch& L, hipStream_t st);
 int launch_seed(int radius, const SeedLaunch& L, hipStream_t st);

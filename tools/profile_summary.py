@@ -1,19 +1,30 @@
 """Summarise a round profile (tools/round_profile.sh) into profiles/.
 
-Writes
+    python3 tools/profile_summary.py <round> <out dir> <frames per call>
+
+Reads the passes under <out dir> (trace/, fetch/, write/, sq1/, sq2/; raw
+CSVs, optionally gzipped) and writes
   profiles/<round>_kernel_stats.csv   rocprofv3 --stats output (copied)
-  profiles/<round>_summary.md         per-kernel table, the pyramid stage from
+  profiles/<round>_summary.md         per-kernel table; the pyramid stage from
                                       the trace next to bench.py's own number,
-                                      and HBM traffic from the PMC passes
-  profiles/pmc_traffic.json           per-frame pyramid traffic, read by
+                                      per launch position (octave, blur) of the
+                                      serialised pass; HBM traffic from the
+                                      PMC passes; SQ counters per kernel
+  profiles/pmc_traffic.json           pyramid traffic per launch, read by
                                       bench.py for roofline.traffic
+and copies of them into <out dir>/profiles/ (gpurun merges only gpurun_out/).
 HBM bytes follow MI355X_MICROARCH.md (HBM section): FETCH_SIZE and WRITE_SIZE
 are in KiB; on gfx950 FETCH_SIZE counts half the bytes of 16-B-per-lane
 streaming reads (doubled here); WRITE_SIZE is exact for 16-B stores.
+SQ_* cycle counters count quad-cycles (x4 = cycles); GRBM_GUI_ACTIVE is summed
+over the 8 XCDs.
 """
 import csv
 import glob
+import gzip
+import io
 import json
+import math
 import os
 import re
 import shutil
@@ -24,7 +35,9 @@ ROUND, OUT, FRAMES = sys.argv[1], sys.argv[2], int(sys.argv[3])
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PROF = os.path.join(ROOT, "profiles")
 os.makedirs(PROF, exist_ok=True)
-PYR = ("k_seed", "k_blur")
+PYR = ("k_seed", "k_blur", "k_octave_tail")
+W, H = 1920, 1080
+N_SIMD = 256 * 4
 
 
 def short(n):
@@ -32,11 +45,22 @@ def short(n):
 
 
 def one(pattern):
-    f = glob.glob(os.path.join(OUT, pattern), recursive=True)
+    f = sorted(glob.glob(os.path.join(OUT, pattern), recursive=True))
+    f += sorted(glob.glob(os.path.join(OUT, pattern + ".gz"), recursive=True))
     return f[0] if f else None
 
 
+def rows_of(path):
+    if path is None:
+        return []
+    raw = gzip.open(path, "rt") if path.endswith(".gz") else open(path)
+    with raw as fh:
+        return list(csv.DictReader(io.StringIO(fh.read())))
+
+
 def bench_line(log):
+    if not os.path.exists(log):
+        return None
     for line in open(log):
         if line.startswith("{"):
             return json.loads(line)
@@ -45,109 +69,183 @@ def bench_line(log):
 
 trace = one("trace/**/run_kernel_trace.csv")
 stats = one("trace/**/run_kernel_stats.csv")
-shutil.copy(stats, os.path.join(PROF, f"{ROUND}_kernel_stats.csv"))
+if stats:
+    shutil.copy(stats, os.path.join(PROF, f"{ROUND}_kernel_stats.csv"))
 b = bench_line(os.path.join(OUT, "bench_trace.log"))
+steps = b["steps"] if b else 3
 
+# ---- trace: per kernel totals -------------------------------------------------
 agg = defaultdict(lambda: [0, 0.0])
-rows = list(csv.DictReader(open(trace)))
+rows = rows_of(trace)
 for r in rows:
     k = short(r["Kernel_Name"])
     agg[k][0] += 1
     agg[k][1] += (int(r["End_Timestamp"]) - int(r["Start_Timestamp"])) / 1e3
-tot = sum(v[1] for k, v in agg.items() if "siftmi" in k or k.startswith("k_"))
-pyr_us = sum(v[1] for k, v in agg.items() if k.startswith(PYR))
-pyr_n = sum(v[0] for k, v in agg.items() if k.startswith(PYR))
-n_chunks = agg["k_seed<5, 32>"][0] if "k_seed<5, 32>" in agg else max(1, sum(v[0] for k, v in agg.items() if k.startswith("k_seed")))
+tot = sum(v[1] for k, v in agg.items() if k.startswith("k_") or "rocprim" in k)
 
-# The serialised stage-timing pass of bench.py (the roofline's HIP-event
+# ---- the serialised stage-timing pass of bench.py (the roofline's HIP-event
 # average): the longest run of consecutive sift kernels on a single stream.
-# Its chunks start at k_seed; the last `steps` x chunks-per-call of them are
-# the timed steps (one warmup step precedes them).
+# Its chunks start at k_seed*; one warmup step precedes the timed steps.
 sk = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Stream_Id"], short(r["Kernel_Name"]))
              for r in rows if short(r["Kernel_Name"]).startswith("k_") or "rocprim" in r["Kernel_Name"]))
-best, cur = (0, 0), [0, 0]
+best, c0 = (0, 0), 0
 for i in range(1, len(sk) + 1):
-    if i == len(sk) or sk[i][2] != sk[cur[0]][2]:
-        if i - cur[0] > best[1] - best[0]:
-            best = (cur[0], i)
-        cur = [i, i]
+    if i == len(sk) or sk[i][2] != sk[c0][2]:
+        if i - c0 > best[1] - best[0]:
+            best = (c0, i)
+        c0 = i
 run = sk[best[0]:best[1]]
 seeds = [i for i, x in enumerate(run) if x[3].startswith("k_seed")]
-steps = b["steps"] if b else 3
-chunks_per_call = max(1, len(seeds) // (steps + 1))
-# complete chunks of the serialised pass: a seed and every blur after it up to
-# the next seed (a group cut short at the run's end is dropped); the last
-# steps * chunks_per_call complete groups are the timed steps
 groups = []
 for a, z in zip(seeds, seeds[1:] + [len(run)]):
-    g = [x for x in run[a:z] if x[3].startswith(PYR)]
-    groups.append(g)
-full = max((len(g) for g in groups), default=0)
-groups = [g for g in groups if len(g) == full]
-timed = [x for g in groups[-steps * chunks_per_call:] for x in g]
-iso = [(e - s0) / 1e3 for s0, e, _, k in timed]
-iso_us, iso_n = sum(iso), len(iso)
-
-
-def pmc(kind, name):
-    f = one(f"{kind}/**/run_counter_collection.csv")
-    v, n = 0.0, 0
-    for r in csv.DictReader(open(f)):
-        if r["Counter_Name"] == name and short(r["Kernel_Name"]).startswith(PYR):
-            v += float(r["Counter_Value"])
-            n += 1
-    return v * 1024.0, n  # KiB -> bytes
-
-
-fetch, n_f = pmc("fetch", "FETCH_SIZE")
-fetch *= 2.0  # gfx950: half of 16-B streaming reads counted
-write, n_w = pmc("write", "WRITE_SIZE")
-W, H = 1920, 1080
-sum_p, ow, oh = 0, 2 * W, 2 * H
-for _ in range(int(round(__import__("math").log2(min(2 * W, 2 * H)) - 2)) + 1):
-    sum_p += ow * oh
-    ow //= 2
-    oh //= 2
-algo_pf = W * H + 44 * sum_p  # G_0..G_5 + D_0..D_4 written once (the batch path writes G only)
-# host auto_chunk (host.cpp): <= 64 frames and ~32 GB of pyramid per chunk,
-# balanced, at least two chunks per call
-cmax = min(64, max(1, int(32e9 // (44.0 * sum_p))))
+    groups.append(run[a:z])
+full = max((sum(1 for x in g if x[3].startswith(PYR)) for g in groups), default=0)
+groups = [g for g in groups if sum(1 for x in g if x[3].startswith(PYR)) == full]
+chunks_per_call = max(1, len(groups) // (steps + 1))
+timed = groups[-steps * chunks_per_call:]
+n_oct = int(round(math.log2(min(2 * W, 2 * H)) - 2)) + 1
+dims = [((2 * W) >> o, (2 * H) >> o) for o in range(n_oct)]
+sum_p = sum(w * h for w, h in dims)
+algo_pf = W * H + 44 * sum_p  # u8 read once, G_0..G_5 + D_0..D_4 written once
+cmax = min(64, max(1, int(32e9 // (44.0 * sum_p))))  # host auto_chunk
 nck = max(-(-FRAMES // cmax), 2 if FRAMES >= 2 else 1)
 chunk = -(-FRAMES // nck)
-launches_per_chunk = pyr_n / max(1, n_chunks)
-traffic_pl = fetch / max(1, n_f) + write / max(1, n_w)  # HBM bytes per pyramid launch
-traffic_pf = traffic_pl * launches_per_chunk / chunk
-json.dump({"round": ROUND, "frame": f"{W}x{H}", "frames_per_call": FRAMES, "frames_per_chunk": chunk,
-           "pyramid_hbm_bytes_per_launch": traffic_pl, "pyramid_hbm_bytes_per_frame": traffic_pf,
-           "fetch_bytes_per_launch": fetch / max(1, n_f), "write_bytes_per_launch": write / max(1, n_w),
-           "algorithmic_bytes_per_frame": algo_pf,
-           "source": f"profiles/{ROUND}_summary.md (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)"},
-          open(os.path.join(PROF, "pmc_traffic.json"), "w"), indent=1)
 
-with open(os.path.join(PROF, f"{ROUND}_summary.md"), "w") as f:
-    f.write(f"# {ROUND} profile: `bench.py --frames {FRAMES} --steps 3 --warmup 1` on one MI355X\n\n")
+pos = defaultdict(list)     # launch position in the chunk -> durations (us)
+stage = defaultdict(float)  # non-pyramid kernels of the timed chunks (us)
+for g in timed:
+    pyr = [x for x in g if x[3].startswith(PYR)]
+    for j, x in enumerate(pyr):
+        pos[(j, x[3])].append((x[1] - x[0]) / 1e3)
+    for x in g:
+        if not x[3].startswith(PYR):
+            stage[x[3]] += (x[1] - x[0]) / 1e3
+iso_us = sum(sum(v) for v in pos.values())
+iso_n = sum(len(v) for v in pos.values())
+
+
+def pos_bytes(j):
+    """Actual HBM bytes of the launch at position j of a chunk: the seed reads
+    the u8 frame and writes G_0; blur s of octave o reads G_{s-1} and writes
+    G_s (8 B/px), and s = 3 also writes the next octave's G_0 (1 B/px)."""
+    if j == 0:
+        return chunk * (W * H + 4 * dims[0][0] * dims[0][1])
+    o, s = (j - 1) // 5, (j - 1) % 5 + 1
+    px = dims[o][0] * dims[o][1]
+    return chunk * (8 * px + (px // 4 * 4 if s == 3 and o + 1 < n_oct else 0))
+
+
+# ---- PMC passes ---------------------------------------------------------------
+def pmc_rows(kind):
+    return rows_of(one(f"{kind}/**/run_counter_collection.csv"))
+
+
+def pmc_sum(rows_, name, pred):
+    v, n = 0.0, 0
+    for r in rows_:
+        if r["Counter_Name"] == name and pred(short(r["Kernel_Name"])):
+            v += float(r["Counter_Value"])
+            n += 1
+    return v, n
+
+
+fr, wr = pmc_rows("fetch"), pmc_rows("write")
+is_pyr = lambda k: k.startswith(PYR)
+fetch, n_f = pmc_sum(fr, "FETCH_SIZE", is_pyr)
+fetch *= 2.0 * 1024.0  # KiB -> bytes; gfx950: half of 16-B streaming reads counted
+write, n_w = pmc_sum(wr, "WRITE_SIZE", is_pyr)
+write *= 1024.0
+launches_per_chunk = full
+traffic_pl = fetch / max(1, n_f) + write / max(1, n_w)
+traffic_pf = traffic_pl * launches_per_chunk / chunk
+if n_f and n_w:
+    tj = {"round": ROUND, "frame": f"{W}x{H}", "frames_per_call": FRAMES, "frames_per_chunk": chunk,
+          "pyramid_hbm_bytes_per_launch": traffic_pl, "pyramid_hbm_bytes_per_frame": traffic_pf,
+          "fetch_bytes_per_launch": fetch / max(1, n_f), "write_bytes_per_launch": write / max(1, n_w),
+          "algorithmic_bytes_per_frame": algo_pf,
+          "source": f"profiles/{ROUND}_summary.md (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)"}
+    json.dump(tj, open(os.path.join(PROF, "pmc_traffic.json"), "w"), indent=1)
+
+# per-kernel SQ counters (sums over every dispatch of the kernel in the pass)
+sq = defaultdict(lambda: defaultdict(float))
+sq_n = defaultdict(int)
+for kind in ("sq1", "sq2", "fetch", "write"):
+    seen = set()
+    for r in pmc_rows(kind):
+        k = short(r["Kernel_Name"])
+        sq[k][r["Counter_Name"]] += float(r["Counter_Value"])
+        if kind == "sq1" and (r.get("Dispatch_Id"), k) not in seen:
+            seen.add((r.get("Dispatch_Id"), k))
+            sq_n[k] += 1
+
+out_md = os.path.join(PROF, f"{ROUND}_summary.md")
+with open(out_md, "w") as f:
+    f.write(f"# {ROUND} profile: `bench.py --frames {FRAMES} --steps {steps} --warmup 1 --no-configs` on one MI355X\n\n")
     f.write("Command: `bash tools/round_profile.sh` (rocprofv3 --kernel-trace --stats; then separate "
-            "--pmc FETCH_SIZE and --pmc WRITE_SIZE passes of the same command).\n\n")
+            "--pmc passes: FETCH_SIZE; WRITE_SIZE; two SQ counter groups). Summarised by "
+            "`tools/profile_summary.py`.\n\n")
     if b:
         f.write(f"bench line (traced run): value = {b['value']:.4g} keypoints/s, ms_per_step = "
                 f"{b['ms_per_step']:.2f}, stage_ms_per_step = {json.dumps(b['stage_ms_per_step'])}\n\n")
-    f.write("## Pyramid stage (the roofline kernel group: k_seed + k_blur<R>)\n\n")
-    f.write(f"* trace, all passes: {pyr_n} launches, {pyr_us / 1e3:.3f} ms total, {pyr_us / max(1, pyr_n):.1f} us "
-            f"per launch (two-lane passes overlap two chunks, which stretches each launch)\n")
-    f.write(f"* trace, serialised stage-timing pass, timed steps: {iso_n} launches, "
-            f"{iso_us / max(1, iso_n):.1f} us per launch (under the profiler)\n")
+    f.write("## Pyramid stage (the roofline kernel group: k_seed* + k_blur*)\n\n")
+    f.write(f"* trace, serialised stage-timing pass, timed steps: {iso_n} launches "
+            f"({len(timed)} chunks of {chunk} frames, {launches_per_chunk} launches each), "
+            f"{iso_us / max(1, iso_n):.1f} us per launch, {iso_us / max(1, len(timed)) / 1e3:.3f} ms per chunk\n")
     if b:
         f.write(f"* bench.py (HIP events on the compute stream, serialised pass): pyramid_ms per step = "
                 f"{b['stage_ms_per_step']['pyramid_ms']:.3f}, avg launch = {b['roofline']['avg_launch_ms'] * 1e3:.1f} us\n")
     f.write(f"* algorithmic bytes per frame (W*H + 44*sum P_o) = {algo_pf / 1e6:.1f} MB; per launch "
-            f"{algo_pf * chunk / launches_per_chunk / 1e6:.1f} MB ({launches_per_chunk:.0f} launches per chunk of {chunk} frames)\n")
-    f.write(f"* HBM traffic (PMC, FETCH_SIZE x2 + WRITE_SIZE, mean over {n_f} pyramid dispatches) = "
-            f"{traffic_pl / 1e6:.1f} MB per launch = {traffic_pf / 1e6:.1f} MB per frame "
-            f"(read {fetch / max(1, n_f) / 1e6:.1f} MB, write {write / max(1, n_w) / 1e6:.1f} MB per launch); "
-            f"traffic / algorithmic = {traffic_pf / algo_pf:.2f}\n\n")
-    f.write("## Kernels (trace, all calls)\n\n| kernel | launches | total ms | avg us | share |\n|---|---|---|---|---|\n")
+            f"{algo_pf * chunk / max(1, launches_per_chunk) / 1e6:.1f} MB\n")
+    if n_f and n_w:
+        f.write(f"* HBM traffic (PMC, FETCH_SIZE x2 + WRITE_SIZE, mean over {n_f} pyramid dispatches) = "
+                f"{traffic_pl / 1e6:.1f} MB per launch = {traffic_pf / 1e6:.1f} MB per frame "
+                f"(read {fetch / max(1, n_f) / 1e6:.1f} MB, write {write / max(1, n_w) / 1e6:.1f} MB per launch); "
+                f"traffic / algorithmic = {traffic_pf / algo_pf:.2f}\n")
+    f.write("\n### Per launch position (serialised pass; actual bytes = what the launch must read + write)\n\n")
+    f.write("| pos | octave | blur | kernel | avg us | actual MB | TB/s | share of stage |\n|---|---|---|---|---|---|---|---|\n")
+    for (j, k), v in sorted(pos.items()):
+        us = sum(v) / len(v)
+        by = pos_bytes(j)
+        o, s = ((j - 1) // 5, (j - 1) % 5 + 1) if j else (0, 0)
+        f.write(f"| {j} | {o} | {'seed' if j == 0 else s} | `{k}` | {us:.1f} | {by / 1e6:.1f} | "
+                f"{by / (us * 1e-6) / 1e12:.2f} | {100 * sum(v) / max(1e-9, iso_us):.1f}% |\n")
+    if stage:
+        f.write("\n### Other stages in the same serialised chunks (ms per chunk)\n\n| kernel | ms |\n|---|---|\n")
+        for k, us in sorted(stage.items(), key=lambda kv: -kv[1]):
+            f.write(f"| `{k[:60]}` | {us / max(1, len(timed)) / 1e3:.3f} |\n")
+    if sq:
+        f.write("\n## SQ counters per kernel (all dispatches of the profiled command)\n\n")
+        f.write("Wave-cycle fractions are of SQ_WAVE_CYCLES (quad-cycles, summed over waves): `valu` = "
+                "SQ_ACTIVE_INST_VALU, `lds` = SQ_ACTIVE_INST_LDS, `wait` = SQ_WAIT_ANY (parked at a waitcnt / "
+                "barrier), `stall` = SQ_WAIT_INST_ANY (ready but not issued). `VALU busy` = 4 x SQ_ACTIVE_INST_VALU "
+                "/ 1024 SIMDs / (GRBM_GUI_ACTIVE / 8 XCDs): the share of SIMD cycles issuing VALU while the "
+                "kernel ran. `bank` = SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS.\n\n")
+        f.write("| kernel | dispatches | VALU insts / wave | valu | lds | wait | stall | VALU busy | bank |\n"
+                "|---|---|---|---|---|---|---|---|---|\n")
+        keys = sorted(sq, key=lambda k: -sq[k].get("SQ_WAVE_CYCLES", 0))
+        for k in keys:
+            c = sq[k]
+            wc = c.get("SQ_WAVE_CYCLES", 0)
+            if wc <= 0 or not (k.startswith("k_") or "rocprim" in k):
+                continue
+            waves = max(1.0, c.get("SQ_WAVES", 0))
+            gui = c.get("GRBM_GUI_ACTIVE", 0) / 8
+            vb = 4 * c.get("SQ_ACTIVE_INST_VALU", 0) / N_SIMD / gui if gui else float("nan")
+            lds = c.get("SQ_ACTIVE_INST_LDS", 0)
+            f.write(f"| `{k[:48]}` | {sq_n[k]} | {c.get('SQ_INSTS_VALU', 0) / waves:.0f} | "
+                    f"{c.get('SQ_ACTIVE_INST_VALU', 0) / wc:.2f} | {lds / wc:.2f} | "
+                    f"{c.get('SQ_WAIT_ANY', 0) / wc:.2f} | {c.get('SQ_WAIT_INST_ANY', 0) / wc:.2f} | "
+                    f"{vb:.2f} | {c.get('SQ_LDS_BANK_CONFLICT', 0) / lds if lds else 0:.3f} |\n")
+    f.write("\n## Kernels (trace, all calls)\n\n| kernel | launches | total ms | avg us | share |\n|---|---|---|---|---|\n")
     for k, (n, us) in sorted(agg.items(), key=lambda kv: -kv[1][1]):
-        if not (k.startswith("k_") or "hipcub" in k or "rocprim" in k):
+        if not (k.startswith("k_") or "rocprim" in k):
             continue
-        f.write(f"| `{k}` | {n} | {us / 1e3:.3f} | {us / n:.1f} | {100 * us / tot:.1f}% |\n")
-print(open(os.path.join(PROF, f"{ROUND}_summary.md")).read())
+        f.write(f"| `{k[:90]}` | {n} | {us / 1e3:.3f} | {us / n:.1f} | {100 * us / max(1e-9, tot):.1f}% |\n")
+
+dst = os.path.join(OUT, "profiles")
+os.makedirs(dst, exist_ok=True)
+for name in (f"{ROUND}_summary.md", f"{ROUND}_kernel_stats.csv", "pmc_traffic.json"):
+    p = os.path.join(PROF, name)
+    if os.path.exists(p):
+        shutil.copy(p, os.path.join(dst, name))
+print(open(out_md).read())

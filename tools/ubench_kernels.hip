@@ -166,8 +166,61 @@ void bench_blur(int N, bool arena, bool random) {
     CK(hipFree(base));
 }
 
+// k_octave_tail on the bench's tail geometry (1080p: octaves 5..9 of the 2x
+// seed, 64 frames): whole tail and one octave at a time
+void bench_tail(int N) {
+    const int n_oct = 10;
+    TailLaunch L{};
+    size_t total = 0;
+    for (int o = 0; o < n_oct; o++) {
+        L.ow[o] = 3840 >> o;
+        L.oh[o] = 2160 >> o;
+        L.pitch[o] = (L.ow[o] + 63) & ~63;
+        L.gstride[o] = (size_t)6 * L.pitch[o] * L.oh[o];
+        total += L.gstride[o] * N;
+    }
+    float* base;
+    CK(hipMalloc(&base, total * 4));
+    hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, base, total);
+    size_t off = 0;
+    for (int o = 0; o < n_oct; o++) {
+        L.gauss[o] = base + off;
+        off += L.gstride[o] * N;
+    }
+    const int radii[6] = {0, 5, 6, 8, 10, 13};
+    for (int s = 1; s < 6; s++) {
+        L.r[s] = radii[s];
+        for (int t = 0; t <= radii[s]; t++) L.taps[s].k[t] = 1.0f / (2 * radii[s] + 1);
+    }
+    L.n_img = N;
+    L.profile = kProfileOpenCV;
+    auto timeit = [&](int o0, int o1) {
+        L.o0 = o0;
+        L.n_oct = o1;
+        launch_octave_tail(L, 0);
+        hipEvent_t a, b;
+        CK(hipEventCreate(&a));
+        CK(hipEventCreate(&b));
+        CK(hipEventRecord(a));
+        for (int i = 0; i < 10; i++) launch_octave_tail(L, 0);
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, a, b));
+        return ms / 10;
+    };
+    std::printf("octave tail, %d frames (1080p seed geometry)\n", N);
+    std::printf("  octaves 5..9: %8.1f us\n", 1e3 * timeit(5, 10));
+    for (int o = 5; o < 10; o++) std::printf("  octave %d alone (%dx%d): %8.1f us\n", o, L.ow[o], L.oh[o], 1e3 * timeit(o, o + 1));
+    CK(hipFree(base));
+}
+
 int main(int argc, char** argv) {
     const char* mode = argc > 1 ? argv[1] : "all";
+    if (!strcmp(mode, "tail")) {
+        bench_tail(argc > 2 ? atoi(argv[2]) : 64);
+        return 0;
+    }
     if (!strcmp(mode, "strip")) {
         bench_blur_strip(argc > 2 ? atoi(argv[2]) : 64);
         return 0;
