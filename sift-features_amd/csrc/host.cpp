@@ -741,7 +741,7 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
         float* G = p.gauss(o, lane);
         float* D = p.dog(o, lane);
         const size_t P = p.P[o];
-        for (int s = 1; s < kImagesPerOctave; s++) {
+        auto blur_launch = [&](int s) {
             BlurLaunch B{};
             B.src = G + (size_t)(s - 1) * P;
             B.src_img_stride = p.gstride(o);
@@ -763,6 +763,17 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
             if (c->band_restricted) {
                 B.y0 = rlo[(size_t)o * kImagesPerOctave + s];
                 B.y1 = std::max(rhi[(size_t)o * kImagesPerOctave + s], B.y0 + 1);
+            }
+            return B;
+        };
+        for (int s = 1; s < kImagesPerOctave; s++) {
+            const BlurLaunch B = blur_launch(s);
+            // G_1, G_2 in one pass where the pair kernel applies (the
+            // strip-pair of k_blur2_strip: G_1 never read back from HBM)
+            if (s == 1 && launch_blur_pair(p.oct_r[1], p.oct_r[2], B, blur_launch(2), st) == 0) {
+                launches++;
+                s++;
+                continue;
             }
             if (launch_blur(p.oct_r[s], B, st)) return fail(SIFT_MI_EUNSUPPORTED, "octave blur radius");
             launches++;

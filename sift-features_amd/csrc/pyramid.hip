@@ -350,11 +350,9 @@ __device__ __forceinline__ int strip_index(int p, int n) {
 // chunks (all rows and the strip's whole window inside the image) are one
 // 16-B buffer load per item with the row offset in soffset; border chunks
 // load element-wise through strip_index.
-template <int R, int P>
-__device__ __forceinline__ void strip_load(float4 (&pre)[StripGeom<R>::LPT], __amdgpu_buffer_rsrc_t rs,
-                                           const int (&voff)[StripGeom<R>::LPT], bool cols_in, int r0, int x0,
-                                           int W, int H, int pitch) {
-    using G = StripGeom<R>;
+template <int R, int P, class G = StripGeom<R>>
+__device__ __forceinline__ void strip_load(float4 (&pre)[G::LPT], __amdgpu_buffer_rsrc_t rs, const int (&voff)[G::LPT],
+                                           bool cols_in, int r0, int x0, int W, int H, int pitch) {
     if (cols_in && r0 >= 0 && r0 + G::S <= H) {
         const int so = r0 * pitch * 4;
 #pragma unroll
@@ -570,6 +568,202 @@ __global__ __launch_bounds__(256, StripGeom<R>::MINB) void k_blur_strip(
         break;
             COLPASS(0) COLPASS(1) COLPASS(2) COLPASS(3)
 #undef COLPASS
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_blur2_strip: two consecutive blurs of the chain, G_{s-1} -> G_s -> G_{s+1},
+// in one streaming pass (OpenCV profile, both radii <= 8, 16-row chunks).
+// G_s is written once and read zero times from HBM: 12 B per pixel of the
+// pair instead of 16.
+//
+// A strip owns the 112 output columns [X, X + 112).  Blur A (radius Ra) is
+// the strip scheme above with its 128 columns starting at X - 8: its column
+// pass writes G_s rows into a ring of three LDS slots laid out as blur B's
+// (radius Rb) input window [X - 8, X + 136), so B's row pass is the same
+// 16-item lane map (its last 16 outputs read junk and are dropped) and B's
+// column pass stores lanes 0..55.  Vertically B lags A by two chunks:
+//   step k:  P1  store A-input chunk k + 1 (prefetched), prefetch k + 2
+//            P2  row pass A on chunk k + 1 | row pass B on G_s chunk k - 1
+//            P3  column pass A -> G_s chunk k (slot k % 3, HBM rows of this
+//                segment) | column pass B -> G_{s+1} rows of chunk k - 2
+// (one phase's two halves touch disjoint slots).
+//
+// Exactness at the image borders: G_s rows above / below the image come out
+// of A's column pass as the reflect-101 images of real rows bit for bit (the
+// pass is centre product + (below + above) pair sums, symmetric under
+// reflection, and A's input rows are reflected), so only G_s COLUMNS outside
+// the image -- A's row pass is an FMA chain from the leftmost tap, not
+// symmetric -- are replaced by their reflect-101 sources before B's row pass.
+// ---------------------------------------------------------------------------
+template <int Ra, int Rb>
+struct PairGeom {
+    using GA = StripGeom<Ra, 16>;
+    using GB = StripGeom<Rb, 16>;
+    static constexpr int HB = GB::HWL;             // G_s halo columns of B's window
+    static constexpr int TWO = GA::TW - 2 * HB;   // output columns per strip
+    static constexpr int LDS_FLOATS = 2 * GA::SLOT + 3 * GB::SLOT;
+    static_assert(HB == 8 && GA::HWL == 8, "radii 5..8: 8-column halos");
+    static_assert(GB::IWV >= GA::TW, "B's window holds A's 128 columns");
+};
+
+// A's column pass for wave WV: G_s rows y0 .. y0 + VB - 1 (y0 = first row of
+// the chunk + WV*VB) of columns xa + 2*lane into B's slot, and into HBM for
+// the rows [gys, gye) and columns [X, min(X + TWO, W)) this strip owns.
+template <class GA, int WV>
+__device__ __forceinline__ void pair_colpass_a(const float* sa, const float* sb, float* bslot, int bip,
+                                               const BlurTaps& taps, int lane, int y, int gys, int gye, int xa, int W,
+                                               int pitch, int two, __amdgpu_buffer_rsrc_t rd) {
+    constexpr int R = GA::R;
+    constexpr int NR = GA::VB + 2 * R;
+    f2v v[NR];
+#pragma unroll
+    for (int j = 0; j < NR; j++) {
+        const int L = WV * GA::VB + j;
+        const float* rp = L < GA::S ? sa + L * GA::IWP : sb + (L - GA::S) * GA::IWP;
+        v[j] = *(const lds_f2v*)(rp + 2 * lane);
+    }
+    const f2v k0 = {taps.k[0], taps.k[0]};
+    const int y0 = y + WV * GA::VB;
+    const int gx = xa + 2 * lane;
+    const bool own = gx >= xa + 8 && gx < xa + 8 + two && gx < W;  // this strip's columns
+    const bool pair = gx + 1 < W;
+#pragma unroll
+    for (int o = 0; o < GA::VB; o++) {
+        f2v acc = v[o + R] * k0;
+#pragma unroll
+        for (int t = 1; t <= R; t++) {
+            const f2v kt = {taps.k[t], taps.k[t]};
+            acc = __builtin_elementwise_fma(v[o + R + t] + v[o + R - t], kt, acc);
+        }
+        *(f2v*)(bslot + (WV * GA::VB + o) * bip + 2 * lane) = acc;
+        const int gy = y0 + o;
+        if (own && gy >= gys && gy < gye) {
+            const int off = (gy * pitch + gx) * 4;
+            if (pair)
+                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, acc), rd, off, 0, 0);
+            else
+                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc.x), rd, off, 0, 0);
+        }
+    }
+}
+
+template <int Ra, int Rb>
+__global__ __launch_bounds__(256, 3) void k_blur2_strip(const float* __restrict__ src, size_t img_stride,
+                                                        float* __restrict__ dst_a, float* __restrict__ dst_b, int W,
+                                                        int H, int pitch, const BlurTaps taps_a,
+                                                        const BlurTaps taps_b, int ya, int yb, int seg) {
+    using Q = PairGeom<Ra, Rb>;
+    using GA = typename Q::GA;
+    using GB = typename Q::GB;
+    constexpr int S = GA::S;
+    __shared__ __attribute__((aligned(16))) float lds[Q::LDS_FLOATS];
+    float* aslot = lds;                   // 2 x GA::SLOT: A's input chunks (row-filtered in place)
+    float* bslot = lds + 2 * GA::SLOT;    // 3 x GB::SLOT: G_s chunks (row-filtered in place)
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const TileId tile = xcd_tile();
+    const int X = tile.x * Q::TWO;        // output columns [X, X + TWO)
+    const int xa = X - Q::HB;             // A's 128 columns (= B's window) start here
+    const int ys = ya + tile.y * seg, ye = min(yb, ys + seg);
+    if (ys >= ye) return;
+    const size_t b = tile.z;
+    const uint32_t plane_bytes = (uint32_t)H * (uint32_t)pitch * 4u;
+    const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(src + b * img_stride, plane_bytes);
+    const __amdgpu_buffer_rsrc_t ra = uniform_rsrc(dst_a + b * img_stride, plane_bytes);
+    const __amdgpu_buffer_rsrc_t rb = uniform_rsrc(dst_b + b * img_stride, plane_bytes);
+    const bool cols_in = xa - GA::HWL >= 0 && xa + GA::TW + GA::HWL <= W;
+    int voff[GA::LPT];
+#pragma unroll
+    for (int j = 0; j < GA::LPT; j++) {
+        const int i = min(tid + 64 * GA::NW * j, GA::NLOAD4 - 1);
+        const int ly = i / GA::C4, c4 = i - ly * GA::C4;
+        voff[j] = (ly * pitch + xa - GA::HWL + 4 * c4) * 4;
+    }
+    int prow, pq;  // row-pass lane map (see strip_rowpass; S = 16: wave w rows 4w .. 4w + 3)
+    {
+        const int l = lane & 31;
+        int g, k;
+        if (l < 4) { g = 0; k = l; }
+        else if (l < 12) { g = 1; k = l - 4; }
+        else if (l < 16) { g = 0; k = l - 8; }
+        else if (l < 20) { g = 1; k = l - 8; }
+        else if (l < 28) { g = 0; k = l - 12; }
+        else { g = 1; k = l - 16; }
+        const int grp = (lane >> 5) * 2 + g;
+        prow = wv * 4 + (grp >> 1) * 2 + (k >> 3);
+        pq = (grp & 1) * 8 + (k & 7);
+    }
+    // G_s columns outside the image in a B slot row: replaced by their
+    // reflect-101 sources (this wave's 4 rows, before its row pass B); only
+    // strips at the left / right image border have any
+    const bool fix_l = xa < 0, fix_r = xa + GA::TW > W;
+    auto fixup = [&](float* slot) {
+        if (!(fix_l || fix_r)) return;
+        const int r = wv * 4 + (lane >> 4), j = lane & 15;
+        const int x = j < 8 ? xa + j : W + (j - 8);  // left halo xa .. xa + 7, right W .. W + 7
+        const bool act = j < 8 ? (fix_l && x < 0) : (fix_r && x - xa < GA::TW);
+        float val = 0.0f;
+        if (act) val = slot[r * GB::IWP + (reflect101(x, W) - xa)];
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        if (act) slot[r * GB::IWP + (x - xa)] = val;
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    };
+    const int nout = (ye - ys + S - 1) / S;  // G_{s+1} chunks; G_s chunks 0 .. nout; A-input chunks 0 .. nout + 1
+    const int ga = ys - Rb - Ra;             // first A-input row (chunk 0)
+    float4 pre[GA::LPT];
+    strip_load<Ra, kProfileOpenCV, GA>(pre, rs, voff, cols_in, ga, xa, W, H, pitch);
+    strip_store<GA>(pre, aslot);
+    strip_load<Ra, kProfileOpenCV, GA>(pre, rs, voff, cols_in, ga + S, xa, W, H, pitch);
+    __syncthreads();
+    strip_rowpass<GA, kProfileOpenCV>(aslot, taps_a, prow, pq);
+    for (int k = 0; k <= nout + 1; k++) {
+        __syncthreads();  // P1
+        if (k + 1 <= nout + 1) {
+            strip_store<GA>(pre, aslot + ((k + 1) & 1) * GA::SLOT);
+            if (k + 2 <= nout + 1) strip_load<Ra, kProfileOpenCV, GA>(pre, rs, voff, cols_in, ga + (k + 2) * S, xa, W, H, pitch);
+        }
+        __syncthreads();  // P2
+        if (k + 1 <= nout + 1) strip_rowpass<GA, kProfileOpenCV>(aslot + ((k + 1) & 1) * GA::SLOT, taps_a, prow, pq);
+        if (k >= 1 && k - 1 <= nout) {
+            float* s1 = bslot + ((k - 1) % 3) * GB::SLOT;
+            fixup(s1);
+            strip_rowpass<GB, kProfileOpenCV>(s1, taps_b, prow, pq);
+        }
+        __syncthreads();  // P3
+        if (k <= nout) {
+            const float* s0 = aslot + (k & 1) * GA::SLOT;
+            const float* s1 = aslot + ((k + 1) & 1) * GA::SLOT;
+            float* dstb = bslot + (k % 3) * GB::SLOT;
+            const int y = ys - Rb + k * S;  // first G_s row of chunk k
+            switch (wv) {
+#define COLA(w)                                                                                                  \
+    case w:                                                                                                      \
+        pair_colpass_a<GA, w>(s0, s1, dstb, GB::IWP, taps_a, lane, y, ys, ye, xa, W, pitch, Q::TWO, ra);         \
+        break;
+                COLA(0) COLA(1) COLA(2) COLA(3)
+#undef COLA
+            }
+        }
+        if (k >= 2 && k - 2 < nout) {
+            const float* s0 = bslot + ((k - 2) % 3) * GB::SLOT;
+            const float* s1 = bslot + ((k - 1) % 3) * GB::SLOT;
+            const int y = ys + (k - 2) * S;
+            // after B's in-place row pass slot column c is output column X + c: lanes 0 .. TWO/2 - 1 are
+            // this strip's columns (the rest read the junk past A's 128 columns)
+            switch (wv) {
+#define COLB(w)                                                                                                  \
+    case w:                                                                                                      \
+        if (lane < Q::TWO / 2)                                                                                   \
+            strip_colpass<GB, kProfileOpenCV, w, false>(s0, s1, taps_b, lane, y, ye, X, W, pitch, rb, rb, 0, 0,  \
+                                                        0);                                                      \
+        break;
+                COLB(0) COLB(1) COLB(2) COLB(3)
+#undef COLB
+            }
         }
     }
 }
@@ -1113,6 +1307,43 @@ static void launch_blur_strip_r(const BlurLaunch& L, hipStream_t st) {
         launch_blur_strip_rp<R, kProfileImageproc>(L, grid, ya, yb, seg, st);
     else
         launch_blur_strip_rp<R, kProfileOpenCV>(L, grid, ya, yb, seg, st);
+}
+
+static bool strip_blur_enabled();
+
+template <int Ra, int Rb>
+static void launch_blur2_rr(const BlurLaunch& A, const BlurLaunch& B, hipStream_t st) {
+    using Q = PairGeom<Ra, Rb>;
+    constexpr int S = Q::GA::S;
+    const int strips = (A.W + Q::TWO - 1) / Q::TWO;
+    const long per = (long)strips * A.n_img;
+    int nseg = (int)std::min<long>(A.H / (2 * S) + 1, (12288 + per - 1) / per);
+    nseg = std::max(1, nseg);
+    const int seg = (A.H + nseg - 1) / nseg;
+    nseg = (A.H + seg - 1) / seg;
+    hipLaunchKernelGGL((k_blur2_strip<Ra, Rb>), dim3(strips, nseg, A.n_img), dim3(256), 0, st, A.src, A.src_img_stride,
+                       A.dst, B.dst, A.W, A.H, A.pitch, A.taps, B.taps, 0, A.H, seg);
+}
+
+// SIFT_MI_PAIR=0 disables the pair kernel (A/B and test knob, read per launch)
+static bool pair_blur_enabled() {
+    const char* e = getenv("SIFT_MI_PAIR");
+    return !(e && !strcmp(e, "0"));
+}
+
+int launch_blur_pair(int ra, int rb, const BlurLaunch& A, const BlurLaunch& B, hipStream_t st) {
+    // A: G_{s-1} -> G_s, B: G_s -> G_{s+1} of one octave arena (same geometry
+    // and image stride); whole planes, no DoG / next-octave output
+    const bool ok = A.profile == kProfileOpenCV && B.profile == kProfileOpenCV && !A.dog && !B.dog && !A.nxt &&
+                    !B.nxt && A.y1 <= A.y0 && B.y1 <= B.y0 && A.dst && B.dst && B.src == A.dst && A.W == B.W &&
+                    A.H == B.H && A.pitch == B.pitch && A.src_img_stride == A.dst_img_stride &&
+                    B.src_img_stride == A.src_img_stride && B.dst_img_stride == A.src_img_stride && A.W >= 64 &&
+                    A.H >= 64 && (uint64_t)A.H * (uint64_t)A.pitch * 4 < (1ull << 31) && strip_blur_enabled() &&
+                    pair_blur_enabled();
+    if (!ok) return -1;
+    if (ra == 5 && rb == 6) { launch_blur2_rr<5, 6>(A, B, st); return 0; }
+    if (ra == 6 && rb == 8) { launch_blur2_rr<6, 8>(A, B, st); return 0; }
+    return -1;
 }
 
 // SIFT_MI_BLUR_KERNEL=tile forces the one-tile-per-workgroup kernels (A/B

@@ -107,6 +107,9 @@ void launch_octave_tail(const TailLaunch& L, hipStream_t st);
 
 // pyramid.hip
 int launch_blur(int radius, const BlurLaunch& L, hipStream_t st);
+// two consecutive blurs of an octave (A then B, B.src == A.dst) in one pass;
+// -1 when the pair kernel does not apply (the caller launches them singly)
+int launch_blur_pair(int ra, int rb, const BlurLaunch& A, const BlurLaunch& B, hipStream_t st);
 int launch_seed(int radius, const SeedLaunch& L, hipStream_t st);
 // D_s = G_{s+1} - G_s (s < 5) of an octave's G stack, for n images
 void launch_dog(const float* gauss, size_t plane, size_t g_img_stride, float* dog, size_t dog_img_stride, int W, int H,

@@ -215,8 +215,62 @@ void bench_tail(int N) {
     CK(hipFree(base));
 }
 
+// k_blur2_strip (two blurs in one pass) vs the two strip launches, octave-0
+// geometry of the bench (64 frames of 3840x2160 in a 6-plane arena)
+void bench_pair(int N, int W, int H) {
+    const int pitch = (W + 63) & ~63;
+    const size_t plane = (size_t)pitch * H;
+    float* base;
+    CK(hipMalloc(&base, plane * 6 * N * 4));
+    hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, base, plane * 6 * N);
+    CK(hipDeviceSynchronize());
+    auto mk = [&](int s, int R) {
+        BlurLaunch L{};
+        L.src = base + (s - 1) * plane;
+        L.dst = base + s * plane;
+        L.src_img_stride = L.dst_img_stride = plane * 6;
+        L.W = W;
+        L.H = H;
+        L.pitch = pitch;
+        L.n_img = N;
+        for (int t = 0; t <= R; t++) L.taps.k[t] = 1.0f / (2 * R + 1);
+        return L;
+    };
+    auto timeit = [&](auto&& f) {
+        f();
+        hipEvent_t a, b;
+        CK(hipEventCreate(&a));
+        CK(hipEventCreate(&b));
+        CK(hipEventRecord(a));
+        for (int i = 0; i < 5; i++) f();
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, a, b));
+        return ms / 5;
+    };
+    const double px = (double)W * H * N;
+    std::printf("blur pairs, %d x %dx%d: two strip launches (16 B/px) vs k_blur2_strip (12 B/px)\n", N, W, H);
+    const int pr[2][2] = {{5, 6}, {6, 8}};
+    for (auto& q : pr) {
+        const BlurLaunch A = mk(1, q[0]), B = mk(2, q[1]);
+        const float t2 = timeit([&] { launch_blur(q[0], A, 0); launch_blur(q[1], B, 0); });
+        const float t1 = timeit([&] { if (launch_blur_pair(q[0], q[1], A, B, 0)) std::exit(2); });
+        std::printf("  R=%d,%d  singles %8.3f ms %7.1f GB/s | pair %8.3f ms %7.1f GB/s (%.1f GB/s of the singles' bytes)\n",
+                    q[0], q[1], t2, 16 * px / (t2 * 1e-3) / 1e9, t1, 12 * px / (t1 * 1e-3) / 1e9,
+                    16 * px / (t1 * 1e-3) / 1e9);
+    }
+    CK(hipFree(base));
+}
+
 int main(int argc, char** argv) {
     const char* mode = argc > 1 ? argv[1] : "all";
+    if (!strcmp(mode, "pair")) {
+        bench_pair(argc > 2 ? atoi(argv[2]) : 64, 3840, 2160);
+        bench_pair(argc > 2 ? atoi(argv[2]) : 64, 1920, 1080);
+        bench_pair(argc > 2 ? atoi(argv[2]) : 64, 960, 540);
+        return 0;
+    }
     if (!strcmp(mode, "tail")) {
         bench_tail(argc > 2 ? atoi(argv[2]) : 64);
         return 0;
