@@ -1286,6 +1286,28 @@ static void launch_blur_strip_rp(const BlurLaunch& L, dim3 grid, int ya, int yb,
                            L.pitch, L.taps, ya, yb, seg);
 }
 
+// workgroups per strip launch the segment count aims for (SIFT_MI_STRIP_WG:
+// tuning knob, read per launch)
+static long strip_wg_target() {
+    const char* e = getenv("SIFT_MI_STRIP_WG");
+    return e ? std::max(1L, atol(e)) : 12288L;
+}
+
+// Row segments of a strip launch over `rows` rows with `per` strips x frames:
+// ~strip_wg_target() workgroups, but no segment shorter than ~320 rows unless
+// the launch would then have fewer than ~2048 workgroups (then down to ~40
+// rows) -- a segment re-filters its halo rows and fills / drains its chunk
+// pipeline, so short segments cost more than the extra parallelism buys
+// (measured, tools/ubench_kernels.hip segs: octave 1 of 64 1080p frames,
+// R = 13, 319 us at 13 segments of 84 rows vs 254 us at 3 of 360), while the
+// small octaves need the segments to fill the chip.  Returns the segment length.
+static int strip_segment_rows(int rows, long per) {
+    const long few = std::min<long>((2048 + per - 1) / per, rows / 40);
+    long nseg = std::min<long>((strip_wg_target() + per - 1) / per, std::max<long>(rows / 320, few));
+    nseg = std::max(1L, nseg);
+    return (int)((rows + nseg - 1) / nseg);
+}
+
 template <int R>
 static void launch_blur_strip_r(const BlurLaunch& L, hipStream_t st) {
     using G = StripGeom<R>;
@@ -1297,11 +1319,8 @@ static void launch_blur_strip_r(const BlurLaunch& L, hipStream_t st) {
     // round of equal-sized workgroups is a small fraction), none shorter than
     // two chunks (each segment re-filters its 2R halo rows)
     const int rows = yb - ya;
-    const long per = (long)strips * L.n_img;
-    int nseg = (int)std::min<long>(rows / (2 * G::S) + 1, (12288 + per - 1) / per);
-    nseg = std::max(1, nseg);
-    const int seg = (rows + nseg - 1) / nseg;
-    nseg = (rows + seg - 1) / seg;
+    const int seg = strip_segment_rows(rows, (long)strips * L.n_img);
+    const int nseg = (rows + seg - 1) / seg;
     const dim3 grid(strips, nseg, L.n_img);
     if (L.profile == kProfileImageproc)
         launch_blur_strip_rp<R, kProfileImageproc>(L, grid, ya, yb, seg, st);
@@ -1314,13 +1333,9 @@ static bool strip_blur_enabled();
 template <int Ra, int Rb>
 static void launch_blur2_rr(const BlurLaunch& A, const BlurLaunch& B, hipStream_t st) {
     using Q = PairGeom<Ra, Rb>;
-    constexpr int S = Q::GA::S;
     const int strips = (A.W + Q::TWO - 1) / Q::TWO;
-    const long per = (long)strips * A.n_img;
-    int nseg = (int)std::min<long>(A.H / (2 * S) + 1, (12288 + per - 1) / per);
-    nseg = std::max(1, nseg);
-    const int seg = (A.H + nseg - 1) / nseg;
-    nseg = (A.H + seg - 1) / seg;
+    const int seg = strip_segment_rows(A.H, (long)strips * A.n_img);
+    const int nseg = (A.H + seg - 1) / seg;
     hipLaunchKernelGGL((k_blur2_strip<Ra, Rb>), dim3(strips, nseg, A.n_img), dim3(256), 0, st, A.src, A.src_img_stride,
                        A.dst, B.dst, A.W, A.H, A.pitch, A.taps, B.taps, 0, A.H, seg);
 }
@@ -1425,11 +1440,8 @@ int launch_seed(int R, const SeedLaunch& L, hipStream_t st) {
         if (yb <= ya) return 0;
         const int strips = (L.W + G::TW - 1) / G::TW;
         const int rows = yb - ya;
-        const long per = (long)strips * L.n_img;
-        int nseg = (int)std::min<long>(rows / (2 * G::S) + 1, (12288 + per - 1) / per);
-        nseg = std::max(1, nseg);
-        const int seg = (rows + nseg - 1) / nseg;
-        nseg = (rows + seg - 1) / seg;
+        const int seg = strip_segment_rows(rows, (long)strips * L.n_img);
+        const int nseg = (rows + seg - 1) / seg;
         hipLaunchKernelGGL((k_seed_strip<5>), dim3(strips, nseg, L.n_img), dim3(256), 0, st, L.frames, L.frame_pitch,
                            L.row_stride, L.sh, L.sw, L.tab, L.dst, L.dst_img_stride, L.W, L.H, L.pitch, L.taps, ya,
                            yb, seg);

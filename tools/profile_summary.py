@@ -124,15 +124,42 @@ iso_us = sum(sum(v) for v in pos.values())
 iso_n = sum(len(v) for v in pos.values())
 
 
-def pos_bytes(j):
-    """Actual HBM bytes of the launch at position j of a chunk: the seed reads
-    the u8 frame and writes G_0; blur s of octave o reads G_{s-1} and writes
-    G_s (8 B/px), and s = 3 also writes the next octave's G_0 (1 B/px)."""
-    if j == 0:
-        return chunk * (W * H + 4 * dims[0][0] * dims[0][1])
-    o, s = (j - 1) // 5, (j - 1) % 5 + 1
-    px = dims[o][0] * dims[o][1]
-    return chunk * (8 * px + (px // 4 * 4 if s == 3 and o + 1 < n_oct else 0))
+def launch_blurs(k):
+    """Blurs of the chain a pyramid launch performs (seed: 0)."""
+    if k.startswith("k_seed"):
+        return 0
+    if k.startswith("k_blur2"):
+        return 2
+    if k.startswith("k_octave_tail"):
+        return None  # every remaining octave
+    return 1
+
+
+def pos_info(seq):
+    """(octave, first blur, actual HBM bytes) per launch of a chunk, from the
+    kernel sequence: the seed reads the u8 frame and writes G_0; a blur reads
+    G_{s-1} and writes G_s (8 B/px), a pair reads G_{s-1} and writes G_s,
+    G_{s+1} (12 B/px); blur s = 3 also writes the next octave's G_0 (1 B/px);
+    the tail reads G_0 of its first octave and writes everything after it."""
+    out, done = [], 0
+    for k in seq:
+        nb = launch_blurs(k)
+        if nb == 0:
+            out.append((0, "seed", chunk * (W * H + 4 * dims[0][0] * dims[0][1])))
+            continue
+        o, s = done // 5, done % 5 + 1
+        if nb is None:
+            by = 4 * dims[o][0] * dims[o][1]
+            for oo in range(o, n_oct):
+                by += 4 * 5 * dims[oo][0] * dims[oo][1] + (4 * dims[oo + 1][0] * dims[oo + 1][1] if oo + 1 < n_oct else 0)
+            out.append((o, f"{o}..{n_oct - 1}", chunk * by))
+            done = 5 * n_oct
+            continue
+        px = dims[o][0] * dims[o][1]
+        by = (4 + 4 * nb) * px + (px if (s <= 3 < s + nb) and o + 1 < n_oct else 0)
+        out.append((o, f"{s}" if nb == 1 else f"{s},{s + 1}", chunk * by))
+        done += nb
+    return out
 
 
 # ---- PMC passes ---------------------------------------------------------------
@@ -203,11 +230,11 @@ with open(out_md, "w") as f:
                 f"traffic / algorithmic = {traffic_pf / algo_pf:.2f}\n")
     f.write("\n### Per launch position (serialised pass; actual bytes = what the launch must read + write)\n\n")
     f.write("| pos | octave | blur | kernel | avg us | actual MB | TB/s | share of stage |\n|---|---|---|---|---|---|---|---|\n")
-    for (j, k), v in sorted(pos.items()):
+    items = sorted(pos.items())
+    info = pos_info([k for (j, k), v in items])
+    for ((j, k), v), (o, sl, by) in zip(items, info):
         us = sum(v) / len(v)
-        by = pos_bytes(j)
-        o, s = ((j - 1) // 5, (j - 1) % 5 + 1) if j else (0, 0)
-        f.write(f"| {j} | {o} | {'seed' if j == 0 else s} | `{k}` | {us:.1f} | {by / 1e6:.1f} | "
+        f.write(f"| {j} | {o} | {sl} | `{k}` | {us:.1f} | {by / 1e6:.1f} | "
                 f"{by / (us * 1e-6) / 1e12:.2f} | {100 * sum(v) / max(1e-9, iso_us):.1f}% |\n")
     if stage:
         f.write("\n### Other stages in the same serialised chunks (ms per chunk)\n\n| kernel | ms |\n|---|---|\n")

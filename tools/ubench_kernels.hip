@@ -263,8 +263,65 @@ void bench_pair(int N, int W, int H) {
     CK(hipFree(base));
 }
 
+// segment-count target sweep (SIFT_MI_STRIP_WG) for the strip / pair kernels
+// at the bench's octave 0..3 geometries (64 frames)
+void bench_segs(int N) {
+    const int dims[4][2] = {{3840, 2160}, {1920, 1080}, {960, 540}, {480, 270}};
+    const long targets[7] = {1024, 2048, 4096, 8192, 12288, 24576, 49152};
+    for (auto& d : dims) {
+        const int W = d[0], H = d[1], pitch = (W + 63) & ~63;
+        const size_t plane = (size_t)pitch * H;
+        float* base;
+        CK(hipMalloc(&base, plane * 6 * N * 4));
+        hipLaunchKernelGGL(k_fill, dim3(4096), dim3(256), 0, 0, base, plane * 6 * N);
+        CK(hipDeviceSynchronize());
+        auto mk = [&](int s, int R) {
+            BlurLaunch L{};
+            L.src = base + (s - 1) * plane;
+            L.dst = base + s * plane;
+            L.src_img_stride = L.dst_img_stride = plane * 6;
+            L.W = W;
+            L.H = H;
+            L.pitch = pitch;
+            L.n_img = N;
+            for (int t = 0; t <= R; t++) L.taps.k[t] = 1.0f / (2 * R + 1);
+            return L;
+        };
+        auto timeit = [&](auto&& f) {
+            f();
+            hipEvent_t a, b;
+            CK(hipEventCreate(&a));
+            CK(hipEventCreate(&b));
+            CK(hipEventRecord(a));
+            for (int i = 0; i < 5; i++) f();
+            CK(hipEventRecord(b));
+            CK(hipEventSynchronize(b));
+            float ms;
+            CK(hipEventElapsedTime(&ms, a, b));
+            return ms / 5;
+        };
+        std::printf("%dx%d x %d: us per launch (R=8 | R=13 | pair 5,6) by workgroup target\n", W, H, N);
+        for (long t : targets) {
+            char buf[32];
+            std::snprintf(buf, sizeof buf, "%ld", t);
+            setenv("SIFT_MI_STRIP_WG", buf, 1);
+            const BlurLaunch A = mk(1, 8), C = mk(1, 13), P1 = mk(1, 5), P2 = mk(2, 6);
+            const float t8 = timeit([&] { launch_blur(8, A, 0); });
+            const float t13 = timeit([&] { launch_blur(13, C, 0); });
+            const float tp = timeit([&] { launch_blur_pair(5, 6, P1, P2, 0); });
+            std::printf("  %6ld: %8.1f %8.1f %8.1f\n", t, 1e3 * t8, 1e3 * t13, 1e3 * tp);
+        }
+        unsetenv("SIFT_MI_STRIP_WG");
+        CK(hipFree(base));
+    }
+}
+
 int main(int argc, char** argv) {
     const char* mode = argc > 1 ? argv[1] : "all";
+    if (!strcmp(mode, "segs")) {
+        bench_segs(argc > 2 ? atoi(argv[2]) : 64);
+        return 0;
+    }
     if (!strcmp(mode, "pair")) {
         bench_pair(argc > 2 ? atoi(argv[2]) : 64, 3840, 2160);
         bench_pair(argc > 2 ? atoi(argv[2]) : 64, 1920, 1080);
