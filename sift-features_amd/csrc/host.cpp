@@ -768,9 +768,9 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
         };
         for (int s = 1; s < kImagesPerOctave; s++) {
             const BlurLaunch B = blur_launch(s);
-            // G_1, G_2 in one pass where the pair kernel applies (the
-            // strip-pair of k_blur2_strip: G_1 never read back from HBM)
-            if (s == 1 && launch_blur_pair(p.oct_r[1], p.oct_r[2], B, blur_launch(2), st) == 0) {
+            // G_1, G_2 and G_3, G_4 in one pass each where the pair kernel
+            // applies (k_blur2_strip: G_1 / G_3 never read back from HBM)
+            if ((s == 1 || s == 3) && launch_blur_pair(p.oct_r[s], p.oct_r[s + 1], B, blur_launch(s + 1), st) == 0) {
                 launches++;
                 s++;
                 continue;

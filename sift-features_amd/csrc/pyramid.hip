@@ -315,7 +315,8 @@ struct StripGeom {
     static constexpr int LDS_FLOATS = 2 * SLOT;
     // resident workgroups per CU that the LDS allows (<= 4): the register budget follows
     static constexpr int MINB = 163840 / (4 * LDS_FLOATS) < 4 ? 163840 / (4 * LDS_FLOATS) : 4;
-    static_assert(2 * R <= S, "the column pass reads two chunks");
+    static constexpr int NCW = (2 * R + S - 1) / S + 1;  // chunks in a column-pass window (2, or 3 for S < 2R)
+    static_assert(2 * R <= 2 * S, "a column-pass window spans at most three chunks");
     static_assert((IWP / 4) % 2 == 1, "row-pass lane groups: odd float4 pitch");
     static_assert(4 * NV <= IWV - TW + QW, "row-pass reads stay inside the loaded row");
     static_assert(S % 16 == 0 && TW / QW == 16, "row pass: a wave filters 4 rows x 16 items");
@@ -436,14 +437,15 @@ __device__ __forceinline__ void strip_rowpass(float* slot, const BlurTaps& taps,
 template <class G, int P, int WV, bool NXT>
 __device__ __forceinline__ void strip_colpass(const float* sa, const float* sb, const BlurTaps& taps, int lane,
                                               int y, int ye, int x0, int W, int pitch, __amdgpu_buffer_rsrc_t rd,
-                                              __amdgpu_buffer_rsrc_t rn, int pitch_n, int wn, int hn) {
+                                              __amdgpu_buffer_rsrc_t rn, int pitch_n, int wn, int hn,
+                                              const float* sc = nullptr) {
     constexpr int R = G::R;
     constexpr int NR = G::VB + 2 * R;
     f2v v[NR];
 #pragma unroll
     for (int j = 0; j < NR; j++) {
-        const int L = WV * G::VB + j;
-        const float* rp = L < G::S ? sa + L * G::IWP : sb + (L - G::S) * G::IWP;
+        const int L = WV * G::VB + j;  // window row: slot a, b or (S < 2R) c
+        const float* rp = L < G::S ? sa + L * G::IWP : (L < 2 * G::S ? sb + (L - G::S) * G::IWP : sc + (L - 2 * G::S) * G::IWP);
         v[j] = *(const lds_f2v*)(rp + 2 * lane);
     }
     f2v out[G::VB];
@@ -507,6 +509,7 @@ __global__ __launch_bounds__(256, StripGeom<R>::MINB) void k_blur_strip(
     float* __restrict__ nxt, size_t nxt_img_stride, int pitch_n, int wn, int hn, int W, int H, int pitch,
     const BlurTaps taps, int ya, int yb, int seg) {
     using G = StripGeom<R>;
+    static_assert(G::NCW == 2, "two chunk slots");
     __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -603,18 +606,23 @@ struct PairGeom {
     using GB = StripGeom<Rb, 16>;
     static constexpr int HB = GB::HWL;             // G_s halo columns of B's window
     static constexpr int TWO = GA::TW - 2 * HB;   // output columns per strip
-    static constexpr int LDS_FLOATS = 2 * GA::SLOT + 3 * GB::SLOT;
-    static_assert(HB == 8 && GA::HWL == 8, "radii 5..8: 8-column halos");
+    static constexpr int NBW = GB::NCW;           // G_s chunks in a column-pass window of B
+    static constexpr int NBR = NBW + 1;           // B ring: the window + the chunk being written
+    static constexpr int LDS_FLOATS = 2 * GA::SLOT + NBR * GB::SLOT;
+    static constexpr int MINB = 163840 / (4 * LDS_FLOATS) < 4 ? 163840 / (4 * LDS_FLOATS) : 4;
+    static_assert(GA::HWL == 8 && GA::NCW == 2, "A: radius <= 8");
     static_assert(GB::IWV >= GA::TW, "B's window holds A's 128 columns");
 };
 
 // A's column pass for wave WV: G_s rows y0 .. y0 + VB - 1 (y0 = first row of
 // the chunk + WV*VB) of columns xa + 2*lane into B's slot, and into HBM for
-// the rows [gys, gye) and columns [X, min(X + TWO, W)) this strip owns.
-template <class GA, int WV>
+// the rows [gys, gye) and columns [X, min(X + TWO, W)) this strip owns (NXT:
+// with the next octave's base, nearest 1/2 = pixel (2x, 2y)).
+template <class GA, int WV, bool NXT>
 __device__ __forceinline__ void pair_colpass_a(const float* sa, const float* sb, float* bslot, int bip,
-                                               const BlurTaps& taps, int lane, int y, int gys, int gye, int xa, int W,
-                                               int pitch, int two, __amdgpu_buffer_rsrc_t rd) {
+                                               const BlurTaps& taps, int lane, int y, int gys, int gye, int xa,
+                                               int hb, int W, int pitch, int two, __amdgpu_buffer_rsrc_t rd,
+                                               __amdgpu_buffer_rsrc_t rn, int pitch_n, int wn, int hn) {
     constexpr int R = GA::R;
     constexpr int NR = GA::VB + 2 * R;
     f2v v[NR];
@@ -626,8 +634,8 @@ __device__ __forceinline__ void pair_colpass_a(const float* sa, const float* sb,
     }
     const f2v k0 = {taps.k[0], taps.k[0]};
     const int y0 = y + WV * GA::VB;
-    const int gx = xa + 2 * lane;
-    const bool own = gx >= xa + 8 && gx < xa + 8 + two && gx < W;  // this strip's columns
+    const int gx = xa + 2 * lane;  // even
+    const bool own = gx >= xa + hb && gx < xa + hb + two && gx < W;  // this strip's columns
     const bool pair = gx + 1 < W;
 #pragma unroll
     for (int o = 0; o < GA::VB; o++) {
@@ -645,22 +653,28 @@ __device__ __forceinline__ void pair_colpass_a(const float* sa, const float* sb,
                 __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, acc), rd, off, 0, 0);
             else
                 __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc.x), rd, off, 0, 0);
+            if constexpr (NXT) {
+                if ((gy & 1) == 0 && (gy >> 1) < hn && (gx >> 1) < wn)
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc.x), rn,
+                                                          ((gy >> 1) * pitch_n + (gx >> 1)) * 4, 0, 0);
+            }
         }
     }
 }
 
-template <int Ra, int Rb>
-__global__ __launch_bounds__(256, 3) void k_blur2_strip(const float* __restrict__ src, size_t img_stride,
-                                                        float* __restrict__ dst_a, float* __restrict__ dst_b, int W,
-                                                        int H, int pitch, const BlurTaps taps_a,
-                                                        const BlurTaps taps_b, int ya, int yb, int seg) {
+template <int Ra, int Rb, bool NXT>
+__global__ __launch_bounds__(256, (PairGeom<Ra, Rb>::MINB)) void k_blur2_strip(
+    const float* __restrict__ src, size_t img_stride, float* __restrict__ dst_a, float* __restrict__ dst_b,
+    float* __restrict__ nxt, size_t nxt_img_stride, int pitch_n, int wn, int hn, int W, int H, int pitch,
+    const BlurTaps taps_a, const BlurTaps taps_b, int ya, int yb, int seg) {
     using Q = PairGeom<Ra, Rb>;
     using GA = typename Q::GA;
     using GB = typename Q::GB;
     constexpr int S = GA::S;
+    constexpr int NBW = Q::NBW, NBR = Q::NBR;
     __shared__ __attribute__((aligned(16))) float lds[Q::LDS_FLOATS];
     float* aslot = lds;                   // 2 x GA::SLOT: A's input chunks (row-filtered in place)
-    float* bslot = lds + 2 * GA::SLOT;    // 3 x GB::SLOT: G_s chunks (row-filtered in place)
+    float* bslot = lds + 2 * GA::SLOT;    // NBR x GB::SLOT: G_s chunks (row-filtered in place)
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const TileId tile = xcd_tile();
@@ -673,6 +687,8 @@ __global__ __launch_bounds__(256, 3) void k_blur2_strip(const float* __restrict_
     const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(src + b * img_stride, plane_bytes);
     const __amdgpu_buffer_rsrc_t ra = uniform_rsrc(dst_a + b * img_stride, plane_bytes);
     const __amdgpu_buffer_rsrc_t rb = uniform_rsrc(dst_b + b * img_stride, plane_bytes);
+    __amdgpu_buffer_rsrc_t rn = ra;
+    if constexpr (NXT) rn = uniform_rsrc(nxt + b * nxt_img_stride, (uint32_t)hn * (uint32_t)pitch_n * 4u);
     const bool cols_in = xa - GA::HWL >= 0 && xa + GA::TW + GA::HWL <= W;
     int voff[GA::LPT];
 #pragma unroll
@@ -701,57 +717,73 @@ __global__ __launch_bounds__(256, 3) void k_blur2_strip(const float* __restrict_
     const bool fix_l = xa < 0, fix_r = xa + GA::TW > W;
     auto fixup = [&](float* slot) {
         if (!(fix_l || fix_r)) return;
-        const int r = wv * 4 + (lane >> 4), j = lane & 15;
-        const int x = j < 8 ? xa + j : W + (j - 8);  // left halo xa .. xa + 7, right W .. W + 7
-        const bool act = j < 8 ? (fix_l && x < 0) : (fix_r && x - xa < GA::TW);
-        float val = 0.0f;
-        if (act) val = slot[r * GB::IWP + (reflect101(x, W) - xa)];
+        constexpr int NE = 4 * 2 * Q::HB, NIT = (NE + 63) / 64;
+        float val[NIT];
+        bool act[NIT];
+        int dst[NIT];
+#pragma unroll
+        for (int it = 0; it < NIT; it++) {
+            const int e = lane + 64 * it;
+            const int r = wv * 4 + e / (2 * Q::HB), j = e % (2 * Q::HB);
+            const int x = j < Q::HB ? xa + j : W + (j - Q::HB);  // left halo xa .. xa + HB - 1, right W .. W + HB - 1
+            act[it] = e < NE && (j < Q::HB ? (fix_l && x < 0) : (fix_r && x - xa < GA::TW));
+            dst[it] = r * GB::IWP + (x - xa);
+            val[it] = act[it] ? slot[r * GB::IWP + (reflect101(x, W) - xa)] : 0.0f;
+        }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
-        if (act) slot[r * GB::IWP + (x - xa)] = val;
+#pragma unroll
+        for (int it = 0; it < NIT; it++)
+            if (act[it]) slot[dst[it]] = val[it];
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
     };
-    const int nout = (ye - ys + S - 1) / S;  // G_{s+1} chunks; G_s chunks 0 .. nout; A-input chunks 0 .. nout + 1
-    const int ga = ys - Rb - Ra;             // first A-input row (chunk 0)
+    // chunks: G_{s+1} 0 .. nout-1; G_s 0 .. ng (B's windows reach NBW - 1
+    // chunks past the last output chunk); A's input 0 .. ng + 1
+    const int nout = (ye - ys + S - 1) / S;
+    const int ng = nout + NBW - 2, na = ng + 1;
+    const int ga = ys - Rb - Ra;  // first A-input row (chunk 0)
     float4 pre[GA::LPT];
     strip_load<Ra, kProfileOpenCV, GA>(pre, rs, voff, cols_in, ga, xa, W, H, pitch);
     strip_store<GA>(pre, aslot);
     strip_load<Ra, kProfileOpenCV, GA>(pre, rs, voff, cols_in, ga + S, xa, W, H, pitch);
     __syncthreads();
     strip_rowpass<GA, kProfileOpenCV>(aslot, taps_a, prow, pq);
-    for (int k = 0; k <= nout + 1; k++) {
+    for (int k = 0; k <= nout + NBW - 1; k++) {
         __syncthreads();  // P1
-        if (k + 1 <= nout + 1) {
+        if (k + 1 <= na) {
             strip_store<GA>(pre, aslot + ((k + 1) & 1) * GA::SLOT);
-            if (k + 2 <= nout + 1) strip_load<Ra, kProfileOpenCV, GA>(pre, rs, voff, cols_in, ga + (k + 2) * S, xa, W, H, pitch);
+            if (k + 2 <= na) strip_load<Ra, kProfileOpenCV, GA>(pre, rs, voff, cols_in, ga + (k + 2) * S, xa, W, H, pitch);
         }
         __syncthreads();  // P2
-        if (k + 1 <= nout + 1) strip_rowpass<GA, kProfileOpenCV>(aslot + ((k + 1) & 1) * GA::SLOT, taps_a, prow, pq);
-        if (k >= 1 && k - 1 <= nout) {
-            float* s1 = bslot + ((k - 1) % 3) * GB::SLOT;
+        if (k + 1 <= na) strip_rowpass<GA, kProfileOpenCV>(aslot + ((k + 1) & 1) * GA::SLOT, taps_a, prow, pq);
+        if (k >= 1 && k - 1 <= ng) {
+            float* s1 = bslot + ((k - 1) % NBR) * GB::SLOT;
             fixup(s1);
             strip_rowpass<GB, kProfileOpenCV>(s1, taps_b, prow, pq);
         }
         __syncthreads();  // P3
-        if (k <= nout) {
+        if (k <= ng) {
             const float* s0 = aslot + (k & 1) * GA::SLOT;
             const float* s1 = aslot + ((k + 1) & 1) * GA::SLOT;
-            float* dstb = bslot + (k % 3) * GB::SLOT;
+            float* dstb = bslot + (k % NBR) * GB::SLOT;
             const int y = ys - Rb + k * S;  // first G_s row of chunk k
             switch (wv) {
-#define COLA(w)                                                                                                  \
-    case w:                                                                                                      \
-        pair_colpass_a<GA, w>(s0, s1, dstb, GB::IWP, taps_a, lane, y, ys, ye, xa, W, pitch, Q::TWO, ra);         \
+#define COLA(w)                                                                                                       \
+    case w:                                                                                                           \
+        pair_colpass_a<GA, w, NXT>(s0, s1, dstb, GB::IWP, taps_a, lane, y, ys, ye, xa, Q::HB, W, pitch, Q::TWO, ra,   \
+                                   rn, pitch_n, wn, hn);                                                              \
         break;
                 COLA(0) COLA(1) COLA(2) COLA(3)
 #undef COLA
             }
         }
-        if (k >= 2 && k - 2 < nout) {
-            const float* s0 = bslot + ((k - 2) % 3) * GB::SLOT;
-            const float* s1 = bslot + ((k - 1) % 3) * GB::SLOT;
-            const int y = ys + (k - 2) * S;
+        if (k >= NBW && k - NBW < nout) {
+            const int j = k - NBW;  // output chunk: G_s chunks j .. j + NBW - 1
+            const float* s0 = bslot + (j % NBR) * GB::SLOT;
+            const float* s1 = bslot + ((j + 1) % NBR) * GB::SLOT;
+            const float* s2 = bslot + ((j + 2) % NBR) * GB::SLOT;
+            const int y = ys + j * S;
             // after B's in-place row pass slot column c is output column X + c: lanes 0 .. TWO/2 - 1 are
             // this strip's columns (the rest read the junk past A's 128 columns)
             switch (wv) {
@@ -759,7 +791,7 @@ __global__ __launch_bounds__(256, 3) void k_blur2_strip(const float* __restrict_
     case w:                                                                                                      \
         if (lane < Q::TWO / 2)                                                                                   \
             strip_colpass<GB, kProfileOpenCV, w, false>(s0, s1, taps_b, lane, y, ye, X, W, pitch, rb, rb, 0, 0,  \
-                                                        0);                                                      \
+                                                        0, s2);                                                  \
         break;
                 COLB(0) COLB(1) COLB(2) COLB(3)
 #undef COLB
@@ -1336,8 +1368,15 @@ static void launch_blur2_rr(const BlurLaunch& A, const BlurLaunch& B, hipStream_
     const int strips = (A.W + Q::TWO - 1) / Q::TWO;
     const int seg = strip_segment_rows(A.H, (long)strips * A.n_img);
     const int nseg = (A.H + seg - 1) / seg;
-    hipLaunchKernelGGL((k_blur2_strip<Ra, Rb>), dim3(strips, nseg, A.n_img), dim3(256), 0, st, A.src, A.src_img_stride,
-                       A.dst, B.dst, A.W, A.H, A.pitch, A.taps, B.taps, 0, A.H, seg);
+    const dim3 grid(strips, nseg, A.n_img);
+    if (A.nxt)
+        hipLaunchKernelGGL((k_blur2_strip<Ra, Rb, true>), grid, dim3(256), 0, st, A.src, A.src_img_stride, A.dst,
+                           B.dst, A.nxt, A.nxt_img_stride, A.pitch_n, A.wn, A.hn, A.W, A.H, A.pitch, A.taps, B.taps,
+                           0, A.H, seg);
+    else
+        hipLaunchKernelGGL((k_blur2_strip<Ra, Rb, false>), grid, dim3(256), 0, st, A.src, A.src_img_stride, A.dst,
+                           B.dst, A.nxt, A.nxt_img_stride, A.pitch_n, A.wn, A.hn, A.W, A.H, A.pitch, A.taps, B.taps,
+                           0, A.H, seg);
 }
 
 // SIFT_MI_PAIR=0 disables the pair kernel (A/B and test knob, read per launch)
@@ -1349,7 +1388,8 @@ static bool pair_blur_enabled() {
 int launch_blur_pair(int ra, int rb, const BlurLaunch& A, const BlurLaunch& B, hipStream_t st) {
     // A: G_{s-1} -> G_s, B: G_s -> G_{s+1} of one octave arena (same geometry
     // and image stride); whole planes, no DoG / next-octave output
-    const bool ok = A.profile == kProfileOpenCV && B.profile == kProfileOpenCV && !A.dog && !B.dog && !A.nxt &&
+    // (A may write the next octave's base: blur s = 3 of a pair (3, 4))
+    const bool ok = A.profile == kProfileOpenCV && B.profile == kProfileOpenCV && !A.dog && !B.dog &&
                     !B.nxt && A.y1 <= A.y0 && B.y1 <= B.y0 && A.dst && B.dst && B.src == A.dst && A.W == B.W &&
                     A.H == B.H && A.pitch == B.pitch && A.src_img_stride == A.dst_img_stride &&
                     B.src_img_stride == A.src_img_stride && B.dst_img_stride == A.src_img_stride && A.W >= 64 &&
@@ -1357,7 +1397,13 @@ int launch_blur_pair(int ra, int rb, const BlurLaunch& A, const BlurLaunch& B, h
                     pair_blur_enabled();
     if (!ok) return -1;
     if (ra == 5 && rb == 6) { launch_blur2_rr<5, 6>(A, B, st); return 0; }
-    if (ra == 6 && rb == 8) { launch_blur2_rr<6, 8>(A, B, st); return 0; }
+    // (8, 10) -- blurs 3, 4 -- builds and is exact, but its 4-slot G_s ring
+    // (10-row halos need 3-chunk windows at 16-row chunks) leaves 2 workgroups
+    // per CU: measured 2.06 ms against 1.78 ms for the two single launches
+    // (64 frames of 3840x2160, tools/ubench_kernels.hip pair), so it is not used
+#ifdef SIFT_PAIR_8_10
+    if (ra == 8 && rb == 10) { launch_blur2_rr<8, 10>(A, B, st); return 0; }
+#endif
     return -1;
 }
 
