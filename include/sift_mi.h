@@ -107,6 +107,14 @@ int sift_mi_extract_batch_device(sift_mi_ctx* ctx, const uint8_t* d_frames, size
  * descriptors, slower.  Keypoints are identical in both modes. */
 int sift_mi_set_exact_descriptors(sift_mi_ctx* ctx, int exact);
 
+/* LABELLED EXTENSION (not in the crate): cap the octave count at max_octaves
+ * (0 = the crate's formula round(log2(min(2W, 2H)) - 2) + 1, src/lib.rs:133-134,
+ * the default).  The kept octaves are computed exactly as without the cap, so
+ * the result is the uncapped result's keypoints of octaves < max_octaves (a
+ * prefix of the emission order).  For the "5 octaves" / "7 octaves" wording of
+ * BASELINE.json's configs; parity runs leave it at 0. */
+int sift_mi_set_max_octaves(sift_mi_ctx* ctx, int max_octaves);
+
 /* Batch pipeline lanes: 2 (default) runs consecutive chunks on two streams
  * with their own pyramid arenas, so one chunk's kernels overlap the other's;
  * 1 runs the chunks one after another on the context's stream (half the
@@ -215,9 +223,19 @@ typedef struct {
     uint64_t keypoints;
     uint64_t band_reruns;  /* row-band calls re-run on the whole-frame pyramid (sift_mi_set_row_band) */
     uint64_t stage_reruns; /* chunks re-run because a stage count exceeded its buffer bound */
+    /* gradient samples evaluated (sift_mi_set_sample_counting on, else 0):
+     * orientation = patch positions of gradient_direction_histogram
+     * (src/lib.rs:657-757) inside the image, descriptors = samples of the
+     * rotated 4x4 region that compute_descriptor (src/lib.rs:785-990) enumerates */
+    uint64_t orient_samples;
+    uint64_t desc_samples;
 } sift_mi_stats;
 int sift_mi_get_stats(sift_mi_ctx* ctx, sift_mi_stats* out);
 int sift_mi_reset_stats(sift_mi_ctx* ctx);
+/* Measurement only: count the samples the orientation and descriptor kernels
+ * evaluate (one device atomic per workgroup / per descriptor wave; off by
+ * default, and off in every timed run).  Read with sift_mi_get_stats. */
+int sift_mi_set_sample_counting(sift_mi_ctx* ctx, int on);
 
 /* Library version string and last error (thread-local). */
 const char* sift_mi_version(void);

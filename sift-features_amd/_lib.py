@@ -16,7 +16,7 @@ LIB_PATH = os.environ.get("SIFT_MI_LIB") or os.path.join(HERE, "libsift_mi.so")
 EXPORTS = [
     "sift_mi_create", "sift_mi_destroy", "sift_mi_set_stream", "sift_mi_set_chunk",
     "sift_mi_extract", "sift_mi_fetch", "sift_mi_fetch_keys", "sift_mi_extract_batch",
-    "sift_mi_extract_batch_device", "sift_mi_set_exact_descriptors", "sift_mi_set_keep_on_device", "sift_mi_device_results",
+    "sift_mi_extract_batch_device", "sift_mi_set_exact_descriptors", "sift_mi_set_max_octaves", "sift_mi_set_sample_counting", "sift_mi_set_keep_on_device", "sift_mi_device_results",
     "sift_mi_set_pipeline_lanes", "sift_mi_set_row_band",
     "sift_mi_precompute", "sift_mi_octave_dims", "sift_mi_read_scale_space", "sift_mi_read_dog",
     "sift_mi_sift_with_precomputed", "sift_mi_compute_descriptor", "sift_mi_gaussian_blur",
@@ -47,7 +47,8 @@ class Stats(ctypes.Structure):
                 ("pyramid_bytes", ctypes.c_uint64), ("pyramid_launches", ctypes.c_uint64),
                 ("frames", ctypes.c_uint64), ("extrema", ctypes.c_uint64),
                 ("keypoints", ctypes.c_uint64), ("band_reruns", ctypes.c_uint64),
-                ("stage_reruns", ctypes.c_uint64)]
+                ("stage_reruns", ctypes.c_uint64), ("orient_samples", ctypes.c_uint64),
+                ("desc_samples", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -89,6 +90,8 @@ def lib():
         "sift_mi_set_pipeline_lanes": [vp, i32],
         "sift_mi_set_row_band": [vp, ctypes.c_uint32, ctypes.c_uint32],
         "sift_mi_set_exact_descriptors": [vp, i32],
+        "sift_mi_set_max_octaves": [vp, i32],
+        "sift_mi_set_sample_counting": [vp, i32],
         "sift_mi_device_results": [vp, P(vp), P(vp), P(sz)],
         "sift_mi_precompute": [vp, vp, u32, u32, sz, P(sz)],
         "sift_mi_octave_dims": [vp, sz, P(u32), P(u32)],

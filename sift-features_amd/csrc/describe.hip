@@ -373,7 +373,7 @@ template <int kShare, int kAblate = 0, class Mid = NoHook>
 __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img, int pitch, int width, int height,
                                                    float xf, float yf, float scale, float orientation,
                                                    DescScratchFast<kShare>& sc, uint8_t* __restrict__ out, int lane,
-                                                   Mid mid = Mid()) {
+                                                   Mid mid = Mid(), uint32_t* n_samples = nullptr) {
     constexpr int NS = 64 / kShare;  // slices
     const int32_t x = (int32_t)sat_u32(roundf(xf));
     const int32_t y = (int32_t)sat_u32(roundf(yf));
@@ -396,6 +396,7 @@ __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img
     // fails) are not enumerated
     build_row_table(sc.rowlo, sc.rowpre, radius, cos_s, sin_s, lane, 1 - x, width - 2 - x, 1 - y, height - 2 - y);
     const int total = (kAblate & 64) ? 0 : sc.rowpre[n];  // kAblate bit 6: no samples (per-keypoint overhead)
+    if (n_samples) *n_samples += (uint32_t)total;
     // Lane-strided samples: one load instruction touches ~64 neighbouring
     // pixels (2-3 cache lines) instead of 64 scattered ones.  Each iteration
     // takes two samples per lane (k, k + 64) -- packed math, independent
@@ -592,6 +593,7 @@ __global__ __launch_bounds__(64) void k_describe(const DescLaunch L) {
     issue();
     uint32_t i = take();
     KpRec kp = record(i);
+    uint32_t nsamp = 0;  // samples enumerated by this wave (sample counting)
     while (i < n) {
         if (drained < kDescQueues) issue();
         const int o = __builtin_amdgcn_readfirstlane(kp.octave);
@@ -616,7 +618,7 @@ __global__ __launch_bounds__(64) void k_describe(const DescLaunch L) {
             next();
         } else {
             describe_wave_fast<kExact ? 1 : kMode, kAblate>(img, pitch, W, H, kp.x * osf, kp.y * osf, kp_size, angle,
-                                                            scr, out, lane, next);
+                                                            scr, out, lane, next, L.samples ? &nsamp : nullptr);
         }
         if (lane == 0) {
             if (L.out_kp) {
@@ -634,6 +636,7 @@ __global__ __launch_bounds__(64) void k_describe(const DescLaunch L) {
         i = ni;
         kp = nkp;
     }
+    if (L.samples && lane == 0 && nsamp) atomicAdd(L.samples + (blockIdx.x & 7), (unsigned long long)nsamp);
 }
 
 void launch_describe(const DescLaunch& L, hipStream_t st) {

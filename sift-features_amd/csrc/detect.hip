@@ -353,7 +353,7 @@ __global__ __launch_bounds__(256, SIFT_ORIENT_MIN_WAVES) void k_orient(const Ori
     __shared__ __attribute__((aligned(16))) float sval[4][OR_LDS];
     __shared__ __attribute__((aligned(16))) uint8_t sbin[4][OR_LDS];
     __shared__ float swt[4][OR_WT];  // per-wave Gaussian weight table
-    __shared__ uint32_t wcount[4], wbase;
+    __shared__ uint32_t wcount[4], wbase, wsamp[4];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t n_ext = min(*L.n_ext, L.ext_cap);
     // one group of 4 extrema per workgroup; the grid covers the bound, the
@@ -365,6 +365,7 @@ __global__ __launch_bounds__(256, SIFT_ORIENT_MIN_WAVES) void k_orient(const Ori
         const bool active = r < n_ext;
         ExtRec e;
         int W = 1, H = 1, pitch = 1, radius = 0, n = 1, N = 0;
+        uint32_t nin = 0;  // patch positions inside the image (sample counting)
         float kp_scale = 0.f, kp_x = 0.f, kp_y = 0.f, osf = 1.f;
         const float* img = nullptr;
         if (active) {
@@ -450,6 +451,12 @@ __global__ __launch_bounds__(256, SIFT_ORIENT_MIN_WAVES) void k_orient(const Ori
                 sval[wave][idx] = val;
                 sbin[wave][idx] = bin;
             }
+            if (L.samples) {  // measurement only
+                const int x = e.x, y = e.y;
+                const int y0 = max(y - radius, 1), y1 = min(y + radius, H - 2);
+                const int x0 = max(x - radius, 1), x1 = min(x + radius, W - 2);
+                nin = (y1 >= y0 && x1 >= x0) ? (uint32_t)((y1 - y0 + 1) * (x1 - x0 + 1)) : 0u;
+            }
         }
         __syncthreads();
         // sequential per-bin sums (lane = bin); inactive waves run on an empty list
@@ -490,10 +497,14 @@ __global__ __launch_bounds__(256, SIFT_ORIENT_MIN_WAVES) void k_orient(const Ori
         const uint32_t npk = (uint32_t)__popcll(mask);
         // one global atomic per workgroup (4 waves)
         if (lane == 0) wcount[wave] = npk;
+        if (L.samples && lane == 0) wsamp[wave] = nin;
         __syncthreads();
         if (threadIdx.x == 0) {
             const uint32_t tot = wcount[0] + wcount[1] + wcount[2] + wcount[3];
             wbase = tot ? atomicAdd(L.counter, tot) : 0u;
+            if (L.samples)
+                atomicAdd(L.samples + (blockIdx.x & 7),
+                          (unsigned long long)(wsamp[0] + wsamp[1] + wsamp[2] + wsamp[3]));
         }
         __syncthreads();
         uint32_t base = wbase;

@@ -349,6 +349,7 @@ struct ResizeTabDev {
 struct Plan {
     uint32_t w = 0, h = 0, chunk = 0;
     int n_oct = 0;
+    int max_oct = 0;  // the context's max_octaves the plan was built for
     std::vector<int> ow, oh, opitch;
     std::vector<size_t> P;           // floats per octave image plane (pitch * H)
     std::vector<size_t> px;          // real pixels per octave image (W * H)
@@ -452,6 +453,9 @@ struct sift_mi_ctx {
     bool band_restricted = false;     // this call computes only the band's pyramid rows
     bool band_whole = false;          // re-run of a band on the whole-frame pyramid
     int exact_descriptors = 0;
+    int max_octaves = 0;                    // sift_mi_set_max_octaves (0: the crate's formula)
+    int count_samples = 0;                  // sift_mi_set_sample_counting (measurement only)
+    DevBuf<unsigned long long> samples;     // [0, 8): orientation, [8, 16): descriptor sample counters
     Plan plan;
     DevBuf<uint8_t> staging;  // host-sourced frames
     Slot slot[2];  // slot = pipeline lane: chunk k runs on lane k & 1
@@ -533,8 +537,10 @@ int ensure_lane(sift_mi_ctx* c, int lane) {
 
 int ensure_plan(sift_mi_ctx* c, uint32_t w, uint32_t h, uint32_t chunk) {
     Plan& p = c->plan;
-    if (p.w == w && p.h == h && p.chunk >= chunk && p.arena[0].p && p.profile == (int)c->profile) return 0;
-    if (!(p.w == w && p.h == h && p.profile == (int)c->profile)) {
+    if (p.w == w && p.h == h && p.chunk >= chunk && p.arena[0].p && p.profile == (int)c->profile &&
+        p.max_oct == c->max_octaves)
+        return 0;
+    if (!(p.w == w && p.h == h && p.profile == (int)c->profile && p.max_oct == c->max_octaves)) {
         p.release();
         // per-frame stage high-water marks belong to a frame size
         c->pf_cand = c->pf_ext = c->pf_kp = 0;
@@ -545,6 +551,10 @@ int ensure_plan(sift_mi_ctx* c, uint32_t w, uint32_t h, uint32_t chunk) {
     p.h = h;
     p.chunk = chunk;
     p.n_oct = n_octaves_for(w, h);
+    // labelled extension (sift_mi_set_max_octaves): fewer octaves than the
+    // crate's formula (src/lib.rs:133-134); the kept octaves are unchanged
+    if (c->max_octaves > 0) p.n_oct = std::min(p.n_oct, c->max_octaves);
+    p.max_oct = c->max_octaves;
     p.ow.assign(p.n_oct, 0);
     p.oh.assign(p.n_oct, 0);
     p.opitch.assign(p.n_oct, 0);
@@ -967,6 +977,7 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
     O.counter = cnt + 2;
     O.img_base = 0;
     O.cap = B.bk;
+    O.samples = c->count_samples ? c->samples.p : nullptr;
     launch_orient(O, st);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(S.ev[3], st));
@@ -1024,6 +1035,7 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
     DL.out_key = S.out_key.p;
     DL.out_desc = S.out_desc.p;
     DL.exact = c->exact_descriptors;
+    DL.samples = c->count_samples ? c->samples.p + 8 : nullptr;
     launch_describe(DL, st);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(S.ev[5], st));
@@ -1366,6 +1378,15 @@ int sift_mi_set_stream(sift_mi_ctx* c, void* s) {
 int sift_mi_set_chunk(sift_mi_ctx* c, uint32_t k) {
     if (!c) return fail(SIFT_MI_EINVAL, "ctx is null");
     c->chunk_override = k;
+    return 0;
+}
+
+int sift_mi_set_max_octaves(sift_mi_ctx* c, int max_octaves) {
+    if (!c || max_octaves < 0) return fail(SIFT_MI_EINVAL, "max_octaves must be >= 0");
+    CHK(set_device(c));
+    CHK(sync_lanes(c));
+    c->max_octaves = max_octaves;  // the plan is rebuilt on the next call
+    c->have_pyramid = false;
     return 0;
 }
 
@@ -1748,12 +1769,40 @@ int sift_mi_decode_jpeg_batch(sift_mi_ctx* c, const uint8_t* const* data, const 
 int sift_mi_get_stats(sift_mi_ctx* c, sift_mi_stats* out) {
     if (!c || !out) return fail(SIFT_MI_EINVAL, "bad arguments");
     *out = c->stats;
+    if (c->count_samples && c->samples.p) {
+        CHK(set_device(c));
+        CHK(sync_lanes(c));
+        unsigned long long h[16];
+        HIPCHK(hipMemcpy(h, c->samples.p, sizeof h, hipMemcpyDeviceToHost));
+        out->orient_samples = out->desc_samples = 0;
+        for (int i = 0; i < 8; i++) {
+            out->orient_samples += h[i];
+            out->desc_samples += h[8 + i];
+        }
+    }
     return 0;
 }
 
 int sift_mi_reset_stats(sift_mi_ctx* c) {
     if (!c) return fail(SIFT_MI_EINVAL, "ctx is null");
     c->stats = sift_mi_stats{};
+    if (c->samples.p) {
+        CHK(set_device(c));
+        CHK(sync_lanes(c));
+        HIPCHK(hipMemset(c->samples.p, 0, 16 * sizeof(unsigned long long)));
+    }
+    return 0;
+}
+
+int sift_mi_set_sample_counting(sift_mi_ctx* c, int on) {
+    if (!c) return fail(SIFT_MI_EINVAL, "ctx is null");
+    CHK(set_device(c));
+    CHK(sync_lanes(c));
+    if (on && !c->samples.p) {
+        CHK(c->samples.ensure(16));
+        HIPCHK(hipMemset(c->samples.p, 0, 16 * sizeof(unsigned long long)));
+    }
+    c->count_samples = on ? 1 : 0;
     return 0;
 }
 

@@ -173,6 +173,7 @@ struct OrientLaunch {
     uint32_t* counter;
     int img_base;
     uint32_t cap;
+    unsigned long long* samples;  // 8 counters (measurement only; null: off)
 };
 void launch_orient(const OrientLaunch& L, hipStream_t st);
 
@@ -234,6 +235,7 @@ struct DescLaunch {
     uint64_t* out_key; // may be null
     uint8_t* out_desc;
     int exact;         // 1: bit-exact bin-owner accumulation (describe_wave_exact)
+    unsigned long long* samples;  // 8 counters (measurement only; null: off)
 };
 void launch_describe(const DescLaunch& L, hipStream_t st);
 

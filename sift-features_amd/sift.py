@@ -147,6 +147,17 @@ class Context:
         """Bit-exact descriptor accumulation order (slower); default off."""
         check(lib().sift_mi_set_exact_descriptors(self._h, 1 if exact else 0))
 
+    def set_max_octaves(self, max_octaves):
+        """LABELLED EXTENSION (not in the crate): cap the octave count (0 = the
+        crate's formula, src/lib.rs:133-134).  The result is the uncapped
+        result's keypoints of octaves < max_octaves."""
+        check(lib().sift_mi_set_max_octaves(self._h, int(max_octaves)))
+
+    def set_sample_counting(self, on=True):
+        """Measurement only: count the gradient samples the orientation and
+        descriptor kernels evaluate (stats() orient_samples / desc_samples)."""
+        check(lib().sift_mi_set_sample_counting(self._h, 1 if on else 0))
+
     def set_row_band(self, band, n_bands):
         """Keypoint stages over octave rows [H_o*band/n_bands, H_o*(band+1)/n_bands)
         only (include/sift_mi.h); band 0 of 1 = the whole frame.  Merge the

@@ -39,3 +39,9 @@ def ctx(pkg):
 def load_golden(name):
     d = np.load(os.path.join(GOLDEN, name + ".npz"))
     return {k: d[k] for k in d.files}
+
+
+@pytest.fixture(scope="session")
+def synth():
+    import synth as S
+    return S

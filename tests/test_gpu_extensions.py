@@ -1,0 +1,112 @@
+"""Labelled extensions and tooling around the path, on the GPU.
+
+* `set_max_octaves` (LABELLED EXTENSION, not in the crate; for the configs'
+  "5 octaves" / "7 octaves" wording): the capped result is exactly the
+  uncapped result's keypoints of octaves < cap -- a prefix of the emission
+  order (octave-major, src/lib.rs:281-294), since octave o's images depend
+  only on octaves <= o (src/lib.rs:213-267).  Checked bit for bit against the
+  uncapped GPU result (itself oracle-checked in test_gpu_parity).
+* sample counting (measurement only): counts are the closed-form patch sizes
+  and leave the results unchanged.
+* run_sift.py, the examples/run-sift.rs counterpart: prints the keypoint
+  count of `sift()` on the reference's own test JPEGs, equal to the oracle's
+  count on the decoded image (imageproc profile, the crate's `sift()`), and
+  the snapshot counts with --processing opencv (src/snapshots: 225 / 1270).
+"""
+import os
+import subprocess
+import sys
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+JPEG = os.path.join(ROOT, "tests", "golden", "jpeg")
+
+
+def _octaves(keys):
+    return (np.asarray(keys, np.uint64) >> np.uint64(38)) & np.uint64(0xF)
+
+
+@pytest.mark.parametrize("shape,cap", [((240, 320), 3), ((1080, 1920), 5), ((480, 640), 1)])
+def test_max_octaves_is_a_prefix(pkg, synth, shape, cap):
+    h, w = shape
+    img = synth.frame(w, h, 11)
+    c = pkg.Context(0, pkg.OpenCVProcessing)
+    try:
+        full = c.sift(img)
+        c.set_max_octaves(cap)
+        capped = c.sift(img)
+        c.set_max_octaves(0)
+        again = c.sift(img)
+    finally:
+        c.close()
+    octs = _octaves(full.keys)
+    keep = octs < cap
+    n = int(keep.sum())
+    assert 0 < n < len(full)
+    assert keep[:n].all() and not keep[n:].any()  # octave-major emission order
+    assert len(capped) == n
+    assert np.array_equal(capped.keypoints_array, full.keypoints_array[:n])
+    assert np.array_equal(capped.descriptors, full.descriptors[:n])
+    assert np.array_equal(again.keypoints_array, full.keypoints_array)
+
+
+def test_max_octaves_batch(pkg, synth):
+    frames = np.stack([synth.frame(640, 480, s) for s in range(3)])
+    c = pkg.Context(0, pkg.OpenCVProcessing)
+    try:
+        full = c.sift_batch(frames)
+        c.set_max_octaves(4)
+        capped = c.sift_batch(frames)
+    finally:
+        c.close()
+    for f, g in zip(full, capped):
+        n = int((_octaves(f.keys) < 4).sum())
+        assert np.array_equal(g.keypoints_array, f.keypoints_array[:n])
+        assert np.array_equal(g.descriptors, f.descriptors[:n])
+
+
+def test_sample_counting(pkg, synth):
+    img = synth.frame(640, 480, 3)
+    c = pkg.Context(0, pkg.OpenCVProcessing)
+    try:
+        ref = c.sift(img)
+        c.set_sample_counting(True)
+        c.reset_stats()
+        res = c.sift(img)
+        st = c.stats()
+        c.set_sample_counting(False)
+    finally:
+        c.close()
+    assert np.array_equal(res.keypoints_array, ref.keypoints_array)
+    assert np.array_equal(res.descriptors, ref.descriptors)
+    n_ext = st["extrema"]
+    # every extremum's patch is (2r + 1)^2 <= 33^2 positions, r >= 1
+    assert 9 * n_ext <= st["orient_samples"] <= 33 * 33 * n_ext
+    # a descriptor window covers ~(5 * 3 * sigma)^2 samples, sigma >= 1.6
+    assert st["desc_samples"] >= 100 * len(res)
+    assert st["desc_samples"] <= 79 * 79 * len(res)
+
+
+@pytest.mark.parametrize("name", ["bird_small", "tree_small"])
+def test_run_sift_cli(pkg, oracle, name):
+    path = os.path.join(JPEG, name + ".jpg")
+    env = dict(os.environ)
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "sift-features_amd", "run_sift.py"), path],
+                         capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 0, out.stderr
+    c = pkg.Context(0, pkg.ImageprocProcessing)
+    try:
+        with open(path, "rb") as f:
+            img = c.decode_jpeg(f.read())
+    finally:
+        c.close()
+    kp_o, _ = oracle.sift(img, profile=oracle.PROFILE_IMAGEPROC)
+    assert out.stdout.strip() == f"{len(kp_o)} keypoints"
+    out = subprocess.run([sys.executable, os.path.join(ROOT, "sift-features_amd", "run_sift.py"), path,
+                          "--processing", "opencv"], capture_output=True, text=True, timeout=300, env=env)
+    assert out.returncode == 0, out.stderr
+    assert out.stdout.strip() == {"bird_small": "225 keypoints", "tree_small": "1270 keypoints"}[name]
