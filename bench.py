@@ -63,14 +63,17 @@ def parse():
     return p.parse_args()
 
 
-def run_config(pkg, synth, dev, device_index, n, W, H, steps, seed0=1000):
+def run_config(pkg, synth, dev, device_index, n, W, H, steps, seed0=1000, max_octaves=0):
     """One BASELINE config on one GPU: `n` device-resident W x H frames per
     call, results left in HBM; keypoints/s from two-lane calls, the pyramid
-    stage's HIP-event time (and its roofline fraction) from a serialised pass."""
+    stage's HIP-event time (and its roofline fraction) from a serialised pass.
+    max_octaves > 0: the labelled octave-cap extension (not the crate)."""
     import torch
     fr = synth.frames_torch(n, W, H, seed0=seed0, device=dev)
     torch.cuda.synchronize()
     c = pkg.Context(device_index, pkg.OpenCVProcessing)
+    if max_octaves:
+        c.set_max_octaves(max_octaves)
     call = (fr.data_ptr(), n, W, H, fr.stride(1), fr.stride(0))
 
     def go():
@@ -94,8 +97,9 @@ def run_config(pkg, synth, dev, device_index, n, W, H, steps, seed0=1000):
     del fr
     torch.cuda.empty_cache()
     gbs = st["pyramid_bytes"] / (st["pyramid_ms"] * 1e-3) / 1e9 if st["pyramid_ms"] > 0 else 0.0
+    n_oct = int(round(np.log2(min(2 * W, 2 * H)) - 2)) + 1
     return {"frames_per_call": n, "frame": f"{W}x{H}",
-            "octaves": int(round(np.log2(min(2 * W, 2 * H)) - 2)) + 1,
+            "octaves": min(n_oct, max_octaves) if max_octaves else n_oct,
             "ms_per_call": 1e3 * dt, "keypoints_per_s": kp / steps / dt, "frames_per_s": n / dt,
             "keypoints_per_frame": kp / steps / n, "pyramid_ms_per_call": st["pyramid_ms"] / steps,
             "pyramid_gbs": gbs, "pyramid_frac": gbs / HBM_PEAK_GBS}
@@ -172,7 +176,27 @@ def main():
     torch.cuda.synchronize()
     serial_ms = 1e3 * (time.perf_counter() - t1) / args.steps
     st = ctx.stats()
+    # one more (untimed) step with the measurement-only sample counters: the
+    # gradient samples the orientation and descriptor kernels evaluate per
+    # step, divided by their serialised-pass stage time above
+    ctx.set_sample_counting(True)
+    ctx.reset_stats()
+    step()
+    torch.cuda.synchronize()
+    sc = ctx.stats()
+    ctx.set_sample_counting(False)
     ctx.set_pipeline_lanes(2)
+    kp_stages = {
+        "extrema_per_step": sc["extrema"], "keypoints_per_step": sc["keypoints"],
+        "orientation": {"ms_per_step": st["orient_ms"] / args.steps, "samples_per_step": sc["orient_samples"],
+                        "samples_per_s": sc["orient_samples"] / (st["orient_ms"] / args.steps * 1e-3),
+                        "extrema_per_s": sc["extrema"] / (st["orient_ms"] / args.steps * 1e-3)},
+        "descriptor": {"ms_per_step": st["descriptor_ms"] / args.steps, "samples_per_step": sc["desc_samples"],
+                       "samples_per_s": sc["desc_samples"] / (st["descriptor_ms"] / args.steps * 1e-3),
+                       "keypoints_per_s": sc["keypoints"] / (st["descriptor_ms"] / args.steps * 1e-3)},
+        "note": "samples = patch positions / rotated-region samples the kernels evaluate (rank 0, one step, "
+                "sift_mi_set_sample_counting); times from the serialised stage-timing pass",
+    }
 
     dt_max, total_kp, total_frames = shard.reduce_run(dt, n_kp, B * args.steps, dist if world > 1 else None)
 
@@ -269,6 +293,12 @@ def main():
             "single_1080p": run_config(pkg, synth, dev, local, 1, 1920, 1080, max(10, args.steps)),
             "vga_256": run_config(pkg, synth, dev, local, 256, 640, 480, max(3, args.steps)),
             "giant_8192": run_config(pkg, synth, dev, local, 1, 8192, 8192, max(3, args.steps)),
+            # LABELLED EXTENSION (sift_mi_set_max_octaves, not the crate): the
+            # configs' "5 octaves" (#2) and "7 octaves" (#5) wording
+            "ext_single_1080p_5oct": run_config(pkg, synth, dev, local, 1, 1920, 1080, max(10, args.steps),
+                                                max_octaves=5),
+            "ext_giant_8192_7oct": run_config(pkg, synth, dev, local, 1, 8192, 8192, max(3, args.steps),
+                                              max_octaves=7),
         }
         configs["single_1080p"]["latency_host_fetch_ms"] = latency_ms
 
@@ -318,6 +348,7 @@ def main():
                          "avg_launch_ms": per_launch_ms},
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_all,
+            "keypoint_stages": kp_stages,
             "gather": gather,
             "configs": configs,
         }
