@@ -244,10 +244,11 @@ with open(out_md, "w") as f:
         f.write("\n## SQ counters per kernel (all dispatches of the profiled command)\n\n")
         f.write("Wave-cycle fractions are of SQ_WAVE_CYCLES (quad-cycles, summed over waves): `valu` = "
                 "SQ_ACTIVE_INST_VALU, `lds` = SQ_ACTIVE_INST_LDS, `wait` = SQ_WAIT_ANY (parked at a waitcnt / "
-                "barrier), `stall` = SQ_WAIT_INST_ANY (ready but not issued). `VALU busy` = 4 x SQ_ACTIVE_INST_VALU "
-                "/ 1024 SIMDs / (GRBM_GUI_ACTIVE / 8 XCDs): the share of SIMD cycles issuing VALU while the "
-                "kernel ran. `bank` = SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS.\n\n")
-        f.write("| kernel | dispatches | VALU insts / wave | valu | lds | wait | stall | VALU busy | bank |\n"
+                "barrier), `stall` = SQ_WAIT_INST_ANY (ready but not issued). `waves/SIMD` = SQ_WAVE_CYCLES / "
+                "(1024 SIMDs x GRBM_GUI_ACTIVE / 8 XCDs / 4): mean resident waves per SIMD while the kernel "
+                "ran, so `valu` x `waves/SIMD` approximates the SIMD's VALU issue share. `bank` = "
+                "SQ_LDS_BANK_CONFLICT / SQ_ACTIVE_INST_LDS.\n\n")
+        f.write("| kernel | dispatches | VALU insts / wave | valu | lds | wait | stall | waves/SIMD | bank |\n"
                 "|---|---|---|---|---|---|---|---|---|\n")
         keys = sorted(sq, key=lambda k: -sq[k].get("SQ_WAVE_CYCLES", 0))
         for k in keys:
@@ -257,7 +258,7 @@ with open(out_md, "w") as f:
                 continue
             waves = max(1.0, c.get("SQ_WAVES", 0))
             gui = c.get("GRBM_GUI_ACTIVE", 0) / 8
-            vb = 4 * c.get("SQ_ACTIVE_INST_VALU", 0) / N_SIMD / gui if gui else float("nan")
+            vb = wc / (N_SIMD * gui / 4) if gui else float("nan")
             lds = c.get("SQ_ACTIVE_INST_LDS", 0)
             f.write(f"| `{k[:48]}` | {sq_n[k]} | {c.get('SQ_INSTS_VALU', 0) / waves:.0f} | "
                     f"{c.get('SQ_ACTIVE_INST_VALU', 0) / wc:.2f} | {lds / wc:.2f} | "
