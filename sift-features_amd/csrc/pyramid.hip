@@ -313,8 +313,17 @@ struct StripGeom {
     static constexpr int LPT = (NLOAD4 + 64 * NW - 1) / (64 * NW);
     static constexpr int SLOT = S * IWP;
     static constexpr int LDS_FLOATS = 2 * SLOT;
-    // resident workgroups per CU that the LDS allows (<= 4): the register budget follows
-    static constexpr int MINB = 163840 / (4 * LDS_FLOATS) < 4 ? 163840 / (4 * LDS_FLOATS) : 4;
+    // resident workgroups per CU that the LDS allows (<= 4): the register
+    // budget follows.  R >= 10: at most 3 -- at 4 the R = 10 kernel spills
+    // (128 VGPRs); at 3 it does not and runs 4% faster (octave 0 of 64
+    // frames, tools/ubench_kernels.hip strip).  A second register buffer for
+    // a prefetch depth of 2 chunks was slower at R = 8, 10 and no faster
+    // elsewhere.
+#ifndef SIFT_STRIP_MINB_CAP_R10
+#define SIFT_STRIP_MINB_CAP_R10 3
+#endif
+    static constexpr int MINB0 = 163840 / (4 * LDS_FLOATS) < 4 ? 163840 / (4 * LDS_FLOATS) : 4;
+    static constexpr int MINB = (R >= 10 && MINB0 > SIFT_STRIP_MINB_CAP_R10) ? SIFT_STRIP_MINB_CAP_R10 : MINB0;
     static constexpr int NCW = (2 * R + S - 1) / S + 1;  // chunks in a column-pass window (2, or 3 for S < 2R)
     static_assert(2 * R <= 2 * S, "a column-pass window spans at most three chunks");
     static_assert((IWP / 4) % 2 == 1, "row-pass lane groups: odd float4 pitch");
