@@ -343,7 +343,7 @@ def main():
             "roofline": {"bound": "hbm", "achieved": pyr_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": pyr_gbs / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "kernel": "pyramid stage (k_seed + k_blur<R>), rank 0",
+                         "kernel": "pyramid stage (k_seed_strip + k_blur2_strip + k_blur_strip<R> + k_octave_tail), rank 0",
                          "algorithmic_bytes_per_launch": per_launch_bytes,
                          "avg_launch_ms": per_launch_ms},
             "cpu_baseline": cpu,
