@@ -219,3 +219,24 @@ def test_world2_gather_device_results(pkg):
         p.join(timeout=30)
         assert p.exitcode == 0
     assert all(r[0] == "ok" and r[2] for r in res), res
+
+
+@pytest.mark.gpu
+def test_batch_fused_kernels_equal_single_launches(pkg, monkeypatch):
+    """The batch path (no DoG planes) with the pair and tail kernels equals the
+    batch path with single-blur launches only, bit for bit (1080p frames:
+    the pair covers octaves 0-4, the tail octaves 5-9)."""
+    import synth
+    frames = np.stack([synth.frame(1920, 1080, s) for s in range(2)])
+    c = pkg.Context(0, pkg.OpenCVProcessing)
+    try:
+        fused = c.sift_batch(frames)
+        monkeypatch.setenv("SIFT_MI_PAIR", "0")
+        monkeypatch.setenv("SIFT_MI_TAIL", "0")
+        single = c.sift_batch(frames)
+    finally:
+        c.close()
+    for a, b in zip(fused, single):
+        assert np.array_equal(a.keypoints_array, b.keypoints_array)
+        assert np.array_equal(a.descriptors, b.descriptors)
+        assert np.array_equal(a.keys, b.keys)

@@ -80,17 +80,31 @@ def test_pyramid_bit_exact(ctx, oracle, name):
         assert np.array_equal(d, do), (o, np.abs(d - do).max())
 
 
-@pytest.mark.parametrize("kernel", ["strip", "tile"])
+_KERNEL_ENV = {
+    "strip": {"SIFT_MI_BLUR_KERNEL": "strip"},
+    "tile": {"SIFT_MI_BLUR_KERNEL": "tile"},
+    "nopair": {"SIFT_MI_PAIR": "0"},
+    "notail": {"SIFT_MI_TAIL": "0"},
+    "single": {"SIFT_MI_PAIR": "0", "SIFT_MI_TAIL": "0"},
+}
+
+
+@pytest.mark.parametrize("kernel", sorted(_KERNEL_ENV))
 @pytest.mark.parametrize("name", ["synth_640x480", "synth_301x207", "synth_97x61", "synth_1000x333",
                                   "synth_90x700", "synth_2000x40", "synth_33x17"])
 def test_pyramid_blur_kernels(ctx, oracle, monkeypatch, kernel, name):
-    """Both blur kernel families against the oracle's blur chain, bit for bit:
-    "strip" (k_seed_strip / k_blur_strip: 128-column strips streamed down in
-    row chunks, many row segments per octave at these sizes, partial strips,
-    reflect-101 at every border; the tile kernels where a strip does not
-    apply: tiny octaves, W or H <= R) and "tile" (SIFT_MI_BLUR_KERNEL=tile:
-    one 64-column tile per workgroup everywhere)."""
-    monkeypatch.setenv("SIFT_MI_BLUR_KERNEL", kernel)
+    """Every blur kernel family against the oracle's blur chain, bit for bit:
+    "strip" (the default: k_seed_strip, the k_blur2_strip pair for G_1, G_2,
+    k_blur_strip for the rest -- 128-column strips streamed down in row
+    chunks, many row segments per octave at these sizes, partial strips,
+    reflect-101 at every border -- and k_octave_tail from the first octave that
+    fits LDS; the tile kernels where a strip does not apply: tiny octaves, W
+    or H <= R), "tile" (SIFT_MI_BLUR_KERNEL=tile: one 64-column tile per
+    workgroup everywhere), "nopair" / "notail" / "single" (SIFT_MI_PAIR=0,
+    SIFT_MI_TAIL=0: single-blur strips instead of the pair kernel, per-blur
+    launches for the small octaves)."""
+    for k, v in _KERNEL_ENV[kernel].items():
+        monkeypatch.setenv(k, v)
     img = INPUTS[name] if name in INPUTS else _extra(name)
     pre = ctx.precompute_images(img)
     opy = oracle.Pyramid(img)
