@@ -343,7 +343,7 @@ void launch_refine(const RefineLaunch& L, hipStream_t st) {
 // LDS list in the reference's row-major order; lane k < 36 then sums bin k
 // sequentially over the list (bit-identical to `raw_hist[bin + 2] += w*mag`).
 // ---------------------------------------------------------------------------
-constexpr int OR_LDS = 1092;
+constexpr int OR_LDS = 1104;  // >= 33 * 33 samples, a multiple of 16 (16-byte bin reads)
 constexpr int OR_WT = 17 * 18 / 2;  // weight table entries at the largest radius (16)
 
 #ifndef SIFT_ORIENT_MIN_WAVES
@@ -465,8 +465,26 @@ __global__ __launch_bounds__(256, SIFT_ORIENT_MIN_WAVES) void k_orient(const Ori
         {
             const float4* v4 = reinterpret_cast<const float4*>(sval[wave]);
             const uint32_t* b4 = reinterpret_cast<const uint32_t*>(sbin[wave]);
+            const uint4* b16 = reinterpret_cast<const uint4*>(sbin[wave]);
             const uint32_t me = (uint32_t)lane;
             int j = 0;
+            // 16 samples per iteration: all five LDS reads in flight together
+            // (one latency per 16 samples instead of per 4); the adds stay in
+            // sample order
+            for (; j + 16 <= N; j += 16) {
+                const uint4 bb = b16[j >> 4];
+                const float4 va = v4[(j >> 2) + 0], vb = v4[(j >> 2) + 1], vc = v4[(j >> 2) + 2],
+                             vd = v4[(j >> 2) + 3];
+                const uint32_t w[4] = {bb.x, bb.y, bb.z, bb.w};
+                const float4 vv[4] = {va, vb, vc, vd};
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    acc += ((w[q] & 0xff) == me) ? vv[q].x : 0.0f;
+                    acc += (((w[q] >> 8) & 0xff) == me) ? vv[q].y : 0.0f;
+                    acc += (((w[q] >> 16) & 0xff) == me) ? vv[q].z : 0.0f;
+                    acc += ((w[q] >> 24) == me) ? vv[q].w : 0.0f;
+                }
+            }
             for (; j + 4 <= N; j += 4) {
                 const float4 v = v4[j >> 2];
                 const uint32_t bb = b4[j >> 2];
