@@ -622,7 +622,12 @@ struct PairGeom {
     static constexpr int HB = GB::HWL;             // G_s halo columns of B's window
     static constexpr int TWO = GA::TW - 2 * HB;   // output columns per strip
     static constexpr int NBW = GB::NCW;           // G_s chunks in a column-pass window of B
-    static constexpr int NBR = NBW + 1;           // B ring: the window + the chunk being written
+    // B ring: the window + the chunk being written (two-chunk windows: the
+    // two column passes share a phase); three-chunk windows use a ring of 3
+    // with the column passes in separate phases (one more barrier per step,
+    // but 3 workgroups per CU instead of 2)
+    static constexpr bool SPLIT = NBW == 3;
+    static constexpr int NBR = SPLIT ? 3 : NBW + 1;
     static constexpr int LDS_FLOATS = 2 * GA::SLOT + NBR * GB::SLOT;
     static constexpr int MINB = 163840 / (4 * LDS_FLOATS) < 4 ? 163840 / (4 * LDS_FLOATS) : 4;
     static_assert(GA::HWL == 8 && GA::NCW == 2, "A: radius <= 8");
@@ -777,23 +782,11 @@ __global__ __launch_bounds__(256, (PairGeom<Ra, Rb>::MINB)) void k_blur2_strip(
             fixup(s1);
             strip_rowpass<GB, kProfileOpenCV>(s1, taps_b, prow, pq);
         }
-        __syncthreads();  // P3
-        if (k <= ng) {
-            const float* s0 = aslot + (k & 1) * GA::SLOT;
-            const float* s1 = aslot + ((k + 1) & 1) * GA::SLOT;
-            float* dstb = bslot + (k % NBR) * GB::SLOT;
-            const int y = ys - Rb + k * S;  // first G_s row of chunk k
-            switch (wv) {
-#define COLA(w)                                                                                                       \
-    case w:                                                                                                           \
-        pair_colpass_a<GA, w, NXT>(s0, s1, dstb, GB::IWP, taps_a, lane, y, ys, ye, xa, Q::HB, W, pitch, Q::TWO, ra,   \
-                                   rn, pitch_n, wn, hn);                                                              \
-        break;
-                COLA(0) COLA(1) COLA(2) COLA(3)
-#undef COLA
-            }
-        }
-        if (k >= NBW && k - NBW < nout) {
+        // column pass B -> G_{s+1} rows of output chunk k - NBW (its G_s
+        // chunks are row-filtered); with SPLIT it runs before column pass A
+        // overwrites the ring slot of the oldest of those chunks
+        auto colb = [&]() {
+            if (!(k >= NBW && k - NBW < nout)) return;
             const int j = k - NBW;  // output chunk: G_s chunks j .. j + NBW - 1
             const float* s0 = bslot + (j % NBR) * GB::SLOT;
             const float* s1 = bslot + ((j + 1) % NBR) * GB::SLOT;
@@ -811,7 +804,28 @@ __global__ __launch_bounds__(256, (PairGeom<Ra, Rb>::MINB)) void k_blur2_strip(
                 COLB(0) COLB(1) COLB(2) COLB(3)
 #undef COLB
             }
+        };
+        __syncthreads();  // P3
+        if constexpr (Q::SPLIT) {
+            colb();
+            __syncthreads();  // P4: slot k % NBR held chunk k - 3, read by that column pass B
         }
+        if (k <= ng) {
+            const float* s0 = aslot + (k & 1) * GA::SLOT;
+            const float* s1 = aslot + ((k + 1) & 1) * GA::SLOT;
+            float* dstb = bslot + (k % NBR) * GB::SLOT;
+            const int y = ys - Rb + k * S;  // first G_s row of chunk k
+            switch (wv) {
+#define COLA(w)                                                                                                       \
+    case w:                                                                                                           \
+        pair_colpass_a<GA, w, NXT>(s0, s1, dstb, GB::IWP, taps_a, lane, y, ys, ye, xa, Q::HB, W, pitch, Q::TWO, ra,   \
+                                   rn, pitch_n, wn, hn);                                                              \
+        break;
+                COLA(0) COLA(1) COLA(2) COLA(3)
+#undef COLA
+            }
+        }
+        if constexpr (!Q::SPLIT) colb();
     }
 }
 
@@ -1430,10 +1444,12 @@ int launch_blur_pair(int ra, int rb, const BlurLaunch& A, const BlurLaunch& B, h
                     pair_blur_enabled();
     if (!ok) return -1;
     if (ra == 5 && rb == 6) { launch_blur2_rr<5, 6>(A, B, st); return 0; }
-    // (8, 10) -- blurs 3, 4 -- builds and is exact, but its 4-slot G_s ring
-    // (10-row halos need 3-chunk windows at 16-row chunks) leaves 2 workgroups
-    // per CU: measured 2.06 ms against 1.78 ms for the two single launches
-    // (64 frames of 3840x2160, tools/ubench_kernels.hip pair), so it is not used
+    // (8, 10) -- blurs 3, 4 -- builds and is exact (tests pass with
+    // -DSIFT_PAIR_8_10), but is slower than the two single launches: with a
+    // 4-slot G_s ring (10-row halos need 3-chunk windows at 16-row chunks) it
+    // ran at 2 workgroups per CU, 2.06 vs 1.78 ms; with the split-phase 3-slot
+    // ring at 3 workgroups per CU, 1.75 vs 1.62 ms (64 frames of 3840x2160,
+    // tools/ubench_kernels.hip pair; pyramid 14.3 -> 14.5 ms per step)
 #ifdef SIFT_PAIR_8_10
     if (ra == 8 && rb == 10) { launch_blur2_rr<8, 10>(A, B, st); return 0; }
 #endif
