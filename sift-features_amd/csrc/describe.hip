@@ -62,6 +62,18 @@ __device__ __forceinline__ float row_hi(float hi0, float kk, bool row_only, floa
     return row_only ? (row_in(fy, k, c) ? 1e9f : -1e9f) : hi0 + kk * fy;
 }
 
+// Inclusive wave prefix sum with DPP row shifts and row broadcasts (no LDS
+// permutes): within each 16-lane row, then across rows.
+__device__ __forceinline__ int wave_incl_scan(int v) {
+    v += __builtin_amdgcn_update_dpp(0, v, 0x111, 0xf, 0xf, false);  // row_shr:1
+    v += __builtin_amdgcn_update_dpp(0, v, 0x112, 0xf, 0xf, false);  // row_shr:2
+    v += __builtin_amdgcn_update_dpp(0, v, 0x114, 0xf, 0xf, false);  // row_shr:4
+    v += __builtin_amdgcn_update_dpp(0, v, 0x118, 0xf, 0xf, false);  // row_shr:8
+    v += __builtin_amdgcn_update_dpp(0, v, 0x142, 0xa, 0xf, false);  // row_bcast:15 -> rows 1, 3
+    v += __builtin_amdgcn_update_dpp(0, v, 0x143, 0xc, 0xf, false);  // row_bcast:31 -> rows 2, 3
+    return v;
+}
+
 // Per-row column intervals of the rotated 4x4 region (window rows
 // -radius..radius, n <= 79: lanes own rows lane and lane + 64), widened by one
 // column on each side -- the reference's f32 predicate decides membership per
@@ -103,20 +115,23 @@ __device__ __forceinline__ void build_row_table(int* rowlo, int* rowpre, int rad
             cnt[h] = (empty || ihi < ilo) ? 0 : ihi - ilo + 1;
         }
     }
-    int s0 = cnt[0], s1 = cnt[1];
-#pragma unroll
-    for (int o = 1; o < 64; o <<= 1) {
-        const int a = __shfl_up(s0, o), b = __shfl_up(s1, o);
-        if (lane >= o) {
-            s0 += a;
-            s1 += b;
-        }
-    }
-    const int t0 = __shfl(s0, 63);
+    const int s0 = wave_incl_scan(cnt[0]), s1 = wave_incl_scan(cnt[1]);
+    const int t0 = __builtin_amdgcn_readlane(s0, 63);
     if (lane < n) rowpre[lane + 1] = s0;
     if (lane + 64 < n) rowpre[lane + 65] = s1 + t0;
     if (lane == 0) rowpre[0] = 0;
     wave_sync();
+}
+
+// Sequential sum s[0] + s[2] + ... + s[62] over the even lanes (the
+// reference's chunk order) with v_readlane: the 32 reads are independent and
+// the adds take scalar operands, instead of a chain of 31 LDS permutes.
+__device__ __forceinline__ float chunk_sum(float s) {
+    const int si = __float_as_int(s);
+    float t = __int_as_float(__builtin_amdgcn_readlane(si, 0));
+#pragma unroll
+    for (int j = 1; j < 32; j++) t = t + __int_as_float(__builtin_amdgcn_readlane(si, 2 * j));
+    return t;
 }
 
 // Normalisation (src/lib.rs:951-989) of the 128 interior bins held two per
@@ -129,8 +144,7 @@ __device__ __forceinline__ void describe_normalize(float acc0, float acc1, uint8
     s += acc1 * acc1;
     s += c_hi0 * c_hi0;
     s += c_hi1 * c_hi1;
-    float l2 = __shfl(s, 0);
-    for (int j = 1; j < 32; j++) l2 = l2 + __shfl(s, 2 * j);
+    float l2 = chunk_sum(s);
     l2 = sqrtf(l2);
     const float cap = l2 * 0.2f;
     const float v0 = fminf(acc0, cap), v1 = fminf(acc1, cap);
@@ -140,8 +154,7 @@ __device__ __forceinline__ void describe_normalize(float acc0, float acc1, uint8
     s += v1 * v1;
     s += d_hi0 * d_hi0;
     s += d_hi1 * d_hi1;
-    float l2c = __shfl(s, 0);
-    for (int j = 1; j < 32; j++) l2c = l2c + __shfl(s, 2 * j);
+    float l2c = chunk_sum(s);
     l2c = sqrtf(l2c);
     const float norm = 512.0f / fmaxf(l2c, FLT_EPSILON);
     const int32_t q0 = sat_i32(roundf(v0 * norm)), q1v = sat_i32(roundf(v1 * norm));
@@ -554,8 +567,13 @@ __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img
 
 // kMode 0: bit-exact (describe_wave_exact); 1 / 2 / 4: fast path with that
 // slice-sharing factor.
+// 4 waves per SIMD (<= 128 VGPRs, no spills): the 16 waves per CU the LDS
+// footprint allows (141 VGPRs unconstrained = 12 waves; the stage is ~4% faster)
+#ifndef SIFT_DESC_WPE
+#define SIFT_DESC_WPE 4
+#endif
 template <int kMode, int kAblate>
-__global__ __launch_bounds__(64) void k_describe(const DescLaunch L) {
+__global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kMode == 0 ? 1 : SIFT_DESC_WPE))) void k_describe(const DescLaunch L) {
     constexpr bool kExact = kMode == 0;
     using Scratch = typename std::conditional<kExact, DescScratch, DescScratchFast<kExact ? 1 : kMode>>::type;
     __shared__ __attribute__((aligned(16))) Scratch scr;

@@ -111,7 +111,10 @@ __device__ __forceinline__ float dpp_from_right(float v) {  // lane i <- lane i 
     return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
 }
 
-__global__ __launch_bounds__(256) void k_detect_rows(const DetectLaunch L) {
+#ifndef SIFT_DETECT_WPE
+#define SIFT_DETECT_WPE 1
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_DETECT_WPE))) void k_detect_rows(const DetectLaunch L) {
     __shared__ uint64_t lcand[DR_LCAP];
     __shared__ uint32_t lcount, gbase;
     const int W = L.W, H = L.H, pitch = L.pitch;
@@ -313,7 +316,10 @@ __device__ __forceinline__ bool refine_one(const RefineLaunch& L, uint64_t key, 
     return true;
 }
 
-__global__ __launch_bounds__(256) void k_refine(const RefineLaunch L) {
+#ifndef SIFT_REFINE_WPE
+#define SIFT_REFINE_WPE 1
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_REFINE_WPE))) void k_refine(const RefineLaunch L) {
     const uint32_t n = min(*L.n_cand, L.cand_cap);
     const int lane = threadIdx.x & 63;
     for (uint32_t base = blockIdx.x * 256; base < n; base += gridDim.x * 256) {
