@@ -353,7 +353,7 @@ constexpr int OR_LDS = 1104;  // >= 33 * 33 samples, a multiple of 16 (16-byte b
 constexpr int OR_WT = 17 * 18 / 2;  // weight table entries at the largest radius (16)
 
 #ifndef SIFT_ORIENT_MIN_WAVES
-#define SIFT_ORIENT_MIN_WAVES 6  // 6 waves per SIMD (24 per CU, LDS-bound): -10% orientation time despite a few spills
+#define SIFT_ORIENT_MIN_WAVES 6  // 6 waves per SIMD (24 per CU, LDS-bound): -10% orientation time despite a few spills (48 B since the f64 angle pass moved out of the sample loop; 5 waves: no spills, 8% slower)
 #endif
 __global__ __launch_bounds__(256, SIFT_ORIENT_MIN_WAVES) void k_orient(const OrientLaunch L) {
     __shared__ __attribute__((aligned(16))) float sval[4][OR_LDS];
@@ -421,9 +421,18 @@ __global__ __launch_bounds__(256, SIFT_ORIENT_MIN_WAVES) void k_orient(const Ori
                 u = rw[-pitch];
                 d = rw[pitch];
             };
+            auto to_bin = [&](float ori) -> uint8_t {
+                int bi = sat_i32(roundf(bin_step * ori));
+                if (bi >= kOriBins)
+                    bi -= kOriBins;
+                else if (bi < 0)
+                    bi += kOriBins;
+                return (uint8_t)bi;
+            };
             float nl = 0.f, nr = 0.f, nu = 0.f, nd = 0.f;
+            uint32_t defer = 0;  // bit it: the lane's sample lane + 64 * it needs the f64 angle
             if (lane < N && H > 2 && W > 2) fetch(lane, nl, nr, nu, nd);
-            for (int idx = lane; idx < N; idx += 64) {
+            for (int idx = lane, it = 0; idx < N; idx += 64, it++) {
                 const float gl = nl, gr = nr, gu = nu, gd = nd;
                 if (idx + 64 < N && H > 2 && W > 2) fetch(idx + 64, nl, nr, nu, nd);
                 const int iy = idx / n;
@@ -441,21 +450,29 @@ __global__ __launch_bounds__(256, SIFT_ORIENT_MIN_WAVES) void k_orient(const Ori
                     // The sample only needs its bin, round(bin_step * atan2f): a fast
                     // f32 atan2 (|error| <= 2.4e-7 rad -> the product moves by
                     // < 2e-6) decides it unless the product lies within 2e-5 of a
-                    // rounding boundary; those rare lanes (~4e-5 of samples)
-                    // recompute the correctly rounded angle in f64.
-                    float ori = atan2_fast(dy, dx);
+                    // rounding boundary; those rare samples (~4e-5) get the
+                    // correctly rounded f64 angle in a pass after this loop (kept
+                    // out of it: the f64 atan2 alone costs ~50 VGPRs here).
+                    const float ori = atan2_fast(dy, dx);
                     const float tf = bin_step * ori;
-                    if (fabsf(tf - floorf(tf) - 0.5f) < 2e-5f) ori = (float)atan2((double)dy, (double)dx);
-                    int bi = sat_i32(roundf(bin_step * ori));
-                    if (bi >= kOriBins)
-                        bi -= kOriBins;
-                    else if (bi < 0)
-                        bi += kOriBins;
-                    bin = (uint8_t)bi;
+                    if (fabsf(tf - floorf(tf) - 0.5f) < 2e-5f)
+                        defer |= 1u << it;
+                    else
+                        bin = to_bin(ori);
                     val = weight * mag;
                 }
                 sval[wave][idx] = val;
                 sbin[wave][idx] = bin;
+            }
+            while (defer) {  // the lane's deferred samples (its own LDS entries)
+                const int it = __builtin_ctz(defer);
+                defer &= defer - 1;
+                const int idx = lane + 64 * it;
+                float gl, gr, gu, gd;
+                fetch(idx, gl, gr, gu, gd);
+                const float dx = gr - gl;
+                const float dy = gu - gd;
+                sbin[wave][idx] = to_bin((float)atan2((double)dy, (double)dx));
             }
             if (L.samples) {  // measurement only
                 const int x = e.x, y = e.y;
