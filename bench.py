@@ -60,18 +60,21 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-latency", action="store_true")
     p.add_argument("--no-configs", action="store_true", help="skip the other single-GPU BASELINE configs")
+    p.add_argument("--no-jpeg", action="store_true", help="skip the JPEG -> keypoints end-to-end field")
     return p.parse_args()
 
 
-def run_config(pkg, synth, dev, device_index, n, W, H, steps, seed0=1000, max_octaves=0):
+def run_config(pkg, synth, dev, device_index, n, W, H, steps, seed0=1000, max_octaves=0, processing=None):
     """One BASELINE config on one GPU: `n` device-resident W x H frames per
     call, results left in HBM; keypoints/s from two-lane calls, the pyramid
     stage's HIP-event time (and its roofline fraction) from a serialised pass.
-    max_octaves > 0: the labelled octave-cap extension (not the crate)."""
+    max_octaves > 0: the labelled octave-cap extension (not the crate).
+    processing: the Processing profile (default OpenCVProcessing, the one the
+    reference's snapshots pin; ImageprocProcessing is the crate's sift())."""
     import torch
     fr = synth.frames_torch(n, W, H, seed0=seed0, device=dev)
     torch.cuda.synchronize()
-    c = pkg.Context(device_index, pkg.OpenCVProcessing)
+    c = pkg.Context(device_index, processing or pkg.OpenCVProcessing)
     if max_octaves:
         c.set_max_octaves(max_octaves)
     call = (fr.data_ptr(), n, W, H, fr.stride(1), fr.stride(0))
@@ -99,10 +102,66 @@ def run_config(pkg, synth, dev, device_index, n, W, H, steps, seed0=1000, max_oc
     gbs = st["pyramid_bytes"] / (st["pyramid_ms"] * 1e-3) / 1e9 if st["pyramid_ms"] > 0 else 0.0
     n_oct = int(round(np.log2(min(2 * W, 2 * H)) - 2)) + 1
     return {"frames_per_call": n, "frame": f"{W}x{H}",
+            "profile": "imageproc" if processing is pkg.ImageprocProcessing else "opencv",
             "octaves": min(n_oct, max_octaves) if max_octaves else n_oct,
             "ms_per_call": 1e3 * dt, "keypoints_per_s": kp / steps / dt, "frames_per_s": n / dt,
             "keypoints_per_frame": kp / steps / n, "pyramid_ms_per_call": st["pyramid_ms"] / steps,
             "pyramid_gbs": gbs, "pyramid_frac": gbs / HBM_PEAK_GBS}
+
+
+def run_jpeg_e2e(pkg, synth, device_index, n, W, H, steps, threads):
+    """JPEG bytes -> keypoints (examples/run-sift.rs:8
+    decodes with image::open + grayscale): n synthetic W x H RGB JPEGs (4:2:0,
+    quality 90, PIL-encoded from the bench's frames) in host memory; one step
+    = sift_mi_decode_jpeg_batch (host-threaded entropy decoding + GPU
+    reconstruction into device frames) and sift_batch_device over them,
+    pipelined: a second context decodes batch k + 1 while batch k runs."""
+    import io
+    import threading
+    import torch
+    from PIL import Image
+    base = synth.frames(8, W, H, seed0=0)
+    datas = []
+    for i in range(n):
+        f = np.roll(base[i % 8], 17 * i, 1)
+        rgb = np.stack([f, np.roll(f, 5, 1), 255 - f], -1)
+        b = io.BytesIO()
+        Image.fromarray(rgb).save(b, "JPEG", quality=90, subsampling=2)
+        datas.append(b.getvalue())
+    ctx = pkg.Context(device_index, pkg.OpenCVProcessing)
+    dctx = pkg.Context(device_index, pkg.OpenCVProcessing)
+    bufs = [torch.empty((n, H, W), dtype=torch.uint8, device="cuda") for _ in range(2)]
+    fp, rs = bufs[0].stride(0), bufs[0].stride(1)
+
+    def dec_into(buf):
+        dctx.decode_jpeg_batch_device(datas, buf.data_ptr(), fp, rs, threads)
+
+    def run(k):
+        th = threading.Thread(target=dec_into, args=(bufs[(k + 1) % 2],))
+        th.start()
+        offs, _ = ctx.sift_batch_device(bufs[k % 2].data_ptr(), n, W, H, rs, fp, fetch=False)
+        th.join()
+        return int(offs[-1])
+
+    dec_into(bufs[0])
+    run(0)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    nkp = sum(run(k + 1) for k in range(steps))
+    torch.cuda.synchronize()
+    dt = (time.perf_counter() - t0) / steps
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        dec_into(bufs[0])
+    torch.cuda.synchronize()
+    dec = (time.perf_counter() - t0) / steps
+    dctx.close()
+    ctx.close()
+    return {"frames_per_step": n, "frame": f"{W}x{H}", "jpeg_mean_bytes": float(np.mean([len(d) for d in datas])),
+            "host_threads": threads, "frames_per_s": n / dt, "keypoints_per_s": nkp / steps / dt,
+            "decode_only_frames_per_s": n / dec,
+            "note": "pipelined: decode of batch k+1 (second context, host threads) beside sift() of batch k; "
+                    "JPEGs in host memory, results kept on the device"}
 
 
 def main():
@@ -299,8 +358,15 @@ def main():
                                                 max_octaves=5),
             "ext_giant_8192_7oct": run_config(pkg, synth, dev, local, 1, 8192, 8192, max(3, args.steps),
                                               max_octaves=7),
+            # the crate's own default sift() profile (ImageprocProcessing,
+            # src/lib.rs:71-73, 993-1007) on the headline batch
+            "imageproc_batch_1080p": run_config(pkg, synth, dev, local, B, W, H, max(3, args.steps),
+                                                processing=pkg.ImageprocProcessing),
         }
         configs["single_1080p"]["latency_host_fetch_ms"] = latency_ms
+        if not args.no_jpeg:
+            configs["jpeg_e2e"] = run_jpeg_e2e(pkg, synth, local, B, W, H, max(3, args.steps),
+                                               min(16, int(os.environ.get("OMP_NUM_THREADS", "16") or 16)))
 
     # HBM traffic of the same launch group from the committed PMC passes
     # (tools/round_profile.sh -> profiles/pmc_traffic.json), scaled to one

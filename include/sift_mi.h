@@ -109,10 +109,13 @@ int sift_mi_set_exact_descriptors(sift_mi_ctx* ctx, int exact);
 
 /* LABELLED EXTENSION (not in the crate): cap the octave count at max_octaves
  * (0 = the crate's formula round(log2(min(2W, 2H)) - 2) + 1, src/lib.rs:133-134,
- * the default).  The kept octaves are computed exactly as without the cap, so
- * the result is the uncapped result's keypoints of octaves < max_octaves (a
- * prefix of the emission order).  For the "5 octaves" / "7 octaves" wording of
- * BASELINE.json's configs; parity runs leave it at 0. */
+ * the default).  The kept octaves are computed exactly as without the cap.
+ * With features_limit None the result is the uncapped result's keypoints of
+ * octaves < max_octaves (a prefix of the emission order).  With a limit, the
+ * cap applies first: the limit ranks the capped keypoint set (src/lib.rs:156-161
+ * on the prefix), which is not in general a subset of the uncapped limited
+ * result.  For the "5 octaves" / "7 octaves" wording of BASELINE.json's
+ * configs; parity runs leave it at 0. */
 int sift_mi_set_max_octaves(sift_mi_ctx* ctx, int max_octaves);
 
 /* Batch pipeline lanes: 2 (default) runs consecutive chunks on two streams
@@ -237,7 +240,11 @@ int sift_mi_reset_stats(sift_mi_ctx* ctx);
  * default, and off in every timed run).  Read with sift_mi_get_stats. */
 int sift_mi_set_sample_counting(sift_mi_ctx* ctx, int on);
 
-/* Library version string and last error (thread-local). */
+/* Library version string and last error (thread-local).
+ * 0.3.0: no ABI change from 0.2.
+ * 0.2.0: emission keys (sift_mi_fetch_keys) widened x / y to 15 bits -- image
+ *        field moved from bit 40 to bit 42; sift_mi_stats gained band_reruns,
+ *        stage_reruns, orient_samples, desc_samples (a larger struct). */
 const char* sift_mi_version(void);
 const char* sift_mi_last_error(void);
 

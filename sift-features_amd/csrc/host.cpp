@@ -443,6 +443,9 @@ struct sift_mi_ctx {
     hipStream_t stream = nullptr;  // compute stream (own or the caller's)
     hipStream_t cstream = nullptr; // device->host result copies
     hipStream_t own2 = nullptr;    // compute stream of pipeline lane 1 (lane 0 runs on `stream`)
+    hipStream_t aux[2] = {};       // per lane: blurs 4, 5 of each octave beside the next octave
+    hipEvent_t oct_ev[2][kTailMaxOct + 1] = {};  // per lane: octave o's G_3 done / aux joined
+    int oct_overlap = 1;           // SIFT_MI_OCT_OVERLAP=0: one stream per lane (A/B, tests)
     hipEvent_t fork = nullptr;     // orders lane 1 after / before the caller's stream
     int lanes = 2;                 // pipeline lanes (sift_mi_set_pipeline_lanes)
     uint32_t chunk_override = 0;
@@ -486,6 +489,7 @@ int arena_of(const sift_mi_ctx* c, int si) { return c->lanes == 2 ? si : 0; }
 int sync_lanes(sift_mi_ctx* c) {
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipStreamSynchronize(c->own2));
+    for (auto& a : c->aux) HIPCHK(hipStreamSynchronize(a));
     return 0;
 }
 
@@ -722,22 +726,6 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
     }
     if (launch_seed(p.seed_r, S, st)) return fail(SIFT_MI_EUNSUPPORTED, "seed blur radius");
     uint64_t launches = 1;
-    uint64_t bytes = p.algo_bytes_per_frame;  // per frame, SURVEY.md 8(d)
-    if (c->band_restricted) {
-        // the same yardstick over the rows this band computes: 4 B per pixel
-        // of each of its 6 Gaussian rows and 5 DoG rows, plus the input rows
-        // the seed reads
-        double b = (double)p.w * std::min<int>((int)p.h, (S.y1 - S.y0 + 1) / 2 + 2);
-        for (int o = 0; o < p.n_oct; o++) {
-            double rows = 0;
-            for (int s = 0; s < kImagesPerOctave; s++) {
-                const int r = std::max(0, rhi[(size_t)o * kImagesPerOctave + s] - rlo[(size_t)o * kImagesPerOctave + s]);
-                rows += (s < kDogPerOctave ? 2.0 : 1.0) * r;
-            }
-            b += 4.0 * p.ow[o] * rows;
-        }
-        bytes = (uint64_t)b;
-    }
     // the small octaves from o_tail on: one k_octave_tail launch
     // (SIFT_MI_TAIL=0: per-blur launches for every octave; A/B and test knob)
     int o_tail = p.n_oct;
@@ -747,6 +735,25 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
             o_tail = tail_octave_start(p.ow.data(), p.oh.data(), p.n_oct,
                                        *std::max_element(p.oct_r + 1, p.oct_r + kImagesPerOctave));
     }
+    uint64_t bytes = p.algo_bytes_per_frame;  // per frame, SURVEY.md 8(d)
+    if (c->band_restricted) {
+        // the same yardstick over the rows this band computes: 4 B per pixel
+        // of each of its 6 Gaussian rows and 5 DoG rows, plus the input rows
+        // the seed reads; the tail launch computes its octaves whole
+        double b = (double)p.w * std::min<int>((int)p.h, (S.y1 - S.y0 + 1) / 2 + 2);
+        for (int o = 0; o < p.n_oct; o++) {
+            double rows = 0;
+            for (int s = 0; s < kImagesPerOctave; s++) {
+                const int r = o >= o_tail ? p.oh[o]
+                                          : std::max(0, rhi[(size_t)o * kImagesPerOctave + s] -
+                                                            rlo[(size_t)o * kImagesPerOctave + s]);
+                rows += (s < kDogPerOctave ? 2.0 : 1.0) * r;
+            }
+            b += 4.0 * p.ow[o] * rows;
+        }
+        bytes = (uint64_t)b;
+    }
+    const bool overlap = c->oct_overlap && p.n_oct <= kTailMaxOct;
     for (int o = 0; o < o_tail; o++) {
         float* G = p.gauss(o, lane);
         float* D = p.dog(o, lane);
@@ -776,21 +783,32 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
             }
             return B;
         };
+        // octave o + 1 needs only G_3 of octave o (its G_0 is written by blur
+        // 3), so blurs 4, 5 (and the DoG planes of precompute_images) run on
+        // the aux stream beside the next octave's blurs: every launch's tail
+        // and the small octaves' short launches share the chip with the
+        // other stream's work instead of leaving it idle
+        hipStream_t s45 = st;
         for (int s = 1; s < kImagesPerOctave; s++) {
+            if (s == 4 && overlap) {
+                HIPCHK(hipEventRecord(c->oct_ev[lane][o], st));
+                HIPCHK(hipStreamWaitEvent(c->aux[lane], c->oct_ev[lane][o], 0));
+                s45 = c->aux[lane];
+            }
             const BlurLaunch B = blur_launch(s);
-            // G_1, G_2 and G_3, G_4 in one pass each where the pair kernel
-            // applies (k_blur2_strip: G_1 / G_3 never read back from HBM)
-            if ((s == 1 || s == 3) && launch_blur_pair(p.oct_r[s], p.oct_r[s + 1], B, blur_launch(s + 1), st) == 0) {
+            // G_1, G_2 in one pass where the pair kernel applies (k_blur2_strip:
+            // G_1 never read back from HBM)
+            if (s == 1 && launch_blur_pair(p.oct_r[s], p.oct_r[s + 1], B, blur_launch(s + 1), st) == 0) {
                 launches++;
                 s++;
                 continue;
             }
-            if (launch_blur(p.oct_r[s], B, st)) return fail(SIFT_MI_EUNSUPPORTED, "octave blur radius");
+            if (launch_blur(p.oct_r[s], B, s >= 4 ? s45 : st)) return fail(SIFT_MI_EUNSUPPORTED, "octave blur radius");
             launches++;
         }
         // precompute_images: D_s = G_{s+1} - G_s, the same f32 subtraction
         // the keypoint stages form where they read the DoG
-        if (full) launch_dog(G, P, p.gstride(o), D, p.dstride(o), p.ow[o], p.oh[o], p.opitch[o], (int)n, st);
+        if (full) launch_dog(G, P, p.gstride(o), D, p.dstride(o), p.ow[o], p.oh[o], p.opitch[o], (int)n, s45);
     }
     if (o_tail < p.n_oct) {
         // whole octaves (a row band's restricted rows are a subset: rows outside
@@ -817,6 +835,10 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
             for (int o = o_tail; o < p.n_oct; o++)
                 launch_dog(p.gauss(o, lane), p.P[o], p.gstride(o), p.dog(o, lane), p.dstride(o), p.ow[o], p.oh[o],
                            p.opitch[o], (int)n, st);
+    }
+    if (overlap && o_tail > 0) {  // join: the aux stream's blurs before the keypoint stages
+        HIPCHK(hipEventRecord(c->oct_ev[lane][kTailMaxOct], c->aux[lane]));
+        HIPCHK(hipStreamWaitEvent(st, c->oct_ev[lane][kTailMaxOct], 0));
     }
     HIPCHK(hipGetLastError());
     c->stats.pyramid_launches += launches;
@@ -1178,6 +1200,11 @@ int extract_device(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, 
     CHK(check_frame_args(w, h, stride));
     if (n > (1u << (64 - kKeyImgShift))) return fail(SIFT_MI_EINVAL, "more than 2^22 frames in one call (key field)");
     const sift_mi_stats stats0 = c->stats;  // restored if a banded pass is redone on the whole pyramid
+    unsigned long long samples0[16] = {};   // and the device sample counters with it
+    if (c->band_n > 1 && c->count_samples && c->samples.p) {
+        CHK(sync_lanes(c));
+        HIPCHK(hipMemcpy(samples0, c->samples.p, sizeof samples0, hipMemcpyDeviceToHost));
+    }
     if (c->band_n > 1 && limit >= 0)
         return fail(SIFT_MI_EINVAL, "features_limit ranks a whole frame's keypoints: apply it after merging row bands");
     const uint32_t chunk =
@@ -1238,6 +1265,8 @@ int extract_device(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, 
             c->stats = stats0;
             c->stats.band_reruns = reruns;
             c->stats.stage_reruns = stage_reruns;
+            if (c->count_samples && c->samples.p)
+                HIPCHK(hipMemcpy(c->samples.p, samples0, sizeof samples0, hipMemcpyHostToDevice));
             c->band_whole = true;
             const int rc = extract_device(c, d_frames, frame_pitch, n, w, h, stride, limit, offsets);
             c->band_whole = false;
@@ -1296,7 +1325,7 @@ int upload_frames(sift_mi_ctx* c, const uint8_t* const* frames, uint32_t n, uint
 // ===========================================================================
 extern "C" {
 
-const char* sift_mi_version(void) { return "sift_mi 0.1.0 (gfx950)"; }
+const char* sift_mi_version(void) { return "sift_mi 0.3.0 (gfx950)"; }
 const char* sift_mi_last_error(void) { return g_err.c_str(); }
 
 int sift_mi_create(int device_ordinal, sift_mi_profile profile, sift_mi_ctx** out) {
@@ -1323,6 +1352,10 @@ int sift_mi_create(int device_ordinal, sift_mi_profile profile, sift_mi_ctx** ou
     bool ok = hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking) == hipSuccess &&
               hipStreamCreateWithFlags(&c->own2, hipStreamNonBlocking) == hipSuccess;
     ok = ok && hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) == hipSuccess;
+    for (auto& a : c->aux) ok = ok && hipStreamCreateWithFlags(&a, hipStreamNonBlocking) == hipSuccess;
+    for (auto& lane : c->oct_ev)
+        for (auto& e : lane) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+    if (const char* e = getenv("SIFT_MI_OCT_OVERLAP")) c->oct_overlap = strcmp(e, "0") != 0;
     for (auto& S : c->slot) {
         for (auto& e : S.ev) ok = ok && hipEventCreate(&e) == hipSuccess;
         ok = ok && hipEventCreateWithFlags(&S.copied, hipEventDisableTiming) == hipSuccess;
@@ -1357,6 +1390,13 @@ void sift_mi_destroy(sift_mi_ctx* c) {
         if (S.copied) (void)hipEventDestroy(S.copied);
     }
     if (c->fork) (void)hipEventDestroy(c->fork);
+    for (auto& a : c->aux)
+        if (a) (void)hipStreamSynchronize(a);
+    for (auto& lane : c->oct_ev)
+        for (auto& e : lane)
+            if (e) (void)hipEventDestroy(e);
+    for (auto& a : c->aux)
+        if (a) (void)hipStreamDestroy(a);
     c->r_kp.release();
     c->r_desc.release();
     c->r_key.release();

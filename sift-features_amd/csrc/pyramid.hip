@@ -452,15 +452,14 @@ __device__ __forceinline__ void strip_rowpass(float* slot, const BlurTaps& taps,
 template <class G, int P, int WV, bool NXT>
 __device__ __forceinline__ void strip_colpass(const float* sa, const float* sb, const BlurTaps& taps, int lane,
                                               int y, int ye, int x0, int W, int pitch, __amdgpu_buffer_rsrc_t rd,
-                                              __amdgpu_buffer_rsrc_t rn, int pitch_n, int wn, int hn,
-                                              const float* sc = nullptr) {
+                                              __amdgpu_buffer_rsrc_t rn, int pitch_n, int wn, int hn) {
     constexpr int R = G::R;
     constexpr int NR = G::VB + 2 * R;
     f2v v[NR];
 #pragma unroll
     for (int j = 0; j < NR; j++) {
-        const int L = WV * G::VB + j;  // window row: slot a, b or (S < 2R) c
-        const float* rp = L < G::S ? sa + L * G::IWP : (L < 2 * G::S ? sb + (L - G::S) * G::IWP : sc + (L - 2 * G::S) * G::IWP);
+        const int L = WV * G::VB + j;  // window row: slot a or b
+        const float* rp = L < G::S ? sa + L * G::IWP : sb + (L - G::S) * G::IWP;
         v[j] = *(const lds_f2v*)(rp + 2 * lane);
     }
     f2v out[G::VB];
@@ -622,15 +621,13 @@ struct PairGeom {
     static constexpr int HB = GB::HWL;             // G_s halo columns of B's window
     static constexpr int TWO = GA::TW - 2 * HB;   // output columns per strip
     static constexpr int NBW = GB::NCW;           // G_s chunks in a column-pass window of B
-    // B ring: the window + the chunk being written (two-chunk windows: the
-    // two column passes share a phase); three-chunk windows use a ring of 3
-    // with the column passes in separate phases (one more barrier per step,
-    // but 3 workgroups per CU instead of 2)
-    static constexpr bool SPLIT = NBW == 3;
-    static constexpr int NBR = SPLIT ? 3 : NBW + 1;
+    // B ring: the two-chunk window + the chunk being written (the two column
+    // passes share a phase)
+    static constexpr int NBR = NBW + 1;
     static constexpr int LDS_FLOATS = 2 * GA::SLOT + NBR * GB::SLOT;
     static constexpr int MINB = 163840 / (4 * LDS_FLOATS) < 4 ? 163840 / (4 * LDS_FLOATS) : 4;
     static_assert(GA::HWL == 8 && GA::NCW == 2, "A: radius <= 8");
+    static_assert(NBW == 2, "B: radius <= 8 (two-chunk column windows)");
     static_assert(GB::IWV >= GA::TW, "B's window holds A's 128 columns");
 };
 
@@ -783,14 +780,12 @@ __global__ __launch_bounds__(256, (PairGeom<Ra, Rb>::MINB)) void k_blur2_strip(
             strip_rowpass<GB, kProfileOpenCV>(s1, taps_b, prow, pq);
         }
         // column pass B -> G_{s+1} rows of output chunk k - NBW (its G_s
-        // chunks are row-filtered); with SPLIT it runs before column pass A
-        // overwrites the ring slot of the oldest of those chunks
+        // chunks are row-filtered)
         auto colb = [&]() {
             if (!(k >= NBW && k - NBW < nout)) return;
             const int j = k - NBW;  // output chunk: G_s chunks j .. j + NBW - 1
             const float* s0 = bslot + (j % NBR) * GB::SLOT;
             const float* s1 = bslot + ((j + 1) % NBR) * GB::SLOT;
-            const float* s2 = bslot + ((j + 2) % NBR) * GB::SLOT;
             const int y = ys + j * S;
             // after B's in-place row pass slot column c is output column X + c: lanes 0 .. TWO/2 - 1 are
             // this strip's columns (the rest read the junk past A's 128 columns)
@@ -799,17 +794,13 @@ __global__ __launch_bounds__(256, (PairGeom<Ra, Rb>::MINB)) void k_blur2_strip(
     case w:                                                                                                      \
         if (lane < Q::TWO / 2)                                                                                   \
             strip_colpass<GB, kProfileOpenCV, w, false>(s0, s1, taps_b, lane, y, ye, X, W, pitch, rb, rb, 0, 0,  \
-                                                        0, s2);                                                  \
+                                                        0);                                                      \
         break;
                 COLB(0) COLB(1) COLB(2) COLB(3)
 #undef COLB
             }
         };
         __syncthreads();  // P3
-        if constexpr (Q::SPLIT) {
-            colb();
-            __syncthreads();  // P4: slot k % NBR held chunk k - 3, read by that column pass B
-        }
         if (k <= ng) {
             const float* s0 = aslot + (k & 1) * GA::SLOT;
             const float* s1 = aslot + ((k + 1) & 1) * GA::SLOT;
@@ -825,7 +816,7 @@ __global__ __launch_bounds__(256, (PairGeom<Ra, Rb>::MINB)) void k_blur2_strip(
 #undef COLA
             }
         }
-        if constexpr (!Q::SPLIT) colb();
+        colb();
     }
 }
 
@@ -1027,7 +1018,7 @@ struct SeedStrip {
 };
 
 template <int R>
-__global__ __launch_bounds__(256, 4) void k_seed_strip(const uint8_t* __restrict__ frames, size_t frame_pitch,
+__global__ __launch_bounds__(256, 4) void k_seed_strip_old(const uint8_t* __restrict__ frames, size_t frame_pitch,
                                                        size_t row_stride, int sh, int sw, const ResizeTab tab,
                                                        float* __restrict__ dst, size_t dst_img_stride, int W, int H,
                                                        int pitch, const BlurTaps taps, int ya, int yb, int seg) {
@@ -1206,6 +1197,232 @@ __global__ __launch_bounds__(256, 4) void k_seed_strip(const uint8_t* __restrict
         __syncthreads();
         vres(sb);
         strip_rowpass<G, kProfileOpenCV>(sb, taps, prow, pq);
+        __syncthreads();
+        const int y = ys + k * G::S;
+        switch (wv) {
+#define COLPASS(w)                                                                                              \
+    case w:                                                                                                     \
+        strip_colpass<G, kProfileOpenCV, w, false>(sa, sb, taps, lane, y, ye, x0, W, pitch, rd, rd, 0, 0, 0); \
+        break;
+            COLPASS(0) COLPASS(1) COLPASS(2) COLPASS(3)
+#undef COLPASS
+        }
+    }
+}
+
+// ---------------------------------------------------------------------------
+// k_seed_strip: the seed as a strip blur (StripGeom<5>: 128 columns, 32-row
+// chunks, the same row / column passes and barriers as k_blur_strip) whose
+// chunk loader computes the 2x bilinear upsample in registers instead of
+// loading a plane.
+//
+// For an exact 2x upsample (W = 2 sw, H = 2 sh) cv_linear_coeffs has a closed
+// form (src/lib.rs:201-205): destination index d = 0 takes
+// source 0 with coefficients (1, 0); d = n - 1 the last source alone (rows:
+// (1, 0) on a clamped second row); every other d takes sources (d - 1) >> 1
+// and the next one with (0.75, 0.25) for odd d, (0.25, 0.75) for even d.  So
+// no table is read.  A loader item is one window row x 4 window columns: the
+// 4 columns read at most 4 consecutive source bytes of each of the row's two
+// source rows (reflect-101 keeps the span), fetched as the one or two
+// 4-byte-aligned dwords that contain them (no dword without a needed byte is
+// read, so no access leaves the frame, whatever its stride or alignment),
+// then v / 255, HResizeLinear (two rounded products + add) per source row and
+// VResizeLinear (S0 b0 + S1 b1).  The items of chunk k + 2 are fetched while
+// chunk k + 1 is row-filtered, as k_blur_strip prefetches its rows.
+// Wave w owns chunk rows 8w .. 8w + 7 (8 x 36 items): item i = lane + 64 j is
+// row 8w + i / 36, column group i % 36, so a wave's load touches one or two
+// source rows at consecutive 2-byte steps (coalesced) and its ds_write_b128
+// groups write 128 contiguous bytes (conflict-free).
+// ---------------------------------------------------------------------------
+// 2x bilinear source index and coefficients of destination d (0 <= d < n,
+// n = 2 * ns): see above; `two` false: the single last source
+__device__ __forceinline__ void seed_axis(int d, int n, int ns, int& s, float& a0, float& a1, bool& two) {
+    two = true;
+    if (d == 0) {
+        s = 0;
+        a0 = 1.0f;
+        a1 = 0.0f;
+    } else if (d == n - 1) {
+        s = ns - 1;
+        a0 = 1.0f;
+        a1 = 0.0f;
+        two = false;
+    } else {
+        s = (d - 1) >> 1;
+        a0 = (d & 1) ? 0.75f : 0.25f;
+        a1 = (d & 1) ? 0.25f : 0.75f;
+    }
+}
+
+// ABL: timing ablations for tools/ubench_kernels.hip only (the product
+// launches ABL = 0): 1 drops the plane stores (zero-size buffer), 2 the
+// loader's loads and upsample, 4 the row pass
+template <int R, int ABL = 0>
+__global__ __launch_bounds__(256, StripGeom<R>::MINB) void k_seed_strip(const uint8_t* __restrict__ frames,
+                                                                        size_t frame_pitch, size_t row_stride, int sh,
+                                                                        int sw, float* __restrict__ dst,
+                                                                        size_t dst_img_stride, int W, int H, int pitch,
+                                                                        const BlurTaps taps, int ya, int yb, int seg) {
+    using G = StripGeom<R>;
+    constexpr int NQ = G::C4;                       // 4-column groups of the window (36)
+    constexpr int NI = NQ * G::VB;                  // items per wave (8 rows)
+    constexpr int NJ = (NI + 63) / 64;              // items per lane
+    static_assert(G::S == 32 && G::NW == 4, "wave w loads chunk rows 8w .. 8w + 7");
+    __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const TileId tile = xcd_tile();
+    const int x0 = tile.x * G::TW;
+    const int ys = ya + tile.y * seg, ye = min(yb, ys + seg);
+    if (ys >= ye) return;
+    const __amdgpu_buffer_rsrc_t rd =
+        uniform_rsrc(dst + (size_t)tile.z * dst_img_stride, (ABL & 1) ? 0u : (uint32_t)H * (uint32_t)pitch * 4u);
+    // the frame as a buffer from its 4-byte-aligned base (boff bytes before
+    // it), sized to whole dwords: a dword holding a frame byte never faults
+    const uint8_t* src = frames + (size_t)tile.z * frame_pitch;
+    const uint32_t boff = (uint32_t)(uintptr_t)src & 3u;
+    const uint32_t nbytes = (boff + (uint32_t)(sh - 1) * (uint32_t)row_stride + (uint32_t)sw + 3u) & ~3u;
+    const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(src - boff, nbytes);
+    // border items (a window column outside [1, W - 2]): per column group
+    // the first source byte, the bytes needed, and per column its source
+    // offset from there, single / two taps and coefficients
+    __shared__ int t_smin[NQ], t_need[NQ], t_info[NQ];
+    __shared__ __attribute__((aligned(16))) float t_a0[NQ * 4], t_a1[NQ * 4];
+    auto interior = [&](int q) {
+        const int c0 = x0 - G::HWL + 4 * q;
+        return c0 >= 1 && c0 + 3 <= W - 2;
+    };
+    if (tid < NQ && !interior(tid)) {
+        const int c0 = x0 - G::HWL + 4 * tid;
+        int sx[4], info = 0, lo = 1 << 30, hi = -1;
+#pragma unroll
+        for (int k = 0; k < 4; k++) {
+            bool two;
+            seed_axis(strip_index<kProfileOpenCV>(c0 + k, W), W, sw, sx[k], t_a0[4 * tid + k], t_a1[4 * tid + k], two);
+            lo = min(lo, sx[k]);
+            hi = max(hi, two ? sx[k] + 1 : sx[k]);
+            info |= (two ? 1 : 0) << (8 * k + 4);
+        }
+#pragma unroll
+        for (int k = 0; k < 4; k++) info |= (sx[k] - lo) << (8 * k);  // 0 .. 3
+        t_smin[tid] = lo;
+        t_need[tid] = hi - lo + 1;
+        t_info[tid] = info;
+    }
+    __syncthreads();
+    // prefetched chunk, per item the dwords holding the 4 source bytes of
+    // each of its two source rows (raw: the byte alignment waits until the
+    // chunk is stored, so the loads stay in flight across a row and a column
+    // pass)
+    uint32_t plo[NJ][2], phi[NJ][2];
+    uint32_t psh = 0;  // byte offsets: 2 bits per (item, source row)
+    auto item = [&](int j, int& r, int& q) {
+        const int i = lane + 64 * j;
+        r = wv * G::VB + i / NQ;
+        q = i - (i / NQ) * NQ;
+    };
+    auto src_rows = [&](int g, int& sy0, int& sy1, float& b0, float& b1) {
+        bool two;
+        seed_axis(strip_index<kProfileOpenCV>(g, H), H, sh, sy0, b0, b1, two);
+        sy1 = min(sy0 + 1, sh - 1);
+    };
+    auto prefetch = [&](int g0) {
+        psh = 0;
+        if constexpr ((ABL & 2) != 0) return;
+#pragma unroll
+        for (int j = 0; j < NJ; j++) {
+            if (NI % 64 == 0 || lane + 64 * j < NI) {
+                int r, q, sy0, sy1;
+                float b0, b1;
+                item(j, r, q);
+                src_rows(g0 + r, sy0, sy1, b0, b1);
+                const bool in = interior(q);
+                const int smin = in ? (x0 - G::HWL + 4 * q) / 2 - 1 : t_smin[q];
+                const int need = in ? 4 : t_need[q];
+#pragma unroll
+                for (int k = 0; k < 2; k++) {
+                    const uint32_t off = boff + (uint32_t)(k ? sy1 : sy0) * (uint32_t)row_stride + (uint32_t)smin;
+                    const uint32_t sa = off & 3u;
+                    plo[j][k] = __builtin_amdgcn_raw_buffer_load_b32(rs, off & ~3u, 0, 0);
+                    phi[j][k] = (int)sa + need > 4 ? __builtin_amdgcn_raw_buffer_load_b32(rs, (off & ~3u) + 4u, 0, 0)
+                                                   : 0u;
+                    psh |= sa << (4 * j + 2 * k);
+                }
+            }
+        }
+    };
+    // the prefetched chunk (window rows from g0) -> upsampled rows in the slot
+    auto store = [&](float* slot, int g0) {
+#pragma unroll
+        for (int j = 0; j < NJ; j++) {
+            if (!(NI % 64 == 0 || lane + 64 * j < NI)) continue;
+            int r, q, sy0, sy1;
+            float b0, b1;
+            item(j, r, q);
+            if constexpr ((ABL & 2) != 0) {
+                *reinterpret_cast<float4*>(slot + r * G::IWP + 4 * q) = make_float4(0.5f, 0.25f, (float)g0, 1.0f);
+                continue;
+            }
+            src_rows(g0 + r, sy0, sy1, b0, b1);
+            const bool in = interior(q);
+            float h[2][4];
+#pragma unroll
+            for (int k = 0; k < 2; k++) {
+                const uint32_t w = __builtin_amdgcn_alignbyte(phi[j][k], plo[j][k], (psh >> (4 * j + 2 * k)) & 3u);
+                const float p0 = u8_unit(w & 0xff), p1 = u8_unit((w >> 8) & 0xff), p2 = u8_unit((w >> 16) & 0xff),
+                            p3 = u8_unit(w >> 24);
+                if (in) {
+                    // HResizeLinear: t = S[sx]*a0 + S[sx+1]*a1 (two roundings + add)
+                    h[k][0] = p0 * 0.25f + p1 * 0.75f;
+                    h[k][1] = p1 * 0.75f + p2 * 0.25f;
+                    h[k][2] = p1 * 0.25f + p2 * 0.75f;
+                    h[k][3] = p2 * 0.75f + p3 * 0.25f;
+                } else {
+                    const int info = t_info[q];
+#pragma unroll
+                    for (int c = 0; c < 4; c++) {
+                        const int d = (info >> (8 * c)) & 15;
+                        const float v0 = d == 0 ? p0 : (d == 1 ? p1 : (d == 2 ? p2 : p3));
+                        const float v1 = d == 0 ? p1 : (d == 1 ? p2 : p3);
+                        h[k][c] = (info >> (8 * c + 4)) & 1 ? v0 * t_a0[4 * q + c] + v1 * t_a1[4 * q + c] : v0;
+                    }
+                }
+            }
+            // VResizeLinear: S0*b0 + S1*b1
+            *reinterpret_cast<float4*>(slot + r * G::IWP + 4 * q) =
+                make_float4(h[0][0] * b0 + h[1][0] * b1, h[0][1] * b0 + h[1][1] * b1, h[0][2] * b0 + h[1][2] * b1,
+                            h[0][3] * b0 + h[1][3] * b1);
+        }
+    };
+    int prow, pq;  // row-pass lane map (see strip_rowpass)
+    {
+        const int l = lane & 31;
+        int g, k;
+        if (l < 4) { g = 0; k = l; }
+        else if (l < 12) { g = 1; k = l - 4; }
+        else if (l < 16) { g = 0; k = l - 8; }
+        else if (l < 20) { g = 1; k = l - 8; }
+        else if (l < 28) { g = 0; k = l - 12; }
+        else { g = 1; k = l - 16; }
+        const int grp = (lane >> 5) * 2 + g;
+        prow = wv * 4 + (grp >> 1) * 2 + (k >> 3);
+        pq = (grp & 1) * 8 + (k & 7);
+    }
+    const int nsteps = (ye - ys + G::S - 1) / G::S;
+    const int gb = ys - R;  // window row of chunk 0
+    prefetch(gb);
+    store(lds, gb);
+    prefetch(gb + G::S);
+    __syncthreads();
+    if constexpr ((ABL & 4) == 0) strip_rowpass<G, kProfileOpenCV>(lds, taps, prow, pq);
+    for (int k = 0; k < nsteps; k++) {
+        float* sa = lds + (k & 1) * G::SLOT;
+        float* sb = lds + ((k + 1) & 1) * G::SLOT;
+        __syncthreads();  // column pass k - 1 is done with slot b
+        store(sb, gb + (k + 1) * G::S);
+        if (k + 2 <= nsteps) prefetch(gb + (k + 2) * G::S);
+        __syncthreads();
+        if constexpr ((ABL & 4) == 0) strip_rowpass<G, kProfileOpenCV>(sb, taps, prow, pq);
         __syncthreads();
         const int y = ys + k * G::S;
         switch (wv) {
@@ -1443,16 +1660,11 @@ int launch_blur_pair(int ra, int rb, const BlurLaunch& A, const BlurLaunch& B, h
                     A.H >= 64 && (uint64_t)A.H * (uint64_t)A.pitch * 4 < (1ull << 31) && strip_blur_enabled() &&
                     pair_blur_enabled();
     if (!ok) return -1;
+    // only (5, 6) -- blurs 1, 2.  A (8, 10) pair for blurs 3, 4 (three-chunk
+    // column windows at 16-row chunks) was built, exact and slower than the
+    // two single launches (1.75 vs 1.62 ms per 64 frames of 3840x2160, round
+    // 2), and was removed.
     if (ra == 5 && rb == 6) { launch_blur2_rr<5, 6>(A, B, st); return 0; }
-    // (8, 10) -- blurs 3, 4 -- builds and is exact (tests pass with
-    // -DSIFT_PAIR_8_10), but is slower than the two single launches: with a
-    // 4-slot G_s ring (10-row halos need 3-chunk windows at 16-row chunks) it
-    // ran at 2 workgroups per CU, 2.06 vs 1.78 ms; with the split-phase 3-slot
-    // ring at 3 workgroups per CU, 1.75 vs 1.62 ms (64 frames of 3840x2160,
-    // tools/ubench_kernels.hip pair; pyramid 14.3 -> 14.5 ms per step)
-#ifdef SIFT_PAIR_8_10
-    if (ra == 8 && rb == 10) { launch_blur2_rr<8, 10>(A, B, st); return 0; }
-#endif
     return -1;
 }
 
@@ -1529,7 +1741,7 @@ int launch_seed(int R, const SeedLaunch& L, hipStream_t st) {
     // reflection of every window (else the tile kernel)
     if (L.W == 2 * L.sw && L.H == 2 * L.sh && L.W >= 160 && L.H >= 64 &&
         (uint64_t)L.H * (uint64_t)L.pitch * 4 < (1ull << 31) && strip_blur_enabled()) {
-        using G = StripGeom<5, 16>;
+        using G = StripGeom<5>;
         const int ya = L.y1 > L.y0 ? std::max(L.y0, 0) : 0;
         const int yb = L.y1 > L.y0 ? std::min(L.y1, L.H) : L.H;
         if (yb <= ya) return 0;
@@ -1537,9 +1749,14 @@ int launch_seed(int R, const SeedLaunch& L, hipStream_t st) {
         const int rows = yb - ya;
         const int seg = strip_segment_rows(rows, (long)strips * L.n_img);
         const int nseg = (rows + seg - 1) / seg;
-        hipLaunchKernelGGL((k_seed_strip<5>), dim3(strips, nseg, L.n_img), dim3(256), 0, st, L.frames, L.frame_pitch,
-                           L.row_stride, L.sh, L.sw, L.tab, L.dst, L.dst_img_stride, L.W, L.H, L.pitch, L.taps, ya,
-                           yb, seg);
+        if (getenv("SIFT_MI_SEED_OLD"))
+            hipLaunchKernelGGL((k_seed_strip_old<5>), dim3(strips, (rows + seg - 1) / seg, L.n_img), dim3(256), 0, st,
+                               L.frames, L.frame_pitch, L.row_stride, L.sh, L.sw, L.tab, L.dst, L.dst_img_stride, L.W,
+                               L.H, L.pitch, L.taps, ya, yb, seg);
+        else
+            hipLaunchKernelGGL((k_seed_strip<5>), dim3(strips, nseg, L.n_img), dim3(256), 0, st, L.frames,
+                               L.frame_pitch, L.row_stride, L.sh, L.sw, L.dst, L.dst_img_stride, L.W, L.H, L.pitch,
+                               L.taps, ya, yb, seg);
         return 0;
     }
     launch_seed_r<5>(L, st);

@@ -1,11 +1,12 @@
 """Labelled extensions and tooling around the path, on the GPU.
 
 * `set_max_octaves` (LABELLED EXTENSION, not in the crate; for the configs'
-  "5 octaves" / "7 octaves" wording): the capped result is exactly the
-  uncapped result's keypoints of octaves < cap -- a prefix of the emission
-  order (octave-major, src/lib.rs:281-294), since octave o's images depend
-  only on octaves <= o (src/lib.rs:213-267).  Checked bit for bit against the
-  uncapped GPU result (itself oracle-checked in test_gpu_parity).
+  "5 octaves" / "7 octaves" wording): without a limit the capped result is
+  exactly the uncapped result's keypoints of octaves < cap -- a prefix of the
+  emission order (octave-major, src/lib.rs:281-294), since octave o's images
+  depend only on octaves <= o (src/lib.rs:213-267).  With a limit, the limit
+  ranks that prefix.  Checked bit for bit against the uncapped GPU result
+  (itself oracle-checked in test_gpu_parity).
 * sample counting (measurement only): counts are the closed-form patch sizes
   and leave the results unchanged.
 * run_sift.py, the examples/run-sift.rs counterpart: prints the keypoint
@@ -67,6 +68,28 @@ def test_max_octaves_batch(pkg, synth):
         n = int((_octaves(f.keys) < 4).sum())
         assert np.array_equal(g.keypoints_array, f.keypoints_array[:n])
         assert np.array_equal(g.descriptors, f.descriptors[:n])
+
+
+def test_max_octaves_with_limit(pkg, synth):
+    """With features_limit the cap applies first: the result is the limit
+    (response-descending stable sort, emission order on ties, then truncate;
+    src/lib.rs:156-161) applied to the capped keypoint set, i.e. to the
+    uncapped result's octave prefix."""
+    img = synth.frame(640, 480, 5)
+    c = pkg.Context(0, pkg.OpenCVProcessing)
+    try:
+        full = c.sift(img)
+        c.set_max_octaves(3)
+        capped = c.sift(img)
+        lim = c.sift(img, features_limit=40)
+    finally:
+        c.close()
+    n = len(capped)
+    assert 40 < n < len(full)
+    kp = full.keypoints_array[:n]
+    order = np.argsort(-kp[:, 4], kind="stable")[:40]
+    assert np.array_equal(lim.keypoints_array, kp[order])
+    assert np.array_equal(lim.descriptors, full.descriptors[:n][order])
 
 
 def test_sample_counting(pkg, synth):

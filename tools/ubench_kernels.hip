@@ -320,6 +320,163 @@ void bench_segs(int N) {
     }
 }
 
+
+// seed (u8 -> 2x bilinear -> R = 5 blur): the product launcher's kernel vs
+// SIFT_MI_SEED_OLD (the round-2 LDS-staged strip seed), bit-identical check +
+// time, N frames of sw x sh (row stride `stride` >= sw)
+static void cv_linear_tab(int ssz, int dsz, std::vector<int>& ofs, std::vector<float>& a0, std::vector<float>& a1,
+                          int* lim) {
+    const double scale = 1. / ((double)dsz / ssz);
+    int xmax = dsz;
+    ofs.resize(dsz);
+    a0.resize(dsz);
+    a1.resize(dsz);
+    for (int d = 0; d < dsz; d++) {
+        float f = (float)((d + 0.5) * scale - 0.5);
+        int s = (int)floorf(f);
+        f -= (float)s;
+        if (s < 0) { f = 0; s = 0; }
+        if (s + 1 >= ssz) {
+            if (d < xmax) xmax = d;
+            if (s >= ssz - 1) { f = 0; s = ssz - 1; }
+        }
+        ofs[d] = s;
+        a0[d] = 1.f - f;
+        a1[d] = f;
+    }
+    *lim = xmax;
+}
+
+void bench_seed(int N, int sw, int sh, int stride) {
+    const int W = 2 * sw, H = 2 * sh, pitch = (W + 63) & ~63;
+    std::vector<uint8_t> hf((size_t)N * stride * sh);
+    uint32_t x = 12345;
+    for (auto& v : hf) { x = x * 1664525u + 1013904223u; v = (uint8_t)(x >> 24); }
+    uint8_t* df;
+    CK(hipMalloc(&df, hf.size()));
+    CK(hipMemcpy(df, hf.data(), hf.size(), hipMemcpyHostToDevice));
+    std::vector<int> xo, yo;
+    std::vector<float> xa, xb, ya, yb;
+    int xmax, ymax;
+    cv_linear_tab(sw, W, xo, xa, xb, &xmax);
+    cv_linear_tab(sh, H, yo, ya, yb, &ymax);
+    int *dxo, *dyo;
+    float *dxa, *dxb, *dya, *dyb;
+    CK(hipMalloc(&dxo, W * 4)); CK(hipMalloc(&dxa, W * 4)); CK(hipMalloc(&dxb, W * 4));
+    CK(hipMalloc(&dyo, H * 4)); CK(hipMalloc(&dya, H * 4)); CK(hipMalloc(&dyb, H * 4));
+    CK(hipMemcpy(dxo, xo.data(), W * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dxa, xa.data(), W * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dxb, xb.data(), W * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dyo, yo.data(), H * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dya, ya.data(), H * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dyb, yb.data(), H * 4, hipMemcpyHostToDevice));
+    const size_t plane = (size_t)pitch * H;
+    float *d0, *d1;
+    CK(hipMalloc(&d0, plane * N * 4));
+    CK(hipMalloc(&d1, plane * N * 4));
+    SeedLaunch L{};
+    L.frames = df;
+    L.frame_pitch = (size_t)stride * sh;
+    L.row_stride = stride;
+    L.sh = sh;
+    L.sw = sw;
+    L.tab = ResizeTab{dxo, dxa, dxb, dyo, dya, dyb, xmax};
+    L.profile = kProfileOpenCV;
+    L.dst_img_stride = plane;
+    L.W = W;
+    L.H = H;
+    L.pitch = pitch;
+    L.n_img = N;
+    const double s = 1.2489996;
+    for (int t = 0; t <= 5; t++) L.taps.k[t] = (float)std::exp(-(t * t) / (2 * s * s)) / 3.1f;
+    auto timeit = [&](float* dst) {
+        L.dst = dst;
+        launch_seed(5, L, 0);
+        hipEvent_t a, b;
+        CK(hipEventCreate(&a));
+        CK(hipEventCreate(&b));
+        CK(hipEventRecord(a));
+        for (int i = 0; i < 10; i++) launch_seed(5, L, 0);
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, a, b));
+        return ms / 10;
+    };
+    CK(hipMemset(d0, 0, plane * N * 4));
+    CK(hipMemset(d1, 0, plane * N * 4));
+    setenv("SIFT_MI_SEED_OLD", "1", 1);
+    const float t_old = timeit(d0);
+    unsetenv("SIFT_MI_SEED_OLD");
+    const float t_new = timeit(d1);
+    std::vector<float> h0(plane * N), h1(plane * N);
+    CK(hipMemcpy(h0.data(), d0, plane * N * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(h1.data(), d1, plane * N * 4, hipMemcpyDeviceToHost));
+    size_t diff = 0, first = (size_t)-1;
+    for (int b = 0; b < N; b++)
+        for (int y = 0; y < H; y++)
+            for (int xx = 0; xx < W; xx++) {
+                const size_t i = (size_t)b * plane + (size_t)y * pitch + xx;
+                if (std::memcmp(&h0[i], &h1[i], 4)) {
+                    if (!diff) first = i;
+                    diff++;
+                }
+            }
+    const double bytes = (double)N * (sw * (double)sh + 4.0 * W * H);
+    std::printf("seed %d x %dx%d (stride %d): old %8.1f us %6.2f TB/s | new %8.1f us %6.2f TB/s | differing px %zu",
+                N, sw, sh, stride, 1e3 * t_old, bytes / (t_old * 1e-3) / 1e12, 1e3 * t_new,
+                bytes / (t_new * 1e-3) / 1e12, diff);
+    if (diff) std::printf(" (first at frame %zu y %zu x %zu)", first / plane, (first % plane) / pitch, first % pitch);
+    std::printf("\n");
+    CK(hipFree(df)); CK(hipFree(d0)); CK(hipFree(d1));
+    CK(hipFree(dxo)); CK(hipFree(dxa)); CK(hipFree(dxb)); CK(hipFree(dyo)); CK(hipFree(dya)); CK(hipFree(dyb));
+}
+
+// k_seed_strip timing ablations (ABL bits: 1 no plane stores, 2 no loads /
+// upsample, 4 no row pass), 64 frames of 1920x1080 -> 3840x2160
+template <int ABL>
+float time_seed_abl(const uint8_t* df, float* dst, int N) {
+    const int sw = 1920, sh = 1080, W = 3840, H = 2160, pitch = 3840;
+    using G = StripGeom<5>;
+    const int strips = W / G::TW;
+    BlurTaps taps{};
+    for (int t = 0; t <= 5; t++) taps.k[t] = 1.0f / 11;
+    const int seg = 360, nseg = H / seg;
+    auto go = [&]() {
+        hipLaunchKernelGGL((k_seed_strip<5, ABL>), dim3(strips, nseg, N), dim3(256), 0, 0, df, (size_t)sw * sh,
+                           (size_t)sw, sh, sw, dst, (size_t)pitch * H, W, H, pitch, taps, 0, H, seg);
+    };
+    go();
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    CK(hipEventRecord(a));
+    for (int i = 0; i < 10; i++) go();
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    return ms / 10;
+}
+
+void bench_seed_abl(int N) {
+    uint8_t* df;
+    CK(hipMalloc(&df, (size_t)N * 1920 * 1080));
+    CK(hipMemset(df, 77, (size_t)N * 1920 * 1080));
+    float* dst;
+    CK(hipMalloc(&dst, (size_t)N * 3840 * 2160 * 4));
+    std::printf("seed ablations, %d x 1920x1080 (seg 360): us\n", N);
+    std::printf("  full           %8.1f\n", 1e3 * time_seed_abl<0>(df, dst, N));
+    std::printf("  -stores        %8.1f\n", 1e3 * time_seed_abl<1>(df, dst, N));
+    std::printf("  -loader        %8.1f\n", 1e3 * time_seed_abl<2>(df, dst, N));
+    std::printf("  -rowpass       %8.1f\n", 1e3 * time_seed_abl<4>(df, dst, N));
+    std::printf("  -stores-loader %8.1f\n", 1e3 * time_seed_abl<3>(df, dst, N));
+    std::printf("  -loader-rowpass %8.1f\n", 1e3 * time_seed_abl<6>(df, dst, N));
+    std::printf("  colpass only (no stores) %8.1f\n", 1e3 * time_seed_abl<7>(df, dst, N));
+    CK(hipFree(df));
+    CK(hipFree(dst));
+}
+
 int main(int argc, char** argv) {
     const char* mode = argc > 1 ? argv[1] : "all";
     if (!strcmp(mode, "segs")) {
@@ -330,6 +487,19 @@ int main(int argc, char** argv) {
         bench_pair(argc > 2 ? atoi(argv[2]) : 64, 3840, 2160);
         bench_pair(argc > 2 ? atoi(argv[2]) : 64, 1920, 1080);
         bench_pair(argc > 2 ? atoi(argv[2]) : 64, 960, 540);
+        return 0;
+    }
+    if (!strcmp(mode, "seedabl")) {
+        bench_seed_abl(argc > 2 ? atoi(argv[2]) : 64);
+        return 0;
+    }
+    if (!strcmp(mode, "seed")) {
+        const int n = argc > 2 ? atoi(argv[2]) : 64;
+        bench_seed(n, 1920, 1080, 1920);
+        bench_seed(4, 1921, 1079, 1923);
+        bench_seed(4, 333, 97, 335);
+        bench_seed(4, 80, 40, 81);
+        bench_seed(n, 960, 540, 960);
         return 0;
     }
     if (!strcmp(mode, "tail")) {
