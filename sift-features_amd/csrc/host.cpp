@@ -732,8 +732,7 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
     {
         const char* e = getenv("SIFT_MI_TAIL");
         if (!(e && !strcmp(e, "0")) && p.n_oct <= kTailMaxOct)
-            o_tail = tail_octave_start(p.ow.data(), p.oh.data(), p.n_oct,
-                                       *std::max_element(p.oct_r + 1, p.oct_r + kImagesPerOctave));
+            o_tail = tail_octave_start(p.ow.data(), p.oh.data(), p.n_oct, p.oct_r);
     }
     uint64_t bytes = p.algo_bytes_per_frame;  // per frame, SURVEY.md 8(d)
     if (c->band_restricted) {

@@ -339,6 +339,22 @@ constexpr int kStripMaxR = 16;
 #endif
 
 typedef unsigned int u32x2 __attribute__((ext_vector_type(2)));
+// buffer offset past every plane (planes are < 2^31 bytes): a store there is
+// dropped by the buffer's range check
+constexpr uint32_t kStoreDrop = 0xfffffff0u;
+
+// N stores the buffer drops.  A strip kernel's loop waits at its top for the
+// chunk loads of the previous iteration, with the column pass's stores issued
+// after them; the compiler counts those stores only if EVERY path into the
+// loop top has as many -- so the prologue, which enters it after its loads
+// and no column pass, issues the same number of dropped stores.
+template <int N>
+__device__ __forceinline__ void drop_stores(__amdgpu_buffer_rsrc_t r) {
+#pragma unroll
+    for (int i = 0; i < N; i++)  // distinct offsets: not merged as redundant stores
+        __builtin_amdgcn_raw_buffer_store_b32(0u, r, kStoreDrop - 16u * (uint32_t)i, 0, 0);
+}
+
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
 // Buffer resource over `bytes` bytes at p (wave-uniform inputs: the halves of
@@ -487,38 +503,56 @@ __device__ __forceinline__ void strip_colpass(const float* sa, const float* sb, 
         out[o] = acc;
     }
     const int y0 = y + WV * G::VB;
+    // Every row issues one store (two with NXT) whatever the row / column
+    // bounds: a store outside them gets its offset OR-ed with kStoreDrop (out
+    // of range: the buffer drops it) instead of a branch, so the number of
+    // stores after the next chunk's loads is static and the compiler's wait
+    // for those loads does not also wait for these stores (loads and stores
+    // share vmcnt on gfx9).  A pair whose second column is past the image
+    // writes it into the row's padding (W odd: pitch > W), which nothing reads.
     const int nrow = min(G::VB, ye - y0);
     const int gx = x0 + 2 * lane;
-    const bool cols_full = x0 + G::TW <= W;
-    const bool pair = gx + 1 < W;
-    int so = (y0 * pitch + x0) * 4;
+    // offset = (row part, uniform) + (column part, per lane), OR-ed with
+    // the row's and the lane's drop flags
+    const uint32_t lane_col = (uint32_t)(gx * 4), lane_bad = gx < W ? 0u : kStoreDrop;
+    const uint32_t lane_ncol = (uint32_t)((gx >> 1) * 4);
+    const uint32_t lane_nbad = ((gx >> 1) < wn && (P == kProfileOpenCV || gx + 1 < W)) ? 0u : kStoreDrop;
 #pragma unroll
     for (int o = 0; o < G::VB; o++) {
-        if (o >= nrow) break;
-        if (cols_full || pair) {
-            __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, out[o]), rd, 8 * lane, so, SIFT_STORE_CPOL);
-        } else if (gx < W) {
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, out[o].x), rd, 8 * lane, so, 0);
+        const int gy = y0 + o;
+        const uint32_t row_bad = o < nrow ? 0u : kStoreDrop;  // uniform
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, out[o]), rd,
+                                              ((uint32_t)(gy * pitch * 4) + lane_col) | lane_bad | row_bad, 0,
+                                              SIFT_STORE_CPOL);
+        // nearest 1/2: pixel (2x, 2y) (cv::resize INTER_NEAREST) / (2x + 1, 2y + 1)
+        // (image's Nearest); y0 is even (segments start at even rows,
+        // strip_segment_rows), so those are the even / odd o
+        if (NXT && (o & 1) == (P == kProfileOpenCV ? 0 : 1)) {  // o: unrolled constant
+            const uint32_t nrow_bad = (gy >> 1) < hn ? row_bad : kStoreDrop;  // uniform
+            const float val = P == kProfileOpenCV ? out[o].x : out[o].y;
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, val), rn,
+                                                  ((uint32_t)((gy >> 1) * pitch_n * 4) + lane_ncol) | lane_nbad |
+                                                      nrow_bad,
+                                                  0, 0);
         }
-        if constexpr (NXT) {
-            // nearest 1/2: pixel (2x, 2y) (cv::resize INTER_NEAREST) / (2x + 1, 2y + 1) (image's Nearest)
-            const int gy = y0 + o;
-            const bool row = P == kProfileOpenCV ? (gy & 1) == 0 : (gy & 1) == 1;
-            if (row && (gy >> 1) < hn && (gx >> 1) < wn && (P == kProfileOpenCV || pair)) {
-                const float val = P == kProfileOpenCV ? out[o].x : out[o].y;
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, val), rn, 4 * lane,
-                                                      ((gy >> 1) * pitch_n + (x0 >> 1)) * 4, 0);
-            }
-        }
-        so += pitch * 4;
     }
 }
 
 // grid: (strips, segments, frames); segment sg covers output rows
 // [ya + sg * seg, min(yb, ya + (sg + 1) * seg)).  G_{s-1} / G_s planes are
 // H * pitch floats (< 2^31 bytes: checked by the launcher).
+// the next-octave stores of NXT (blur 3, R = 8) push it past 128 VGPRs:
+// 3 workgroups per CU there instead of spilling (SIFT_STRIP_NXT_MINB)
+#ifndef SIFT_STRIP_NXT_MINB
+#define SIFT_STRIP_NXT_MINB 3
+#endif
+template <int R, bool NXT>
+constexpr int strip_minb() {
+    return (NXT && R >= 7 && StripGeom<R>::MINB > SIFT_STRIP_NXT_MINB) ? SIFT_STRIP_NXT_MINB : StripGeom<R>::MINB;
+}
+
 template <int R, int P, bool NXT>
-__global__ __launch_bounds__(256, StripGeom<R>::MINB) void k_blur_strip(
+__global__ __launch_bounds__(256, (strip_minb<R, NXT>())) void k_blur_strip(
     const float* __restrict__ src, size_t src_img_stride, float* __restrict__ dst, size_t dst_img_stride,
     float* __restrict__ nxt, size_t nxt_img_stride, int pitch_n, int wn, int hn, int W, int H, int pitch,
     const BlurTaps taps, int ya, int yb, int seg) {
@@ -566,6 +600,7 @@ __global__ __launch_bounds__(256, StripGeom<R>::MINB) void k_blur_strip(
     strip_load<R, P>(pre, rs, voff, cols_in, ys - R, x0, W, H, pitch);
     strip_store<G>(pre, lds);
     strip_load<R, P>(pre, rs, voff, cols_in, ys - R + G::S, x0, W, H, pitch);
+    drop_stores<G::VB * (NXT ? 2 : 1)>(rd);
     __syncthreads();
     strip_rowpass<G, P>(lds, taps, prow, pq);
     for (int k = 0; k < nsteps; k++) {
@@ -584,6 +619,8 @@ __global__ __launch_bounds__(256, StripGeom<R>::MINB) void k_blur_strip(
         strip_colpass<G, P, w, NXT>(sa, sb, taps, lane, y, ye, x0, W, pitch, rd, rn, pitch_n, wn, hn); \
         break;
             COLPASS(0) COLPASS(1) COLPASS(2) COLPASS(3)
+            default:
+                __builtin_unreachable();  // wv < 4: no store-free path (static vmcnt)
 #undef COLPASS
         }
     }
@@ -653,7 +690,8 @@ __device__ __forceinline__ void pair_colpass_a(const float* sa, const float* sb,
     const int y0 = y + WV * GA::VB;
     const int gx = xa + 2 * lane;  // even
     const bool own = gx >= xa + hb && gx < xa + hb + two && gx < W;  // this strip's columns
-    const bool pair = gx + 1 < W;
+    const uint32_t colbad = own ? 0u : kStoreDrop;
+
 #pragma unroll
     for (int o = 0; o < GA::VB; o++) {
         f2v acc = v[o + R] * k0;
@@ -663,18 +701,19 @@ __device__ __forceinline__ void pair_colpass_a(const float* sa, const float* sb,
             acc = __builtin_elementwise_fma(v[o + R + t] + v[o + R - t], kt, acc);
         }
         *(f2v*)(bslot + (WV * GA::VB + o) * bip + 2 * lane) = acc;
+        // predicated by out-of-range offsets, a static store count (see strip_colpass)
         const int gy = y0 + o;
-        if (own && gy >= gys && gy < gye) {
-            const int off = (gy * pitch + gx) * 4;
-            if (pair)
-                __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, acc), rd, off, 0, SIFT_STORE_CPOL);
-            else
-                __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc.x), rd, off, 0, 0);
-            if constexpr (NXT) {
-                if ((gy & 1) == 0 && (gy >> 1) < hn && (gx >> 1) < wn)
-                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc.x), rn,
-                                                          ((gy >> 1) * pitch_n + (gx >> 1)) * 4, 0, 0);
-            }
+        const uint32_t rowbad = gy >= gys && gy < gye ? 0u : kStoreDrop;  // uniform
+        const uint32_t off = (uint32_t)((gy * pitch + gx) * 4);
+        // (a pair past the image's last column writes into the row padding)
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, acc), rd, off | colbad | rowbad, 0,
+                                              SIFT_STORE_CPOL);
+        if constexpr (NXT) {
+            const uint32_t nbad = (gy & 1) == 0 && (gy >> 1) < hn ? rowbad : kStoreDrop;
+            const uint32_t ncol = (gx >> 1) < wn ? colbad : kStoreDrop;
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, acc.x), rn,
+                                                  (uint32_t)(((gy >> 1) * pitch_n + (gx >> 1)) * 4) | ncol | nbad, 0,
+                                                  0);
         }
     }
 }
@@ -797,6 +836,8 @@ __global__ __launch_bounds__(256, (PairGeom<Ra, Rb>::MINB)) void k_blur2_strip(
                                                         0);                                                      \
         break;
                 COLB(0) COLB(1) COLB(2) COLB(3)
+                default:
+                    __builtin_unreachable();
 #undef COLB
             }
         };
@@ -813,6 +854,8 @@ __global__ __launch_bounds__(256, (PairGeom<Ra, Rb>::MINB)) void k_blur2_strip(
                                    rn, pitch_n, wn, hn);                                                              \
         break;
                 COLA(0) COLA(1) COLA(2) COLA(3)
+                default:
+                    __builtin_unreachable();
 #undef COLA
             }
         }
@@ -1205,6 +1248,8 @@ __global__ __launch_bounds__(256, 4) void k_seed_strip_old(const uint8_t* __rest
         strip_colpass<G, kProfileOpenCV, w, false>(sa, sb, taps, lane, y, ye, x0, W, pitch, rd, rd, 0, 0, 0); \
         break;
             COLPASS(0) COLPASS(1) COLPASS(2) COLPASS(3)
+            default:
+                __builtin_unreachable();  // wv < 4: no store-free path (static vmcnt)
 #undef COLPASS
         }
     }
@@ -1221,18 +1266,23 @@ __global__ __launch_bounds__(256, 4) void k_seed_strip_old(const uint8_t* __rest
 // source 0 with coefficients (1, 0); d = n - 1 the last source alone (rows:
 // (1, 0) on a clamped second row); every other d takes sources (d - 1) >> 1
 // and the next one with (0.75, 0.25) for odd d, (0.25, 0.75) for even d.  So
-// no table is read.  A loader item is one window row x 4 window columns: the
-// 4 columns read at most 4 consecutive source bytes of each of the row's two
-// source rows (reflect-101 keeps the span), fetched as the one or two
-// 4-byte-aligned dwords that contain them (no dword without a needed byte is
-// read, so no access leaves the frame, whatever its stride or alignment),
-// then v / 255, HResizeLinear (two rounded products + add) per source row and
-// VResizeLinear (S0 b0 + S1 b1).  The items of chunk k + 2 are fetched while
-// chunk k + 1 is row-filtered, as k_blur_strip prefetches its rows.
-// Wave w owns chunk rows 8w .. 8w + 7 (8 x 36 items): item i = lane + 64 j is
-// row 8w + i / 36, column group i % 36, so a wave's load touches one or two
-// source rows at consecutive 2-byte steps (coalesced) and its ds_write_b128
-// groups write 128 contiguous bytes (conflict-free).
+// no table is read.
+//
+// Loader item = 12 window columns x a pair of window rows (g, g + 1), g odd:
+// in the interior both rows read source rows (g - 1) / 2 and the next, so
+// HResizeLinear (two rounded products + add) runs once per source row for
+// two output rows, and the 12 columns need 8 consecutive source bytes per
+// source row -- fetched as the 4-byte-aligned dwords that hold them (no
+// dword without a needed byte is read, so no access leaves the frame,
+// whatever its stride or alignment).  Then v / 255 and VResizeLinear
+// (S0 b0 + S1 b1), in packed f32 (two independently rounded lanes, the same
+// bits as scalar).  Border items (a column outside [1, W - 2], a reflected
+// or last row) take per-column tables and up to three source rows.  Wave w
+// owns chunk rows 8w .. 8w + 7: lane l < 48 row pair 4w + (l & 3), column
+// group l >> 2.  The items of chunk k + 2 are fetched while chunk k + 1 is
+// row-filtered, as k_blur_strip prefetches its rows.  Chunks start at odd
+// window rows when segments start at even rows (the launcher's choice);
+// any start is exact, odd ones keep the interior pairs on two source rows.
 // ---------------------------------------------------------------------------
 // 2x bilinear source index and coefficients of destination d (0 <= d < n,
 // n = 2 * ns): see above; `two` false: the single last source
@@ -1254,6 +1304,13 @@ __device__ __forceinline__ void seed_axis(int d, int n, int ns, int& s, float& a
     }
 }
 
+// v / 255 of two bytes (u8_unit, packed)
+__device__ __forceinline__ f2v u8_unit2(float a, float b) {
+    const f2v fv = {a, b}, c = {1.0f / 255.0f, 1.0f / 255.0f};
+    const f2v q = fv * c;
+    return __builtin_elementwise_fma(__builtin_elementwise_fma(-q, f2v{255.0f, 255.0f}, fv), c, q);
+}
+
 // ABL: timing ablations for tools/ubench_kernels.hip only (the product
 // launches ABL = 0): 1 drops the plane stores (zero-size buffer), 2 the
 // loader's loads and upsample, 4 the row pass
@@ -1264,10 +1321,10 @@ __global__ __launch_bounds__(256, StripGeom<R>::MINB) void k_seed_strip(const ui
                                                                         size_t dst_img_stride, int W, int H, int pitch,
                                                                         const BlurTaps taps, int ya, int yb, int seg) {
     using G = StripGeom<R>;
-    constexpr int NQ = G::C4;                       // 4-column groups of the window (36)
-    constexpr int NI = NQ * G::VB;                  // items per wave (8 rows)
-    constexpr int NJ = (NI + 63) / 64;              // items per lane
-    static_assert(G::S == 32 && G::NW == 4, "wave w loads chunk rows 8w .. 8w + 7");
+    constexpr int CW = 12;                 // window columns per item
+    constexpr int NCG = G::IWV / CW;       // column groups (12)
+    constexpr int NPW = G::VB / 2;         // row pairs per wave (4)
+    static_assert(G::S == 32 && G::NW == 4 && G::IWV % CW == 0 && NCG * NPW <= 64, "loader item map");
     __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1283,115 +1340,158 @@ __global__ __launch_bounds__(256, StripGeom<R>::MINB) void k_seed_strip(const ui
     const uint32_t boff = (uint32_t)(uintptr_t)src & 3u;
     const uint32_t nbytes = (boff + (uint32_t)(sh - 1) * (uint32_t)row_stride + (uint32_t)sw + 3u) & ~3u;
     const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(src - boff, nbytes);
-    // border items (a window column outside [1, W - 2]): per column group
-    // the first source byte, the bytes needed, and per column its source
-    // offset from there, single / two taps and coefficients
-    __shared__ int t_smin[NQ], t_need[NQ], t_info[NQ];
-    __shared__ __attribute__((aligned(16))) float t_a0[NQ * 4], t_a1[NQ * 4];
-    auto interior = [&](int q) {
-        const int c0 = x0 - G::HWL + 4 * q;
-        return c0 >= 1 && c0 + 3 <= W - 2;
-    };
-    if (tid < NQ && !interior(tid)) {
-        const int c0 = x0 - G::HWL + 4 * tid;
-        int sx[4], info = 0, lo = 1 << 30, hi = -1;
+    // this lane's item: row pair pr of the wave, column group cg
+    const bool act = lane < NCG * NPW;
+    const int pr = wv * NPW + (lane & (NPW - 1)), cg = lane / NPW;
+    const int c0 = x0 - G::HWL + CW * cg;  // first window column (even)
+    const bool xin = c0 >= 1 && c0 + CW - 1 <= W - 2;
+    // border columns: per window column its source offset from the item's
+    // first source byte (bits 0-3), single / two taps (bit 4), coefficients
+    __shared__ int t_info[G::IWV];
+    __shared__ float t_a0[G::IWV], t_a1[G::IWV];
+    __shared__ int t_smin[NCG], t_need[NCG];
+    if (tid < NCG) {
+        const int cb = x0 - G::HWL + CW * tid;
+        int lo = 1 << 30, hi = -1;
+        int sx[CW];
+        bool two[CW];
 #pragma unroll
-        for (int k = 0; k < 4; k++) {
-            bool two;
-            seed_axis(strip_index<kProfileOpenCV>(c0 + k, W), W, sw, sx[k], t_a0[4 * tid + k], t_a1[4 * tid + k], two);
+        for (int k = 0; k < CW; k++) {
+            seed_axis(strip_index<kProfileOpenCV>(cb + k, W), W, sw, sx[k], t_a0[CW * tid + k], t_a1[CW * tid + k],
+                      two[k]);
             lo = min(lo, sx[k]);
-            hi = max(hi, two ? sx[k] + 1 : sx[k]);
-            info |= (two ? 1 : 0) << (8 * k + 4);
+            hi = max(hi, two[k] ? sx[k] + 1 : sx[k]);
         }
 #pragma unroll
-        for (int k = 0; k < 4; k++) info |= (sx[k] - lo) << (8 * k);  // 0 .. 3
+        for (int k = 0; k < CW; k++) t_info[CW * tid + k] = (sx[k] - lo) | (two[k] ? 16 : 0);
         t_smin[tid] = lo;
-        t_need[tid] = hi - lo + 1;
-        t_info[tid] = info;
+        t_need[tid] = hi - lo + 1;  // <= 8 (12 columns span <= 7 sources)
     }
     __syncthreads();
-    // prefetched chunk, per item the dwords holding the 4 source bytes of
-    // each of its two source rows (raw: the byte alignment waits until the
-    // chunk is stored, so the loads stay in flight across a row and a column
-    // pass)
-    uint32_t plo[NJ][2], phi[NJ][2];
-    uint32_t psh = 0;  // byte offsets: 2 bits per (item, source row)
-    auto item = [&](int j, int& r, int& q) {
-        const int i = lane + 64 * j;
-        r = wv * G::VB + i / NQ;
-        q = i - (i / NQ) * NQ;
-    };
-    auto src_rows = [&](int g, int& sy0, int& sy1, float& b0, float& b1) {
+    // wave-uniform path choice: a wave takes the table path when any of its
+    // items needs it (only the first / last strip of a row)
+    const bool wxin = __builtin_amdgcn_ballot_w64(act && !xin) == 0;
+    const int smin = wxin ? c0 / 2 - 1 : t_smin[cg];
+    const int need = wxin ? 8 : t_need[cg];
+    // prefetched chunk: per source row (up to 3) the <= 3 dwords holding the
+    // item's bytes, raw (the byte alignment waits until the chunk is stored,
+    // so the loads stay in flight across a row and a column pass)
+    uint32_t pw[3][3];
+    uint32_t psh = 0;  // byte offset of each source row (2 bits each)
+    int pbase = 0;     // first source row
+    auto rows_of = [&](int g, int& sy0, int& sy1, float& b0, float& b1) {
         bool two;
         seed_axis(strip_index<kProfileOpenCV>(g, H), H, sh, sy0, b0, b1, two);
         sy1 = min(sy0 + 1, sh - 1);
     };
     auto prefetch = [&](int g0) {
-        psh = 0;
         if constexpr ((ABL & 2) != 0) return;
+        if (!act) return;
+        const int g = g0 + 2 * pr;
+        int a0, a1, c0_, c1_;
+        float f0, f1;
+        rows_of(g, a0, a1, f0, f1);
+        rows_of(g + 1, c0_, c1_, f0, f1);
+        pbase = min(a0, c0_);
+        const int nrows = max(a1, c1_) - pbase + 1;  // 2 in the interior, <= 3
+        psh = 0;
 #pragma unroll
-        for (int j = 0; j < NJ; j++) {
-            if (NI % 64 == 0 || lane + 64 * j < NI) {
-                int r, q, sy0, sy1;
-                float b0, b1;
-                item(j, r, q);
-                src_rows(g0 + r, sy0, sy1, b0, b1);
-                const bool in = interior(q);
-                const int smin = in ? (x0 - G::HWL + 4 * q) / 2 - 1 : t_smin[q];
-                const int need = in ? 4 : t_need[q];
+        for (int r = 0; r < 3; r++) {
+            if (r < nrows) {
+                const uint32_t off = boff + (uint32_t)(pbase + r) * (uint32_t)row_stride + (uint32_t)smin;
+                const uint32_t sa = off & 3u, o4 = off & ~3u;
+                pw[r][0] = __builtin_amdgcn_raw_buffer_load_b32(rs, o4, 0, 0);
+                pw[r][1] = (int)sa + need > 4 ? __builtin_amdgcn_raw_buffer_load_b32(rs, o4 + 4u, 0, 0) : 0u;
+                pw[r][2] = (int)sa + need > 8 ? __builtin_amdgcn_raw_buffer_load_b32(rs, o4 + 8u, 0, 0) : 0u;
+                psh |= sa << (2 * r);
+            }
+        }
+    };
+    // HResizeLinear of one source row's 12 columns from its 8 bytes p[0..7]
+    auto hres = [&](const uint32_t (&w)[3], uint32_t sh3, float (&h)[CW]) {
+        const uint32_t lo = __builtin_amdgcn_alignbyte(w[1], w[0], sh3);
+        const uint32_t hi = __builtin_amdgcn_alignbyte(w[2], w[1], sh3);
+        // (float)(byte k): v_cvt_f32_ubyte{0..3}
+        auto by = [](uint32_t w, int k) { return (float)((w >> (8 * k)) & 0xffu); };
+        const f2v p01 = u8_unit2(by(lo, 0), by(lo, 1));
+        const f2v p23 = u8_unit2(by(lo, 2), by(lo, 3));
+        const f2v p45 = u8_unit2(by(hi, 0), by(hi, 1));
+        const f2v p67 = u8_unit2(by(hi, 2), by(hi, 3));
+        const float p[8] = {p01.x, p01.y, p23.x, p23.y, p45.x, p45.y, p67.x, p67.y};
+        if (wxin) {
+            // column c0 + 2i: S[i] * 0.25 + S[i + 1] * 0.75; c0 + 2i + 1:
+            // S[i + 1] * 0.75 + S[i + 2] * 0.25 (t = S[sx]*a0 + S[sx+1]*a1)
+            const f2v ka = {0.25f, 0.75f}, kb = {0.75f, 0.25f};
 #pragma unroll
-                for (int k = 0; k < 2; k++) {
-                    const uint32_t off = boff + (uint32_t)(k ? sy1 : sy0) * (uint32_t)row_stride + (uint32_t)smin;
-                    const uint32_t sa = off & 3u;
-                    plo[j][k] = __builtin_amdgcn_raw_buffer_load_b32(rs, off & ~3u, 0, 0);
-                    phi[j][k] = (int)sa + need > 4 ? __builtin_amdgcn_raw_buffer_load_b32(rs, (off & ~3u) + 4u, 0, 0)
-                                                   : 0u;
-                    psh |= sa << (4 * j + 2 * k);
+            for (int i = 0; i < CW / 2; i++) {
+                const f2v v = f2v{p[i], p[i + 1]} * ka + f2v{p[i + 1], p[i + 2]} * kb;
+                h[2 * i] = v.x;
+                h[2 * i + 1] = v.y;
+            }
+        } else {
+#pragma unroll
+            for (int k = 0; k < CW; k++) {
+                const int info = t_info[CW * cg + k], d = info & 15;
+                float v0 = p[0], v1 = p[1];
+#pragma unroll
+                for (int e = 1; e < 7; e++) {
+                    v0 = d == e ? p[e] : v0;
+                    v1 = d == e ? p[e + 1] : v1;
                 }
+                h[k] = (info & 16) ? v0 * t_a0[CW * cg + k] + v1 * t_a1[CW * cg + k] : v0;
             }
         }
     };
     // the prefetched chunk (window rows from g0) -> upsampled rows in the slot
     auto store = [&](float* slot, int g0) {
+        if (!act) return;
+        const int g = g0 + 2 * pr;
+        float* out = slot + (2 * pr) * G::IWP + CW * cg;
+        if constexpr ((ABL & 2) != 0) {
 #pragma unroll
-        for (int j = 0; j < NJ; j++) {
-            if (!(NI % 64 == 0 || lane + 64 * j < NI)) continue;
-            int r, q, sy0, sy1;
-            float b0, b1;
-            item(j, r, q);
-            if constexpr ((ABL & 2) != 0) {
-                *reinterpret_cast<float4*>(slot + r * G::IWP + 4 * q) = make_float4(0.5f, 0.25f, (float)g0, 1.0f);
-                continue;
+            for (int k = 0; k < CW; k += 4) {
+                *reinterpret_cast<float4*>(out + k) = make_float4(0.5f, 0.25f, (float)g, 1.0f);
+                *reinterpret_cast<float4*>(out + G::IWP + k) = make_float4(0.5f, 0.25f, (float)g, 1.0f);
             }
-            src_rows(g0 + r, sy0, sy1, b0, b1);
-            const bool in = interior(q);
-            float h[2][4];
+            return;
+        }
+        int sy[2][2];
+        float b[2][2];
+        rows_of(g, sy[0][0], sy[0][1], b[0][0], b[0][1]);
+        rows_of(g + 1, sy[1][0], sy[1][1], b[1][0], b[1][1]);
+        float h0[CW], h1[CW];
+        hres(pw[0], psh & 3u, h0);
+        hres(pw[1], (psh >> 2) & 3u, h1);
+        // wave-uniform: every pair of the wave on two source rows (all but the
+        // first / last chunks of a frame)
+        const bool two_rows = __builtin_amdgcn_ballot_w64(act && !(sy[0][0] == pbase && sy[1][0] == pbase &&
+                                                                  sy[0][1] == pbase + 1 && sy[1][1] == pbase + 1)) == 0;
 #pragma unroll
-            for (int k = 0; k < 2; k++) {
-                const uint32_t w = __builtin_amdgcn_alignbyte(phi[j][k], plo[j][k], (psh >> (4 * j + 2 * k)) & 3u);
-                const float p0 = u8_unit(w & 0xff), p1 = u8_unit((w >> 8) & 0xff), p2 = u8_unit((w >> 16) & 0xff),
-                            p3 = u8_unit(w >> 24);
-                if (in) {
-                    // HResizeLinear: t = S[sx]*a0 + S[sx+1]*a1 (two roundings + add)
-                    h[k][0] = p0 * 0.25f + p1 * 0.75f;
-                    h[k][1] = p1 * 0.75f + p2 * 0.25f;
-                    h[k][2] = p1 * 0.25f + p2 * 0.75f;
-                    h[k][3] = p2 * 0.75f + p3 * 0.25f;
-                } else {
-                    const int info = t_info[q];
+        for (int r = 0; r < 2; r++) {
+            float v[CW];
+            if (two_rows) {
+                // VResizeLinear: S0*b0 + S1*b1
+                const f2v b0 = {b[r][0], b[r][0]}, b1 = {b[r][1], b[r][1]};
 #pragma unroll
-                    for (int c = 0; c < 4; c++) {
-                        const int d = (info >> (8 * c)) & 15;
-                        const float v0 = d == 0 ? p0 : (d == 1 ? p1 : (d == 2 ? p2 : p3));
-                        const float v1 = d == 0 ? p1 : (d == 1 ? p2 : p3);
-                        h[k][c] = (info >> (8 * c + 4)) & 1 ? v0 * t_a0[4 * q + c] + v1 * t_a1[4 * q + c] : v0;
-                    }
+                for (int k = 0; k < CW; k += 2) {
+                    const f2v o = f2v{h0[k], h0[k + 1]} * b0 + f2v{h1[k], h1[k + 1]} * b1;
+                    v[k] = o.x;
+                    v[k + 1] = o.y;
+                }
+            } else {  // border rows: any two of the three source rows
+                float h2[CW];
+                hres(pw[2], (psh >> 4) & 3u, h2);
+                const int i0 = sy[r][0] - pbase, i1 = sy[r][1] - pbase;
+#pragma unroll
+                for (int k = 0; k < CW; k++) {
+                    const float s0 = i0 == 0 ? h0[k] : (i0 == 1 ? h1[k] : h2[k]);
+                    const float s1 = i1 == 0 ? h0[k] : (i1 == 1 ? h1[k] : h2[k]);
+                    v[k] = s0 * b[r][0] + s1 * b[r][1];
                 }
             }
-            // VResizeLinear: S0*b0 + S1*b1
-            *reinterpret_cast<float4*>(slot + r * G::IWP + 4 * q) =
-                make_float4(h[0][0] * b0 + h[1][0] * b1, h[0][1] * b0 + h[1][1] * b1, h[0][2] * b0 + h[1][2] * b1,
-                            h[0][3] * b0 + h[1][3] * b1);
+#pragma unroll
+            for (int k = 0; k < CW; k += 4)
+                *reinterpret_cast<float4*>(out + r * G::IWP + k) = make_float4(v[k], v[k + 1], v[k + 2], v[k + 3]);
         }
     };
     int prow, pq;  // row-pass lane map (see strip_rowpass)
@@ -1413,6 +1513,7 @@ __global__ __launch_bounds__(256, StripGeom<R>::MINB) void k_seed_strip(const ui
     prefetch(gb);
     store(lds, gb);
     prefetch(gb + G::S);
+    drop_stores<G::VB>(rd);
     __syncthreads();
     if constexpr ((ABL & 4) == 0) strip_rowpass<G, kProfileOpenCV>(lds, taps, prow, pq);
     for (int k = 0; k < nsteps; k++) {
@@ -1431,6 +1532,8 @@ __global__ __launch_bounds__(256, StripGeom<R>::MINB) void k_seed_strip(const ui
         strip_colpass<G, kProfileOpenCV, w, false>(sa, sb, taps, lane, y, ye, x0, W, pitch, rd, rd, 0, 0, 0); \
         break;
             COLPASS(0) COLPASS(1) COLPASS(2) COLPASS(3)
+            default:
+                __builtin_unreachable();  // wv < 4: no store-free path (static vmcnt)
 #undef COLPASS
         }
     }
@@ -1601,13 +1704,17 @@ static int strip_segment_rows(int rows, long per) {
     const long few = std::min<long>((2048 + per - 1) / per, rows / 40);
     long nseg = std::min<long>((strip_wg_target() + per - 1) / per, std::max<long>(rows / 320, few));
     nseg = std::max(1L, nseg);
-    return (int)((rows + nseg - 1) / nseg);
+    // even: with an even first row every segment starts at an even row (the
+    // strip kernels' next-octave rows are then the even / odd rows of each
+    // column pass statically; the seed's row pairs share source rows)
+    return (int)(((rows + nseg - 1) / nseg + 1) & ~1);
 }
 
 template <int R>
 static void launch_blur_strip_r(const BlurLaunch& L, hipStream_t st) {
     using G = StripGeom<R>;
-    const int ya = L.y1 > L.y0 ? std::max(L.y0, 0) : 0;
+    // an even first row (one extra row above a band is exact): see strip_segment_rows
+    const int ya = L.y1 > L.y0 ? std::max(L.y0, 0) & ~1 : 0;
     const int yb = L.y1 > L.y0 ? std::min(L.y1, L.H) : L.H;
     if (yb <= ya) return;
     const int strips = (L.W + G::TW - 1) / G::TW;
@@ -1742,7 +1849,9 @@ int launch_seed(int R, const SeedLaunch& L, hipStream_t st) {
     if (L.W == 2 * L.sw && L.H == 2 * L.sh && L.W >= 160 && L.H >= 64 &&
         (uint64_t)L.H * (uint64_t)L.pitch * 4 < (1ull << 31) && strip_blur_enabled()) {
         using G = StripGeom<5>;
-        const int ya = L.y1 > L.y0 ? std::max(L.y0, 0) : 0;
+        // segments start at even rows: the loader's row pairs then share their
+        // two source rows (k_seed_strip); an extra row above a band is exact
+        const int ya = L.y1 > L.y0 ? std::max(L.y0, 0) & ~1 : 0;
         const int yb = L.y1 > L.y0 ? std::min(L.y1, L.H) : L.H;
         if (yb <= ya) return 0;
         const int strips = (L.W + G::TW - 1) / G::TW;
@@ -1807,11 +1916,14 @@ __device__ __forceinline__ void tail_fill_cols(float* X, int W, int H, int Rm, i
     }
 }
 
-template <int P>
-__device__ __forceinline__ void tail_blur(float* __restrict__ A, float* __restrict__ T, float* __restrict__ B,
-                                          const float* __restrict__ kf, int R, int Rn, int Rm, int W, int H,
-                                          float* __restrict__ g, int pitch, bool nxt, float* __restrict__ N,
-                                          float* __restrict__ gn, int wn, int hn, int pn) {
+// One blur of a tail octave (radius R a compile-time constant: every output's
+// window is read from LDS once into registers and the tap chain runs on
+// registers; the taps come from the kernel argument, i.e. scalar registers).
+template <int P, int R>
+__device__ __forceinline__ void tail_blur_r(float* __restrict__ A, float* __restrict__ T, float* __restrict__ B,
+                                            const BlurTaps& taps, int Rn, int Rm, int W, int H,
+                                            float* __restrict__ g, int pitch, bool nxt, float* __restrict__ N,
+                                            float* __restrict__ gn, int wn, int hn, int pn) {
     constexpr int Q = 4;
     const int PA = W + 2 * Rm;
     // row pass (A's halo columns are in place): fma chain from the leftmost
@@ -1822,15 +1934,18 @@ __device__ __forceinline__ void tail_blur(float* __restrict__ A, float* __restri
     for (int i = threadIdx.x; i < H * qw; i += 1024) {
         const int y = i / qw, x0 = (i - y * qw) * Q;
         const float* p = A + y * PA + Rm + x0 - R;
+        float v[Q + 2 * R];
+#pragma unroll
+        for (int j = 0; j < Q + 2 * R; j++) v[j] = p[j];
         float acc[Q];
 #pragma unroll
-        for (int q = 0; q < Q; q++) acc[q] = p[q] * kf[0];
-#pragma unroll 4
+        for (int q = 0; q < Q; q++) acc[q] = v[q] * taps.k[R];
+#pragma unroll
         for (int t = 1; t <= 2 * R; t++) {
-            const float kt = kf[t];
+            const float kt = taps.k[t > R ? t - R : R - t];
 #pragma unroll
             for (int q = 0; q < Q; q++)
-                acc[q] = P == kProfileOpenCV ? __builtin_fmaf(p[q + t], kt, acc[q]) : acc[q] + p[q + t] * kt;
+                acc[q] = P == kProfileOpenCV ? __builtin_fmaf(v[q + t], kt, acc[q]) : acc[q] + v[q + t] * kt;
         }
         float* o = T + (y + Rm) * W + x0;
 #pragma unroll
@@ -1852,25 +1967,28 @@ __device__ __forceinline__ void tail_blur(float* __restrict__ A, float* __restri
     constexpr int par = P == kProfileOpenCV ? 0 : 1;  // nearest 1/2: (2x, 2y) / (2x + 1, 2y + 1)
     for (int i = threadIdx.x; i < W * qh; i += 1024) {
         const int yq = i / W, x = i - yq * W, y0 = yq * Q;
-        const float* p = T + (y0 + Rm) * W + x;  // row y0
+        const float* p = T + (y0 - R + Rm) * W + x;  // window row 0 = image row y0 - R
+        float v[Q + 2 * R];
+#pragma unroll
+        for (int j = 0; j < Q + 2 * R; j++) v[j] = p[j * W];
         float acc[Q];
         if constexpr (P == kProfileOpenCV) {
 #pragma unroll
-            for (int q = 0; q < Q; q++) acc[q] = p[q * W] * kf[R];
-#pragma unroll 4
-            for (int t = 1; t <= R; t++) {
-                const float kt = kf[R + t];
+            for (int q = 0; q < Q; q++) acc[q] = v[q + R] * taps.k[0];
 #pragma unroll
-                for (int q = 0; q < Q; q++) acc[q] = __builtin_fmaf(p[(q + t) * W] + p[(q - t) * W], kt, acc[q]);
+            for (int t = 1; t <= R; t++) {
+                const float kt = taps.k[t];
+#pragma unroll
+                for (int q = 0; q < Q; q++) acc[q] = __builtin_fmaf(v[q + R + t] + v[q + R - t], kt, acc[q]);
             }
         } else {
 #pragma unroll
-            for (int q = 0; q < Q; q++) acc[q] = p[(q - R) * W] * kf[0];
-#pragma unroll 4
-            for (int t = 1; t <= 2 * R; t++) {
-                const float kt = kf[t];
+            for (int q = 0; q < Q; q++) acc[q] = v[q] * taps.k[R];
 #pragma unroll
-                for (int q = 0; q < Q; q++) acc[q] = acc[q] + p[(q - R + t) * W] * kt;
+            for (int t = 1; t <= 2 * R; t++) {
+                const float kt = taps.k[t > R ? t - R : R - t];
+#pragma unroll
+                for (int q = 0; q < Q; q++) acc[q] = acc[q] + v[q + t] * kt;
             }
         }
 #pragma unroll
@@ -1892,16 +2010,35 @@ __device__ __forceinline__ void tail_blur(float* __restrict__ A, float* __restri
     }
 }
 
+// radii of the two profiles' octave blurs (OpenCV 5, 6, 8, 10, 13; imageproc
+// 3, 4, 4, 5, 7) get their own instantiations; others return false (the
+// caller then runs the octave per blur: tail_octave_start checks this)
+__host__ __device__ constexpr bool tail_radius_ok(int R) {
+    return R == 3 || R == 4 || R == 5 || R == 6 || R == 7 || R == 8 || R == 10 || R == 13;
+}
+
+template <int P>
+__device__ __forceinline__ void tail_blur(float* __restrict__ A, float* __restrict__ T, float* __restrict__ B,
+                                          const BlurTaps& taps, int R, int Rn, int Rm, int W, int H,
+                                          float* __restrict__ g, int pitch, bool nxt, float* __restrict__ N,
+                                          float* __restrict__ gn, int wn, int hn, int pn) {
+    switch (R) {
+#define TB(r)                                                                                     \
+    case r:                                                                                       \
+        tail_blur_r<P, r>(A, T, B, taps, Rn, Rm, W, H, g, pitch, nxt, N, gn, wn, hn, pn); \
+        break;
+        TB(3) TB(4) TB(5) TB(6) TB(7) TB(8) TB(10) TB(13)
+#undef TB
+        default:
+            break;
+    }
+}
+
 template <int P>
 __global__ __launch_bounds__(1024) void k_octave_tail(const TailLaunch L) {
     __shared__ float lds[kTailLdsFloats];
-    __shared__ float kf[kImagesPerOctave][2 * kMaxBlurRadius + 1];
     const int tid = threadIdx.x;
     const int b = blockIdx.x;
-    if (tid < (kImagesPerOctave - 1) * 64) {
-        const int s = 1 + tid / 64, t = tid % 64, R = L.r[s];
-        if (t <= 2 * R) kf[s][t] = L.taps[s].k[t > R ? t - R : R - t];
-    }
     int Rm = 0;
     for (int s = 1; s < kImagesPerOctave; s++) Rm = max(Rm, L.r[s]);
     for (int o = L.o0; o < L.n_oct; o++) {
@@ -1945,8 +2082,8 @@ __global__ __launch_bounds__(1024) void k_octave_tail(const TailLaunch L) {
         __syncthreads();
 #pragma unroll 1
         for (int s = 1; s < kImagesPerOctave; s++) {
-            tail_blur<P>(A, T, B, kf[s], L.r[s], s + 1 < kImagesPerOctave ? L.r[s + 1] : 0, Rm, W, H, g + s * plane,
-                         pitch, s == 3 && has_next, N, gn, wn, hn, pn);
+            tail_blur<P>(A, T, B, L.taps[s], L.r[s], s + 1 < kImagesPerOctave ? L.r[s + 1] : 0, Rm, W, H,
+                         g + s * plane, pitch, s == 3 && has_next, N, gn, wn, hn, pn);
             float* t = A;
             A = B;
             B = t;
@@ -1954,7 +2091,12 @@ __global__ __launch_bounds__(1024) void k_octave_tail(const TailLaunch L) {
     }
 }
 
-int tail_octave_start(const int* ow, const int* oh, int n_oct, int rmax) {
+int tail_octave_start(const int* ow, const int* oh, int n_oct, const int* radii) {
+    int rmax = 0;
+    for (int s = 1; s < kImagesPerOctave; s++) {
+        if (!tail_radius_ok(radii[s])) return n_oct;  // no instantiation: per-blur launches
+        rmax = std::max(rmax, radii[s]);
+    }
     for (int o = 0; o < n_oct; o++) {
         // the G_0 hand-over copies <= 4 values per thread: the octave after
         // the first tail octave must have at most 4096 pixels

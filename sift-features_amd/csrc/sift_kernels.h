@@ -100,9 +100,9 @@ struct TailLaunch {
     int r[kImagesPerOctave];
     BlurTaps taps[kImagesPerOctave];
 };
-// first octave that fits the tail kernel (n_oct: none); rmax = the largest
-// blur radius of an octave
-int tail_octave_start(const int* ow, const int* oh, int n_oct, int rmax);
+// first octave that fits the tail kernel (n_oct: none); radii[1..5] = the
+// octave's blur radii
+int tail_octave_start(const int* ow, const int* oh, int n_oct, const int* radii);
 void launch_octave_tail(const TailLaunch& L, hipStream_t st);
 
 // pyramid.hip

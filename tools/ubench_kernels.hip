@@ -477,6 +477,64 @@ void bench_seed_abl(int N) {
     CK(hipFree(dst));
 }
 
+// HBM ceilings on the octave-0 plane geometry (64 x 3840 x 2160 f32):
+// read-only, write-only and copy streams, 16 B per lane, grid-stride
+template <int MODE>  // 0 read (sum), 1 write, 2 copy, 3 copy with NT stores, 4 write NT
+__global__ __launch_bounds__(256) void k_stream(const float4* __restrict__ a, float4* __restrict__ b, size_t n,
+                                                float* sink) {
+    float4 acc = make_float4(0.f, 0.f, 0.f, 0.f);
+    for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < n; i += (size_t)gridDim.x * 256) {
+        if (MODE == 0) {
+            const float4 v = a[i];
+            acc.x += v.x; acc.y += v.y; acc.z += v.z; acc.w += v.w;
+        } else if (MODE == 1) {
+            b[i] = make_float4((float)i, 1.f, 2.f, 3.f);
+        } else if (MODE == 4) {
+            __builtin_nontemporal_store(make_float4((float)i, 1.f, 2.f, 3.f), b + i);
+        } else if (MODE == 2) {
+            b[i] = a[i];
+        } else {
+            __builtin_nontemporal_store(a[i], b + i);
+        }
+    }
+    if (MODE == 0 && acc.x + acc.y + acc.z + acc.w == 12345.f) *sink = 1.f;
+}
+
+template <int MODE>
+float time_stream(const float4* a, float4* b, size_t n, float* sink, int grid) {
+    hipLaunchKernelGGL((k_stream<MODE>), dim3(grid), dim3(256), 0, 0, a, b, n, sink);
+    hipEvent_t e0, e1;
+    CK(hipEventCreate(&e0));
+    CK(hipEventCreate(&e1));
+    CK(hipEventRecord(e0));
+    for (int i = 0; i < 5; i++) hipLaunchKernelGGL((k_stream<MODE>), dim3(grid), dim3(256), 0, 0, a, b, n, sink);
+    CK(hipEventRecord(e1));
+    CK(hipEventSynchronize(e1));
+    float ms;
+    CK(hipEventElapsedTime(&ms, e0, e1));
+    return ms / 5;
+}
+
+void bench_stream(int N) {
+    const size_t n = (size_t)N * 3840 * 2160 / 4;
+    float4 *a, *b;
+    float* sink;
+    CK(hipMalloc(&a, n * 16));
+    CK(hipMalloc(&b, n * 16));
+    CK(hipMalloc(&sink, 4));
+    CK(hipMemset(a, 0, n * 16));
+    const double gb = n * 16 / 1e9;
+    for (int grid : {2048, 8192, 32768}) {
+        const float r = time_stream<0>(a, b, n, sink, grid), w = time_stream<1>(a, b, n, sink, grid),
+                    wn = time_stream<4>(a, b, n, sink, grid), c = time_stream<2>(a, b, n, sink, grid),
+                    cn = time_stream<3>(a, b, n, sink, grid);
+        std::printf("stream %d frames-planes, grid %d: read %.2f TB/s | write %.2f | write nt %.2f | copy %.2f (r+w) | copy nt %.2f\n",
+                    N, grid, gb / r, gb / w, gb / wn, 2 * gb / c, 2 * gb / cn);
+    }
+    CK(hipFree(a));
+    CK(hipFree(b));
+}
+
 int main(int argc, char** argv) {
     const char* mode = argc > 1 ? argv[1] : "all";
     if (!strcmp(mode, "segs")) {
@@ -487,6 +545,10 @@ int main(int argc, char** argv) {
         bench_pair(argc > 2 ? atoi(argv[2]) : 64, 3840, 2160);
         bench_pair(argc > 2 ? atoi(argv[2]) : 64, 1920, 1080);
         bench_pair(argc > 2 ? atoi(argv[2]) : 64, 960, 540);
+        return 0;
+    }
+    if (!strcmp(mode, "stream")) {
+        bench_stream(argc > 2 ? atoi(argv[2]) : 64);
         return 0;
     }
     if (!strcmp(mode, "seedabl")) {
