@@ -115,20 +115,24 @@ __device__ __forceinline__ float dpp_from_right(float v) {  // lane i <- lane i 
 #ifndef SIFT_DETECT_WPE
 #define SIFT_DETECT_WPE 1
 #endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_DETECT_WPE))) void k_detect_rows(const DetectLaunch L) {
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_DETECT_WPE))) void k_detect_rows(const DetectLaunch ML) {
     __shared__ uint64_t lcand[DR_LCAP];
     __shared__ uint32_t lcount, gbase;
+    // this block's octave (block-uniform: a scan of <= 16 block offsets)
+    int oi = 0;
+    while (oi + 1 < ML.n_oct && blockIdx.x >= ML.block0[oi + 1]) oi++;
+    const DetectOctave& L = ML.oct[oi];
     const int W = L.W, H = L.H, pitch = L.pitch;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
     const int nsx = (W + DR_COLS - 1) / DR_COLS, nsy = (L.y_hi - L.y_lo + DR_SH - 1) / DR_SH;
-    const uint32_t g = blockIdx.x * 4 + wave;  // strip index: frame-major, then row band, then column
+    const uint32_t g = (blockIdx.x - ML.block0[oi]) * 4 + wave;  // strip index: frame-major, then row band, then column
     const uint32_t per = (uint32_t)(nsx * nsy);
     const int b = (int)(g / per);
     const uint32_t rem = g - (uint32_t)b * per;
     const int sy = (int)(rem / nsx), sx = (int)(rem % nsx);
     if (tid == 0) lcount = 0;
     __syncthreads();
-    if (b < L.n_img) {
+    if (b < ML.n_img) {
         const float* gb = L.gauss + (size_t)b * L.img_stride;
         const size_t P = (size_t)pitch * H;
         const int x = sx * DR_COLS - 1 + lane;  // this lane's column
@@ -221,14 +225,14 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_DETECT
                 while (ok3) {
                     const int bit = __builtin_ctz(ok3);
                     ok3 &= ok3 - 1;
-                    const uint64_t key = make_key((uint32_t)(L.img_base + b), (uint32_t)L.octave, (uint32_t)(bit + 1),
-                                                  (uint32_t)y, (uint32_t)x);
+                    const uint64_t key = make_key((uint32_t)(ML.img_base + b), (uint32_t)L.octave,
+                                                  (uint32_t)(bit + 1), (uint32_t)y, (uint32_t)x);
                     const uint32_t li = atomicAdd(&lcount, 1u);
                     if (li < DR_LCAP) {
                         lcand[li] = key;
                     } else {
-                        const uint32_t slot = atomicAdd(L.counter, 1u);
-                        if (slot < L.cap) L.cand[slot] = key;
+                        const uint32_t slot = atomicAdd(ML.counter, 1u);
+                        if (slot < ML.cap) ML.cand[slot] = key;
                     }
                 }
             }
@@ -253,18 +257,32 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_DETECT
     __syncthreads();
     const uint32_t nl = lcount < DR_LCAP ? lcount : DR_LCAP;
     if (nl == 0) return;
-    if (tid == 0) gbase = atomicAdd(L.counter, nl);
+    if (tid == 0) gbase = atomicAdd(ML.counter, nl);
     __syncthreads();
     for (uint32_t i = tid; i < nl; i += 256)
-        if (gbase + i < L.cap) L.cand[gbase + i] = lcand[i];
+        if (gbase + i < ML.cap) ML.cand[gbase + i] = lcand[i];
 }
 
-void launch_detect(const DetectLaunch& L, hipStream_t st) {
-    if (L.y_lo < 0 || L.y_hi > L.H || L.y_hi <= L.y_lo) return;
-    const uint32_t strips =
-        (uint32_t)((L.W + DR_COLS - 1) / DR_COLS) * ((L.y_hi - L.y_lo + DR_SH - 1) / DR_SH) * L.n_img;
-    if (strips == 0) return;
-    hipLaunchKernelGGL(k_detect_rows, dim3((strips + 3) / 4), dim3(256), 0, st, L);
+void launch_detect(DetectLaunch& L, hipStream_t st) {
+    // drop empty octaves, then lay the octaves' blocks end to end
+    int k = 0;
+    for (int i = 0; i < L.n_oct; i++) {
+        const DetectOctave& d = L.oct[i];
+        if (d.y_lo < 0 || d.y_hi > d.H || d.y_hi <= d.y_lo) continue;
+        L.oct[k++] = d;
+    }
+    L.n_oct = k;
+    uint32_t nb = 0;
+    for (int i = 0; i < k; i++) {
+        const DetectOctave& d = L.oct[i];
+        L.block0[i] = nb;
+        const uint32_t strips =
+            (uint32_t)((d.W + DR_COLS - 1) / DR_COLS) * ((d.y_hi - d.y_lo + DR_SH - 1) / DR_SH) * L.n_img;
+        nb += (strips + 3) / 4;
+    }
+    L.block0[k] = nb;
+    if (nb == 0) return;
+    hipLaunchKernelGGL(k_detect_rows, dim3(nb), dim3(256), 0, st, L);
 }
 
 // ---------------------------------------------------------------------------

@@ -408,6 +408,7 @@ struct Slot {
     hipEvent_t ev[7] = {};   // stage boundaries on the compute stream (ev[6] = chunk done)
     hipEvent_t copied = {};  // results copied to the host (copy stream)
     bool pending_copy = false;
+    bool detected = false;  // this chunk's detection is enqueued (stage overlap: inside the pyramid)
     uint32_t m = 0, frame_base = 0, cap_frames = 0;
     uint32_t bc = 0, be = 0, bk = 0;  // candidate / extremum / keypoint bounds used by this chunk
     // detection / description buffers of this slot's lane (the slot's chunks
@@ -446,6 +447,7 @@ struct sift_mi_ctx {
     hipStream_t aux[2] = {};       // per lane: blurs 4, 5 of each octave beside the next octave
     hipEvent_t oct_ev[2][kTailMaxOct + 1] = {};  // per lane: octave o's G_3 done / aux joined
     int oct_overlap = 1;           // SIFT_MI_OCT_OVERLAP=0: one stream per lane (A/B, tests)
+    int stage_overlap = 1;         // SIFT_MI_STAGE_OVERLAP=0: detection after the whole pyramid
     hipEvent_t fork = nullptr;     // orders lane 1 after / before the caller's stream
     int lanes = 2;                 // pipeline lanes (sift_mi_set_pipeline_lanes)
     uint32_t chunk_override = 0;
@@ -651,6 +653,11 @@ int ensure_plan(sift_mi_ctx* c, uint32_t w, uint32_t h, uint32_t chunk) {
     return ensure_lane(c, 0);
 }
 
+// Detection of octaves [o0, o1) of slot si's chunk of m frames: one
+// multi-octave k_detect_rows launch (candidates into the slot's buffer,
+// bounded by S.bc).
+int launch_detection(sift_mi_ctx* c, int si, uint32_t m, int o0, int o1, hipStream_t st);
+
 // Row bands with a restricted pyramid: rows a refined keypoint may drift from
 // its detection row and still be exact without a re-run, and the rows its
 // orientation / descriptor patch reaches (radius <= 16 / 39, plus the
@@ -664,10 +671,14 @@ constexpr int kBandDrift = 24, kBandPatch = 41;
 // path writes G_0..G_5 only: detection and refinement form D_s = G_{s+1} - G_s
 // where they read it (detect.hip), 16 B per octave pixel less than writing
 // the DoG planes and reading them back.
+// detect_slot >= 0 (stage overlap): the detection of the chunk in that slot
+// is launched from here -- the octaves before the tail on the aux stream right
+// after their last blur, beside the tail kernel; the tail octaves after it.
 int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_pitch, size_t row_stride,
-                uint32_t n, bool full) {
+                uint32_t n, bool full, int detect_slot = -1) {
     Plan& p = c->plan;
     hipStream_t st = lane_stream(c, lane);
+    const int slot = lane;
     lane = arena_of(c, lane);
     // seed: u8 -> 2x bilinear -> blur, fused, -> plane 0 of octave 0
     SeedLaunch S{};
@@ -835,7 +846,14 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
                 launch_dog(p.gauss(o, lane), p.P[o], p.gstride(o), p.dog(o, lane), p.dstride(o), p.ow[o], p.oh[o],
                            p.opitch[o], (int)n, st);
     }
-    if (overlap && o_tail > 0) {  // join: the aux stream's blurs before the keypoint stages
+    (void)slot;
+    if (detect_slot >= 0) {
+        // stage overlap: octaves [0, o_tail) are complete once the aux stream's
+        // last blur is done -- their detection runs there beside the tail
+        CHK(launch_detection(c, detect_slot, n, 0, o_tail, overlap && o_tail > 0 ? c->aux[lane] : st));
+        CHK(launch_detection(c, detect_slot, n, o_tail, p.n_oct, st));
+    }
+    if (overlap && o_tail > 0) {  // join: the aux stream's work before the keypoint stages
         HIPCHK(hipEventRecord(c->oct_ev[lane][kTailMaxOct], c->aux[lane]));
         HIPCHK(hipStreamWaitEvent(st, c->oct_ev[lane][kTailMaxOct], 0));
     }
@@ -922,8 +940,9 @@ int img_bits_for(uint32_t m) {
     return b;
 }
 
-int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_t frame_base, const Bounds& B) {
-    Plan& p = c->plan;
+// Per-chunk state and zeroed counters of slot si, before any of its kernels
+// (detection may start inside the pyramid: stage overlap).
+int prepare_chunk(sift_mi_ctx* c, int si, uint32_t m, uint32_t frame_base, const Bounds& B) {
     Slot& S = c->slot[si];
     hipStream_t st = lane_stream(c, si);
     S.m = m;
@@ -932,34 +951,58 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
     S.bc = B.bc;
     S.be = B.be;
     S.bk = B.bk;
+    S.detected = false;
+    uint32_t* cnt = S.counters.p;
+    HIPCHK(hipMemsetAsync(cnt, 0, 4 * sizeof(uint32_t), st));
+    HIPCHK(hipMemsetAsync(cnt + 4 + 2 * m, 0, kDescWorkWords * sizeof(uint32_t), st));  // descriptor work queues
+    HIPCHK(hipMemsetAsync(cnt + 4, 0xff, m * sizeof(uint32_t), st));                   // frame starts
+    return 0;
+}
+
+int launch_detection(sift_mi_ctx* c, int si, uint32_t m, int o0, int o1, hipStream_t st) {
+    Plan& p = c->plan;
+    Slot& S = c->slot[si];
+    DetectLaunch D{};
+    D.n_img = (int)m;
+    D.img_base = 0;
+    D.cand = S.cand.p;
+    D.counter = S.counters.p + 0;
+    D.cap = S.bc;
+    int k = 0;
+    for (int o = o0; o < o1; o++) {
+        if (p.oh[o] < 2 * kImageBorder || p.ow[o] < 2 * kImageBorder) continue;  // src/lib.rs:315
+        DetectOctave& d = D.oct[k++];
+        d.gauss = p.gauss(o, arena_of(c, si));
+        d.img_stride = p.gstride(o);
+        d.W = p.ow[o];
+        d.H = p.oh[o];
+        d.pitch = p.opitch[o];
+        d.octave = o;
+        // row band: octave rows [H*r/n, H*(r+1)/n) -- the bands of one
+        // octave partition its rows, so every candidate (keyed by its
+        // initial octave, scale, y, x) belongs to exactly one band
+        d.y_lo = (int)((uint64_t)p.oh[o] * c->band_r / c->band_n);
+        d.y_hi = (int)((uint64_t)p.oh[o] * (c->band_r + 1) / c->band_n);
+    }
+    D.n_oct = k;
+    if (k) launch_detect(D, st);
+    S.detected = true;
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_t frame_base, const Bounds& B) {
+    Plan& p = c->plan;
+    Slot& S = c->slot[si];
+    hipStream_t st = lane_stream(c, si);
+    (void)frame_base;
     uint32_t* cnt = S.counters.p;
     uint32_t* starts = cnt + 4;
     uint32_t* out_cnt = cnt + 4 + m;
     uint32_t* work = cnt + 4 + 2 * m;  // descriptor work queues
-    HIPCHK(hipMemsetAsync(cnt, 0, 4 * sizeof(uint32_t), st));
-    HIPCHK(hipMemsetAsync(work, 0, kDescWorkWords * sizeof(uint32_t), st));
-    HIPCHK(hipMemsetAsync(starts, 0xff, m * sizeof(uint32_t), st));
-    for (int o = 0; o < p.n_oct; o++) {
-        if (p.oh[o] < 2 * kImageBorder || p.ow[o] < 2 * kImageBorder) continue;  // src/lib.rs:315
-        DetectLaunch D{};
-        D.gauss = p.gauss(o, arena_of(c, si));
-        D.img_stride = p.gstride(o);
-        D.W = p.ow[o];
-        D.H = p.oh[o];
-        D.pitch = p.opitch[o];
-        D.octave = o;
-        D.n_img = (int)m;
-        D.img_base = 0;
-        // row band: octave rows [H*r/n, H*(r+1)/n) -- the bands of one
-        // octave partition its rows, so every candidate (keyed by its
-        // initial octave, scale, y, x) belongs to exactly one band
-        D.y_lo = (int)((uint64_t)p.oh[o] * c->band_r / c->band_n);
-        D.y_hi = (int)((uint64_t)p.oh[o] * (c->band_r + 1) / c->band_n);
-        D.cand = S.cand.p;
-        D.counter = cnt + 0;
-        D.cap = B.bc;
-        launch_detect(D, st);
-    }
+    (void)starts;
+    (void)work;
+    if (!S.detected) CHK(launch_detection(c, si, m, 0, p.n_oct, st));
     RefineLaunch R{};
     R.cand = S.cand.p;
     R.n_cand = cnt + 0;
@@ -1084,7 +1127,12 @@ int enqueue_chunk(sift_mi_ctx* c, int si, const uint8_t* d_frames, size_t frame_
     CHK(reserve_chunk(c, si, B, c->plan.chunk));
     hipStream_t st = lane_stream(c, si);
     HIPCHK(hipEventRecord(S.ev[0], st));
-    if (pyramid) CHK(run_pyramid(c, si, d_frames, frame_pitch, stride, m, false));
+    CHK(prepare_chunk(c, si, m, frame_base, B));
+    // stage overlap (two-lane mode; the one-lane mode times the stages apart):
+    // detection starts inside the pyramid (run_pyramid), so ev[1]..ev[2] is
+    // then only the refinement
+    const bool fused = pyramid && c->lanes == 2 && c->stage_overlap;
+    if (pyramid) CHK(run_pyramid(c, si, d_frames, frame_pitch, stride, m, false, fused ? si : -1));
     HIPCHK(hipEventRecord(S.ev[1], st));
     return enqueue_keypoints(c, si, m, limit, frame_base, B);
 }
@@ -1355,6 +1403,7 @@ int sift_mi_create(int device_ordinal, sift_mi_profile profile, sift_mi_ctx** ou
     for (auto& lane : c->oct_ev)
         for (auto& e : lane) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
     if (const char* e = getenv("SIFT_MI_OCT_OVERLAP")) c->oct_overlap = strcmp(e, "0") != 0;
+    if (const char* e = getenv("SIFT_MI_STAGE_OVERLAP")) c->stage_overlap = strcmp(e, "0") != 0;
     for (auto& S : c->slot) {
         for (auto& e : S.ev) ok = ok && hipEventCreate(&e) == hipSuccess;
         ok = ok && hipEventCreateWithFlags(&S.copied, hipEventDisableTiming) == hipSuccess;

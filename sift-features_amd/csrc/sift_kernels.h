@@ -124,16 +124,24 @@ void launch_resize_nearest_f32(const float* src, int sw, const int* xofs, const 
                                hipStream_t st);
 
 // detect.hip
-struct DetectLaunch {
+// One launch over several octaves: octave i's strips take the blocks
+// [block0[i], block0[i + 1]).
+struct DetectOctave {
     const float* gauss;  // octave G_0 base, image b at gauss + b*img_stride, plane s at + s*pitch*H
     size_t img_stride;   // (the DoG planes are formed from G_0..G_5 as they are read)
-    int W, H, pitch, octave, n_img, img_base;
+    int W, H, pitch, octave;
     int y_lo, y_hi;  // candidate rows [y_lo, y_hi) (a row band; 0, H for the whole octave)
+};
+struct DetectLaunch {
+    DetectOctave oct[kTailMaxOct];
+    uint32_t block0[kTailMaxOct + 1];
+    int n_oct, n_img, img_base;
     uint64_t* cand;  // packed candidate keys (frame, octave, scale, y, x)
     uint32_t* counter;
     uint32_t cap;
 };
-void launch_detect(const DetectLaunch& L, hipStream_t st);
+// octaves L.oct[0 .. n_oct) (block0 is filled here)
+void launch_detect(DetectLaunch& L, hipStream_t st);
 
 // Stage sizes live in device counters (no host round trip between stages):
 // every consumer reads its count from device memory, clamps it to the buffer

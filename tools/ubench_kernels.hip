@@ -490,11 +490,11 @@ __global__ __launch_bounds__(256) void k_stream(const float4* __restrict__ a, fl
         } else if (MODE == 1) {
             b[i] = make_float4((float)i, 1.f, 2.f, 3.f);
         } else if (MODE == 4) {
-            __builtin_nontemporal_store(make_float4((float)i, 1.f, 2.f, 3.f), b + i);
+            __builtin_nontemporal_store(f4v{(float)i, 1.f, 2.f, 3.f}, reinterpret_cast<f4v*>(b + i));
         } else if (MODE == 2) {
             b[i] = a[i];
         } else {
-            __builtin_nontemporal_store(a[i], b + i);
+            __builtin_nontemporal_store(reinterpret_cast<const f4v*>(a)[i], reinterpret_cast<f4v*>(b + i));
         }
     }
     if (MODE == 0 && acc.x + acc.y + acc.z + acc.w == 12345.f) *sink = 1.f;
