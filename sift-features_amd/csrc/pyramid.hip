@@ -1384,26 +1384,38 @@ __global__ __launch_bounds__(256, StripGeom<R>::MINB) void k_seed_strip(const ui
         seed_axis(strip_index<kProfileOpenCV>(g, H), H, sh, sy0, b0, b1, two);
         sy1 = min(sy0 + 1, sh - 1);
     };
+    // interior chunk (uniform): window rows g0 .. g0 + 31 in [1, H - 2] and
+    // g0 odd -- every pair (g, g + 1) reads source rows (g - 1) / 2 and the
+    // next with coefficients (0.75, 0.25) / (0.25, 0.75), no table path
+    auto rows_in = [&](int g0) { return g0 >= 1 && g0 + G::S <= H - 1 && (g0 & 1) != 0; };
     auto prefetch = [&](int g0) {
         if constexpr ((ABL & 2) != 0) return;
         if (!act) return;
         const int g = g0 + 2 * pr;
-        int a0, a1, c0_, c1_;
-        float f0, f1;
-        rows_of(g, a0, a1, f0, f1);
-        rows_of(g + 1, c0_, c1_, f0, f1);
-        pbase = min(a0, c0_);
-        const int nrows = max(a1, c1_) - pbase + 1;  // 2 in the interior, <= 3
+        int nrows = 2;
+        if (rows_in(g0)) {
+            pbase = (g - 1) >> 1;
+        } else {
+            int a0, a1, c0_, c1_;
+            float f0, f1;
+            rows_of(g, a0, a1, f0, f1);
+            rows_of(g + 1, c0_, c1_, f0, f1);
+            pbase = min(a0, c0_);
+            nrows = max(a1, c1_) - pbase + 1;  // <= 3
+        }
         psh = 0;
+        (void)need;
 #pragma unroll
         for (int r = 0; r < 3; r++) {
-            if (r < nrows) {
+            if (r < 2 || r < nrows) {
+                // the three dwords from the one holding the first byte: the
+                // buffer returns 0 for any past the frame's end
                 const uint32_t off = boff + (uint32_t)(pbase + r) * (uint32_t)row_stride + (uint32_t)smin;
-                const uint32_t sa = off & 3u, o4 = off & ~3u;
+                const uint32_t o4 = off & ~3u;
                 pw[r][0] = __builtin_amdgcn_raw_buffer_load_b32(rs, o4, 0, 0);
-                pw[r][1] = (int)sa + need > 4 ? __builtin_amdgcn_raw_buffer_load_b32(rs, o4 + 4u, 0, 0) : 0u;
-                pw[r][2] = (int)sa + need > 8 ? __builtin_amdgcn_raw_buffer_load_b32(rs, o4 + 8u, 0, 0) : 0u;
-                psh |= sa << (2 * r);
+                pw[r][1] = __builtin_amdgcn_raw_buffer_load_b32(rs, o4 + 4u, 0, 0);
+                pw[r][2] = __builtin_amdgcn_raw_buffer_load_b32(rs, o4 + 8u, 0, 0);
+                psh |= (off & 3u) << (2 * r);
             }
         }
     };
@@ -1457,15 +1469,26 @@ __global__ __launch_bounds__(256, StripGeom<R>::MINB) void k_seed_strip(const ui
         }
         int sy[2][2];
         float b[2][2];
-        rows_of(g, sy[0][0], sy[0][1], b[0][0], b[0][1]);
-        rows_of(g + 1, sy[1][0], sy[1][1], b[1][0], b[1][1]);
+        const bool rin = rows_in(g0);
+        if (rin) {
+            sy[0][0] = sy[1][0] = pbase;
+            sy[0][1] = sy[1][1] = pbase + 1;
+            b[0][0] = 0.75f;  // g odd
+            b[0][1] = 0.25f;
+            b[1][0] = 0.25f;  // g + 1 even
+            b[1][1] = 0.75f;
+        } else {
+            rows_of(g, sy[0][0], sy[0][1], b[0][0], b[0][1]);
+            rows_of(g + 1, sy[1][0], sy[1][1], b[1][0], b[1][1]);
+        }
         float h0[CW], h1[CW];
         hres(pw[0], psh & 3u, h0);
         hres(pw[1], (psh >> 2) & 3u, h1);
         // wave-uniform: every pair of the wave on two source rows (all but the
         // first / last chunks of a frame)
-        const bool two_rows = __builtin_amdgcn_ballot_w64(act && !(sy[0][0] == pbase && sy[1][0] == pbase &&
-                                                                  sy[0][1] == pbase + 1 && sy[1][1] == pbase + 1)) == 0;
+        const bool two_rows =
+            rin || __builtin_amdgcn_ballot_w64(act && !(sy[0][0] == pbase && sy[1][0] == pbase &&
+                                                       sy[0][1] == pbase + 1 && sy[1][1] == pbase + 1)) == 0;
 #pragma unroll
         for (int r = 0; r < 2; r++) {
             float v[CW];
