@@ -653,10 +653,10 @@ int ensure_plan(sift_mi_ctx* c, uint32_t w, uint32_t h, uint32_t chunk) {
     return ensure_lane(c, 0);
 }
 
-// Detection of octaves [o0, o1) of slot si's chunk of m frames: one
-// multi-octave k_detect_rows launch (candidates into the slot's buffer,
+// Detection of octaves [o0, o1) of frames [f0, f0 + nf) of slot si's chunk:
+// one multi-octave k_detect_rows launch (candidates into the slot's buffer,
 // bounded by S.bc).
-int launch_detection(sift_mi_ctx* c, int si, uint32_t m, int o0, int o1, hipStream_t st);
+int launch_detection(sift_mi_ctx* c, int si, uint32_t f0, uint32_t nf, int o0, int o1, hipStream_t st);
 
 // Row bands with a restricted pyramid: rows a refined keypoint may drift from
 // its detection row and still be exact without a re-run, and the rows its
@@ -671,32 +671,20 @@ constexpr int kBandDrift = 24, kBandPatch = 41;
 // path writes G_0..G_5 only: detection and refinement form D_s = G_{s+1} - G_s
 // where they read it (detect.hip), 16 B per octave pixel less than writing
 // the DoG planes and reading them back.
+// Octave overlap: octave o + 1 needs only G_3 of octave o (its G_0 is
+// written by blur 3), so blurs 4, 5 of each octave run on the lane's aux
+// stream beside the next octave's blurs (SIFT_MI_OCT_OVERLAP=0: off).  Tried
+// and measured slower or no faster (round 3): the chunk's
+// frames split in two halves on the two streams; seed + octave 0 in
+// sub-batches of 2-32 frames for Infinity Cache reuse; a second aux stream.
 // detect_slot >= 0 (stage overlap): the detection of the chunk in that slot
-// is launched from here -- the octaves before the tail on the aux stream right
-// after their last blur, beside the tail kernel; the tail octaves after it.
+// is launched from here, each part's octaves as soon as their blurs are done.
 int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_pitch, size_t row_stride,
                 uint32_t n, bool full, int detect_slot = -1) {
     Plan& p = c->plan;
     hipStream_t st = lane_stream(c, lane);
-    const int slot = lane;
     lane = arena_of(c, lane);
-    // seed: u8 -> 2x bilinear -> blur, fused, -> plane 0 of octave 0
-    SeedLaunch S{};
-    S.frames = d_frames;
-    S.frame_pitch = frame_pitch;
-    S.row_stride = row_stride;
-    S.sh = (int)p.h;
-    S.sw = (int)p.w;
-    S.tab = p.seed_tab.tab;
-    S.iptab = p.seed_iptab.tab();
-    S.profile = p.profile;
-    S.dst = p.gauss(0, lane);
-    S.dst_img_stride = p.gstride(0);
-    S.W = p.ow[0];
-    S.H = p.oh[0];
-    S.pitch = p.opitch[0];
-    S.n_img = (int)n;
-    S.taps = p.seed_taps;
+    hipStream_t aux = c->aux[lane];
     // row bands (sift_mi_set_row_band): the rows of every Gaussian the band's
     // keypoint stages read, propagated back through the blur chain and the
     // octave downsampling.  Detection covers octave rows [H*r/n, H*(r+1)/n);
@@ -706,6 +694,7 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
     // the whole pyramid.
     std::vector<int> rlo((size_t)p.n_oct * kImagesPerOctave, 0), rhi((size_t)p.n_oct * kImagesPerOctave, 0);
     c->band_restricted = c->band_n > 1 && !full && !c->band_whole && p.profile == (int)SIFT_MI_PROFILE_OPENCV;
+    int seed_y0 = 0, seed_y1 = 0;
     if (c->band_restricted) {
         int need_lo = 0, need_hi = 0;  // octave o + 1's G_0 rows, in octave o + 1 coordinates
         for (int o = p.n_oct - 1; o >= 0; o--) {
@@ -732,11 +721,9 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
             need_lo = lo[0];
             need_hi = hi[0];
         }
-        S.y0 = rlo[0];
-        S.y1 = std::max(rhi[0], rlo[0] + 1);
+        seed_y0 = rlo[0];
+        seed_y1 = std::max(rhi[0], rlo[0] + 1);
     }
-    if (launch_seed(p.seed_r, S, st)) return fail(SIFT_MI_EUNSUPPORTED, "seed blur radius");
-    uint64_t launches = 1;
     // the small octaves from o_tail on: one k_octave_tail launch
     // (SIFT_MI_TAIL=0: per-blur launches for every octave; A/B and test knob)
     int o_tail = p.n_oct;
@@ -750,7 +737,7 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
         // the same yardstick over the rows this band computes: 4 B per pixel
         // of each of its 6 Gaussian rows and 5 DoG rows, plus the input rows
         // the seed reads; the tail launch computes its octaves whole
-        double b = (double)p.w * std::min<int>((int)p.h, (S.y1 - S.y0 + 1) / 2 + 2);
+        double b = (double)p.w * std::min<int>((int)p.h, (seed_y1 - seed_y0 + 1) / 2 + 2);
         for (int o = 0; o < p.n_oct; o++) {
             double rows = 0;
             for (int s = 0; s < kImagesPerOctave; s++) {
@@ -763,100 +750,132 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
         }
         bytes = (uint64_t)b;
     }
-    const bool overlap = c->oct_overlap && p.n_oct <= kTailMaxOct;
-    for (int o = 0; o < o_tail; o++) {
-        float* G = p.gauss(o, lane);
-        float* D = p.dog(o, lane);
-        const size_t P = p.P[o];
-        auto blur_launch = [&](int s) {
-            BlurLaunch B{};
-            B.src = G + (size_t)(s - 1) * P;
-            B.src_img_stride = p.gstride(o);
-            B.dst = G + (size_t)s * P;
-            B.dst_img_stride = p.gstride(o);
-            if (s == 3 && o + 1 < p.n_oct) {
-                B.nxt = p.gauss(o + 1, lane);
-                B.nxt_img_stride = p.gstride(o + 1);
-                B.pitch_n = p.opitch[o + 1];
-                B.wn = p.ow[o + 1];
-                B.hn = p.oh[o + 1];
-            }
-            B.W = p.ow[o];
-            B.H = p.oh[o];
-            B.pitch = p.opitch[o];
-            B.n_img = (int)n;
-            B.taps = p.oct_taps[s];
-            B.profile = p.profile;
-            if (c->band_restricted) {
-                B.y0 = rlo[(size_t)o * kImagesPerOctave + s];
-                B.y1 = std::max(rhi[(size_t)o * kImagesPerOctave + s], B.y0 + 1);
-            }
-            return B;
-        };
-        // octave o + 1 needs only G_3 of octave o (its G_0 is written by blur
-        // 3), so blurs 4, 5 (and the DoG planes of precompute_images) run on
-        // the aux stream beside the next octave's blurs: every launch's tail
-        // and the small octaves' short launches share the chip with the
-        // other stream's work instead of leaving it idle
-        hipStream_t s45 = st;
-        for (int s = 1; s < kImagesPerOctave; s++) {
-            if (s == 4 && overlap) {
-                HIPCHK(hipEventRecord(c->oct_ev[lane][o], st));
-                HIPCHK(hipStreamWaitEvent(c->aux[lane], c->oct_ev[lane][o], 0));
-                s45 = c->aux[lane];
-            }
-            const BlurLaunch B = blur_launch(s);
-            // G_1, G_2 in one pass where the pair kernel applies (k_blur2_strip:
-            // G_1 never read back from HBM)
-            if (s == 1 && launch_blur_pair(p.oct_r[s], p.oct_r[s + 1], B, blur_launch(s + 1), st) == 0) {
-                launches++;
-                s++;
-                continue;
-            }
-            if (launch_blur(p.oct_r[s], B, s >= 4 ? s45 : st)) return fail(SIFT_MI_EUNSUPPORTED, "octave blur radius");
-            launches++;
-        }
-        // precompute_images: D_s = G_{s+1} - G_s, the same f32 subtraction
-        // the keypoint stages form where they read the DoG
-        if (full) launch_dog(G, P, p.gstride(o), D, p.dstride(o), p.ow[o], p.oh[o], p.opitch[o], (int)n, s45);
-    }
-    if (o_tail < p.n_oct) {
-        // whole octaves (a row band's restricted rows are a subset: rows outside
-        // them depend only on rows outside them, so the exact rows stay exact)
-        TailLaunch T{};
-        for (int o = 0; o < p.n_oct; o++) {
-            T.gauss[o] = p.gauss(o, lane);
-            T.gstride[o] = p.gstride(o);
-            T.ow[o] = p.ow[o];
-            T.oh[o] = p.oh[o];
-            T.pitch[o] = p.opitch[o];
-        }
-        T.o0 = o_tail;
-        T.n_oct = p.n_oct;
-        T.n_img = (int)n;
-        T.profile = p.profile;
-        for (int s = 1; s < kImagesPerOctave; s++) {
-            T.r[s] = p.oct_r[s];
-            T.taps[s] = p.oct_taps[s];
-        }
-        launch_octave_tail(T, st);
+    uint64_t launches = 0;
+    // frames [f0, f0 + nf): seed, octave chain, tail (and their detection) on
+    // stream sm; ov: blurs 4, 5 of each octave on the aux stream
+    auto seed = [&](uint32_t f0, uint32_t nf, hipStream_t sm) -> int {
+        SeedLaunch S{};
+        S.frames = d_frames + (size_t)f0 * frame_pitch;
+        S.frame_pitch = frame_pitch;
+        S.row_stride = row_stride;
+        S.sh = (int)p.h;
+        S.sw = (int)p.w;
+        S.tab = p.seed_tab.tab;
+        S.iptab = p.seed_iptab.tab();
+        S.profile = p.profile;
+        S.dst = p.gauss(0, lane) + (size_t)f0 * p.gstride(0);
+        S.dst_img_stride = p.gstride(0);
+        S.W = p.ow[0];
+        S.H = p.oh[0];
+        S.pitch = p.opitch[0];
+        S.n_img = (int)nf;
+        S.taps = p.seed_taps;
+        S.y0 = seed_y0;
+        S.y1 = seed_y1;
+        if (launch_seed(p.seed_r, S, sm)) return fail(SIFT_MI_EUNSUPPORTED, "seed blur radius");
         launches++;
-        if (full)
-            for (int o = o_tail; o < p.n_oct; o++)
-                launch_dog(p.gauss(o, lane), p.P[o], p.gstride(o), p.dog(o, lane), p.dstride(o), p.ow[o], p.oh[o],
-                           p.opitch[o], (int)n, st);
-    }
-    (void)slot;
-    if (detect_slot >= 0) {
-        // stage overlap: octaves [0, o_tail) are complete once the aux stream's
-        // last blur is done -- their detection runs there beside the tail
-        CHK(launch_detection(c, detect_slot, n, 0, o_tail, overlap && o_tail > 0 ? c->aux[lane] : st));
-        CHK(launch_detection(c, detect_slot, n, o_tail, p.n_oct, st));
-    }
-    if (overlap && o_tail > 0) {  // join: the aux stream's work before the keypoint stages
-        HIPCHK(hipEventRecord(c->oct_ev[lane][kTailMaxOct], c->aux[lane]));
-        HIPCHK(hipStreamWaitEvent(st, c->oct_ev[lane][kTailMaxOct], 0));
-    }
+        return 0;
+    };
+    // octaves [o0, o1) of frames [f0, f0 + nf)
+    auto octaves = [&](uint32_t f0, uint32_t nf, int o0, int o1, hipStream_t sm, bool ov) -> int {
+        hipStream_t s45 = sm;
+        for (int o = o0; o < o1; o++) {
+            float* G = p.gauss(o, lane) + (size_t)f0 * p.gstride(o);
+            float* D = p.dog(o, lane) + (size_t)f0 * p.dstride(o);
+            const size_t P = p.P[o];
+            auto blur_launch = [&](int s) {
+                BlurLaunch B{};
+                B.src = G + (size_t)(s - 1) * P;
+                B.src_img_stride = p.gstride(o);
+                B.dst = G + (size_t)s * P;
+                B.dst_img_stride = p.gstride(o);
+                if (s == 3 && o + 1 < p.n_oct) {
+                    B.nxt = p.gauss(o + 1, lane) + (size_t)f0 * p.gstride(o + 1);
+                    B.nxt_img_stride = p.gstride(o + 1);
+                    B.pitch_n = p.opitch[o + 1];
+                    B.wn = p.ow[o + 1];
+                    B.hn = p.oh[o + 1];
+                }
+                B.W = p.ow[o];
+                B.H = p.oh[o];
+                B.pitch = p.opitch[o];
+                B.n_img = (int)nf;
+                B.taps = p.oct_taps[s];
+                B.profile = p.profile;
+                if (c->band_restricted) {
+                    B.y0 = rlo[(size_t)o * kImagesPerOctave + s];
+                    B.y1 = std::max(rhi[(size_t)o * kImagesPerOctave + s], B.y0 + 1);
+                }
+                return B;
+            };
+            for (int s = 1; s < kImagesPerOctave; s++) {
+                if (s == 4 && ov) {
+                    HIPCHK(hipEventRecord(c->oct_ev[lane][o], sm));
+                    HIPCHK(hipStreamWaitEvent(aux, c->oct_ev[lane][o], 0));
+                    s45 = aux;
+                }
+                const BlurLaunch B = blur_launch(s);
+                // G_1, G_2 in one pass where the pair kernel applies
+                // (k_blur2_strip: G_1 never read back from HBM)
+                if (s == 1 && launch_blur_pair(p.oct_r[s], p.oct_r[s + 1], B, blur_launch(s + 1), sm) == 0) {
+                    launches++;
+                    s++;
+                    continue;
+                }
+                if (launch_blur(p.oct_r[s], B, s >= 4 ? s45 : sm))
+                    return fail(SIFT_MI_EUNSUPPORTED, "octave blur radius");
+                launches++;
+            }
+            // precompute_images: D_s = G_{s+1} - G_s, the same f32 subtraction
+            // the keypoint stages form where they read the DoG
+            if (full) launch_dog(G, P, p.gstride(o), D, p.dstride(o), p.ow[o], p.oh[o], p.opitch[o], (int)nf, s45);
+        }
+        return 0;
+    };
+    auto part = [&](uint32_t f0, uint32_t nf, hipStream_t sm, bool ov) -> int {
+        CHK(seed(f0, nf, sm));
+        CHK(octaves(f0, nf, 0, o_tail, sm, ov));
+        if (o_tail < p.n_oct) {
+            // whole octaves (a row band's restricted rows are a subset: rows
+            // outside them depend only on rows outside them, so the exact rows
+            // stay exact)
+            TailLaunch T{};
+            for (int o = 0; o < p.n_oct; o++) {
+                T.gauss[o] = p.gauss(o, lane) + (size_t)f0 * p.gstride(o);
+                T.gstride[o] = p.gstride(o);
+                T.ow[o] = p.ow[o];
+                T.oh[o] = p.oh[o];
+                T.pitch[o] = p.opitch[o];
+            }
+            T.o0 = o_tail;
+            T.n_oct = p.n_oct;
+            T.n_img = (int)nf;
+            T.profile = p.profile;
+            for (int s = 1; s < kImagesPerOctave; s++) {
+                T.r[s] = p.oct_r[s];
+                T.taps[s] = p.oct_taps[s];
+            }
+            launch_octave_tail(T, sm);
+            launches++;
+            if (full)
+                for (int o = o_tail; o < p.n_oct; o++)
+                    launch_dog(p.gauss(o, lane) + (size_t)f0 * p.gstride(o), p.P[o], p.gstride(o),
+                               p.dog(o, lane) + (size_t)f0 * p.dstride(o), p.dstride(o), p.ow[o], p.oh[o],
+                               p.opitch[o], (int)nf, sm);
+        }
+        if (detect_slot >= 0) {
+            // octaves [0, o_tail) are complete once their last blur is done:
+            // with ov their detection runs on the aux stream beside the tail
+            CHK(launch_detection(c, detect_slot, f0, nf, 0, o_tail, ov && o_tail > 0 ? aux : sm));
+            CHK(launch_detection(c, detect_slot, f0, nf, o_tail, p.n_oct, sm));
+        }
+        if (ov && o_tail > 0) {  // join: the aux stream's work before what follows on sm
+            HIPCHK(hipEventRecord(c->oct_ev[lane][kTailMaxOct], aux));
+            HIPCHK(hipStreamWaitEvent(sm, c->oct_ev[lane][kTailMaxOct], 0));
+        }
+        return 0;
+    };
+    CHK(part(0, n, st, c->oct_overlap && p.n_oct <= kTailMaxOct));
     HIPCHK(hipGetLastError());
     c->stats.pyramid_launches += launches;
     c->stats.pyramid_bytes += bytes * n;
@@ -959,12 +978,12 @@ int prepare_chunk(sift_mi_ctx* c, int si, uint32_t m, uint32_t frame_base, const
     return 0;
 }
 
-int launch_detection(sift_mi_ctx* c, int si, uint32_t m, int o0, int o1, hipStream_t st) {
+int launch_detection(sift_mi_ctx* c, int si, uint32_t f0, uint32_t nf, int o0, int o1, hipStream_t st) {
     Plan& p = c->plan;
     Slot& S = c->slot[si];
     DetectLaunch D{};
-    D.n_img = (int)m;
-    D.img_base = 0;
+    D.n_img = (int)nf;
+    D.img_base = (int)f0;  // frame index within the chunk (emission keys)
     D.cand = S.cand.p;
     D.counter = S.counters.p + 0;
     D.cap = S.bc;
@@ -972,7 +991,7 @@ int launch_detection(sift_mi_ctx* c, int si, uint32_t m, int o0, int o1, hipStre
     for (int o = o0; o < o1; o++) {
         if (p.oh[o] < 2 * kImageBorder || p.ow[o] < 2 * kImageBorder) continue;  // src/lib.rs:315
         DetectOctave& d = D.oct[k++];
-        d.gauss = p.gauss(o, arena_of(c, si));
+        d.gauss = p.gauss(o, arena_of(c, si)) + (size_t)f0 * p.gstride(o);
         d.img_stride = p.gstride(o);
         d.W = p.ow[o];
         d.H = p.oh[o];
@@ -1002,7 +1021,7 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
     uint32_t* work = cnt + 4 + 2 * m;  // descriptor work queues
     (void)starts;
     (void)work;
-    if (!S.detected) CHK(launch_detection(c, si, m, 0, p.n_oct, st));
+    if (!S.detected) CHK(launch_detection(c, si, 0, m, 0, p.n_oct, st));
     RefineLaunch R{};
     R.cand = S.cand.p;
     R.n_cand = cnt + 0;

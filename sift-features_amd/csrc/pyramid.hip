@@ -419,11 +419,28 @@ __device__ __forceinline__ void strip_store(const float4 (&pre)[G::LPT], float* 
     }
 }
 
+// Row-pass lane map: wave wv filters rows 4 wv .. 4 wv + 3 of each 16-row
+// group, 16 items (8 outputs each) per row; lanes 0-31 rows 0, 1 (A, B),
+// lanes 32-63 rows 2, 3.  An item's reads are float4 slots 2 pq + j of its
+// row, its writes slots 2 pq and 2 pq + 1; the row pitch IWP / 4 is odd, so
+// A's slots and B's have opposite parity.  Per 32 lanes, with k = lane & 3:
+//     lanes   0-3  4-7  8-11  12-15  16-19  20-23  24-27  28-31
+//     row      A    B    A     B      B      A      B      A
+//     pq       k    k   8+k   8+k    4+k    4+k   12+k   12+k
+// ds_read_b128 groups ({0-3,12-15,20-27}, {4-11,16-19,28-31}; banks = slot
+// mod 16) hold 8 A items with pq distinct mod 8 and 8 B items likewise;
+// ds_write_b128 groups (8 contiguous lanes; banks = slot mod 8) hold 4 A and
+// 4 B items with pq distinct mod 4 -> reads and writes conflict-free.
+__device__ __forceinline__ void strip_rowpass_map(int lane, int wv, int& prow, int& pq) {
+    const int idx = (lane >> 2) & 7, k = lane & 3;
+    const int b = (idx & 1) ^ (idx >> 2);
+    prow = wv * 4 + (lane >> 5) * 2 + b;
+    pq = ((idx >> 1) & 1) * 8 + (idx >> 2) * 4 + k;
+}
+
 // Row pass of one chunk, in place: item = (row, 8 consecutive outputs), an FMA
 // chain from the leftmost tap (OpenCV RowFilter) / unfused acc + p * k
-// (imageproc).  Lane -> (row, item) follows the ds_read_b128 lane groups: each
-// 16-lane group reads two adjacent rows x 8 items, whose float4 slots are the
-// even / odd slots of a bank row (IWP / 4 odd) -> conflict-free.
+// (imageproc).  Lane -> (row, item): strip_rowpass_map.
 template <class G, int P>
 __device__ __forceinline__ void strip_rowpass(float* slot, const BlurTaps& taps, int prow, int pq) {
     constexpr int R = G::R;
@@ -580,21 +597,8 @@ __global__ __launch_bounds__(256, (strip_minb<R, NXT>())) void k_blur_strip(
         const int ly = i / G::C4, c4 = i - ly * G::C4;
         voff[j] = (ly * pitch + x0 - G::HWL + 4 * c4) * 4;
     }
-    // row-pass lane map (see strip_rowpass)
-    int prow, pq;
-    {
-        const int l = lane & 31;
-        int g, k;
-        if (l < 4) { g = 0; k = l; }
-        else if (l < 12) { g = 1; k = l - 4; }
-        else if (l < 16) { g = 0; k = l - 8; }
-        else if (l < 20) { g = 1; k = l - 8; }
-        else if (l < 28) { g = 0; k = l - 12; }
-        else { g = 1; k = l - 16; }
-        const int grp = (lane >> 5) * 2 + g;  // rows (grp >> 1) * 2 + (k >> 3), items (grp & 1) * 8 + (k & 7)
-        prow = wv * 4 + (grp >> 1) * 2 + (k >> 3);
-        pq = (grp & 1) * 8 + (k & 7);
-    }
+    int prow, pq;  // row-pass lane map
+    strip_rowpass_map(lane, wv, prow, pq);
     const int nsteps = (ye - ys + G::S - 1) / G::S;
     float4 pre[G::LPT];
     strip_load<R, P>(pre, rs, voff, cols_in, ys - R, x0, W, H, pitch);
@@ -753,20 +757,8 @@ __global__ __launch_bounds__(256, (PairGeom<Ra, Rb>::MINB)) void k_blur2_strip(
         const int ly = i / GA::C4, c4 = i - ly * GA::C4;
         voff[j] = (ly * pitch + xa - GA::HWL + 4 * c4) * 4;
     }
-    int prow, pq;  // row-pass lane map (see strip_rowpass; S = 16: wave w rows 4w .. 4w + 3)
-    {
-        const int l = lane & 31;
-        int g, k;
-        if (l < 4) { g = 0; k = l; }
-        else if (l < 12) { g = 1; k = l - 4; }
-        else if (l < 16) { g = 0; k = l - 8; }
-        else if (l < 20) { g = 1; k = l - 8; }
-        else if (l < 28) { g = 0; k = l - 12; }
-        else { g = 1; k = l - 16; }
-        const int grp = (lane >> 5) * 2 + g;
-        prow = wv * 4 + (grp >> 1) * 2 + (k >> 3);
-        pq = (grp & 1) * 8 + (k & 7);
-    }
+    int prow, pq;  // row-pass lane map
+    strip_rowpass_map(lane, wv, prow, pq);
     // G_s columns outside the image in a B slot row: replaced by their
     // reflect-101 sources (this wave's 4 rows, before its row pass B); only
     // strips at the left / right image border have any
@@ -1041,221 +1033,6 @@ __global__ __launch_bounds__(256) void k_seed(const uint8_t* __restrict__ frames
 }
 
 // ---------------------------------------------------------------------------
-// k_seed_strip: the seed in the strip scheme (StripGeom<5, 16>: 128 columns,
-// 16-row chunks).  Per chunk of 16 window rows, the source bytes it needs
-// (<= 12 rows x 80 columns: an exact 2x upsample reads source floor(g / 2 -
-// 0.25) and the next one) are prefetched one chunk ahead with the chunk's
-// row coefficients; then u8 -> v / 255 into LDS, HResizeLinear per source row
-// (hbuf), VResizeLinear into the chunk slot by the wave that row-filters those
-// rows, and the R = 5 blur exactly as k_blur_strip.  The upsampled image never
-// touches HBM; its bytes are read once per strip.
-// ---------------------------------------------------------------------------
-template <int R>
-struct SeedStrip {
-    using G = StripGeom<R, 16>;
-    static constexpr int SR = G::S / 2 + 4;   // source rows per chunk (<= 11 used)
-    static constexpr int NWD = 20;            // source dwords per row (<= 20 used: 74 columns + alignment)
-    static constexpr int SC = 4 * NWD;
-    static_assert(SR * NWD + G::S <= 256, "one prefetch item per thread: bytes, then the row tables");
-    static_assert(G::IWV <= 2 * SC - 12, "source columns of the window fit the row");
-};
-
-template <int R>
-__global__ __launch_bounds__(256, 4) void k_seed_strip_old(const uint8_t* __restrict__ frames, size_t frame_pitch,
-                                                       size_t row_stride, int sh, int sw, const ResizeTab tab,
-                                                       float* __restrict__ dst, size_t dst_img_stride, int W, int H,
-                                                       int pitch, const BlurTaps taps, int ya, int yb, int seg) {
-    using Q = SeedStrip<R>;
-    using G = typename Q::G;
-    __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
-    __shared__ __attribute__((aligned(16))) float srcf[Q::SR * Q::SC];     // v / 255, columns from a0
-    __shared__ __attribute__((aligned(16))) float hbuf[Q::SR * G::IWV];    // HResizeLinear per source row
-    __shared__ __attribute__((aligned(16))) int txo[G::IWV];               // source column - a0 (< 0: single tap)
-    __shared__ __attribute__((aligned(16))) float txa0[G::IWV], txa1[G::IWV];
-    __shared__ int tyo0[G::S], tyo1[G::S];                                 // source rows - sya of a window row
-    __shared__ float tya0[G::S], tya1[G::S];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const TileId tile = xcd_tile();
-    const int x0 = tile.x * G::TW;
-    const int ys = ya + tile.y * seg, ye = min(yb, ys + seg);
-    if (ys >= ye) return;
-    const size_t b = tile.z;
-    const uint8_t* src = frames + b * frame_pitch;
-    const __amdgpu_buffer_rsrc_t rd =
-        uniform_rsrc(dst + b * dst_img_stride, (uint32_t)H * (uint32_t)pitch * 4u);
-    // source columns of the strip's window (reflect-101 in the 2x image)
-    int sxa, sxb;
-    {
-        int glo, ghi;
-        reflect_range(x0 - G::HWL, G::IWV, W, glo, ghi);
-        sxa = max(glo / 2 - 1, 0);
-        sxb = min(ghi / 2 + 1, sw - 1);
-    }
-    const int a0 = sxa & ~3;  // first source dword
-    const int nwr = (sxb - a0) / 4 + 1;
-    if (tid < G::IWV) {
-        const int g = strip_index<kProfileOpenCV>(x0 - G::HWL + tid, W);
-        const int s0 = tab.xofs[g];
-        txo[tid] = g < tab.xmax ? s0 - a0 : -1 - (s0 - a0);
-        txa0[tid] = tab.xa0[g];
-        txa1[tid] = tab.xa1[g];
-    }
-    // prefetch item of this thread: a source dword (tid < SR * NWD) or a row's coefficients
-    const int pr = tid / Q::NWD, pw = tid - pr * Q::NWD;
-    const int trow = tid - Q::SR * Q::NWD;  // 0 .. S-1: window row of the chunk (tables)
-    uint32_t pv = 0;                        // bytes
-    int py0 = 0, py1 = 0;                   // source rows (absolute)
-    float pb0 = 0.f, pb1 = 0.f;
-    auto chunk_rows = [&](int g0, int& sya, int& nr) {
-        int glo, ghi;
-        reflect_range(g0, G::S, H, glo, ghi);
-        sya = max(glo / 2 - 1, 0);
-        nr = min(ghi / 2 + 1, sh - 1) - sya + 1;
-    };
-    auto prefetch = [&](int g0) {
-        int sya, nr;
-        chunk_rows(g0, sya, nr);
-        if (tid < Q::SR * Q::NWD) {
-            pv = 0;
-            if (pr < nr && pw < nwr) {
-                const int c = a0 + 4 * pw;
-                const uint8_t* p = src + (size_t)(sya + pr) * row_stride + c;
-                if (c + 3 < sw) {
-                    pv = *reinterpret_cast<const uint32_t*>(p);
-                } else {  // row end: bytes only (the dword could run past the frame)
-                    for (int q = 0; q < 4 && c + q < sw; q++) pv |= (uint32_t)p[q] << (8 * q);
-                }
-            }
-        } else if (trow < G::S) {
-            const int g = strip_index<kProfileOpenCV>(g0 + trow, H);
-            py0 = tab.yofs[g];
-            py1 = min(py0 + 1, sh - 1);
-            pb0 = tab.ya0[g];
-            pb1 = tab.ya1[g];
-        }
-    };
-    auto stage = [&](int g0) {  // prefetched chunk -> srcf / row tables
-        int sya, nr;
-        chunk_rows(g0, sya, nr);
-        if (tid < Q::SR * Q::NWD) {
-            if (pr < nr && pw < nwr)
-                *reinterpret_cast<float4*>(srcf + pr * Q::SC + 4 * pw) =
-                    make_float4(u8_unit(pv & 0xff), u8_unit((pv >> 8) & 0xff), u8_unit((pv >> 16) & 0xff),
-                                u8_unit(pv >> 24));
-        } else if (trow < G::S) {
-            tyo0[trow] = py0 - sya;
-            tyo1[trow] = py1 - sya;
-            tya0[trow] = pb0;
-            tya1[trow] = pb1;
-        }
-    };
-    // interior strips (every window column in [1, W - 2]) of the exact 2x
-    // upsample: destination column g reads source (g - 1) >> 1 and the next
-    // one with coefficients (0.25, 0.75) for even g, (0.75, 0.25) for odd g --
-    // exactly the table entries there (cv_linear_coeffs: f = g / 2 - 0.25,
-    // its fraction 0.75 / 0.25), so the table reads drop out and a 4-column
-    // item needs 4 consecutive sources (seed 955 -> 835 us per 64 1080p frames)
-    const bool fastx = x0 - G::HWL >= 1 && x0 + G::TW + G::HWL <= W - 1;
-    auto hres = [&](int g0) {  // HResizeLinear: t = S[sx]*a0 + S[sx+1]*a1 (two roundings + add)
-        int sya, nr;
-        chunk_rows(g0, sya, nr);
-        constexpr int Q4 = G::IWV / 4;
-        if (fastx) {
-            for (int i = tid; i < nr * Q4; i += 256) {
-                const int r = i / Q4, q = i - r * Q4;
-                const float* sr = srcf + r * Q::SC + ((x0 - G::HWL) / 2 + 2 * q - 1 - a0);
-                const float s0 = sr[0], s1 = sr[1], s2 = sr[2], s3 = sr[3];
-                *reinterpret_cast<float4*>(hbuf + r * G::IWV + 4 * q) =
-                    make_float4(s0 * 0.25f + s1 * 0.75f, s1 * 0.75f + s2 * 0.25f, s1 * 0.25f + s2 * 0.75f,
-                                s2 * 0.75f + s3 * 0.25f);
-            }
-            return;
-        }
-        for (int i = tid; i < nr * Q4; i += 256) {
-            const int r = i / Q4, c = (i - r * Q4) * 4;
-            const int4 xo = *reinterpret_cast<const int4*>(txo + c);
-            const float4 w0 = *reinterpret_cast<const float4*>(txa0 + c);
-            const float4 w1 = *reinterpret_cast<const float4*>(txa1 + c);
-            const float* sr = srcf + r * Q::SC;
-            auto h = [&](int o, float u0, float u1) {
-                const bool two = o >= 0;
-                const int sx = two ? o : -1 - o;
-                const float p0 = sr[sx];
-                return two ? p0 * u0 + sr[sx + 1] * u1 : p0;
-            };
-            *reinterpret_cast<float4*>(hbuf + r * G::IWV + c) =
-                make_float4(h(xo.x, w0.x, w1.x), h(xo.y, w0.y, w1.y), h(xo.z, w0.z, w1.z), h(xo.w, w0.w, w1.w));
-        }
-    };
-    // VResizeLinear (S0*b0 + S1*b1) of this wave's 4 window rows into the slot
-    auto vres = [&](float* slot) {
-        constexpr int Q4 = G::IWV / 4;
-        for (int i = lane; i < 4 * Q4; i += 64) {
-            const int ly = wv * 4 + i / Q4, c = (i % Q4) * 4;
-            const float4 u = *reinterpret_cast<const float4*>(hbuf + tyo0[ly] * G::IWV + c);
-            const float4 v = *reinterpret_cast<const float4*>(hbuf + tyo1[ly] * G::IWV + c);
-            const float b0 = tya0[ly], b1 = tya1[ly];
-            *reinterpret_cast<float4*>(slot + ly * G::IWP + c) =
-                make_float4(u.x * b0 + v.x * b1, u.y * b0 + v.y * b1, u.z * b0 + v.z * b1, u.w * b0 + v.w * b1);
-        }
-        // the wave's row pass reads these rows next (in-order LDS within a wave)
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-    };
-    // row-pass lane map (as k_blur_strip; S = 16: one 16-row iteration, wave w rows 4w..4w+3)
-    int prow, pq;
-    {
-        const int l = lane & 31;
-        int g, k;
-        if (l < 4) { g = 0; k = l; }
-        else if (l < 12) { g = 1; k = l - 4; }
-        else if (l < 16) { g = 0; k = l - 8; }
-        else if (l < 20) { g = 1; k = l - 8; }
-        else if (l < 28) { g = 0; k = l - 12; }
-        else { g = 1; k = l - 16; }
-        const int grp = (lane >> 5) * 2 + g;
-        prow = wv * 4 + (grp >> 1) * 2 + (k >> 3);
-        pq = (grp & 1) * 8 + (k & 7);
-    }
-    const int nsteps = (ye - ys + G::S - 1) / G::S;
-    const int gb = ys - R;  // window row of chunk 0
-    prefetch(gb);
-    stage(gb);
-    prefetch(gb + G::S);
-    __syncthreads();
-    hres(gb);
-    __syncthreads();
-    vres(lds);
-    strip_rowpass<G, kProfileOpenCV>(lds, taps, prow, pq);
-    for (int k = 0; k < nsteps; k++) {
-        float* sa = lds + (k & 1) * G::SLOT;
-        float* sb = lds + ((k + 1) & 1) * G::SLOT;
-        const int g1 = gb + (k + 1) * G::S;
-        __syncthreads();  // column pass k - 1 is done with slot b, vres / hres with the tables and hbuf
-        stage(g1);
-        if (k + 2 <= nsteps) prefetch(g1 + G::S);
-        __syncthreads();
-        hres(g1);
-        __syncthreads();
-        vres(sb);
-        strip_rowpass<G, kProfileOpenCV>(sb, taps, prow, pq);
-        __syncthreads();
-        const int y = ys + k * G::S;
-        switch (wv) {
-#define COLPASS(w)                                                                                              \
-    case w:                                                                                                     \
-        strip_colpass<G, kProfileOpenCV, w, false>(sa, sb, taps, lane, y, ye, x0, W, pitch, rd, rd, 0, 0, 0); \
-        break;
-            COLPASS(0) COLPASS(1) COLPASS(2) COLPASS(3)
-            default:
-                __builtin_unreachable();  // wv < 4: no store-free path (static vmcnt)
-#undef COLPASS
-        }
-    }
-}
-
-// ---------------------------------------------------------------------------
 // k_seed_strip: the seed as a strip blur (StripGeom<5>: 128 columns, 32-row
 // chunks, the same row / column passes and barriers as k_blur_strip) whose
 // chunk loader computes the 2x bilinear upsample in registers instead of
@@ -1517,20 +1294,8 @@ __global__ __launch_bounds__(256, StripGeom<R>::MINB) void k_seed_strip(const ui
                 *reinterpret_cast<float4*>(out + r * G::IWP + k) = make_float4(v[k], v[k + 1], v[k + 2], v[k + 3]);
         }
     };
-    int prow, pq;  // row-pass lane map (see strip_rowpass)
-    {
-        const int l = lane & 31;
-        int g, k;
-        if (l < 4) { g = 0; k = l; }
-        else if (l < 12) { g = 1; k = l - 4; }
-        else if (l < 16) { g = 0; k = l - 8; }
-        else if (l < 20) { g = 1; k = l - 8; }
-        else if (l < 28) { g = 0; k = l - 12; }
-        else { g = 1; k = l - 16; }
-        const int grp = (lane >> 5) * 2 + g;
-        prow = wv * 4 + (grp >> 1) * 2 + (k >> 3);
-        pq = (grp & 1) * 8 + (k & 7);
-    }
+    int prow, pq;  // row-pass lane map
+    strip_rowpass_map(lane, wv, prow, pq);
     const int nsteps = (ye - ys + G::S - 1) / G::S;
     const int gb = ys - R;  // window row of chunk 0
     prefetch(gb);
@@ -1881,14 +1646,9 @@ int launch_seed(int R, const SeedLaunch& L, hipStream_t st) {
         const int rows = yb - ya;
         const int seg = strip_segment_rows(rows, (long)strips * L.n_img);
         const int nseg = (rows + seg - 1) / seg;
-        if (getenv("SIFT_MI_SEED_OLD"))
-            hipLaunchKernelGGL((k_seed_strip_old<5>), dim3(strips, (rows + seg - 1) / seg, L.n_img), dim3(256), 0, st,
-                               L.frames, L.frame_pitch, L.row_stride, L.sh, L.sw, L.tab, L.dst, L.dst_img_stride, L.W,
-                               L.H, L.pitch, L.taps, ya, yb, seg);
-        else
-            hipLaunchKernelGGL((k_seed_strip<5>), dim3(strips, nseg, L.n_img), dim3(256), 0, st, L.frames,
-                               L.frame_pitch, L.row_stride, L.sh, L.sw, L.dst, L.dst_img_stride, L.W, L.H, L.pitch,
-                               L.taps, ya, yb, seg);
+        hipLaunchKernelGGL((k_seed_strip<5>), dim3(strips, nseg, L.n_img), dim3(256), 0, st, L.frames,
+                           L.frame_pitch, L.row_stride, L.sh, L.sw, L.dst, L.dst_img_stride, L.W, L.H, L.pitch,
+                           L.taps, ya, yb, seg);
         return 0;
     }
     launch_seed_r<5>(L, st);

@@ -11,6 +11,8 @@ W, H = int(os.environ.get("W", 1920)), int(os.environ.get("H", 1080))
 n = int(os.environ.get("N", 1))
 fr = synth.frames_torch(n, W, H, seed0=1000, device="cuda")
 c = pkg.Context(0, pkg.OpenCVProcessing)
+if os.environ.get("LANES"): c.set_pipeline_lanes(int(os.environ["LANES"]))
+if os.environ.get("CHUNK"): c.set_chunk(int(os.environ["CHUNK"]))
 call = (fr.data_ptr(), n, W, H, fr.stride(1), fr.stride(0))
 def go(): return int(c.sift_batch_device(*call, fetch=False)[0][-1])
 for _ in range(3): go()

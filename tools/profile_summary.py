@@ -84,21 +84,31 @@ for r in rows:
 tot = sum(v[1] for k, v in agg.items() if k.startswith("k_") or "rocprim" in k)
 
 # ---- the serialised stage-timing pass of bench.py (the roofline's HIP-event
-# average): the longest run of consecutive sift kernels on a single stream.
-# Its chunks start at k_seed*; one warmup step precedes the timed steps.
-sk = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Stream_Id"], short(r["Kernel_Name"]))
+# figure): chunks start at k_seed*; a chunk is every kernel started between its
+# seed and the next one, on any stream (the lane's stream and its aux stream:
+# octave overlap, host.cpp run_pyramid).  A chunk is serialised when it starts
+# after the previous chunk's kernels end and ends before the next seed (the
+# one-lane pass; the two-lane pass overlaps neighbour chunks).  One warmup step
+# precedes the timed steps.
+sk = sorted(((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r["Stream_Id"], short(r["Kernel_Name"]),
+              int(r.get("Dispatch_Id") or 0))
              for r in rows if short(r["Kernel_Name"]).startswith("k_") or "rocprim" in r["Kernel_Name"]))
-best, c0 = (0, 0), 0
-for i in range(1, len(sk) + 1):
-    if i == len(sk) or sk[i][2] != sk[c0][2]:
+seeds = [i for i, x in enumerate(sk) if x[3].startswith("k_seed")]
+chunks = [sk[a:z] for a, z in zip(seeds, seeds[1:] + [len(sk)])]
+ser = []
+for i, g in enumerate(chunks):
+    prev_end = max(x[1] for x in chunks[i - 1]) if i else 0
+    nxt = chunks[i + 1][0][0] if i + 1 < len(chunks) else 1 << 62
+    ser.append(prev_end <= g[0][0] and max(x[1] for x in g) <= nxt)
+best, c0 = (0, 0), None
+for i, sflag in enumerate(ser + [False]):
+    if sflag and c0 is None:
+        c0 = i
+    if not sflag and c0 is not None:
         if i - c0 > best[1] - best[0]:
             best = (c0, i)
-        c0 = i
-run = sk[best[0]:best[1]]
-seeds = [i for i, x in enumerate(run) if x[3].startswith("k_seed")]
-groups = []
-for a, z in zip(seeds, seeds[1:] + [len(run)]):
-    groups.append(run[a:z])
+        c0 = None
+groups = chunks[best[0]:best[1]]
 full = max((sum(1 for x in g if x[3].startswith(PYR)) for g in groups), default=0)
 groups = [g for g in groups if sum(1 for x in g if x[3].startswith(PYR)) == full]
 chunks_per_call = max(1, len(groups) // (steps + 1))
@@ -111,17 +121,21 @@ cmax = min(64, max(1, int(32e9 // (44.0 * sum_p))))  # host auto_chunk
 nck = max(-(-FRAMES // cmax), 2 if FRAMES >= 2 else 1)
 chunk = -(-FRAMES // nck)
 
-pos = defaultdict(list)     # launch position in the chunk -> durations (us)
+pos = defaultdict(list)     # launch position in the chunk (enqueue order) -> (start, duration) (us)
 stage = defaultdict(float)  # non-pyramid kernels of the timed chunks (us)
+spans = []                  # pyramid wall time per chunk: seed start -> last pyramid kernel end (us)
 for g in timed:
-    pyr = [x for x in g if x[3].startswith(PYR)]
+    pyr = sorted((x for x in g if x[3].startswith(PYR)), key=lambda x: x[4])
+    t0 = min(x[0] for x in pyr)
+    spans.append((max(x[1] for x in pyr) - t0) / 1e3)
     for j, x in enumerate(pyr):
-        pos[(j, x[3])].append((x[1] - x[0]) / 1e3)
+        pos[(j, x[3], x[2])].append(((x[0] - t0) / 1e3, (x[1] - x[0]) / 1e3))
     for x in g:
         if not x[3].startswith(PYR):
             stage[x[3]] += (x[1] - x[0]) / 1e3
-iso_us = sum(sum(v) for v in pos.values())
+iso_us = sum(spans)
 iso_n = sum(len(v) for v in pos.values())
+busy_us = sum(d for v in pos.values() for _, d in v)
 
 
 def launch_blurs(k):
@@ -216,8 +230,11 @@ with open(out_md, "w") as f:
                 f"{b['ms_per_step']:.2f}, stage_ms_per_step = {json.dumps(b['stage_ms_per_step'])}\n\n")
     f.write("## Pyramid stage (the roofline kernel group: k_seed* + k_blur*)\n\n")
     f.write(f"* trace, serialised stage-timing pass, timed steps: {iso_n} launches "
-            f"({len(timed)} chunks of {chunk} frames, {launches_per_chunk} launches each), "
-            f"{iso_us / max(1, iso_n):.1f} us per launch, {iso_us / max(1, len(timed)) / 1e3:.3f} ms per chunk\n")
+            f"({len(timed)} chunks of {chunk} frames, {launches_per_chunk} launches each on two streams); "
+            f"pyramid wall time (seed start -> last pyramid kernel end) {iso_us / max(1, len(timed)) / 1e3:.3f} ms "
+            f"per chunk = {iso_us / max(1, iso_n):.1f} us per launch (wall / launches: the figure bench.py's "
+            f"roofline divides by); summed kernel durations {busy_us / max(1, len(timed)) / 1e3:.3f} ms per chunk "
+            f"(> wall: launches of the two streams overlap)\n")
     if b:
         f.write(f"* bench.py (HIP events on the compute stream, serialised pass): pyramid_ms per step = "
                 f"{b['stage_ms_per_step']['pyramid_ms']:.3f}, avg launch = {b['roofline']['avg_launch_ms'] * 1e3:.1f} us\n")
@@ -228,14 +245,18 @@ with open(out_md, "w") as f:
                 f"{traffic_pl / 1e6:.1f} MB per launch = {traffic_pf / 1e6:.1f} MB per frame "
                 f"(read {fetch / max(1, n_f) / 1e6:.1f} MB, write {write / max(1, n_w) / 1e6:.1f} MB per launch); "
                 f"traffic / algorithmic = {traffic_pf / algo_pf:.2f}\n")
-    f.write("\n### Per launch position (serialised pass; actual bytes = what the launch must read + write)\n\n")
-    f.write("| pos | octave | blur | kernel | avg us | actual MB | TB/s | share of stage |\n|---|---|---|---|---|---|---|---|\n")
+    f.write("\n### Per launch position (serialised pass, enqueue order; start / end from the chunk's seed start; "
+            "actual bytes = what the launch must read + write; TB/s over the launch's own duration, while "
+            "it shares the chip with the other stream's launches)\n\n")
+    f.write("| pos | octave | blur | kernel | stream | start us | end us | avg us | actual MB | TB/s |\n"
+            "|---|---|---|---|---|---|---|---|---|---|\n")
     items = sorted(pos.items())
-    info = pos_info([k for (j, k), v in items])
-    for ((j, k), v), (o, sl, by) in zip(items, info):
-        us = sum(v) / len(v)
-        f.write(f"| {j} | {o} | {sl} | `{k}` | {us:.1f} | {by / 1e6:.1f} | "
-                f"{by / (us * 1e-6) / 1e12:.2f} | {100 * sum(v) / max(1e-9, iso_us):.1f}% |\n")
+    info = pos_info([k for (j, k, st), v in items])
+    for ((j, k, st), v), (o, sl, by) in zip(items, info):
+        a0 = sum(x[0] for x in v) / len(v)
+        us = sum(x[1] for x in v) / len(v)
+        f.write(f"| {j} | {o} | {sl} | `{k}` | {st} | {a0:.1f} | {a0 + us:.1f} | {us:.1f} | {by / 1e6:.1f} | "
+                f"{by / (us * 1e-6) / 1e12:.2f} |\n")
     if stage:
         f.write("\n### Other stages in the same serialised chunks (ms per chunk)\n\n| kernel | ms |\n|---|---|\n")
         for k, us in sorted(stage.items(), key=lambda kv: -kv[1]):

@@ -321,9 +321,9 @@ void bench_segs(int N) {
 }
 
 
-// seed (u8 -> 2x bilinear -> R = 5 blur): the product launcher's kernel vs
-// SIFT_MI_SEED_OLD (the round-2 LDS-staged strip seed), bit-identical check +
-// time, N frames of sw x sh (row stride `stride` >= sw)
+// seed (u8 -> 2x bilinear -> R = 5 blur): the product launcher's strip kernel
+// vs the tile kernel (SIFT_MI_BLUR_KERNEL=tile), bit-identical check + time,
+// N frames of sw x sh (row stride `stride` >= sw)
 static void cv_linear_tab(int ssz, int dsz, std::vector<int>& ofs, std::vector<float>& a0, std::vector<float>& a1,
                           int* lim) {
     const double scale = 1. / ((double)dsz / ssz);
@@ -405,9 +405,9 @@ void bench_seed(int N, int sw, int sh, int stride) {
     };
     CK(hipMemset(d0, 0, plane * N * 4));
     CK(hipMemset(d1, 0, plane * N * 4));
-    setenv("SIFT_MI_SEED_OLD", "1", 1);
+    setenv("SIFT_MI_BLUR_KERNEL", "tile", 1);
     const float t_old = timeit(d0);
-    unsetenv("SIFT_MI_SEED_OLD");
+    unsetenv("SIFT_MI_BLUR_KERNEL");
     const float t_new = timeit(d1);
     std::vector<float> h0(plane * N), h1(plane * N);
     CK(hipMemcpy(h0.data(), d0, plane * N * 4, hipMemcpyDeviceToHost));
@@ -423,7 +423,7 @@ void bench_seed(int N, int sw, int sh, int stride) {
                 }
             }
     const double bytes = (double)N * (sw * (double)sh + 4.0 * W * H);
-    std::printf("seed %d x %dx%d (stride %d): old %8.1f us %6.2f TB/s | new %8.1f us %6.2f TB/s | differing px %zu",
+    std::printf("seed %d x %dx%d (stride %d): tile %8.1f us %6.2f TB/s | strip %8.1f us %6.2f TB/s | differing px %zu",
                 N, sw, sh, stride, 1e3 * t_old, bytes / (t_old * 1e-3) / 1e12, 1e3 * t_new,
                 bytes / (t_new * 1e-3) / 1e12, diff);
     if (diff) std::printf(" (first at frame %zu y %zu x %zu)", first / plane, (first % plane) / pitch, first % pitch);
