@@ -81,6 +81,10 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
 // each row's first sample), built with wave scans.
 // Optional clip window [xmin, xmax] x [ymin, ymax] (window coordinates): the
 // fast path drops samples outside the image here instead of testing each one.
+// SHRINK (fast path): the up to 3 end columns of each row that fail the fast
+// path's own f32 region test are dropped here rather than enumerated (the
+// per-sample test stays, so this only removes samples it would reject).
+template <bool SHRINK = false>
 __device__ __forceinline__ void build_row_table(int* rowlo, int* rowpre, int radius, float cos_s, float sin_s,
                                                 int lane, int xmin = INT_MIN, int xmax = INT_MAX,
                                                 int ymin = INT_MIN, int ymax = INT_MAX) {
@@ -110,7 +114,21 @@ __device__ __forceinline__ void build_row_table(int* rowlo, int* rowpre, int rad
             } else {
                 empty = empty || !(fabs(yi * c) < 2.5 + 1e-3);
             }
-            const int ilo = (int)floor(lo), ihi = (int)ceil(hi);
+            int ilo = (int)floor(lo), ihi = (int)ceil(hi);
+            if (SHRINK && !empty) {
+                const float fy = (float)(row - radius);
+                auto inside = [&](int xi) {  // describe_wave_fast's test, same f32 operations
+                    const float fx = (float)xi;
+                    const float col_bin = (fx * cos_s - fy * sin_s) + (float)(kDescHist / 2);
+                    const float row_bin = (fx * sin_s + fy * cos_s) + (float)(kDescHist / 2);
+                    return row_bin > -0.5f && row_bin < (float)kDescHist + 0.5f && col_bin > -0.5f &&
+                           col_bin < (float)kDescHist + 0.5f;
+                };
+#pragma unroll
+                for (int k = 0; k < 3; k++) ilo += (ilo <= ihi && !inside(ilo)) ? 1 : 0;
+#pragma unroll
+                for (int k = 0; k < 3; k++) ihi -= (ihi >= ilo && !inside(ihi)) ? 1 : 0;
+            }
             rowlo[row] = ilo;
             cnt[h] = (empty || ihi < ilo) ? 0 : ihi - ilo + 1;
         }
@@ -137,24 +155,48 @@ __device__ __forceinline__ float chunk_sum(float s) {
 // Normalisation (src/lib.rs:951-989) of the 128 interior bins held two per
 // lane (lane l: flat[2l], flat[2l+1]); chunk j = flat[4j..4j+4) = lanes 2j,
 // 2j+1, summed in the reference's exact chunk-of-4 order.
+// Wave sum in DPP tree order (fast path: its bins already differ from the
+// reference's by summation order, and so may the norms)
+__device__ __forceinline__ float wave_tree_sum(float v) {
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x111, 0xf, 0xf, false));  // row_shr:1
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x112, 0xf, 0xf, false));  // row_shr:2
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x114, 0xf, 0xf, false));  // row_shr:4
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x118, 0xf, 0xf, false));  // row_shr:8
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x142, 0xa, 0xf, false));  // row_bcast:15
+    v += __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x143, 0xc, 0xf, false));  // row_bcast:31
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), 63));
+}
+
+// FAST: the L2 sums in DPP tree order (describe_wave_fast); otherwise the
+// reference's chunk-of-4 order (describe_wave_exact)
+template <bool FAST = false>
 __device__ __forceinline__ void describe_normalize(float acc0, float acc1, uint8_t* __restrict__ out, int lane) {
+    float l2, l2c, v0, v1;
+    if constexpr (FAST) {
+        l2 = sqrtf(wave_tree_sum(acc0 * acc0 + acc1 * acc1));
+        const float cap = l2 * 0.2f;
+        v0 = fminf(acc0, cap);
+        v1 = fminf(acc1, cap);
+        l2c = wave_tree_sum(v0 * v0 + v1 * v1);
+    } else {
     const float c_hi0 = __shfl(acc0, (lane + 1) & 63), c_hi1 = __shfl(acc1, (lane + 1) & 63);
     float s = 0.0f;
     s += acc0 * acc0;
     s += acc1 * acc1;
     s += c_hi0 * c_hi0;
     s += c_hi1 * c_hi1;
-    float l2 = chunk_sum(s);
+    l2 = chunk_sum(s);
     l2 = sqrtf(l2);
     const float cap = l2 * 0.2f;
-    const float v0 = fminf(acc0, cap), v1 = fminf(acc1, cap);
+    v0 = fminf(acc0, cap), v1 = fminf(acc1, cap);
     const float d_hi0 = __shfl(v0, (lane + 1) & 63), d_hi1 = __shfl(v1, (lane + 1) & 63);
     s = 0.0f;
     s += v0 * v0;
     s += v1 * v1;
     s += d_hi0 * d_hi0;
     s += d_hi1 * d_hi1;
-    float l2c = chunk_sum(s);
+    l2c = chunk_sum(s);
+    }
     l2c = sqrtf(l2c);
     const float norm = 512.0f / fmaxf(l2c, FLT_EPSILON);
     const int32_t q0 = sat_i32(roundf(v0 * norm)), q1v = sat_i32(roundf(v1 * norm));
@@ -407,7 +449,11 @@ __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img
         if (i + lane < PRIV_STRIDE * NS / 4) reinterpret_cast<float4*>(sc.h)[i + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
     // samples outside the image (0 < y + yi < height - 1, 0 < x + xi < width - 1
     // fails) are not enumerated
-    build_row_table(sc.rowlo, sc.rowpre, radius, cos_s, sin_s, lane, 1 - x, width - 2 - x, 1 - y, height - 2 - y);
+#ifdef SIFT_EXP_NO_SHRINK  // A/B only
+    build_row_table<false>(sc.rowlo, sc.rowpre, radius, cos_s, sin_s, lane, 1 - x, width - 2 - x, 1 - y, height - 2 - y);
+    if (0)
+#endif
+    build_row_table<true>(sc.rowlo, sc.rowpre, radius, cos_s, sin_s, lane, 1 - x, width - 2 - x, 1 - y, height - 2 - y);
     const int total = (kAblate & 64) ? 0 : sc.rowpre[n];  // kAblate bit 6: no samples (per-keypoint overhead)
     if (n_samples) *n_samples += (uint32_t)total;
     // Lane-strided samples: one load instruction touches ~64 neighbouring
@@ -562,7 +608,11 @@ __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img
     }
     if ((lane & 3) == 0) acc0 += acc8;
     if (kAblate & 1) acc0 += sink.x + sink.y;
-    describe_normalize(acc0, acc1, out, lane);
+#ifdef SIFT_EXP_CHUNK_NORM  // A/B only
+    describe_normalize<false>(acc0, acc1, out, lane);
+#else
+    describe_normalize<true>(acc0, acc1, out, lane);
+#endif
 }
 
 // kMode 0: bit-exact (describe_wave_exact); 1 / 2 / 4: fast path with that

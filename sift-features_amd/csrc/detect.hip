@@ -380,6 +380,9 @@ void launch_refine(const RefineLaunch& L, hipStream_t st) {
 constexpr int OR_LDS = 1104;  // >= 33 * 33 samples, a multiple of 16 (16-byte bin reads)
 constexpr int OR_WT = 17 * 18 / 2;  // weight table entries at the largest radius (16)
 
+#ifndef SIFT_ORIENT_SUM_U
+#define SIFT_ORIENT_SUM_U 2  // samples per step of the per-bin sums
+#endif
 #ifndef SIFT_ORIENT_MIN_WAVES
 #define SIFT_ORIENT_MIN_WAVES 6  // 6 waves per SIMD (24 per CU, LDS-bound): -10% orientation time despite a few spills (48 B since the f64 angle pass moved out of the sample loop; 5 waves: no spills, 8% slower)
 #endif
@@ -440,9 +443,8 @@ __global__ __launch_bounds__(256, SIFT_ORIENT_MIN_WAVES) void k_orient(const Ori
             // outside the image are dropped below); the loads of the lane's
             // next sample are in flight while the current one is evaluated.
             const gfloat* gimg = as_global(img);
-            auto fetch = [&](int idx, float& l, float& r, float& u, float& d) {
-                const int iy = idx / n;
-                const int yy = min(max(y + iy - radius, 1), H - 2), xx = min(max(x + idx - iy * n - radius, 1), W - 2);
+            auto fetch = [&](int iy, int ix, float& l, float& r, float& u, float& d) {
+                const int yy = min(max(y + iy - radius, 1), H - 2), xx = min(max(x + ix - radius, 1), W - 2);
                 const gfloat* rw = gimg + (size_t)yy * pitch + xx;
                 r = rw[1];
                 l = rw[-1];
@@ -459,12 +461,28 @@ __global__ __launch_bounds__(256, SIFT_ORIENT_MIN_WAVES) void k_orient(const Ori
             };
             float nl = 0.f, nr = 0.f, nu = 0.f, nd = 0.f;
             uint32_t defer = 0;  // bit it: the lane's sample lane + 64 * it needs the f64 angle
-            if (lane < N && H > 2 && W > 2) fetch(lane, nl, nr, nu, nd);
+            // patch row / column of the lane's sample (cy, cx) and of its next
+            // one (fy, fx), stepped by 64 samples without a division
+            const int dq = 64 / n, dr = 64 - dq * n;
+            auto adv = [&](int& ry, int& rx) {
+                rx += dr;
+                ry += dq;
+                if (rx >= n) {
+                    rx -= n;
+                    ry++;
+                }
+            };
+            int cy = lane / n, cx = lane - (lane / n) * n;
+            int fy = cy, fx = cx;
+            adv(fy, fx);
+            if (lane < N && H > 2 && W > 2) fetch(cy, cx, nl, nr, nu, nd);
             for (int idx = lane, it = 0; idx < N; idx += 64, it++) {
                 const float gl = nl, gr = nr, gu = nu, gd = nd;
-                if (idx + 64 < N && H > 2 && W > 2) fetch(idx + 64, nl, nr, nu, nd);
-                const int iy = idx / n;
-                const int yp = iy - radius, xp = idx - iy * n - radius;
+                if (idx + 64 < N && H > 2 && W > 2) fetch(fy, fx, nl, nr, nu, nd);
+                const int yp = cy - radius, xp = cx - radius;
+                cy = fy;
+                cx = fx;
+                adv(fy, fx);
                 const int yy = y + yp, xx = x + xp;
                 uint8_t bin = 0xff;
                 float val = 0.0f;
@@ -497,7 +515,7 @@ __global__ __launch_bounds__(256, SIFT_ORIENT_MIN_WAVES) void k_orient(const Ori
                 defer &= defer - 1;
                 const int idx = lane + 64 * it;
                 float gl, gr, gu, gd;
-                fetch(idx, gl, gr, gu, gd);
+                fetch(idx / n, idx - (idx / n) * n, gl, gr, gu, gd);
                 const float dx = gr - gl;
                 const float dy = gu - gd;
                 sbin[wave][idx] = to_bin((float)atan2((double)dy, (double)dx));
@@ -513,21 +531,16 @@ __global__ __launch_bounds__(256, SIFT_ORIENT_MIN_WAVES) void k_orient(const Ori
         // sequential per-bin sums (lane = bin); inactive waves run on an empty list
         if (!active) N = 0;
         float acc = 0.0f;
+#ifdef SIFT_EXP_ORIENT_DENSE  // round-2 dense scan (A/B only): every bin lane reads every sample
         {
             const float4* v4 = reinterpret_cast<const float4*>(sval[wave]);
-            const uint32_t* b4 = reinterpret_cast<const uint32_t*>(sbin[wave]);
             const uint4* b16 = reinterpret_cast<const uint4*>(sbin[wave]);
             const uint32_t me = (uint32_t)lane;
             int j = 0;
-            // 16 samples per iteration: all five LDS reads in flight together
-            // (one latency per 16 samples instead of per 4); the adds stay in
-            // sample order
             for (; j + 16 <= N; j += 16) {
                 const uint4 bb = b16[j >> 4];
-                const float4 va = v4[(j >> 2) + 0], vb = v4[(j >> 2) + 1], vc = v4[(j >> 2) + 2],
-                             vd = v4[(j >> 2) + 3];
+                const float4 vv[4] = {v4[(j >> 2) + 0], v4[(j >> 2) + 1], v4[(j >> 2) + 2], v4[(j >> 2) + 3]};
                 const uint32_t w[4] = {bb.x, bb.y, bb.z, bb.w};
-                const float4 vv[4] = {va, vb, vc, vd};
 #pragma unroll
                 for (int q = 0; q < 4; q++) {
                     acc += ((w[q] & 0xff) == me) ? vv[q].x : 0.0f;
@@ -536,16 +549,50 @@ __global__ __launch_bounds__(256, SIFT_ORIENT_MIN_WAVES) void k_orient(const Ori
                     acc += ((w[q] >> 24) == me) ? vv[q].w : 0.0f;
                 }
             }
-            for (; j + 4 <= N; j += 4) {
-                const float4 v = v4[j >> 2];
-                const uint32_t bb = b4[j >> 2];
-                acc += ((bb & 0xff) == me) ? v.x : 0.0f;
-                acc += (((bb >> 8) & 0xff) == me) ? v.y : 0.0f;
-                acc += (((bb >> 16) & 0xff) == me) ? v.z : 0.0f;
-                acc += ((bb >> 24) == me) ? v.w : 0.0f;
-            }
             for (; j < N; j++) acc += ((uint32_t)sbin[wave][j] == me) ? sval[wave][j] : 0.0f;
         }
+#else
+        // Per 64-sample batch, lane b < 36 gets the mask of the batch's samples
+        // in bin b from six ballots of the bin bits, then adds exactly those
+        // samples in index order: the reference's per-bin order (bit-identical)
+        // at O(largest bin count per batch) instead of every lane reading every
+        // sample (1080p: ~110 vs ~600 steps per extremum).  Samples outside the
+        // image (bin 0xff) and past N match no lane.
+        for (int t = 0; t < N; t += 64) {
+            const int idx = t + lane;
+            const uint32_t bv = idx < N ? (uint32_t)sbin[wave][idx] : 0xffu;
+            uint64_t m = __ballot(bv < (uint32_t)kOriBins);
+#pragma unroll
+            for (int i = 0; i < 6; i++) {
+                const uint64_t bi = __ballot((bv >> i) & 1u);
+                m &= ((lane >> i) & 1) ? bi : ~bi;
+            }
+            // SIFT_ORIENT_SUM_U samples per step: their LDS reads in flight
+            // together; a missing sample adds +0 (exact: acc >= +0)
+            auto run = [&](uint32_t mk, const float* vb) {
+                while (mk) {
+                    int j[SIFT_ORIENT_SUM_U];
+                    bool ok[SIFT_ORIENT_SUM_U];
+                    j[0] = __builtin_ctz(mk);
+                    ok[0] = true;
+                    mk &= mk - 1u;
+#pragma unroll
+                    for (int u = 1; u < SIFT_ORIENT_SUM_U; u++) {
+                        ok[u] = mk != 0u;
+                        j[u] = ok[u] ? __builtin_ctz(mk) : j[0];
+                        mk &= mk - 1u;
+                    }
+                    float v[SIFT_ORIENT_SUM_U];
+#pragma unroll
+                    for (int u = 0; u < SIFT_ORIENT_SUM_U; u++) v[u] = vb[j[u]];
+#pragma unroll
+                    for (int u = 0; u < SIFT_ORIENT_SUM_U; u++) acc += ok[u] ? v[u] : 0.0f;
+                }
+            };
+            run(lane < kOriBins ? (uint32_t)m : 0u, sval[wave] + t);
+            run(lane < kOriBins ? (uint32_t)(m >> 32) : 0u, sval[wave] + t + 32);
+        }
+#endif
         // circular [1,4,6,4,1]/16 smoothing (src/lib.rs:742-755)
         const int k = lane < kOriBins ? lane : 0;
         const float rm2 = __shfl(acc, (k + kOriBins - 2) % kOriBins);

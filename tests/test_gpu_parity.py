@@ -164,13 +164,17 @@ def test_golden_snapshots_gpu(pkg, ctx, oracle):
     ex.set_exact_descriptors(True)
     for name, count in [("tree_small", 1270), ("bird_small", 225)]:
         g = load_golden(name)
-        # default mode: its own +-1 can stack on the oracle's +-1 vs the snapshot
-        for c, min_desc, max_d in ((ctx, 0.95, 2), (ex, MIN_DESC_EQUAL, 1)):
+        # default mode: measured on MI355X (round 3) at the exact mode's max |d|
+        # of 1 and 98.35 % / 97.33 % identical rows (tree / bird; exact mode
+        # 98.35 / 97.78 %): its own +-1 does not stack on the oracle's here
+        for c, min_desc, max_d in ((ctx, 0.97, 1), (ex, MIN_DESC_EQUAL, 1)):
             res = c.sift(g["image"])
             assert len(res) == count
             order = pkg.stable_sort_xy_size(res.keypoints_array)
             pos_exact, rows_close, desc_equal, desc_maxd = golden_agreement(res.keypoints_array[order],
                                                                              res.descriptors[order], g)
+            print(f"golden {name} {'exact' if c is ex else 'default'}: pos_exact {pos_exact:.4f} "
+                  f"rows_close {rows_close:.4f} desc_equal {desc_equal:.4f} desc_maxd {desc_maxd}")
             assert pos_exact >= MIN_POS_EXACT and rows_close >= MIN_ROWS_CLOSE, (name, pos_exact, rows_close)
             assert desc_equal >= min_desc, (name, desc_equal)
             assert desc_maxd <= max_d, (name, desc_maxd)

@@ -11,4 +11,5 @@ for spec in "$@"; do
   env $envs TAG=$tag timeout -k 10 120 python tools/exp/single.py >> gpurun_out/ab/single.log 2>&1 || { echo "$tag single failed"; exit 1; }
 done
 python3 tools/exp/bench_cmp.py gpurun_out/ab/*.log
-cat gpurun_out/ab/single.log
+[ -f gpurun_out/ab/single.log ] && cat gpurun_out/ab/single.log
+exit 0
