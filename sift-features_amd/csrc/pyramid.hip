@@ -295,7 +295,7 @@ __global__ __launch_bounds__(256) void k_blur(const float* __restrict__ src, siz
 // compile-time choice and every LDS read is one ds_read_b64 with an immediate
 // offset.
 // ---------------------------------------------------------------------------
-template <int R_, int S_ = 32>
+template <int R_, int S_ = 32, int HWL_ = -1>
 struct StripGeom {
     static constexpr int R = R_;                      // blur radius
     static constexpr int TW = 128;                    // output columns per strip
@@ -303,7 +303,7 @@ struct StripGeom {
     static constexpr int NW = 4;                      // waves per workgroup
     static constexpr int VB = S / NW;                 // column-pass rows per wave per step
     static constexpr int QW = 8;                      // row-pass outputs per item
-    static constexpr int HWL = (R + 3) & ~3;
+    static constexpr int HWL = HWL_ < 0 ? (R + 3) & ~3 : HWL_;  // window halo (default: R rounded up to 4)
     static constexpr int IWV = TW + 2 * HWL;          // loaded columns per row (multiple of 8)
     static constexpr int IWP = IWV + 4;               // LDS row pitch: IWP / 4 odd
     static constexpr int OFF = HWL - R;
@@ -944,6 +944,9 @@ __global__ __launch_bounds__(256) void k_seed(const uint8_t* __restrict__ frames
     //    entries (threads 0..127: columns, 128..255: rows)
     const int a0 = sxa & ~3;  // first source dword (4-B aligned frame rows)
     const int nwr = (sxb - a0) / 4 + 1, nr = syb - sya + 1;
+    // dword loads only when every row start is 4-byte aligned (odd strides /
+    // unaligned frame bases take the byte path)
+    const bool dw_ok = (((uintptr_t)src | (uintptr_t)row_stride) & 3u) == 0;
     uint32_t wv[NLD];
 #pragma unroll
     for (int j = 0; j < NLD; j++) {
@@ -953,9 +956,9 @@ __global__ __launch_bounds__(256) void k_seed(const uint8_t* __restrict__ frames
         if (fast && r < nr && w < nwr) {
             const int c = a0 + 4 * w;
             const uint8_t* p = src + (size_t)(sya + r) * row_stride + c;
-            if (c + 3 < sw) {
+            if (c + 3 < sw && dw_ok) {
                 wv[j] = *reinterpret_cast<const uint32_t*>(p);
-            } else {  // row end: bytes only (the dword could run past the frame)
+            } else {  // row end / unaligned rows: bytes only (the dword could run past the frame)
                 for (int q = 0; q < 4 && c + q < sw; q++) wv[j] |= (uint32_t)p[q] << (8 * q);
             }
         }
@@ -1091,13 +1094,13 @@ __device__ __forceinline__ f2v u8_unit2(float a, float b) {
 // ABL: timing ablations for tools/ubench_kernels.hip only (the product
 // launches ABL = 0): 1 drops the plane stores (zero-size buffer), 2 the
 // loader's loads and upsample, 4 the row pass
-template <int R, int ABL = 0>
-__global__ __launch_bounds__(256, StripGeom<R>::MINB) void k_seed_strip(const uint8_t* __restrict__ frames,
+template <int R, int P = kProfileOpenCV, int ABL = 0>
+__global__ __launch_bounds__(256, (StripGeom<R, 32, 8>::MINB)) void k_seed_strip(const uint8_t* __restrict__ frames,
                                                                         size_t frame_pitch, size_t row_stride, int sh,
                                                                         int sw, float* __restrict__ dst,
                                                                         size_t dst_img_stride, int W, int H, int pitch,
                                                                         const BlurTaps taps, int ya, int yb, int seg) {
-    using G = StripGeom<R>;
+    using G = StripGeom<R, 32, 8>;         // 8-column halo for any R <= 8: 144 = 12 x 12 window columns
     constexpr int CW = 12;                 // window columns per item
     constexpr int NCG = G::IWV / CW;       // column groups (12)
     constexpr int NPW = G::VB / 2;         // row pairs per wave (4)
@@ -1134,7 +1137,7 @@ __global__ __launch_bounds__(256, StripGeom<R>::MINB) void k_seed_strip(const ui
         bool two[CW];
 #pragma unroll
         for (int k = 0; k < CW; k++) {
-            seed_axis(strip_index<kProfileOpenCV>(cb + k, W), W, sw, sx[k], t_a0[CW * tid + k], t_a1[CW * tid + k],
+            seed_axis(strip_index<P>(cb + k, W), W, sw, sx[k], t_a0[CW * tid + k], t_a1[CW * tid + k],
                       two[k]);
             lo = min(lo, sx[k]);
             hi = max(hi, two[k] ? sx[k] + 1 : sx[k]);
@@ -1158,7 +1161,7 @@ __global__ __launch_bounds__(256, StripGeom<R>::MINB) void k_seed_strip(const ui
     int pbase = 0;     // first source row
     auto rows_of = [&](int g, int& sy0, int& sy1, float& b0, float& b1) {
         bool two;
-        seed_axis(strip_index<kProfileOpenCV>(g, H), H, sh, sy0, b0, b1, two);
+        seed_axis(strip_index<P>(g, H), H, sh, sy0, b0, b1, two);
         sy1 = min(sy0 + 1, sh - 1);
     };
     // interior chunk (uniform): window rows g0 .. g0 + 31 in [1, H - 2] and
@@ -1196,8 +1199,8 @@ __global__ __launch_bounds__(256, StripGeom<R>::MINB) void k_seed_strip(const ui
             }
         }
     };
-    // HResizeLinear of one source row's 12 columns from its 8 bytes p[0..7]
-    auto hres = [&](const uint32_t (&w)[3], uint32_t sh3, float (&h)[CW]) {
+    // the 8 source bytes of one source row as v / 255 (u8_unit)
+    auto units = [&](const uint32_t (&w)[3], uint32_t sh3, float (&p)[8]) {
         const uint32_t lo = __builtin_amdgcn_alignbyte(w[1], w[0], sh3);
         const uint32_t hi = __builtin_amdgcn_alignbyte(w[2], w[1], sh3);
         // (float)(byte k): v_cvt_f32_ubyte{0..3}
@@ -1206,10 +1209,17 @@ __global__ __launch_bounds__(256, StripGeom<R>::MINB) void k_seed_strip(const ui
         const f2v p23 = u8_unit2(by(lo, 2), by(lo, 3));
         const f2v p45 = u8_unit2(by(hi, 0), by(hi, 1));
         const f2v p67 = u8_unit2(by(hi, 2), by(hi, 3));
-        const float p[8] = {p01.x, p01.y, p23.x, p23.y, p45.x, p45.y, p67.x, p67.y};
+        p[0] = p01.x, p[1] = p01.y, p[2] = p23.x, p[3] = p23.y;
+        p[4] = p45.x, p[5] = p45.y, p[6] = p67.x, p[7] = p67.y;
+    };
+    // horizontal 2x step of one row's 12 window columns from its 8 source
+    // values (OpenCV HResizeLinear: t = S[sx]*a0 + S[sx+1]*a1; imageproc's
+    // Triangle horizontal_sample has the same two nonzero taps in the same
+    // order -- its third, zero-weight tap adds +0)
+    auto hmix = [&](const float (&p)[8], float (&h)[CW]) {
         if (wxin) {
             // column c0 + 2i: S[i] * 0.25 + S[i + 1] * 0.75; c0 + 2i + 1:
-            // S[i + 1] * 0.75 + S[i + 2] * 0.25 (t = S[sx]*a0 + S[sx+1]*a1)
+            // S[i + 1] * 0.75 + S[i + 2] * 0.25
             const f2v ka = {0.25f, 0.75f}, kb = {0.75f, 0.25f};
 #pragma unroll
             for (int i = 0; i < CW / 2; i++) {
@@ -1230,6 +1240,12 @@ __global__ __launch_bounds__(256, StripGeom<R>::MINB) void k_seed_strip(const ui
                 h[k] = (info & 16) ? v0 * t_a0[CW * cg + k] + v1 * t_a1[CW * cg + k] : v0;
             }
         }
+    };
+    // HResizeLinear of one source row's 12 columns from its 8 bytes
+    auto hres = [&](const uint32_t (&w)[3], uint32_t sh3, float (&h)[CW]) {
+        float p[8];
+        units(w, sh3, p);
+        hmix(p, h);
     };
     // the prefetched chunk (window rows from g0) -> upsampled rows in the slot
     auto store = [&](float* slot, int g0) {
@@ -1258,40 +1274,81 @@ __global__ __launch_bounds__(256, StripGeom<R>::MINB) void k_seed_strip(const ui
             rows_of(g, sy[0][0], sy[0][1], b[0][0], b[0][1]);
             rows_of(g + 1, sy[1][0], sy[1][1], b[1][0], b[1][1]);
         }
-        float h0[CW], h1[CW];
-        hres(pw[0], psh & 3u, h0);
-        hres(pw[1], (psh >> 2) & 3u, h1);
         // wave-uniform: every pair of the wave on two source rows (all but the
         // first / last chunks of a frame)
         const bool two_rows =
             rin || __builtin_amdgcn_ballot_w64(act && !(sy[0][0] == pbase && sy[1][0] == pbase &&
                                                        sy[0][1] == pbase + 1 && sy[1][1] == pbase + 1)) == 0;
+        if constexpr (P == kProfileOpenCV) {
+            // cv::resize: HResizeLinear per source row, then VResizeLinear
+            float h0[CW], h1[CW];
+            hres(pw[0], psh & 3u, h0);
+            hres(pw[1], (psh >> 2) & 3u, h1);
 #pragma unroll
-        for (int r = 0; r < 2; r++) {
-            float v[CW];
-            if (two_rows) {
-                // VResizeLinear: S0*b0 + S1*b1
-                const f2v b0 = {b[r][0], b[r][0]}, b1 = {b[r][1], b[r][1]};
+            for (int r = 0; r < 2; r++) {
+                float v[CW];
+                if (two_rows) {
+                    // VResizeLinear: S0*b0 + S1*b1
+                    const f2v b0 = {b[r][0], b[r][0]}, b1 = {b[r][1], b[r][1]};
 #pragma unroll
-                for (int k = 0; k < CW; k += 2) {
-                    const f2v o = f2v{h0[k], h0[k + 1]} * b0 + f2v{h1[k], h1[k + 1]} * b1;
-                    v[k] = o.x;
-                    v[k + 1] = o.y;
+                    for (int k = 0; k < CW; k += 2) {
+                        const f2v o = f2v{h0[k], h0[k + 1]} * b0 + f2v{h1[k], h1[k + 1]} * b1;
+                        v[k] = o.x;
+                        v[k + 1] = o.y;
+                    }
+                } else {  // border rows: any two of the three source rows
+                    float h2[CW];
+                    hres(pw[2], (psh >> 4) & 3u, h2);
+                    const int i0 = sy[r][0] - pbase, i1 = sy[r][1] - pbase;
+#pragma unroll
+                    for (int k = 0; k < CW; k++) {
+                        const float s0 = i0 == 0 ? h0[k] : (i0 == 1 ? h1[k] : h2[k]);
+                        const float s1 = i1 == 0 ? h0[k] : (i1 == 1 ? h1[k] : h2[k]);
+                        v[k] = s0 * b[r][0] + s1 * b[r][1];
+                    }
                 }
-            } else {  // border rows: any two of the three source rows
-                float h2[CW];
-                hres(pw[2], (psh >> 4) & 3u, h2);
-                const int i0 = sy[r][0] - pbase, i1 = sy[r][1] - pbase;
 #pragma unroll
-                for (int k = 0; k < CW; k++) {
-                    const float s0 = i0 == 0 ? h0[k] : (i0 == 1 ? h1[k] : h2[k]);
-                    const float s1 = i1 == 0 ? h0[k] : (i1 == 1 ? h1[k] : h2[k]);
-                    v[k] = s0 * b[r][0] + s1 * b[r][1];
-                }
+                for (int k = 0; k < CW; k += 4)
+                    *reinterpret_cast<float4*>(out + r * G::IWP + k) = make_float4(v[k], v[k + 1], v[k + 2], v[k + 3]);
             }
+        } else {
+            // image::imageops::resize Triangle 2x: vertical_sample over the
+            // item's 8 source columns, then horizontal_sample, clamped to
+            // [0, 1].  Per destination index the nonzero taps and their order
+            // are seed_axis' (the zero-weight third tap adds +0).
+            float p0[8], p1[8];
+            units(pw[0], psh & 3u, p0);
+            units(pw[1], (psh >> 2) & 3u, p1);
+            float p2[8];
+            if (!two_rows) units(pw[2], (psh >> 4) & 3u, p2);
 #pragma unroll
-            for (int k = 0; k < CW; k += 4)
-                *reinterpret_cast<float4*>(out + r * G::IWP + k) = make_float4(v[k], v[k + 1], v[k + 2], v[k + 3]);
+            for (int r = 0; r < 2; r++) {
+                float vs[8];
+                if (two_rows) {
+                    const f2v b0 = {b[r][0], b[r][0]}, b1 = {b[r][1], b[r][1]};
+#pragma unroll
+                    for (int k = 0; k < 8; k += 2) {
+                        const f2v o = f2v{p0[k], p0[k + 1]} * b0 + f2v{p1[k], p1[k + 1]} * b1;
+                        vs[k] = o.x;
+                        vs[k + 1] = o.y;
+                    }
+                } else {
+                    const int i0 = sy[r][0] - pbase, i1 = sy[r][1] - pbase;
+#pragma unroll
+                    for (int k = 0; k < 8; k++) {
+                        const float s0 = i0 == 0 ? p0[k] : (i0 == 1 ? p1[k] : p2[k]);
+                        const float s1 = i1 == 0 ? p0[k] : (i1 == 1 ? p1[k] : p2[k]);
+                        vs[k] = s0 * b[r][0] + s1 * b[r][1];
+                    }
+                }
+                float v[CW];
+                hmix(vs, v);
+#pragma unroll
+                for (int k = 0; k < CW; k++) v[k] = fminf(fmaxf(v[k], 0.0f), 1.0f);
+#pragma unroll
+                for (int k = 0; k < CW; k += 4)
+                    *reinterpret_cast<float4*>(out + r * G::IWP + k) = make_float4(v[k], v[k + 1], v[k + 2], v[k + 3]);
+            }
         }
     };
     int prow, pq;  // row-pass lane map
@@ -1303,7 +1360,7 @@ __global__ __launch_bounds__(256, StripGeom<R>::MINB) void k_seed_strip(const ui
     prefetch(gb + G::S);
     drop_stores<G::VB>(rd);
     __syncthreads();
-    if constexpr ((ABL & 4) == 0) strip_rowpass<G, kProfileOpenCV>(lds, taps, prow, pq);
+    if constexpr ((ABL & 4) == 0) strip_rowpass<G, P>(lds, taps, prow, pq);
     for (int k = 0; k < nsteps; k++) {
         float* sa = lds + (k & 1) * G::SLOT;
         float* sb = lds + ((k + 1) & 1) * G::SLOT;
@@ -1311,13 +1368,13 @@ __global__ __launch_bounds__(256, StripGeom<R>::MINB) void k_seed_strip(const ui
         store(sb, gb + (k + 1) * G::S);
         if (k + 2 <= nsteps) prefetch(gb + (k + 2) * G::S);
         __syncthreads();
-        if constexpr ((ABL & 4) == 0) strip_rowpass<G, kProfileOpenCV>(sb, taps, prow, pq);
+        if constexpr ((ABL & 4) == 0) strip_rowpass<G, P>(sb, taps, prow, pq);
         __syncthreads();
         const int y = ys + k * G::S;
         switch (wv) {
 #define COLPASS(w)                                                                                              \
     case w:                                                                                                     \
-        strip_colpass<G, kProfileOpenCV, w, false>(sa, sb, taps, lane, y, ye, x0, W, pitch, rd, rd, 0, 0, 0); \
+        strip_colpass<G, P, w, false>(sa, sb, taps, lane, y, ye, x0, W, pitch, rd, rd, 0, 0, 0); \
         break;
             COLPASS(0) COLPASS(1) COLPASS(2) COLPASS(3)
             default:
@@ -1626,14 +1683,10 @@ static void launch_seed_ip_r(const SeedLaunch& L, hipStream_t st) {
 int launch_seed(int R, const SeedLaunch& L, hipStream_t st) {
     // the seed sigma is a constant: OpenCV cvRound(1.249 * 8 + 1) | 1 = 11
     // taps (R = 5); imageproc ceil(2 * 1.249) = 3
-    if (L.profile == kProfileImageproc) {
-        if (R != 3) return -1;
-        launch_seed_ip_r<3>(L, st);
-        return 0;
-    }
-    if (R != 5) return -1;
+    const bool ip = L.profile == kProfileImageproc;
+    if (R != (ip ? 3 : 5)) return -1;
     // the strip seed: exact 2x geometry, frames wide / tall enough for one
-    // reflection of every window (else the tile kernel)
+    // reflection of every window (else the tile kernels)
     if (L.W == 2 * L.sw && L.H == 2 * L.sh && L.W >= 160 && L.H >= 64 &&
         (uint64_t)L.H * (uint64_t)L.pitch * 4 < (1ull << 31) && strip_blur_enabled()) {
         using G = StripGeom<5>;
@@ -1646,12 +1699,21 @@ int launch_seed(int R, const SeedLaunch& L, hipStream_t st) {
         const int rows = yb - ya;
         const int seg = strip_segment_rows(rows, (long)strips * L.n_img);
         const int nseg = (rows + seg - 1) / seg;
-        hipLaunchKernelGGL((k_seed_strip<5>), dim3(strips, nseg, L.n_img), dim3(256), 0, st, L.frames,
-                           L.frame_pitch, L.row_stride, L.sh, L.sw, L.dst, L.dst_img_stride, L.W, L.H, L.pitch,
-                           L.taps, ya, yb, seg);
+        const dim3 grid(strips, nseg, L.n_img);
+        if (ip)
+            hipLaunchKernelGGL((k_seed_strip<3, kProfileImageproc>), grid, dim3(256), 0, st, L.frames, L.frame_pitch,
+                               L.row_stride, L.sh, L.sw, L.dst, L.dst_img_stride, L.W, L.H, L.pitch, L.taps, ya, yb,
+                               seg);
+        else
+            hipLaunchKernelGGL((k_seed_strip<5, kProfileOpenCV>), grid, dim3(256), 0, st, L.frames, L.frame_pitch,
+                               L.row_stride, L.sh, L.sw, L.dst, L.dst_img_stride, L.W, L.H, L.pitch, L.taps, ya, yb,
+                               seg);
         return 0;
     }
-    launch_seed_r<5>(L, st);
+    if (ip)
+        launch_seed_ip_r<3>(L, st);
+    else
+        launch_seed_r<5>(L, st);
     return 0;
 }
 

@@ -74,6 +74,31 @@ def test_strided_input(ctx):
     assert ctx.sift(view) == ctx.sift(np.ascontiguousarray(view))
 
 
+@pytest.mark.parametrize("w,h,stride", [(241, 61, 241), (77, 45, 77), (161, 97, 163), (39, 30, 41)])
+def test_odd_stride_batch(pkg, ctx, oracle, w, h, stride):
+    """Odd widths / row strides and unaligned frame bases: the strip seed
+    (source width >= 80) and the tile seed (narrower frames) read rows that do
+    not start on 4-byte boundaries; the batch equals the oracle per frame."""
+    from test_gpu_parity import assert_parity
+    import synth
+    import torch
+    n = 3
+    frames = np.stack([synth.frame(w, h, 40 + i) for i in range(n)])
+    got = ctx.sift_batch(frames)  # host frames: packed, odd widths give unaligned rows
+    buf = np.zeros(n * h * stride + 1, np.uint8)  # device frames: odd stride, base at byte 1
+    view = np.lib.stride_tricks.as_strided(buf[1:], (n, h, w), (h * stride, stride, 1))
+    view[:] = frames
+    t = torch.from_numpy(buf).cuda()
+    torch.cuda.synchronize()
+    offs, res = ctx.sift_batch_device(t.data_ptr() + 1, n, w, h, stride, h * stride)
+    for i in range(n):
+        kp_o, desc_o, ext_o = oracle.sift(frames[i], internal=True)
+        assert_parity(pkg, got[i], kp_o, desc_o, ext_o)
+        a, b = int(offs[i]), int(offs[i + 1])
+        assert np.array_equal(res.keypoints_array[a:b], got[i].keypoints_array), i
+        assert np.array_equal(res.descriptors[a:b], got[i].descriptors), i
+
+
 def test_random_noise(pkg, ctx, oracle):
     """White noise: many plateaus/ties and dense extrema (worst case for ordering)."""
     from test_gpu_parity import assert_parity

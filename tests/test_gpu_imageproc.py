@@ -68,3 +68,24 @@ def test_ip_batch_and_limit(pkg, ctx_ip, oracle):
     for f, res in zip(frames, out):
         kp_o, desc_o, ext_o = oracle.sift(f, features_limit=30, profile=PROFILE_IMAGEPROC, internal=True)
         assert_parity(pkg, res, kp_o, desc_o, ext_o)
+
+
+@pytest.mark.parametrize("kernel", ["strip", "tile", "notail"])
+@pytest.mark.parametrize("name", ["synth_640x480", "synth_301x207", "synth_1000x333", "synth_90x700",
+                                  "synth_2000x40", "synth_97x61"])
+def test_ip_pyramid_kernels(ctx_ip, oracle, monkeypatch, kernel, name):
+    """The imageproc profile's kernel families bit for bit against the oracle:
+    "strip" (k_seed_strip<3, imageproc>: the Triangle 2x upsample, vertical then
+    horizontal, clamped, in the strip loader; clamp-to-edge strip blurs and
+    the tail kernel), "tile" (k_seed_ip and the tile blurs), "notail" (per-blur
+    launches for the small octaves)."""
+    from test_gpu_parity import _KERNEL_ENV, _extra
+    for k, v in _KERNEL_ENV[kernel].items():
+        monkeypatch.setenv(k, v)
+    img = INPUTS[name] if name in INPUTS else _extra(name)
+    pre = ctx_ip.precompute_images(img)
+    opy = oracle.Pyramid(img, PROFILE_IMAGEPROC)
+    assert pre.n_octaves == opy.n_octaves
+    for o in range(opy.n_octaves):
+        g, go = pre.scale_space_octave(o), opy.scale_space(o)
+        assert np.array_equal(g, go), (o, np.argwhere(g != go)[:5])

@@ -199,12 +199,14 @@ def test_exact_descriptors_bit_identical(pkg, oracle, name):
     assert neq.sum() <= max(2, len(kp_o) // 200), (neq.sum(0), np.argwhere(neq)[:5])
 
 
+@pytest.mark.parametrize("shape", [(24, 32), (64, 96)])
 @pytest.mark.parametrize("profile", [0, 1])
-def test_seed_all_byte_values(pkg, oracle, profile):
+def test_seed_all_byte_values(pkg, oracle, profile, shape):
     """Every u8 value goes through the seed's v / 255 (fma-corrected
     reciprocal, no table) and the 2x upsample: the first Gaussian of octave 0
-    is bit-identical to the oracle's (which divides)."""
-    img = np.arange(256 * 3, dtype=np.uint32).reshape(24, 32)
+    is bit-identical to the oracle's (which divides).  32x24: the tile seed
+    kernels; 96x64: the strip seed (2x width >= 160)."""
+    img = np.arange(shape[0] * shape[1], dtype=np.uint32).reshape(shape)
     img = ((img * 97 + 13) % 256).astype(np.uint8)  # all 256 values, scrambled
     c = pkg.Context(0, pkg.OpenCVProcessing if profile == 0 else pkg.ImageprocProcessing)
     pre = c.precompute_images(img)

@@ -443,7 +443,7 @@ float time_seed_abl(const uint8_t* df, float* dst, int N) {
     for (int t = 0; t <= 5; t++) taps.k[t] = 1.0f / 11;
     const int seg = 360, nseg = H / seg;
     auto go = [&]() {
-        hipLaunchKernelGGL((k_seed_strip<5, ABL>), dim3(strips, nseg, N), dim3(256), 0, 0, df, (size_t)sw * sh,
+        hipLaunchKernelGGL((k_seed_strip<5, kProfileOpenCV, ABL>), dim3(strips, nseg, N), dim3(256), 0, 0, df, (size_t)sw * sh,
                            (size_t)sw, sh, sw, dst, (size_t)pitch * H, W, H, pitch, taps, 0, H, seg);
     };
     go();
