@@ -447,6 +447,7 @@ struct sift_mi_ctx {
     hipStream_t aux[2] = {};       // per lane: blurs 4, 5 of each octave beside the next octave
     hipEvent_t oct_ev[2][kTailMaxOct + 1] = {};  // per lane: octave o's G_3 done / aux joined
     int oct_overlap = 1;           // SIFT_MI_OCT_OVERLAP=0: one stream per lane (A/B, tests)
+    bool lanes_busy = false;       // this call keeps both pipeline lanes busy (no octave overlap then)
     int stage_overlap = 1;         // SIFT_MI_STAGE_OVERLAP=0: detection after the whole pyramid
     hipEvent_t fork = nullptr;     // orders lane 1 after / before the caller's stream
     int lanes = 2;                 // pipeline lanes (sift_mi_set_pipeline_lanes)
@@ -479,6 +480,7 @@ struct sift_mi_ctx {
     bool have_result = false;
     bool have_pyramid = false;  // single-frame precompute state
     size_t dev_result_n = 0;
+    int res_slot = -1;  // >= 0: the last call's device results are that slot's outputs (one chunk, no copy)
     sift_mi_stats stats{};
 };
 
@@ -676,7 +678,8 @@ constexpr int kBandDrift = 24, kBandPatch = 41;
 // stream beside the next octave's blurs (SIFT_MI_OCT_OVERLAP=0: off).  Tried
 // and measured slower or no faster (round 3): the chunk's
 // frames split in two halves on the two streams; seed + octave 0 in
-// sub-batches of 2-32 frames for Infinity Cache reuse; a second aux stream.
+// sub-batches of 2-32 frames for Infinity Cache reuse; a second aux stream;
+// only octaves 0 .. k-1 (k = 1, 2, 3) on the aux stream.
 // detect_slot >= 0 (stage overlap): the detection of the chunk in that slot
 // is launched from here, each part's octaves as soon as their blurs are done.
 int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_pitch, size_t row_stride,
@@ -875,7 +878,11 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
         }
         return 0;
     };
-    CHK(part(0, n, st, c->oct_overlap && p.n_oct <= kTailMaxOct));
+    // octave overlap only while the other lane is idle: with two chunks in
+    // flight the other lane's kernels already fill the chip, and the extra
+    // stream costs ~2% of batch throughput (30.4 vs 29.8 M keypoints/s,
+    // 128 1080p frames, three A/B pairs)
+    CHK(part(0, n, st, c->oct_overlap && !c->lanes_busy && p.n_oct <= kTailMaxOct));
     HIPCHK(hipGetLastError());
     c->stats.pyramid_launches += launches;
     c->stats.pyramid_bytes += bytes * n;
@@ -972,9 +979,9 @@ int prepare_chunk(sift_mi_ctx* c, int si, uint32_t m, uint32_t frame_base, const
     S.bk = B.bk;
     S.detected = false;
     uint32_t* cnt = S.counters.p;
-    HIPCHK(hipMemsetAsync(cnt, 0, 4 * sizeof(uint32_t), st));
-    HIPCHK(hipMemsetAsync(cnt + 4 + 2 * m, 0, kDescWorkWords * sizeof(uint32_t), st));  // descriptor work queues
-    HIPCHK(hipMemsetAsync(cnt + 4, 0xff, m * sizeof(uint32_t), st));                   // frame starts
+    // stage counters, frame starts (~0), descriptor work queues
+    launch_chunk_init(cnt, (int)m, kDescWorkWords, st);
+    HIPCHK(hipGetLastError());
     return 0;
 }
 
@@ -1159,7 +1166,7 @@ int enqueue_chunk(sift_mi_ctx* c, int si, const uint8_t* d_frames, size_t frame_
 // Wait for slot si's chunk; on success append its per-frame offsets and start
 // the copy of its results to the host.  Returns 1 when a stage count exceeded
 // its bound (the caller re-runs the chunk; the high-water marks now cover it).
-int finalize_chunk(sift_mi_ctx* c, int si, size_t* offsets) {
+int finalize_chunk(sift_mi_ctx* c, int si, size_t* offsets, bool only_chunk = false) {
     Slot& S = c->slot[si];
     HIPCHK(hipEventSynchronize(S.ev[6]));
     const uint32_t* h = S.h_counts.p;
@@ -1184,7 +1191,12 @@ int finalize_chunk(sift_mi_ctx* c, int si, size_t* offsets) {
     }
     c->dev_result_n = n_out;
     c->last_slot = si;
-    if (c->keep_on_device && n_out) {
+    c->res_slot = -1;
+    if (c->keep_on_device && only_chunk) {
+        // the call's only chunk: its outputs ARE the batch's device results
+        // (valid until the next call, sift_mi_device_results) -- no copy
+        c->res_slot = si;
+    } else if (c->keep_on_device && n_out) {
         // whole-batch device arena: device-to-device copies on the copy stream
         const size_t need = base + n_out;
         if (need > c->r_kp.cap || need * kDescSize > c->r_desc.cap || need > c->r_key.cap) {
@@ -1292,6 +1304,11 @@ int extract_device(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, 
     // lane 1 starts after the caller's stream (frames produced there); the
     // caller's stream resumes after lane 1's last chunk
     const bool two = n_chunks > 1 && c->lanes == 2;
+    c->lanes_busy = two;
+    struct Reset {
+        sift_mi_ctx* c;
+        ~Reset() { c->lanes_busy = false; }
+    } reset_busy{c};
     if (two) {
         HIPCHK(hipEventRecord(c->fork, c->stream));
         HIPCHK(hipStreamWaitEvent(c->own2, c->fork, 0));
@@ -1299,7 +1316,7 @@ int extract_device(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, 
     CHK(enqueue(0));
     if (n_chunks > 1) CHK(enqueue(1));
     for (uint32_t k = 0; k < n_chunks; k++) {
-        int rc = finalize_chunk(c, (int)(k & 1), offsets);
+        int rc = finalize_chunk(c, (int)(k & 1), offsets, n_chunks == 1);
         if (rc < 0) return rc;
         for (int attempt = 0; rc == 1; attempt++) {
             // a stage overflowed its bound: drain both lanes (the other lane's
@@ -1307,7 +1324,7 @@ int extract_device(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, 
             if (attempt == 3) return fail(SIFT_MI_ENOMEM, "stage count kept exceeding its buffer bound");
             CHK(sync_lanes(c));
             CHK(enqueue(k));
-            rc = finalize_chunk(c, (int)(k & 1), offsets);
+            rc = finalize_chunk(c, (int)(k & 1), offsets, n_chunks == 1);
             if (rc < 0) return rc;
         }
         if (k + 2 < n_chunks) CHK(enqueue(k + 2));
@@ -1605,8 +1622,10 @@ int sift_mi_device_results(sift_mi_ctx* c, const sift_mi_keypoint** d_kps, const
     if (!c) return fail(SIFT_MI_EINVAL, "ctx is null");
     if (!c->have_result) return fail(SIFT_MI_ESTATE, "no result");
     if (!c->keep_on_device) return fail(SIFT_MI_ESTATE, "results were copied to the host (keep_on_device is 0)");
-    if (d_kps) *d_kps = reinterpret_cast<const sift_mi_keypoint*>(c->r_kp.p);
-    if (d_desc) *d_desc = c->r_desc.p;
+    const bool direct = c->res_slot >= 0;
+    const Slot& S = c->slot[direct ? c->res_slot : 0];
+    if (d_kps) *d_kps = reinterpret_cast<const sift_mi_keypoint*>(direct ? S.out_kp.p : c->r_kp.p);
+    if (d_desc) *d_desc = direct ? S.out_desc.p : c->r_desc.p;
     if (n) *n = c->n_result;
     return 0;
 }

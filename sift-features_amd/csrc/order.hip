@@ -9,6 +9,8 @@
 // stable w.r.t. emission order for ties) and truncated.
 #include <hipcub/hipcub.hpp>
 
+#include <algorithm>
+
 #include "sift_common.h"
 #include "sift_kernels.h"
 
@@ -20,6 +22,20 @@ size_t sort_pairs_u64(void* temp, size_t temp_bytes, const uint64_t* kin, uint64
     if (hipcub::DeviceRadixSort::SortPairs(temp, bytes, kin, kout, vin, vout, (int)n, 0, end_bit, st) != hipSuccess)
         return 0;
     return bytes;
+}
+
+// Per-chunk counters in one launch (instead of three memsets): cnt[0..3] = 0,
+// the m frame starts = ~0 (no keypoint), the descriptor work queues = 0.
+__global__ void k_chunk_init(uint32_t* __restrict__ cnt, int m, int work_words) {
+    const int i = blockIdx.x * blockDim.x + threadIdx.x;
+    if (i < 4) cnt[i] = 0;
+    if (i < m) cnt[4 + i] = 0xffffffffu;
+    if (i < work_words) cnt[4 + 2 * m + i] = 0;
+}
+
+void launch_chunk_init(uint32_t* cnt, int m, int work_words, hipStream_t st) {
+    const int n = std::max(std::max(4, m), work_words);
+    hipLaunchKernelGGL(k_chunk_init, dim3((n + 255) / 256), dim3(256), 0, st, cnt, m, work_words);
 }
 
 __global__ void k_make_sort_keys(const KpRec* __restrict__ kp, const uint32_t* __restrict__ n_dev, uint32_t bound,

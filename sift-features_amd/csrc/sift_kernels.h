@@ -191,6 +191,7 @@ size_t sort_pairs_u64(void* temp, size_t temp_bytes, const uint64_t* kin, uint64
                       uint32_t* vout, uint32_t n, int end_bit, hipStream_t st);
 // keys[i] = emission key of kp i for i < min(*n, bound); keys beyond are
 // padded with `pad` (sorts last); vals[i] = i
+void launch_chunk_init(uint32_t* cnt, int m, int work_words, hipStream_t st);
 void launch_make_sort_keys(const KpRec* kp, const uint32_t* n, uint32_t bound, uint64_t pad, uint64_t* keys,
                            uint32_t* vals, hipStream_t st);
 // starts[f] = first index of frame f in the sorted keys (0xffffffff if none);

@@ -12,7 +12,8 @@ gap = float(sys.argv[2]) * 1e3 if len(sys.argv) > 2 else 30e3
 raw = gzip.open(path, "rt") if path.endswith(".gz") else open(path)
 rows = list(csv.DictReader(io.StringIO(raw.read())))
 short = lambda n: re.sub(r"\(.*", "", n).replace("void ", "").replace("siftmi::", "")
-PYR = ("k_seed", "k_blur", "k_octave_tail")
+import os
+PYR = ("k_seed", "k_blur", "k_octave_tail") if not os.environ.get("ALL") else ("",)  # ALL=1: every kernel of the call
 ks = sorted((int(r["Start_Timestamp"]), int(r["End_Timestamp"]), r.get("Stream_Id", r.get("Queue_Id")), short(r["Kernel_Name"]))
             for r in rows)
 calls, cur, end = [], [], 0
