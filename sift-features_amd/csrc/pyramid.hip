@@ -1091,85 +1091,91 @@ __device__ __forceinline__ f2v u8_unit2(float a, float b) {
     return __builtin_elementwise_fma(__builtin_elementwise_fma(-q, f2v{255.0f, 255.0f}, fv), c, q);
 }
 
-// ABL: timing ablations for tools/ubench_kernels.hip only (the product
-// launches ABL = 0): 1 drops the plane stores (zero-size buffer), 2 the
-// loader's loads and upsample, 4 the row pass
-template <int R, int P = kProfileOpenCV, int ABL = 0>
-__global__ __launch_bounds__(256, (StripGeom<R, 32, 8>::MINB)) void k_seed_strip(const uint8_t* __restrict__ frames,
-                                                                        size_t frame_pitch, size_t row_stride, int sh,
-                                                                        int sw, float* __restrict__ dst,
-                                                                        size_t dst_img_stride, int W, int H, int pitch,
-                                                                        const BlurTaps taps, int ya, int yb, int seg) {
-    using G = StripGeom<R, 32, 8>;         // 8-column halo for any R <= 8: 144 = 12 x 12 window columns
-    constexpr int CW = 12;                 // window columns per item
-    constexpr int NCG = G::IWV / CW;       // column groups (12)
-    constexpr int NPW = G::VB / 2;         // row pairs per wave (4)
-    static_assert(G::S == 32 && G::NW == 4 && G::IWV % CW == 0 && NCG * NPW <= 64, "loader item map");
-    __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
-    const int tid = threadIdx.x, lane = tid & 63;
-    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const TileId tile = xcd_tile();
-    const int x0 = tile.x * G::TW;
-    const int ys = ya + tile.y * seg, ye = min(yb, ys + seg);
-    if (ys >= ye) return;
-    const __amdgpu_buffer_rsrc_t rd =
-        uniform_rsrc(dst + (size_t)tile.z * dst_img_stride, (ABL & 1) ? 0u : (uint32_t)H * (uint32_t)pitch * 4u);
-    // the frame as a buffer from its 4-byte-aligned base (boff bytes before
-    // it), sized to whole dwords: a dword holding a frame byte never faults
-    const uint8_t* src = frames + (size_t)tile.z * frame_pitch;
-    const uint32_t boff = (uint32_t)(uintptr_t)src & 3u;
-    const uint32_t nbytes = (boff + (uint32_t)(sh - 1) * (uint32_t)row_stride + (uint32_t)sw + 3u) & ~3u;
-    const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(src - boff, nbytes);
-    // this lane's item: row pair pr of the wave, column group cg
-    const bool act = lane < NCG * NPW;
-    const int pr = wv * NPW + (lane & (NPW - 1)), cg = lane / NPW;
-    const int c0 = x0 - G::HWL + CW * cg;  // first window column (even)
-    const bool xin = c0 >= 1 && c0 + CW - 1 <= W - 2;
+// 2x upsample chunk loader of the strip seeds (k_seed_strip):
+// the closed-form coefficients and row-pair items described above, for a
+// strip geometry G (S = 16 or 32 rows per chunk, 144 window columns) whose
+// window starts at column xw0.  NOLOAD (timing ablation only): no loads, a
+// constant chunk.
+template <class G, int P, bool NOLOAD = false>
+struct SeedLoader {
+    static constexpr int CW = 12;              // window columns per item
+    static constexpr int NCG = G::IWV / CW;    // column groups (12)
+    static constexpr int NPW = G::VB / 2;      // row pairs per wave (4 at S = 32, 2 at S = 16)
+    static_assert(G::NW == 4 && G::IWV == 144 && NCG * NPW <= 64 && (NPW & (NPW - 1)) == 0, "loader item map");
     // border columns: per window column its source offset from the item's
     // first source byte (bits 0-3), single / two taps (bit 4), coefficients
-    __shared__ int t_info[G::IWV];
-    __shared__ float t_a0[G::IWV], t_a1[G::IWV];
-    __shared__ int t_smin[NCG], t_need[NCG];
-    if (tid < NCG) {
-        const int cb = x0 - G::HWL + CW * tid;
-        int lo = 1 << 30, hi = -1;
-        int sx[CW];
-        bool two[CW];
-#pragma unroll
-        for (int k = 0; k < CW; k++) {
-            seed_axis(strip_index<P>(cb + k, W), W, sw, sx[k], t_a0[CW * tid + k], t_a1[CW * tid + k],
-                      two[k]);
-            lo = min(lo, sx[k]);
-            hi = max(hi, two[k] ? sx[k] + 1 : sx[k]);
-        }
-#pragma unroll
-        for (int k = 0; k < CW; k++) t_info[CW * tid + k] = (sx[k] - lo) | (two[k] ? 16 : 0);
-        t_smin[tid] = lo;
-        t_need[tid] = hi - lo + 1;  // <= 8 (12 columns span <= 7 sources)
-    }
-    __syncthreads();
-    // wave-uniform path choice: a wave takes the table path when any of its
-    // items needs it (only the first / last strip of a row)
-    const bool wxin = __builtin_amdgcn_ballot_w64(act && !xin) == 0;
-    const int smin = wxin ? c0 / 2 - 1 : t_smin[cg];
-    const int need = wxin ? 8 : t_need[cg];
+    struct Tables {
+        int info[G::IWV];
+        float a0[G::IWV], a1[G::IWV];
+        int smin[NCG];
+    };
+    __amdgpu_buffer_rsrc_t rs;
+    uint32_t boff;
+    size_t row_stride;
+    int sh, sw, W, H;
+    const Tables* tb;
+    bool act, wxin;
+    int pr, cg, c0, smin;
     // prefetched chunk: per source row (up to 3) the <= 3 dwords holding the
     // item's bytes, raw (the byte alignment waits until the chunk is stored,
     // so the loads stay in flight across a row and a column pass)
     uint32_t pw[3][3];
-    uint32_t psh = 0;  // byte offset of each source row (2 bits each)
-    int pbase = 0;     // first source row
-    auto rows_of = [&](int g, int& sy0, int& sy1, float& b0, float& b1) {
+    uint32_t psh;  // byte offset of each source row (2 bits each)
+    int pbase;     // first source row
+
+    // threads 0 .. NCG-1 fill the border-column tables; the caller then
+    // synchronises the workgroup before init()
+    static __device__ __forceinline__ void tables(Tables& t, int xw0, int W, int sw) {
+        const int tid = threadIdx.x;
+        if (tid < NCG) {
+            const int cb = xw0 + CW * tid;
+            int lo = 1 << 30;
+            int sx[CW];
+            bool two[CW];
+#pragma unroll
+            for (int k = 0; k < CW; k++) {
+                seed_axis(strip_index<P>(cb + k, W), W, sw, sx[k], t.a0[CW * tid + k], t.a1[CW * tid + k], two[k]);
+                lo = min(lo, sx[k]);
+            }
+#pragma unroll
+            for (int k = 0; k < CW; k++) t.info[CW * tid + k] = (sx[k] - lo) | (two[k] ? 16 : 0);
+            t.smin[tid] = lo;  // 12 columns span <= 8 sources
+        }
+    }
+    __device__ __forceinline__ void init(const uint8_t* src, size_t row_stride_, int sh_, int sw_, int W_, int H_,
+                                         int xw0, const Tables& t, int lane, int wv) {
+        // the frame as a buffer from its 4-byte-aligned base (boff bytes before
+        // it), sized to whole dwords: a dword holding a frame byte never faults
+        row_stride = row_stride_;
+        sh = sh_, sw = sw_, W = W_, H = H_;
+        tb = &t;
+        boff = (uint32_t)(uintptr_t)src & 3u;
+        const uint32_t nbytes = (boff + (uint32_t)(sh - 1) * (uint32_t)row_stride + (uint32_t)sw + 3u) & ~3u;
+        rs = uniform_rsrc(src - boff, nbytes);
+        // this lane's item: row pair pr of the wave, column group cg
+        act = lane < NCG * NPW;
+        pr = wv * NPW + (lane & (NPW - 1));
+        cg = lane / NPW;
+        c0 = xw0 + CW * cg;  // first window column (even)
+        const bool xin = c0 >= 1 && c0 + CW - 1 <= W - 2;
+        // wave-uniform path choice: a wave takes the table path when any of its
+        // items needs it (only the first / last strip of a row)
+        wxin = __builtin_amdgcn_ballot_w64(act && !xin) == 0;
+        smin = wxin ? c0 / 2 - 1 : t.smin[cg];
+        psh = 0;
+        pbase = 0;
+    }
+    __device__ __forceinline__ void rows_of(int g, int& sy0, int& sy1, float& b0, float& b1) const {
         bool two;
         seed_axis(strip_index<P>(g, H), H, sh, sy0, b0, b1, two);
         sy1 = min(sy0 + 1, sh - 1);
-    };
-    // interior chunk (uniform): window rows g0 .. g0 + 31 in [1, H - 2] and
+    }
+    // interior chunk (uniform): window rows g0 .. g0 + S - 1 in [1, H - 2] and
     // g0 odd -- every pair (g, g + 1) reads source rows (g - 1) / 2 and the
     // next with coefficients (0.75, 0.25) / (0.25, 0.75), no table path
-    auto rows_in = [&](int g0) { return g0 >= 1 && g0 + G::S <= H - 1 && (g0 & 1) != 0; };
-    auto prefetch = [&](int g0) {
-        if constexpr ((ABL & 2) != 0) return;
+    __device__ __forceinline__ bool rows_in(int g0) const { return g0 >= 1 && g0 + G::S <= H - 1 && (g0 & 1) != 0; }
+    __device__ __forceinline__ void prefetch(int g0) {
+        if constexpr (NOLOAD) return;
         if (!act) return;
         const int g = g0 + 2 * pr;
         int nrows = 2;
@@ -1184,7 +1190,6 @@ __global__ __launch_bounds__(256, (StripGeom<R, 32, 8>::MINB)) void k_seed_strip
             nrows = max(a1, c1_) - pbase + 1;  // <= 3
         }
         psh = 0;
-        (void)need;
 #pragma unroll
         for (int r = 0; r < 3; r++) {
             if (r < 2 || r < nrows) {
@@ -1198,9 +1203,9 @@ __global__ __launch_bounds__(256, (StripGeom<R, 32, 8>::MINB)) void k_seed_strip
                 psh |= (off & 3u) << (2 * r);
             }
         }
-    };
+    }
     // the 8 source bytes of one source row as v / 255 (u8_unit)
-    auto units = [&](const uint32_t (&w)[3], uint32_t sh3, float (&p)[8]) {
+    __device__ __forceinline__ void units(const uint32_t (&w)[3], uint32_t sh3, float (&p)[8]) const {
         const uint32_t lo = __builtin_amdgcn_alignbyte(w[1], w[0], sh3);
         const uint32_t hi = __builtin_amdgcn_alignbyte(w[2], w[1], sh3);
         // (float)(byte k): v_cvt_f32_ubyte{0..3}
@@ -1211,12 +1216,12 @@ __global__ __launch_bounds__(256, (StripGeom<R, 32, 8>::MINB)) void k_seed_strip
         const f2v p67 = u8_unit2(by(hi, 2), by(hi, 3));
         p[0] = p01.x, p[1] = p01.y, p[2] = p23.x, p[3] = p23.y;
         p[4] = p45.x, p[5] = p45.y, p[6] = p67.x, p[7] = p67.y;
-    };
+    }
     // horizontal 2x step of one row's 12 window columns from its 8 source
     // values (OpenCV HResizeLinear: t = S[sx]*a0 + S[sx+1]*a1; imageproc's
     // Triangle horizontal_sample has the same two nonzero taps in the same
     // order -- its third, zero-weight tap adds +0)
-    auto hmix = [&](const float (&p)[8], float (&h)[CW]) {
+    __device__ __forceinline__ void hmix(const float (&p)[8], float (&h)[CW]) const {
         if (wxin) {
             // column c0 + 2i: S[i] * 0.25 + S[i + 1] * 0.75; c0 + 2i + 1:
             // S[i + 1] * 0.75 + S[i + 2] * 0.25
@@ -1230,36 +1235,29 @@ __global__ __launch_bounds__(256, (StripGeom<R, 32, 8>::MINB)) void k_seed_strip
         } else {
 #pragma unroll
             for (int k = 0; k < CW; k++) {
-                const int info = t_info[CW * cg + k], d = info & 15;
+                const int info = tb->info[CW * cg + k], d = info & 15;
                 float v0 = p[0], v1 = p[1];
 #pragma unroll
                 for (int e = 1; e < 7; e++) {
                     v0 = d == e ? p[e] : v0;
                     v1 = d == e ? p[e + 1] : v1;
                 }
-                h[k] = (info & 16) ? v0 * t_a0[CW * cg + k] + v1 * t_a1[CW * cg + k] : v0;
+                h[k] = (info & 16) ? v0 * tb->a0[CW * cg + k] + v1 * tb->a1[CW * cg + k] : v0;
             }
         }
-    };
+    }
     // HResizeLinear of one source row's 12 columns from its 8 bytes
-    auto hres = [&](const uint32_t (&w)[3], uint32_t sh3, float (&h)[CW]) {
+    __device__ __forceinline__ void hres(const uint32_t (&w)[3], uint32_t sh3, float (&h)[CW]) const {
         float p[8];
         units(w, sh3, p);
         hmix(p, h);
-    };
-    // the prefetched chunk (window rows from g0) -> upsampled rows in the slot
-    auto store = [&](float* slot, int g0) {
+    }
+    // the prefetched chunk (window rows from g0) -> upsampled rows of the
+    // slot (row pitch G::IWP), rows 2 pr, 2 pr + 1
+    __device__ __forceinline__ void store(float* slot, int g0) const {
         if (!act) return;
         const int g = g0 + 2 * pr;
         float* out = slot + (2 * pr) * G::IWP + CW * cg;
-        if constexpr ((ABL & 2) != 0) {
-#pragma unroll
-            for (int k = 0; k < CW; k += 4) {
-                *reinterpret_cast<float4*>(out + k) = make_float4(0.5f, 0.25f, (float)g, 1.0f);
-                *reinterpret_cast<float4*>(out + G::IWP + k) = make_float4(0.5f, 0.25f, (float)g, 1.0f);
-            }
-            return;
-        }
         int sy[2][2];
         float b[2][2];
         const bool rin = rows_in(g0);
@@ -1350,14 +1348,41 @@ __global__ __launch_bounds__(256, (StripGeom<R, 32, 8>::MINB)) void k_seed_strip
                     *reinterpret_cast<float4*>(out + r * G::IWP + k) = make_float4(v[k], v[k + 1], v[k + 2], v[k + 3]);
             }
         }
-    };
+    }
+};
+
+// ABL: timing ablations for tools/ubench_kernels.hip only (the product
+// launches ABL = 0): 1 drops the plane stores (zero-size buffer), 2 the
+// loader's loads and upsample, 4 the row pass
+template <int R, int P = kProfileOpenCV, int ABL = 0>
+__global__ __launch_bounds__(256, (StripGeom<R, 32, 8>::MINB)) void k_seed_strip(const uint8_t* __restrict__ frames,
+                                                                        size_t frame_pitch, size_t row_stride, int sh,
+                                                                        int sw, float* __restrict__ dst,
+                                                                        size_t dst_img_stride, int W, int H, int pitch,
+                                                                        const BlurTaps taps, int ya, int yb, int seg) {
+    using G = StripGeom<R, 32, 8>;  // 8-column halo for any R <= 8: 144 = 12 x 12 window columns
+    using L = SeedLoader<G, P, (ABL & 2) != 0>;
+    __shared__ __attribute__((aligned(16))) float lds[G::LDS_FLOATS];
+    __shared__ typename L::Tables tabs;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const TileId tile = xcd_tile();
+    const int x0 = tile.x * G::TW;
+    const int ys = ya + tile.y * seg, ye = min(yb, ys + seg);
+    if (ys >= ye) return;
+    const __amdgpu_buffer_rsrc_t rd =
+        uniform_rsrc(dst + (size_t)tile.z * dst_img_stride, (ABL & 1) ? 0u : (uint32_t)H * (uint32_t)pitch * 4u);
+    L::tables(tabs, x0 - G::HWL, W, sw);
+    __syncthreads();
+    L ld;
+    ld.init(frames + (size_t)tile.z * frame_pitch, row_stride, sh, sw, W, H, x0 - G::HWL, tabs, lane, wv);
     int prow, pq;  // row-pass lane map
     strip_rowpass_map(lane, wv, prow, pq);
     const int nsteps = (ye - ys + G::S - 1) / G::S;
     const int gb = ys - R;  // window row of chunk 0
-    prefetch(gb);
-    store(lds, gb);
-    prefetch(gb + G::S);
+    ld.prefetch(gb);
+    ld.store(lds, gb);
+    ld.prefetch(gb + G::S);
     drop_stores<G::VB>(rd);
     __syncthreads();
     if constexpr ((ABL & 4) == 0) strip_rowpass<G, P>(lds, taps, prow, pq);
@@ -1365,16 +1390,16 @@ __global__ __launch_bounds__(256, (StripGeom<R, 32, 8>::MINB)) void k_seed_strip
         float* sa = lds + (k & 1) * G::SLOT;
         float* sb = lds + ((k + 1) & 1) * G::SLOT;
         __syncthreads();  // column pass k - 1 is done with slot b
-        store(sb, gb + (k + 1) * G::S);
-        if (k + 2 <= nsteps) prefetch(gb + (k + 2) * G::S);
+        ld.store(sb, gb + (k + 1) * G::S);
+        if (k + 2 <= nsteps) ld.prefetch(gb + (k + 2) * G::S);
         __syncthreads();
         if constexpr ((ABL & 4) == 0) strip_rowpass<G, P>(sb, taps, prow, pq);
         __syncthreads();
         const int y = ys + k * G::S;
         switch (wv) {
-#define COLPASS(w)                                                                                              \
-    case w:                                                                                                     \
-        strip_colpass<G, P, w, false>(sa, sb, taps, lane, y, ye, x0, W, pitch, rd, rd, 0, 0, 0); \
+#define COLPASS(w)                                                                                    \
+    case w:                                                                                           \
+        strip_colpass<G, P, w, false>(sa, sb, taps, lane, y, ye, x0, W, pitch, rd, rd, 0, 0, 0);     \
         break;
             COLPASS(0) COLPASS(1) COLPASS(2) COLPASS(3)
             default:
