@@ -1559,7 +1559,7 @@ static void launch_blur_strip_rp(const BlurLaunch& L, dim3 grid, int ya, int yb,
 // tuning knob, read per launch)
 static long strip_wg_target() {
     const char* e = getenv("SIFT_MI_STRIP_WG");
-    return e ? std::max(1L, atol(e)) : 12288L;
+    return e ? std::max(1L, atol(e)) : 6144L;
 }
 
 // Row segments of a strip launch over `rows` rows with `per` strips x frames:
@@ -1588,9 +1588,11 @@ static void launch_blur_strip_r(const BlurLaunch& L, hipStream_t st) {
     const int yb = L.y1 > L.y0 ? std::min(L.y1, L.H) : L.H;
     if (yb <= ya) return;
     const int strips = (L.W + G::TW - 1) / G::TW;
-    // segments: ~12 k workgroups per launch (a few dozen per CU: the last
-    // round of equal-sized workgroups is a small fraction), none shorter than
-    // two chunks (each segment re-filters its 2R halo rows)
+    // segments: ~6 k workgroups per launch (a few dozen per CU: the last
+    // round of equal-sized workgroups is a small fraction; round 3: 6 k beat
+    // 12 k by 1-2% of pyramid time, octave 0 of 1080p in 4 segments instead
+    // of 7; 3 k, 4 k, 8 k within noise of 6 k), none shorter than two chunks
+    // (each segment re-filters its 2R halo rows)
     const int rows = yb - ya;
     const int seg = strip_segment_rows(rows, (long)strips * L.n_img);
     const int nseg = (rows + seg - 1) / seg;
