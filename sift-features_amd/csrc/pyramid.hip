@@ -555,6 +555,40 @@ __device__ __forceinline__ void strip_colpass(const float* sa, const float* sb, 
     }
 }
 
+// Column pass of wave WV with every row reference clamped to [0, H): the
+// imageproc pair kernel's border chunks, whose G_s rows outside the image
+// (computed from clamped input rows) are not copies of the edge rows as
+// clamp-to-edge needs -- so they are never read: each tap reads the clamped
+// row of the chunk window (window row 0 = G_s row y - R) instead.  Imageproc
+// chain (acc = acc + v * k from the first tap), dynamic LDS offsets.
+template <class G>
+__device__ __forceinline__ void strip_colpass_clamped(const float* sa, const float* sb, const BlurTaps& taps,
+                                                      int lane, int wv, int y, int ye, int x0, int W, int H,
+                                                      int pitch, __amdgpu_buffer_rsrc_t rd) {
+    constexpr int R = G::R;
+    const int y0 = y + wv * G::VB;
+    const int nrow = min(G::VB, ye - y0);
+    const int gx = x0 + 2 * lane;
+    const uint32_t lane_col = (uint32_t)(gx * 4), lane_bad = gx < W ? 0u : kStoreDrop;
+    for (int o = 0; o < G::VB; o++) {
+        const int gy = y0 + o;
+        f2v acc = {0.0f, 0.0f};
+#pragma unroll
+        for (int t = 0; t <= 2 * R; t++) {
+            const int L = min(max(gy - R + t, 0), H - 1) - (y - R);
+            const float* rp = L < G::S ? sa + L * G::IWP : sb + (L - G::S) * G::IWP;
+            const f2v v = *(const lds_f2v*)(rp + 2 * lane);
+            const float k = taps.k[t > R ? t - R : R - t];
+            const f2v kt = {k, k};
+            acc = t == 0 ? v * kt : acc + v * kt;
+        }
+        const uint32_t row_bad = o < nrow ? 0u : kStoreDrop;
+        __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, acc), rd,
+                                              ((uint32_t)(gy * pitch * 4) + lane_col) | lane_bad | row_bad, 0,
+                                              SIFT_STORE_CPOL);
+    }
+}
+
 // grid: (strips, segments, frames); segment sg covers output rows
 // [ya + sg * seg, min(yb, ya + (sg + 1) * seg)).  G_{s-1} / G_s planes are
 // H * pitch floats (< 2^31 bytes: checked by the launcher).
@@ -667,7 +701,7 @@ struct PairGeom {
     static constexpr int NBR = NBW + 1;
     static constexpr int LDS_FLOATS = 2 * GA::SLOT + NBR * GB::SLOT;
     static constexpr int MINB = 163840 / (4 * LDS_FLOATS) < 4 ? 163840 / (4 * LDS_FLOATS) : 4;
-    static_assert(GA::HWL == 8 && GA::NCW == 2, "A: radius <= 8");
+    static_assert(GA::HWL <= 8 && GA::NCW == 2, "A: radius <= 8");
     static_assert(NBW == 2, "B: radius <= 8 (two-chunk column windows)");
     static_assert(GB::IWV >= GA::TW, "B's window holds A's 128 columns");
 };
@@ -676,7 +710,7 @@ struct PairGeom {
 // the chunk + WV*VB) of columns xa + 2*lane into B's slot, and into HBM for
 // the rows [gys, gye) and columns [X, min(X + TWO, W)) this strip owns (NXT:
 // with the next octave's base, nearest 1/2 = pixel (2x, 2y)).
-template <class GA, int WV, bool NXT>
+template <class GA, int WV, bool NXT, int P = kProfileOpenCV>
 __device__ __forceinline__ void pair_colpass_a(const float* sa, const float* sb, float* bslot, int bip,
                                                const BlurTaps& taps, int lane, int y, int gys, int gye, int xa,
                                                int hb, int W, int pitch, int two, __amdgpu_buffer_rsrc_t rd,
@@ -698,11 +732,23 @@ __device__ __forceinline__ void pair_colpass_a(const float* sa, const float* sb,
 
 #pragma unroll
     for (int o = 0; o < GA::VB; o++) {
-        f2v acc = v[o + R] * k0;
+        f2v acc;
+        if constexpr (P == kProfileOpenCV) {
+            acc = v[o + R] * k0;
 #pragma unroll
-        for (int t = 1; t <= R; t++) {
-            const f2v kt = {taps.k[t], taps.k[t]};
-            acc = __builtin_elementwise_fma(v[o + R + t] + v[o + R - t], kt, acc);
+            for (int t = 1; t <= R; t++) {
+                const f2v kt = {taps.k[t], taps.k[t]};
+                acc = __builtin_elementwise_fma(v[o + R + t] + v[o + R - t], kt, acc);
+            }
+        } else {
+            const f2v kr = {taps.k[R], taps.k[R]};
+            acc = v[o] * kr;
+#pragma unroll
+            for (int t = 1; t <= 2 * R; t++) {
+                const float k = taps.k[t > R ? t - R : R - t];
+                const f2v kt = {k, k};
+                acc = acc + v[o + t] * kt;
+            }
         }
         *(f2v*)(bslot + (WV * GA::VB + o) * bip + 2 * lane) = acc;
         // predicated by out-of-range offsets, a static store count (see strip_colpass)
@@ -722,7 +768,7 @@ __device__ __forceinline__ void pair_colpass_a(const float* sa, const float* sb,
     }
 }
 
-template <int Ra, int Rb, bool NXT>
+template <int Ra, int Rb, bool NXT, int P = kProfileOpenCV>
 __global__ __launch_bounds__(256, (PairGeom<Ra, Rb>::MINB)) void k_blur2_strip(
     const float* __restrict__ src, size_t img_stride, float* __restrict__ dst_a, float* __restrict__ dst_b,
     float* __restrict__ nxt, size_t nxt_img_stride, int pitch_n, int wn, int hn, int W, int H, int pitch,
@@ -732,6 +778,7 @@ __global__ __launch_bounds__(256, (PairGeom<Ra, Rb>::MINB)) void k_blur2_strip(
     using GB = typename Q::GB;
     constexpr int S = GA::S;
     constexpr int NBW = Q::NBW, NBR = Q::NBR;
+    static_assert(P == kProfileOpenCV || !NXT, "imageproc pairs: no next-octave output");
     __shared__ __attribute__((aligned(16))) float lds[Q::LDS_FLOATS];
     float* aslot = lds;                   // 2 x GA::SLOT: A's input chunks (row-filtered in place)
     float* bslot = lds + 2 * GA::SLOT;    // NBR x GB::SLOT: G_s chunks (row-filtered in place)
@@ -776,7 +823,8 @@ __global__ __launch_bounds__(256, (PairGeom<Ra, Rb>::MINB)) void k_blur2_strip(
             const int x = j < Q::HB ? xa + j : W + (j - Q::HB);  // left halo xa .. xa + HB - 1, right W .. W + HB - 1
             act[it] = e < NE && (j < Q::HB ? (fix_l && x < 0) : (fix_r && x - xa < GA::TW));
             dst[it] = r * GB::IWP + (x - xa);
-            val[it] = act[it] ? slot[r * GB::IWP + (reflect101(x, W) - xa)] : 0.0f;
+            const int sx = P == kProfileOpenCV ? reflect101(x, W) : clamp_idx(x, W);
+            val[it] = act[it] ? slot[r * GB::IWP + (sx - xa)] : 0.0f;
         }
         __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
         __builtin_amdgcn_wave_barrier();
@@ -792,23 +840,23 @@ __global__ __launch_bounds__(256, (PairGeom<Ra, Rb>::MINB)) void k_blur2_strip(
     const int ng = nout + NBW - 2, na = ng + 1;
     const int ga = ys - Rb - Ra;  // first A-input row (chunk 0)
     float4 pre[GA::LPT];
-    strip_load<Ra, kProfileOpenCV, GA>(pre, rs, voff, cols_in, ga, xa, W, H, pitch);
+    strip_load<Ra, P, GA>(pre, rs, voff, cols_in, ga, xa, W, H, pitch);
     strip_store<GA>(pre, aslot);
-    strip_load<Ra, kProfileOpenCV, GA>(pre, rs, voff, cols_in, ga + S, xa, W, H, pitch);
+    strip_load<Ra, P, GA>(pre, rs, voff, cols_in, ga + S, xa, W, H, pitch);
     __syncthreads();
-    strip_rowpass<GA, kProfileOpenCV>(aslot, taps_a, prow, pq);
+    strip_rowpass<GA, P>(aslot, taps_a, prow, pq);
     for (int k = 0; k <= nout + NBW - 1; k++) {
         __syncthreads();  // P1
         if (k + 1 <= na) {
             strip_store<GA>(pre, aslot + ((k + 1) & 1) * GA::SLOT);
-            if (k + 2 <= na) strip_load<Ra, kProfileOpenCV, GA>(pre, rs, voff, cols_in, ga + (k + 2) * S, xa, W, H, pitch);
+            if (k + 2 <= na) strip_load<Ra, P, GA>(pre, rs, voff, cols_in, ga + (k + 2) * S, xa, W, H, pitch);
         }
         __syncthreads();  // P2
-        if (k + 1 <= na) strip_rowpass<GA, kProfileOpenCV>(aslot + ((k + 1) & 1) * GA::SLOT, taps_a, prow, pq);
+        if (k + 1 <= na) strip_rowpass<GA, P>(aslot + ((k + 1) & 1) * GA::SLOT, taps_a, prow, pq);
         if (k >= 1 && k - 1 <= ng) {
             float* s1 = bslot + ((k - 1) % NBR) * GB::SLOT;
             fixup(s1);
-            strip_rowpass<GB, kProfileOpenCV>(s1, taps_b, prow, pq);
+            strip_rowpass<GB, P>(s1, taps_b, prow, pq);
         }
         // column pass B -> G_{s+1} rows of output chunk k - NBW (its G_s
         // chunks are row-filtered)
@@ -818,14 +866,23 @@ __global__ __launch_bounds__(256, (PairGeom<Ra, Rb>::MINB)) void k_blur2_strip(
             const float* s0 = bslot + (j % NBR) * GB::SLOT;
             const float* s1 = bslot + ((j + 1) % NBR) * GB::SLOT;
             const int y = ys + j * S;
+            // imageproc: a wave whose taps reach rows outside the image reads
+            // clamped rows instead (uniform branch; first / last chunks)
+            if constexpr (P == kProfileImageproc) {
+                const int y0 = y + wv * GB::VB;
+                if (y0 - Rb < 0 || y0 + GB::VB - 1 + Rb > H - 1) {
+                    if (lane < Q::TWO / 2)
+                        strip_colpass_clamped<GB>(s0, s1, taps_b, lane, wv, y, ye, X, W, H, pitch, rb);
+                    return;
+                }
+            }
             // after B's in-place row pass slot column c is output column X + c: lanes 0 .. TWO/2 - 1 are
             // this strip's columns (the rest read the junk past A's 128 columns)
             switch (wv) {
 #define COLB(w)                                                                                                  \
     case w:                                                                                                      \
         if (lane < Q::TWO / 2)                                                                                   \
-            strip_colpass<GB, kProfileOpenCV, w, false>(s0, s1, taps_b, lane, y, ye, X, W, pitch, rb, rb, 0, 0,  \
-                                                        0);                                                      \
+            strip_colpass<GB, P, w, false>(s0, s1, taps_b, lane, y, ye, X, W, pitch, rb, rb, 0, 0, 0);           \
         break;
                 COLB(0) COLB(1) COLB(2) COLB(3)
                 default:
@@ -842,7 +899,7 @@ __global__ __launch_bounds__(256, (PairGeom<Ra, Rb>::MINB)) void k_blur2_strip(
             switch (wv) {
 #define COLA(w)                                                                                                       \
     case w:                                                                                                           \
-        pair_colpass_a<GA, w, NXT>(s0, s1, dstb, GB::IWP, taps_a, lane, y, ys, ye, xa, Q::HB, W, pitch, Q::TWO, ra,   \
+        pair_colpass_a<GA, w, NXT, P>(s0, s1, dstb, GB::IWP, taps_a, lane, y, ys, ye, xa, Q::HB, W, pitch, Q::TWO, ra,\
                                    rn, pitch_n, wn, hn);                                                              \
         break;
                 COLA(0) COLA(1) COLA(2) COLA(3)
@@ -1605,21 +1662,26 @@ static void launch_blur_strip_r(const BlurLaunch& L, hipStream_t st) {
 
 static bool strip_blur_enabled();
 
-template <int Ra, int Rb>
+template <int Ra, int Rb, int P = kProfileOpenCV>
 static void launch_blur2_rr(const BlurLaunch& A, const BlurLaunch& B, hipStream_t st) {
     using Q = PairGeom<Ra, Rb>;
     const int strips = (A.W + Q::TWO - 1) / Q::TWO;
     const int seg = strip_segment_rows(A.H, (long)strips * A.n_img);
     const int nseg = (A.H + seg - 1) / seg;
     const dim3 grid(strips, nseg, A.n_img);
-    if (A.nxt)
+    if constexpr (P == kProfileImageproc) {
+        hipLaunchKernelGGL((k_blur2_strip<Ra, Rb, false, P>), grid, dim3(256), 0, st, A.src, A.src_img_stride, A.dst,
+                           B.dst, A.nxt, A.nxt_img_stride, A.pitch_n, A.wn, A.hn, A.W, A.H, A.pitch, A.taps, B.taps,
+                           0, A.H, seg);
+    } else if (A.nxt) {
         hipLaunchKernelGGL((k_blur2_strip<Ra, Rb, true>), grid, dim3(256), 0, st, A.src, A.src_img_stride, A.dst,
                            B.dst, A.nxt, A.nxt_img_stride, A.pitch_n, A.wn, A.hn, A.W, A.H, A.pitch, A.taps, B.taps,
                            0, A.H, seg);
-    else
+    } else {
         hipLaunchKernelGGL((k_blur2_strip<Ra, Rb, false>), grid, dim3(256), 0, st, A.src, A.src_img_stride, A.dst,
                            B.dst, A.nxt, A.nxt_img_stride, A.pitch_n, A.wn, A.hn, A.W, A.H, A.pitch, A.taps, B.taps,
                            0, A.H, seg);
+    }
 }
 
 // SIFT_MI_PAIR=0 disables the pair kernel (A/B and test knob, read per launch)
@@ -1632,8 +1694,7 @@ int launch_blur_pair(int ra, int rb, const BlurLaunch& A, const BlurLaunch& B, h
     // A: G_{s-1} -> G_s, B: G_s -> G_{s+1} of one octave arena (same geometry
     // and image stride); whole planes, no DoG / next-octave output
     // (A may write the next octave's base: blur s = 3 of a pair (3, 4))
-    const bool ok = A.profile == kProfileOpenCV && B.profile == kProfileOpenCV && !A.dog && !B.dog &&
-                    !B.nxt && A.y1 <= A.y0 && B.y1 <= B.y0 && A.dst && B.dst && B.src == A.dst && A.W == B.W &&
+    const bool ok = A.profile == B.profile && !A.dog && !B.dog && !B.nxt && A.y1 <= A.y0 && B.y1 <= B.y0 && A.dst && B.dst && B.src == A.dst && A.W == B.W &&
                     A.H == B.H && A.pitch == B.pitch && A.src_img_stride == A.dst_img_stride &&
                     B.src_img_stride == A.src_img_stride && B.dst_img_stride == A.src_img_stride && A.W >= 64 &&
                     A.H >= 64 && (uint64_t)A.H * (uint64_t)A.pitch * 4 < (1ull << 31) && strip_blur_enabled() &&
@@ -1643,6 +1704,12 @@ int launch_blur_pair(int ra, int rb, const BlurLaunch& A, const BlurLaunch& B, h
     // column windows at 16-row chunks) was built, exact and slower than the
     // two single launches (1.75 vs 1.62 ms per 64 frames of 3840x2160, round
     // 2), and was removed.
+    if (A.profile == kProfileImageproc) {
+        // imageproc's clamp-to-edge chain: rows outside the image are read
+        // clamped (strip_colpass_clamped); blurs 1, 2 are radii 3, 4
+        if (ra == 3 && rb == 4 && !A.nxt) { launch_blur2_rr<3, 4, kProfileImageproc>(A, B, st); return 0; }
+        return -1;
+    }
     if (ra == 5 && rb == 6) { launch_blur2_rr<5, 6>(A, B, st); return 0; }
     return -1;
 }

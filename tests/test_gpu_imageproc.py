@@ -70,15 +70,17 @@ def test_ip_batch_and_limit(pkg, ctx_ip, oracle):
         assert_parity(pkg, res, kp_o, desc_o, ext_o)
 
 
-@pytest.mark.parametrize("kernel", ["strip", "tile", "notail"])
+@pytest.mark.parametrize("kernel", ["strip", "tile", "notail", "nopair"])
 @pytest.mark.parametrize("name", ["synth_640x480", "synth_301x207", "synth_1000x333", "synth_90x700",
                                   "synth_2000x40", "synth_97x61"])
 def test_ip_pyramid_kernels(ctx_ip, oracle, monkeypatch, kernel, name):
     """The imageproc profile's kernel families bit for bit against the oracle:
     "strip" (k_seed_strip<3, imageproc>: the Triangle 2x upsample, vertical then
-    horizontal, clamped, in the strip loader; clamp-to-edge strip blurs and
-    the tail kernel), "tile" (k_seed_ip and the tile blurs), "notail" (per-blur
-    launches for the small octaves)."""
+    horizontal, clamped, in the strip loader; the k_blur2_strip<3, 4>
+    imageproc pair for G_1, G_2, whose border chunks read clamped G_1 rows;
+    clamp-to-edge strip blurs and the tail kernel), "tile" (k_seed_ip and the
+    tile blurs), "notail" (per-blur launches for the small octaves), "nopair"
+    (single-blur strips for G_1, G_2)."""
     from test_gpu_parity import _KERNEL_ENV, _extra
     for k, v in _KERNEL_ENV[kernel].items():
         monkeypatch.setenv(k, v)
