@@ -12,6 +12,7 @@
 #include <cmath>
 #include <cstdio>
 #include <cstring>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -1406,6 +1407,53 @@ int upload_frames(sift_mi_ctx* c, const uint8_t* const* frames, uint32_t n, uint
 // ===========================================================================
 // C ABI
 // ===========================================================================
+namespace {
+// Process-wide pool of the contexts' streams (per device, in creation
+// order).  HIP maps streams onto a few hardware queues (GPU_MAX_HW_QUEUES,
+// 4 by default) as they are created; a context created after another was
+// destroyed would otherwise get a different, possibly colliding mapping
+// (measured: one 1080p frame per call 0.69 ms in a fresh process, 0.89 ms
+// after a closed batch context -- the octave overlap's two streams had landed
+// on one queue).  A closed context returns its streams here; the next one
+// takes the same stream objects back, so every context sees the queue
+// mapping of the first.
+struct StreamPool {
+    std::mutex mu;
+    std::vector<std::vector<hipStream_t>> free_sets[64];  // per device: sets of kCtxStreams
+};
+StreamPool& stream_pool() {
+    static StreamPool* p = new StreamPool();  // never destroyed: streams live until process exit
+    return *p;
+}
+// the order matters for the queue mapping: lane 0, lane 1, lane 0's aux,
+// the copy stream, lane 1's aux (with 4 queues only the last shares one)
+constexpr int kCtxStreams = 5;
+bool take_streams(int dev, hipStream_t (&out)[kCtxStreams]) {
+    StreamPool& P = stream_pool();
+    {
+        std::lock_guard<std::mutex> g(P.mu);
+        auto& fs = P.free_sets[dev & 63];
+        if (!fs.empty()) {
+            for (int i = 0; i < kCtxStreams; i++) out[i] = fs.back()[i];
+            fs.pop_back();
+            return true;
+        }
+    }
+    for (int i = 0; i < kCtxStreams; i++) {
+        if (hipStreamCreateWithFlags(&out[i], hipStreamNonBlocking) != hipSuccess) {
+            for (int k = 0; k < i; k++) (void)hipStreamDestroy(out[k]);
+            return false;
+        }
+    }
+    return true;
+}
+void give_streams(int dev, const hipStream_t (&in)[kCtxStreams]) {
+    StreamPool& P = stream_pool();
+    std::lock_guard<std::mutex> g(P.mu);
+    P.free_sets[dev & 63].emplace_back(in, in + kCtxStreams);
+}
+}  // namespace
+
 extern "C" {
 
 const char* sift_mi_version(void) { return "sift_mi 0.3.0 (gfx950)"; }
@@ -1427,15 +1475,18 @@ int sift_mi_create(int device_ordinal, sift_mi_profile profile, sift_mi_ctx** ou
     sift_mi_ctx* c = new sift_mi_ctx();
     c->device = device_ordinal;
     c->profile = profile;
-    if (hipStreamCreateWithFlags(&c->own, hipStreamNonBlocking) != hipSuccess) {
+    hipStream_t ss[kCtxStreams];
+    if (!take_streams(device_ordinal, ss)) {
         delete c;
         return fail(SIFT_MI_EHIP, "hipStreamCreate failed");
     }
+    c->own = ss[0];
+    c->own2 = ss[1];
+    c->aux[0] = ss[2];
+    c->cstream = ss[3];
+    c->aux[1] = ss[4];
     c->stream = c->own;
-    bool ok = hipStreamCreateWithFlags(&c->cstream, hipStreamNonBlocking) == hipSuccess &&
-              hipStreamCreateWithFlags(&c->own2, hipStreamNonBlocking) == hipSuccess;
-    ok = ok && hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) == hipSuccess;
-    for (auto& a : c->aux) ok = ok && hipStreamCreateWithFlags(&a, hipStreamNonBlocking) == hipSuccess;
+    bool ok = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) == hipSuccess;
     for (auto& lane : c->oct_ev)
         for (auto& e : lane) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
     if (const char* e = getenv("SIFT_MI_OCT_OVERLAP")) c->oct_overlap = strcmp(e, "0") != 0;
@@ -1479,17 +1530,16 @@ void sift_mi_destroy(sift_mi_ctx* c) {
     for (auto& lane : c->oct_ev)
         for (auto& e : lane)
             if (e) (void)hipEventDestroy(e);
-    for (auto& a : c->aux)
-        if (a) (void)hipStreamDestroy(a);
     c->r_kp.release();
     c->r_desc.release();
     c->r_key.release();
     c->h_kp.release();
     c->h_desc.release();
     c->h_key.release();
-    if (c->cstream) (void)hipStreamDestroy(c->cstream);
-    if (c->own2) (void)hipStreamDestroy(c->own2);
-    if (c->own) (void)hipStreamDestroy(c->own);
+    if (c->own) {  // the streams go back to the pool (synchronised above)
+        const hipStream_t ss[kCtxStreams] = {c->own, c->own2, c->aux[0], c->cstream, c->aux[1]};
+        give_streams(c->device, ss);
+    }
     delete c;
 }
 
