@@ -449,10 +449,6 @@ __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img
         if (i + lane < PRIV_STRIDE * NS / 4) reinterpret_cast<float4*>(sc.h)[i + lane] = make_float4(0.f, 0.f, 0.f, 0.f);
     // samples outside the image (0 < y + yi < height - 1, 0 < x + xi < width - 1
     // fails) are not enumerated
-#ifdef SIFT_EXP_NO_SHRINK  // A/B only
-    build_row_table<false>(sc.rowlo, sc.rowpre, radius, cos_s, sin_s, lane, 1 - x, width - 2 - x, 1 - y, height - 2 - y);
-    if (0)
-#endif
     build_row_table<true>(sc.rowlo, sc.rowpre, radius, cos_s, sin_s, lane, 1 - x, width - 2 - x, 1 - y, height - 2 - y);
     const int total = (kAblate & 64) ? 0 : sc.rowpre[n];  // kAblate bit 6: no samples (per-keypoint overhead)
     if (n_samples) *n_samples += (uint32_t)total;
@@ -608,11 +604,7 @@ __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img
     }
     if ((lane & 3) == 0) acc0 += acc8;
     if (kAblate & 1) acc0 += sink.x + sink.y;
-#ifdef SIFT_EXP_CHUNK_NORM  // A/B only
-    describe_normalize<false>(acc0, acc1, out, lane);
-#else
     describe_normalize<true>(acc0, acc1, out, lane);
-#endif
 }
 
 // kMode 0: bit-exact (describe_wave_exact); 1 / 2 / 4: fast path with that

@@ -527,31 +527,15 @@ __global__ __launch_bounds__(256, SIFT_ORIENT_MIN_WAVES) void k_orient(const Ori
                 nin = (y1 >= y0 && x1 >= x0) ? (uint32_t)((y1 - y0 + 1) * (x1 - x0 + 1)) : 0u;
             }
         }
-        __syncthreads();
+        // the wave's own sample list only: a wave barrier (the block syncs at
+        // the slot atomic below), so a wave with a small patch sums while the
+        // others still sample
+        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
         // sequential per-bin sums (lane = bin); inactive waves run on an empty list
         if (!active) N = 0;
         float acc = 0.0f;
-#ifdef SIFT_EXP_ORIENT_DENSE  // round-2 dense scan (A/B only): every bin lane reads every sample
-        {
-            const float4* v4 = reinterpret_cast<const float4*>(sval[wave]);
-            const uint4* b16 = reinterpret_cast<const uint4*>(sbin[wave]);
-            const uint32_t me = (uint32_t)lane;
-            int j = 0;
-            for (; j + 16 <= N; j += 16) {
-                const uint4 bb = b16[j >> 4];
-                const float4 vv[4] = {v4[(j >> 2) + 0], v4[(j >> 2) + 1], v4[(j >> 2) + 2], v4[(j >> 2) + 3]};
-                const uint32_t w[4] = {bb.x, bb.y, bb.z, bb.w};
-#pragma unroll
-                for (int q = 0; q < 4; q++) {
-                    acc += ((w[q] & 0xff) == me) ? vv[q].x : 0.0f;
-                    acc += (((w[q] >> 8) & 0xff) == me) ? vv[q].y : 0.0f;
-                    acc += (((w[q] >> 16) & 0xff) == me) ? vv[q].z : 0.0f;
-                    acc += ((w[q] >> 24) == me) ? vv[q].w : 0.0f;
-                }
-            }
-            for (; j < N; j++) acc += ((uint32_t)sbin[wave][j] == me) ? sval[wave][j] : 0.0f;
-        }
-#else
         // Per 64-sample batch, lane b < 36 gets the mask of the batch's samples
         // in bin b from six ballots of the bin bits, then adds exactly those
         // samples in index order: the reference's per-bin order (bit-identical)
@@ -592,7 +576,6 @@ __global__ __launch_bounds__(256, SIFT_ORIENT_MIN_WAVES) void k_orient(const Ori
             run(lane < kOriBins ? (uint32_t)m : 0u, sval[wave] + t);
             run(lane < kOriBins ? (uint32_t)(m >> 32) : 0u, sval[wave] + t + 32);
         }
-#endif
         // circular [1,4,6,4,1]/16 smoothing (src/lib.rs:742-755)
         const int k = lane < kOriBins ? lane : 0;
         const float rm2 = __shfl(acc, (k + kOriBins - 2) % kOriBins);

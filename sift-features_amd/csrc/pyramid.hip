@@ -1830,23 +1830,28 @@ int launch_seed(int R, const SeedLaunch& L, hipStream_t st) {
 // pass of their own), so every tap read is a plain offset, and each thread
 // carries four independent chains (four outputs of a row / of a column).
 // LDS layout (floats), with Rm the largest radius of the octave's blurs:
-//   A, B  G_{s-1} / G_s:     H rows of W + 2 Rm (column halos), x at + Rm
-//   T     row-pass output:   H + 2 Rm rows of W (row halos), y at + Rm
+//   A, B  G_{s-1} / G_s:     H rows of pitch PA = (W + 2 Rm) | 1 (column halos), x at + Rm
+//   T     row-pass output:   H + 2 Rm rows of pitch TP = W | 1 (row halos), y at + Rm
 //   N     next octave G_0:   (H / 2) x (W / 2), dense
+// Odd pitches: the row pass maps consecutive lanes to consecutive rows (same
+// columns), so its reads of A and writes of T hit distinct banks; the column
+// pass maps lanes along a row.
 // ---------------------------------------------------------------------------
 template <int P>
 __device__ __forceinline__ int tail_index(int p, int n) {
     return P == kProfileOpenCV ? reflect101(p, n) : clamp_idx(p, n);
 }
 
+__host__ __device__ inline int tail_pa(int W, int rm) { return (W + 2 * rm) | 1; }
+__host__ __device__ inline int tail_tp(int W) { return W | 1; }
 __host__ __device__ inline int tail_lds_floats(int W, int H, int rm) {
-    return 2 * (W + 2 * rm) * H + W * (H + 2 * rm) + (W / 2) * (H / 2);
+    return 2 * tail_pa(W, rm) * H + tail_tp(W) * (H + 2 * rm) + (W / 2) * (H / 2);
 }
 
 // halo columns [-R, 0) and [W, W + R) of every row of X (pitch W + 2 Rm)
 template <int P>
 __device__ __forceinline__ void tail_fill_cols(float* X, int W, int H, int Rm, int R) {
-    const int PA = W + 2 * Rm;
+    const int PA = tail_pa(W, Rm);
     for (int i = threadIdx.x; i < H * 2 * R; i += 1024) {
         const int y = i / (2 * R), j = i - y * (2 * R);
         const int p = j < R ? j - R : W + j - R;
@@ -1864,14 +1869,15 @@ __device__ __forceinline__ void tail_blur_r(float* __restrict__ A, float* __rest
                                             float* __restrict__ g, int pitch, bool nxt, float* __restrict__ N,
                                             float* __restrict__ gn, int wn, int hn, int pn) {
     constexpr int Q = 4;
-    const int PA = W + 2 * Rm;
+    const int PA = tail_pa(W, Rm), TP = tail_tp(W);
     // row pass (A's halo columns are in place): fma chain from the leftmost
-    // tap (OpenCV) / unfused chain (imageproc); item = (row, 4 columns).  The
-    // last item of a row may read past its halo (into the next row / buffer:
-    // still LDS) for columns >= W, which are not stored.
+    // tap (OpenCV) / unfused chain (imageproc); item = (row, 4 columns),
+    // consecutive items down a column of items (lanes on distinct banks).
+    // The last item of a row may read past its halo (into the next row /
+    // buffer: still LDS) for columns >= W, which are not stored.
     const int qw = (W + Q - 1) / Q;
     for (int i = threadIdx.x; i < H * qw; i += 1024) {
-        const int y = i / qw, x0 = (i - y * qw) * Q;
+        const int xq = i / H, y = i - xq * H, x0 = xq * Q;
         const float* p = A + y * PA + Rm + x0 - R;
         float v[Q + 2 * R];
 #pragma unroll
@@ -1886,7 +1892,7 @@ __device__ __forceinline__ void tail_blur_r(float* __restrict__ A, float* __rest
             for (int q = 0; q < Q; q++)
                 acc[q] = P == kProfileOpenCV ? __builtin_fmaf(v[q + t], kt, acc[q]) : acc[q] + v[q + t] * kt;
         }
-        float* o = T + (y + Rm) * W + x0;
+        float* o = T + (y + Rm) * TP + x0;
 #pragma unroll
         for (int q = 0; q < Q; q++)
             if (x0 + q < W) o[q] = acc[q];
@@ -1896,7 +1902,7 @@ __device__ __forceinline__ void tail_blur_r(float* __restrict__ A, float* __rest
     for (int i = threadIdx.x; i < 2 * R * W; i += 1024) {
         const int j = i / W, x = i - j * W;
         const int p = j < R ? j - R : H + j - R;
-        T[(p + Rm) * W + x] = T[(tail_index<P>(p, H) + Rm) * W + x];
+        T[(p + Rm) * TP + x] = T[(tail_index<P>(p, H) + Rm) * TP + x];
     }
     __syncthreads();
     // column pass: centre product + fma of the (below + above) pair sums
@@ -1906,10 +1912,10 @@ __device__ __forceinline__ void tail_blur_r(float* __restrict__ A, float* __rest
     constexpr int par = P == kProfileOpenCV ? 0 : 1;  // nearest 1/2: (2x, 2y) / (2x + 1, 2y + 1)
     for (int i = threadIdx.x; i < W * qh; i += 1024) {
         const int yq = i / W, x = i - yq * W, y0 = yq * Q;
-        const float* p = T + (y0 - R + Rm) * W + x;  // window row 0 = image row y0 - R
+        const float* p = T + (y0 - R + Rm) * TP + x;  // window row 0 = image row y0 - R
         float v[Q + 2 * R];
 #pragma unroll
-        for (int j = 0; j < Q + 2 * R; j++) v[j] = p[j * W];
+        for (int j = 0; j < Q + 2 * R; j++) v[j] = p[j * TP];
         float acc[Q];
         if constexpr (P == kProfileOpenCV) {
 #pragma unroll
@@ -1981,11 +1987,11 @@ __global__ __launch_bounds__(1024) void k_octave_tail(const TailLaunch L) {
     int Rm = 0;
     for (int s = 1; s < kImagesPerOctave; s++) Rm = max(Rm, L.r[s]);
     for (int o = L.o0; o < L.n_oct; o++) {
-        const int W = L.ow[o], H = L.oh[o], pitch = L.pitch[o], PA = W + 2 * Rm;
-        float* A = lds;                    // G_{s-1}
-        float* B = A + PA * H;             // G_s
-        float* T = B + PA * H;             // row-pass output
-        float* N = T + W * (H + 2 * Rm);   // next octave's G_0
+        const int W = L.ow[o], H = L.oh[o], pitch = L.pitch[o], PA = tail_pa(W, Rm);
+        float* A = lds;                         // G_{s-1}
+        float* B = A + PA * H;                  // G_s
+        float* T = B + PA * H;                  // row-pass output
+        float* N = T + tail_tp(W) * (H + 2 * Rm);  // next octave's G_0
         float* g = L.gauss[o] + (size_t)b * L.gstride[o];
         const size_t plane = (size_t)pitch * H;
         const bool has_next = o + 1 < L.n_oct;
@@ -1999,7 +2005,7 @@ __global__ __launch_bounds__(1024) void k_octave_tail(const TailLaunch L) {
                 for (int x = tid & 63; x < W; x += 64) A[y * PA + Rm + x] = g[(size_t)y * pitch + x];
         } else {
             const int Wp = L.ow[o - 1], Hp = L.oh[o - 1];
-            const float* Np = lds + 2 * (Wp + 2 * Rm) * Hp + Wp * (Hp + 2 * Rm);
+            const float* Np = lds + 2 * tail_pa(Wp, Rm) * Hp + tail_tp(Wp) * (Hp + 2 * Rm);
             float v[4];  // W * H <= 4096 here (checked by tail_octave_start)
 #pragma unroll
             for (int k = 0; k < 4; k++) {
