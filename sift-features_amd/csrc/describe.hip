@@ -84,8 +84,8 @@ __device__ __forceinline__ int wave_incl_scan(int v) {
 // SHRINK (fast path): the up to 3 end columns of each row that fail the fast
 // path's own f32 region test are dropped here rather than enumerated (the
 // per-sample test stays, so this only removes samples it would reject).
-template <bool SHRINK = false>
-__device__ __forceinline__ void build_row_table(int* rowlo, int* rowpre, int radius, float cos_s, float sin_s,
+template <bool SHRINK = false, class T = int>
+__device__ __forceinline__ void build_row_table(T* rowlo, T* rowpre, int radius, float cos_s, float sin_s,
                                                 int lane, int xmin = INT_MIN, int xmax = INT_MAX,
                                                 int ymin = INT_MIN, int ymax = INT_MAX) {
     const int n = 2 * radius + 1;
@@ -129,14 +129,14 @@ __device__ __forceinline__ void build_row_table(int* rowlo, int* rowpre, int rad
 #pragma unroll
                 for (int k = 0; k < 3; k++) ihi -= (ihi >= ilo && !inside(ihi)) ? 1 : 0;
             }
-            rowlo[row] = ilo;
+            rowlo[row] = (T)ilo;
             cnt[h] = (empty || ihi < ilo) ? 0 : ihi - ilo + 1;
         }
     }
     const int s0 = wave_incl_scan(cnt[0]), s1 = wave_incl_scan(cnt[1]);
     const int t0 = __builtin_amdgcn_readlane(s0, 63);
-    if (lane < n) rowpre[lane + 1] = s0;
-    if (lane + 64 < n) rowpre[lane + 65] = s1 + t0;
+    if (lane < n) rowpre[lane + 1] = (T)s0;
+    if (lane + 64 < n) rowpre[lane + 65] = (T)(s1 + t0);
     if (lane == 0) rowpre[0] = 0;
     wave_sync();
 }
@@ -375,11 +375,14 @@ __device__ __forceinline__ void describe_wave_exact(const float* __restrict__ im
 // sample's 4 slot pairs never alias, so all reads issue before the writes.
 constexpr int PRIV_STRIDE = 16 * 9 + 4 * 2;
 
+// The row table in 16-bit entries (|column| <= 40, prefix counts <= 3223):
+// 10052 B per wave at kShare 4, so 16 waves fit in a CU's 160 KB of LDS (32-bit
+// entries: 10372 B, 15 waves).
 template <int kShare>
 struct DescScratchFast {
     float h[64 / kShare * PRIV_STRIDE];
-    int rowlo[ROWS_MAX];
-    int rowpre[ROWS_MAX + 1];
+    int16_t rowlo[ROWS_MAX];
+    int16_t rowpre[ROWS_MAX + 1];
 };
 
 // atan2(dy, dx) in degrees for a pair of samples: |t| = min/max in [0, 1]
@@ -437,7 +440,8 @@ __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img
     int radius = sat_i32(roundf(kLambdaDescr * scale * 1.41421356237309504880f * (float)(kDescHist + 1) * 0.5f));
     radius = radius < 0 ? 0 : (radius > (ROWS_MAX - 2) / 2 ? (ROWS_MAX - 2) / 2 : radius);
     const float rad = orientation * (3.14159265358979323846f / 180.0f);  // f32::to_radians
-    const float sin_ori = (float)sin((double)rad), cos_ori = (float)cos((double)rad);
+    const float sin_ori = (kAblate & 128) ? __sinf(rad) : (float)sin((double)rad);
+    const float cos_ori = (kAblate & 128) ? __cosf(rad) : (float)cos((double)rad);
     const float sin_s = sin_ori / hist_width, cos_s = cos_ori / hist_width;
     const int n = 2 * radius + 1;
     // bin b of lane l's slice lives at h[b * 64 + l]: every lane's read-add-write

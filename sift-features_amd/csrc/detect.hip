@@ -14,6 +14,7 @@
 // order.  Emission order (octave, s_init, y_init, x_init, peak) is restored
 // by sorting the 64-bit emission keys afterwards (order.hip).
 #include <algorithm>
+#include <type_traits>
 
 #include "sift_common.h"
 #include "sift_kernels.h"
@@ -373,22 +374,27 @@ void launch_refine(const RefineLaunch& L, hipStream_t st) {
 // ---------------------------------------------------------------------------
 // k_orient: one wave per accepted extremum (4 per workgroup).
 // gradient_direction_histogram (src/lib.rs:657-757) + peak selection
-// (src/lib.rs:369-431).  Samples are evaluated 64 at a time into the wave's
-// LDS list in the reference's row-major order; lane k < 36 then sums bin k
-// sequentially over the list (bit-identical to `raw_hist[bin + 2] += w*mag`).
+// (src/lib.rs:369-431).  Samples are evaluated 64 at a time (one per lane) in
+// the reference's row-major order; after each batch lane k < 36 adds the
+// batch's bin-k samples in order (bit-identical to `raw_hist[bin + 2] +=
+// w*mag`), while the next batch's gradient loads are in flight.
 // ---------------------------------------------------------------------------
-constexpr int OR_LDS = 1104;  // >= 33 * 33 samples, a multiple of 16 (16-byte bin reads)
-constexpr int OR_WT = 17 * 18 / 2;  // weight table entries at the largest radius (16)
+constexpr int OR_WT = 17 * 17;  // weight table (|yp|, |xp|) at the largest radius (16)
 
 #ifndef SIFT_ORIENT_SUM_U
 #define SIFT_ORIENT_SUM_U 2  // samples per step of the per-bin sums
 #endif
 #ifndef SIFT_ORIENT_MIN_WAVES
-#define SIFT_ORIENT_MIN_WAVES 6  // 6 waves per SIMD (24 per CU, LDS-bound): -10% orientation time despite a few spills (48 B since the f64 angle pass moved out of the sample loop; 5 waves: no spills, 8% slower)
+#define SIFT_ORIENT_MIN_WAVES 8  // 8 waves per SIMD (64 VGPRs, 10 dwords spilled; no LDS limit since the sample list went): orientation 3.51 ms vs 3.54 at 7 waves, 3.57-3.62 at 6 (128 1080p frames)
 #endif
+// The correctly rounded angle of a near-tie sample, out of line: the f64
+// atan2 needs ~50 VGPRs, which only the (rare) call site pays for.
+__attribute__((noinline)) __device__ float orient_angle_f64(float dy, float dx) {
+    return (float)atan2((double)dy, (double)dx);
+}
+
 __global__ __launch_bounds__(256, SIFT_ORIENT_MIN_WAVES) void k_orient(const OrientLaunch L) {
-    __shared__ __attribute__((aligned(16))) float sval[4][OR_LDS];
-    __shared__ __attribute__((aligned(16))) uint8_t sbin[4][OR_LDS];
+    __shared__ __attribute__((aligned(16))) float sval[4][64];  // the current batch of sample values
     __shared__ float swt[4][OR_WT];  // per-wave Gaussian weight table
     __shared__ uint32_t wcount[4], wbase, wsamp[4];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
@@ -404,14 +410,14 @@ __global__ __launch_bounds__(256, SIFT_ORIENT_MIN_WAVES) void k_orient(const Ori
         int W = 1, H = 1, pitch = 1, radius = 0, n = 1, N = 0;
         uint32_t nin = 0;  // patch positions inside the image (sample counting)
         float kp_scale = 0.f, kp_x = 0.f, kp_y = 0.f, osf = 1.f;
-        const float* img = nullptr;
+        float acc = 0.0f;  // lane k < 36: raw_hist[k + 2]
         if (active) {
             e = L.ext[r];
             W = L.ow[e.octave];
             H = L.oh[e.octave];
             pitch = L.opitch[e.octave];
-            img = L.gauss[e.octave] + (size_t)(e.img - L.img_base) * L.gauss_img_stride[e.octave] +
-                  (size_t)e.scale * pitch * H;
+            const float* img = L.gauss[e.octave] + (size_t)(e.img - L.img_base) * L.gauss_img_stride[e.octave] +
+                               (size_t)e.scale * pitch * H;
             osf = (float)(1u << e.octave);  // 2_f32.powi(octave)
             kp_scale = 0.8f * pow2_f32(((float)e.scale + e.off_s) / (float)kScalesPerOctave) * 2.f;
             kp_x = ((float)e.x + e.off_x) * osf;
@@ -429,38 +435,38 @@ __global__ __launch_bounds__(256, SIFT_ORIENT_MIN_WAVES) void k_orient(const Ori
             // sample only through (max(|xp|,|yp|), min(|xp|,|yp|)): one
             // correctly rounded exp per triangle entry (<= 153) instead of one
             // per sample (<= 1089), looked up bit-identically below.
+            // Stored at [a][b] and [b][a] of a 17 x 17 table: a sample's entry
+            // is then |yp| * 17 + |xp| (one multiply-add).
             const int T = (radius + 1) * (radius + 2) / 2;
             for (int t = lane; t < T; t += 64) {
                 int a = (int)((sqrtf(8.0f * (float)t + 1.0f) - 1.0f) * 0.5f);
                 a = (a + 1) * (a + 2) / 2 <= t ? a + 1 : (a * (a + 1) / 2 > t ? a - 1 : a);
                 const int bb = t - a * (a + 1) / 2;
-                swt[wave][t] = exp_f32((float)(a * a + bb * bb) * gws);
+                const float wv = exp_f32((float)(a * a + bb * bb) * gws);
+                swt[wave][a * 17 + bb] = wv;
+                swt[wave][bb * 17 + a] = wv;
             }
             __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
             __builtin_amdgcn_wave_barrier();
             __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
             // The four neighbours of a sample, at clamped positions (samples
             // outside the image are dropped below); the loads of the lane's
-            // next sample are in flight while the current one is evaluated.
-            const gfloat* gimg = as_global(img);
+            // next sample are in flight while the current batch is evaluated
+            // and summed.  Buffer resource based one row and one column before
+            // the plane: a sample's four neighbours are one 32-bit offset plus
+            // a uniform soffset (one or two rows) and an immediate (0, 4, 8
+            // bytes); the clamped position keeps every access inside the plane.
+            const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(img - pitch - 1, (uint32_t)((H + 1) * pitch) * 4u);
+            const int s1 = __builtin_amdgcn_readfirstlane(4 * pitch), s2 = 2 * s1;
             auto fetch = [&](int iy, int ix, float& l, float& r, float& u, float& d) {
                 const int yy = min(max(y + iy - radius, 1), H - 2), xx = min(max(x + ix - radius, 1), W - 2);
-                const gfloat* rw = gimg + (size_t)yy * pitch + xx;
-                r = rw[1];
-                l = rw[-1];
-                u = rw[-pitch];
-                d = rw[pitch];
-            };
-            auto to_bin = [&](float ori) -> uint8_t {
-                int bi = sat_i32(roundf(bin_step * ori));
-                if (bi >= kOriBins)
-                    bi -= kOriBins;
-                else if (bi < 0)
-                    bi += kOriBins;
-                return (uint8_t)bi;
+                const int vo = (yy * pitch + xx) * 4;
+                r = buffer_load_f32(rs, vo + 8, s1);
+                l = buffer_load_f32(rs, vo, s1);
+                u = buffer_load_f32(rs, vo + 4, 0);
+                d = buffer_load_f32(rs, vo + 4, s2);
             };
             float nl = 0.f, nr = 0.f, nu = 0.f, nd = 0.f;
-            uint32_t defer = 0;  // bit it: the lane's sample lane + 64 * it needs the f64 angle
             // patch row / column of the lane's sample (cy, cx) and of its next
             // one (fy, fx), stepped by 64 samples without a division
             const int dq = 64 / n, dr = 64 - dq * n;
@@ -472,109 +478,120 @@ __global__ __launch_bounds__(256, SIFT_ORIENT_MIN_WAVES) void k_orient(const Ori
                     ry++;
                 }
             };
-            int cy = lane / n, cx = lane - (lane / n) * n;
-            int fy = cy, fx = cx;
-            adv(fy, fx);
-            if (lane < N && H > 2 && W > 2) fetch(cy, cx, nl, nr, nu, nd);
-            for (int idx = lane, it = 0; idx < N; idx += 64, it++) {
-                const float gl = nl, gr = nr, gu = nu, gd = nd;
-                if (idx + 64 < N && H > 2 && W > 2) fetch(fy, fx, nl, nr, nu, nd);
-                const int yp = cy - radius, xp = cx - radius;
-                cy = fy;
-                cx = fx;
+            float* sv = sval[wave];
+            // IN: the whole patch lies inside the image, rows / columns 1 ..
+            // H-2 / W-2 (most extrema; wave-uniform): no clamps, no per-sample
+            // bounds test
+            auto sample_loop = [&](auto in_tag) {
+                constexpr bool IN = decltype(in_tag)::value;
+                auto fetch_s = [&](int iy, int ix, float& l, float& r, float& u, float& d) {
+                    if constexpr (IN) {
+                        const int vo = ((y + iy - radius) * pitch + (x + ix - radius)) * 4;
+                        r = buffer_load_f32(rs, vo + 8, s1);
+                        l = buffer_load_f32(rs, vo, s1);
+                        u = buffer_load_f32(rs, vo + 4, 0);
+                        d = buffer_load_f32(rs, vo + 4, s2);
+                    } else {
+                        fetch(iy, ix, l, r, u, d);
+                    }
+                };
+                int cy = lane / n, cx = lane - (lane / n) * n;
+                int fy = cy, fx = cx;
                 adv(fy, fx);
-                const int yy = y + yp, xx = x + xp;
-                uint8_t bin = 0xff;
-                float val = 0.0f;
-                if (yy > 0 && yy < H - 1 && xx > 0 && xx < W - 1) {
-                    const float dx = gr - gl;
-                    const float dy = gu - gd;
-                    const int ax = abs(xp), ay = abs(yp);
-                    const int hi = max(ax, ay), lo = min(ax, ay);
-                    const float weight = swt[wave][hi * (hi + 1) / 2 + lo];
-                    const float mag = sqrtf(dx * dx + dy * dy);
-                    // The sample only needs its bin, round(bin_step * atan2f): a fast
-                    // f32 atan2 (|error| <= 2.4e-7 rad -> the product moves by
-                    // < 2e-6) decides it unless the product lies within 2e-5 of a
-                    // rounding boundary; those rare samples (~4e-5) get the
-                    // correctly rounded f64 angle in a pass after this loop (kept
-                    // out of it: the f64 atan2 alone costs ~50 VGPRs here).
-                    const float ori = atan2_fast(dy, dx);
-                    const float tf = bin_step * ori;
-                    if (fabsf(tf - floorf(tf) - 0.5f) < 2e-5f)
-                        defer |= 1u << it;
-                    else
-                        bin = to_bin(ori);
-                    val = weight * mag;
+                if (lane < N && (IN || (H > 2 && W > 2))) fetch_s(cy, cx, nl, nr, nu, nd);
+                // one batch of 64 samples (the reference's row-major order) per
+                // iteration: evaluate (lane = sample), then add the batch into
+                // the per-bin sums (lane = bin)
+                for (int t = 0; t < N; t += 64) {
+                    const int idx = t + lane;
+                    const float gl = nl, gr = nr, gu = nu, gd = nd;
+                    if (idx + 64 < N && (IN || (H > 2 && W > 2))) fetch_s(fy, fx, nl, nr, nu, nd);
+                    const int yp = cy - radius, xp = cx - radius;
+                    cy = fy;
+                    cx = fx;
+                    adv(fy, fx);
+                    const int yy = y + yp, xx = x + xp;
+                    uint32_t bv = 0xffu;  // no bin: past N or outside the image
+                    bool defer = false;
+                    float val = 0.0f, dx = 0.0f, dy = 0.0f;
+                    if (idx < N && (IN || (yy > 0 && yy < H - 1 && xx > 0 && xx < W - 1))) {
+                        dx = gr - gl;
+                        dy = gu - gd;
+                        const float weight = swt[wave][abs(yp) * 17 + abs(xp)];
+                        const float mag = sqrtf(dx * dx + dy * dy);
+                        // The sample only needs its bin, round(bin_step * atan2f): a
+                        // fast f32 atan2 (|error| <= 2.4e-7 rad -> the product moves
+                        // by < 2e-6) decides it unless the product lies within 2e-5
+                        // of a rounding boundary; those rare samples (~4e-5) take the
+                        // correctly rounded f64 angle below.  Away from a tie,
+                        // round(tf) = floor(tf) + (frac > 0.5); |tf| <= 18 (no
+                        // saturation), and only a negative bin wraps.
+                        const float ori = atan2_fast(dy, dx);
+                        const float tf = bin_step * ori;
+                        const float fl = floorf(tf), fr = tf - fl;
+                        defer = fabsf(fr - 0.5f) < 2e-5f;
+                        const int bi = (int)fl + (fr > 0.5f ? 1 : 0);
+                        bv = (uint32_t)(bi < 0 ? bi + kOriBins : (bi >= kOriBins ? bi - kOriBins : bi));
+                        val = weight * mag;
+                    }
+                    if (__ballot(defer)) {  // rare: the batch holds a near-tie sample
+                        if (defer) {
+                            int bi = sat_i32(roundf(bin_step * orient_angle_f64(dy, dx)));
+                            bv = (uint32_t)(bi >= kOriBins ? bi - kOriBins : (bi < 0 ? bi + kOriBins : bi));
+                        }
+                    }
+                    sv[lane] = val;
+                    __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                    __builtin_amdgcn_wave_barrier();
+                    __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                    // Lane b < 36 gets the mask of the batch's samples in bin b from
+                    // six ballots of the bin bits, then adds exactly those samples
+                    // in index order: the reference's per-bin order
+                    // (`raw_hist[bin + 2] += w * mag`, bit-identical) at O(largest
+                    // bin count per batch).  Samples with no bin match no lane.
+                    uint64_t m = __ballot(bv < (uint32_t)kOriBins);
+#pragma unroll
+                    for (int i = 0; i < 6; i++) {
+                        const uint64_t bi = __ballot((bv >> i) & 1u);
+                        m &= ((lane >> i) & 1) ? bi : ~bi;
+                    }
+                    // SIFT_ORIENT_SUM_U samples per step: their LDS reads in flight
+                    // together; a missing sample adds +0 (exact: acc >= +0)
+                    auto run = [&](uint32_t mk, const float* vb) {
+                        while (mk) {
+                            int j[SIFT_ORIENT_SUM_U];
+                            bool ok[SIFT_ORIENT_SUM_U];
+                            j[0] = __builtin_ctz(mk);
+                            ok[0] = true;
+                            mk &= mk - 1u;
+#pragma unroll
+                            for (int u = 1; u < SIFT_ORIENT_SUM_U; u++) {
+                                ok[u] = mk != 0u;
+                                j[u] = ok[u] ? __builtin_ctz(mk) : j[0];
+                                mk &= mk - 1u;
+                            }
+                            float v[SIFT_ORIENT_SUM_U];
+#pragma unroll
+                            for (int u = 0; u < SIFT_ORIENT_SUM_U; u++) v[u] = vb[j[u]];
+#pragma unroll
+                            for (int u = 0; u < SIFT_ORIENT_SUM_U; u++) acc += ok[u] ? v[u] : 0.0f;
+                        }
+                    };
+                    run(lane < kOriBins ? (uint32_t)m : 0u, sv);
+                    run(lane < kOriBins ? (uint32_t)(m >> 32) : 0u, sv + 32);
+                    // the next batch's value store follows these reads in the
+                    // wave's LDS order: no barrier needed before it
                 }
-                sval[wave][idx] = val;
-                sbin[wave][idx] = bin;
-            }
-            while (defer) {  // the lane's deferred samples (its own LDS entries)
-                const int it = __builtin_ctz(defer);
-                defer &= defer - 1;
-                const int idx = lane + 64 * it;
-                float gl, gr, gu, gd;
-                fetch(idx / n, idx - (idx / n) * n, gl, gr, gu, gd);
-                const float dx = gr - gl;
-                const float dy = gu - gd;
-                sbin[wave][idx] = to_bin((float)atan2((double)dy, (double)dx));
-            }
+            };
+            if (y - radius >= 1 && y + radius <= H - 2 && x - radius >= 1 && x + radius <= W - 2)
+                sample_loop(std::true_type{});
+            else
+                sample_loop(std::false_type{});
             if (L.samples) {  // measurement only
-                const int x = e.x, y = e.y;
                 const int y0 = max(y - radius, 1), y1 = min(y + radius, H - 2);
                 const int x0 = max(x - radius, 1), x1 = min(x + radius, W - 2);
                 nin = (y1 >= y0 && x1 >= x0) ? (uint32_t)((y1 - y0 + 1) * (x1 - x0 + 1)) : 0u;
             }
-        }
-        // the wave's own sample list only: a wave barrier (the block syncs at
-        // the slot atomic below), so a wave with a small patch sums while the
-        // others still sample
-        __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-        __builtin_amdgcn_wave_barrier();
-        __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-        // sequential per-bin sums (lane = bin); inactive waves run on an empty list
-        if (!active) N = 0;
-        float acc = 0.0f;
-        // Per 64-sample batch, lane b < 36 gets the mask of the batch's samples
-        // in bin b from six ballots of the bin bits, then adds exactly those
-        // samples in index order: the reference's per-bin order (bit-identical)
-        // at O(largest bin count per batch) instead of every lane reading every
-        // sample (1080p: ~110 vs ~600 steps per extremum).  Samples outside the
-        // image (bin 0xff) and past N match no lane.
-        for (int t = 0; t < N; t += 64) {
-            const int idx = t + lane;
-            const uint32_t bv = idx < N ? (uint32_t)sbin[wave][idx] : 0xffu;
-            uint64_t m = __ballot(bv < (uint32_t)kOriBins);
-#pragma unroll
-            for (int i = 0; i < 6; i++) {
-                const uint64_t bi = __ballot((bv >> i) & 1u);
-                m &= ((lane >> i) & 1) ? bi : ~bi;
-            }
-            // SIFT_ORIENT_SUM_U samples per step: their LDS reads in flight
-            // together; a missing sample adds +0 (exact: acc >= +0)
-            auto run = [&](uint32_t mk, const float* vb) {
-                while (mk) {
-                    int j[SIFT_ORIENT_SUM_U];
-                    bool ok[SIFT_ORIENT_SUM_U];
-                    j[0] = __builtin_ctz(mk);
-                    ok[0] = true;
-                    mk &= mk - 1u;
-#pragma unroll
-                    for (int u = 1; u < SIFT_ORIENT_SUM_U; u++) {
-                        ok[u] = mk != 0u;
-                        j[u] = ok[u] ? __builtin_ctz(mk) : j[0];
-                        mk &= mk - 1u;
-                    }
-                    float v[SIFT_ORIENT_SUM_U];
-#pragma unroll
-                    for (int u = 0; u < SIFT_ORIENT_SUM_U; u++) v[u] = vb[j[u]];
-#pragma unroll
-                    for (int u = 0; u < SIFT_ORIENT_SUM_U; u++) acc += ok[u] ? v[u] : 0.0f;
-                }
-            };
-            run(lane < kOriBins ? (uint32_t)m : 0u, sval[wave] + t);
-            run(lane < kOriBins ? (uint32_t)(m >> 32) : 0u, sval[wave] + t + 32);
         }
         // circular [1,4,6,4,1]/16 smoothing (src/lib.rs:742-755)
         const int k = lane < kOriBins ? lane : 0;

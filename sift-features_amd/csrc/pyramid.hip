@@ -357,18 +357,6 @@ __device__ __forceinline__ void drop_stores(__amdgpu_buffer_rsrc_t r) {
 
 typedef unsigned int u32x4 __attribute__((ext_vector_type(4)));
 
-// Buffer resource over `bytes` bytes at p (wave-uniform inputs: the halves of
-// the pointer and the size go through readfirstlane so the descriptor lives
-// in SGPRs).  Loads / stores then take a 32-bit per-lane voffset and a
-// uniform soffset: no 64-bit address arithmetic per access.
-__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, uint32_t bytes) {
-    const uint64_t a = (uint64_t)p;
-    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
-    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
-    void* q = (void*)(((uint64_t)hi << 32) | lo);
-    return __builtin_amdgcn_make_buffer_rsrc(q, 0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
-}
-
 // Single reflection (the strip kernel runs only when W, H > R, so every index
 // an output uses is in range after one reflection), then clamped: rows /
 // columns loaded past what any output uses stay inside the image.

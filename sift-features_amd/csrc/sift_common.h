@@ -112,6 +112,21 @@ __host__ __device__ __forceinline__ int reflect101(int p, int len) {
 typedef __attribute__((address_space(1))) const float gfloat;
 __device__ __forceinline__ const gfloat* as_global(const float* p) { return (const gfloat*)p; }
 
+// Buffer resource over `bytes` bytes at p (wave-uniform inputs: the halves of
+// the pointer and the size go through readfirstlane so the descriptor lives
+// in SGPRs).  Loads / stores then take a 32-bit per-lane voffset and a
+// uniform soffset: no 64-bit address arithmetic per access.
+__device__ __forceinline__ __amdgpu_buffer_rsrc_t uniform_rsrc(const void* p, uint32_t bytes) {
+    const uint64_t a = (uint64_t)p;
+    const uint32_t lo = __builtin_amdgcn_readfirstlane((uint32_t)a);
+    const uint32_t hi = __builtin_amdgcn_readfirstlane((uint32_t)(a >> 32));
+    void* q = (void*)(((uint64_t)hi << 32) | lo);
+    return __builtin_amdgcn_make_buffer_rsrc(q, 0, (int)__builtin_amdgcn_readfirstlane(bytes), 0x00020000);
+}
+__device__ __forceinline__ float buffer_load_f32(__amdgpu_buffer_rsrc_t r, int voff, int soff) {
+    return __builtin_bit_cast(float, __builtin_amdgcn_raw_buffer_load_b32(r, voff, soff, 0));
+}
+
 // XCD-aware tile order for (tx, ty, frames) grids.  The dispatcher deals
 // workgroups round-robin over the 8 XCDs (each with a private 4 MB L2), so
 // neighbouring tiles of a plain grid land on different XCDs and every halo

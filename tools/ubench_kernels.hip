@@ -649,6 +649,8 @@ int main(int argc, char** argv) {
     std::printf("  fast s4         %8.3f ms\n", time_describe<4, 0>(L, reps));
     std::printf("  fast s4 -rmw    %8.3f ms\n", time_describe<4, 1>(L, reps));
     std::printf("  fast s4 nosample %8.3f ms\n", time_describe<4, 64>(L, reps));
+    std::printf("  fast s4 f32sincos %8.3f ms\n", time_describe<4, 128>(L, reps));
+    std::printf("  fast s4 nosample f32sincos %8.3f ms\n", time_describe<4, 192>(L, reps));
     std::printf("  fast s4 -atan2  %8.3f ms\n", time_describe<4, 2>(L, reps));
     std::printf("  fast s4 -exp    %8.3f ms\n", time_describe<4, 4>(L, reps));
     std::printf("  fast s4 -loads  %8.3f ms\n", time_describe<4, 8>(L, reps));
