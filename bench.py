@@ -82,7 +82,7 @@ def run_config(pkg, synth, dev, device_index, n, W, H, steps, seed0=1000, max_oc
     def go():
         return int(c.sift_batch_device(*call, fetch=False)[0][-1])
 
-    for _ in range(3):  # warm: plan, arenas, clocks
+    for _ in range(10 if n == 1 else 3):  # warm: plan, arenas, clocks (single-frame calls: ~1 ms each)
         go()
     torch.cuda.synchronize()
     ts, kp = [], 0

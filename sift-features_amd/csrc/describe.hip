@@ -599,12 +599,36 @@ __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img
     const float* r1 = r0 + NS;
     const float* r8 = sc.h + ((lane >> 2) * 9 + 8) * NS;  // orientation-0 alias of the cell
     float acc8 = 0.0f;
+    if constexpr (NS % 4 == 0) {
+        // four slices per 16-byte read; the start rotates with the lane, so
+        // each 8-lane group of a read touches 8 distinct 4-bank groups
+#pragma unroll
+        for (int j = 0; j < NS / 4; j++) {
+            const int jj = 4 * ((j + lane) & (NS / 4 - 1));
+            const float4 a = *reinterpret_cast<const float4*>(r0 + jj);
+            const float4 b = *reinterpret_cast<const float4*>(r1 + jj);
+            const float4 c = *reinterpret_cast<const float4*>(r8 + jj);
+            acc0 += a.x;
+            acc0 += a.y;
+            acc0 += a.z;
+            acc0 += a.w;
+            acc1 += b.x;
+            acc1 += b.y;
+            acc1 += b.z;
+            acc1 += b.w;
+            acc8 += c.x;
+            acc8 += c.y;
+            acc8 += c.z;
+            acc8 += c.w;
+        }
+    } else {
 #pragma unroll 8
-    for (int j = 0; j < NS; j++) {
-        const int jj = (j + lane) & (NS - 1);
-        acc0 += r0[jj];
-        acc1 += r1[jj];
-        acc8 += r8[jj];
+        for (int j = 0; j < NS; j++) {
+            const int jj = (j + lane) & (NS - 1);
+            acc0 += r0[jj];
+            acc1 += r1[jj];
+            acc8 += r8[jj];
+        }
     }
     if ((lane & 3) == 0) acc0 += acc8;
     if (kAblate & 1) acc0 += sink.x + sink.y;
