@@ -382,7 +382,7 @@ void launch_refine(const RefineLaunch& L, hipStream_t st) {
 constexpr int OR_WT = 17 * 17;  // weight table (|yp|, |xp|) at the largest radius (16)
 
 #ifndef SIFT_ORIENT_SUM_U
-#define SIFT_ORIENT_SUM_U 2  // samples per step of the per-bin sums
+#define SIFT_ORIENT_SUM_U 1  // samples per step of the per-bin sums (batched kernel: 1 3.43 ms, 2 3.50, 3 3.62, 4 3.67 per 128 frames)
 #endif
 #ifndef SIFT_ORIENT_MIN_WAVES
 #define SIFT_ORIENT_MIN_WAVES 8  // 8 waves per SIMD (64 VGPRs, 10 dwords spilled; no LDS limit since the sample list went): orientation 3.51 ms vs 3.54 at 7 waves, 3.57-3.62 at 6 (128 1080p frames)
