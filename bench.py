@@ -265,9 +265,14 @@ def main():
     dt_max, total_kp, total_frames = shard.reduce_run(dt, n_kp, B * args.steps, dist if world > 1 else None)
 
     # N > 1: the keypoint gather of the throughput path -- every rank's
-    # device-resident results of its last step to rank 0 over RCCL
-    # (shard.gather_device_results: sizes, then point-to-point rows into one
-    # concatenated device tensor), timed on its own outside the steps
+    # device-resident results to rank 0 over RCCL (shard.gather_device_results:
+    # sizes, then point-to-point rows into one concatenated device tensor).
+    # (1) alone, one step's results, timed on its own; (2) inside a timed
+    # loop of the same steps: each step's results are snapshotted in HBM (the
+    # context's result arena is rewritten by the next step) and gathered
+    # while the next step computes -- `value_incl_gather` (configs[3] is
+    # "sharded ... via RCCL/xGMI": this is the config's whole-job rate with
+    # the results on rank 0).
     gather = None
     if world > 1:
         k_dev, d_dev = shard.device_results(ctx)
@@ -279,12 +284,33 @@ def main():
         barrier()
         gms = 1e3 * (time.perf_counter() - t)
         gms = shard.reduce_run(gms / 1e3, 0, 0, dist)[0] * 1e3
+        nk = int(g[0].shape[0]) if rank == 0 else 0
+        del g, k_dev, d_dev
+        barrier()
+        torch.cuda.synchronize()
+        tg = time.perf_counter()
+        n_kp_g, got = 0, 0
+        for _ in range(args.steps):
+            n_kp_g += step()
+            k_dev, d_dev = shard.device_results(ctx)
+            snap = (k_dev.clone(), d_dev.clone())
+            torch.cuda.current_stream().synchronize()  # the next step rewrites the arena
+            g = shard.gather_device_results(snap[0], snap[1], last["offs"], dist, dst=0)
+            if rank == 0:
+                got += int(g[0].shape[0])
+        torch.cuda.synchronize()
+        barrier()
+        dtg = time.perf_counter() - tg
+        dtg_max, total_kp_g, _ = shard.reduce_run(dtg, n_kp_g, 0, dist)
         if rank == 0:
-            nk = int(g[0].shape[0])
+            assert got == total_kp_g, (got, total_kp_g)  # every keypoint of every step arrived
             gather = {"ms": gms, "keypoints": nk, "bytes": nk * (20 + 128),
                       "note": "one step's results of all ranks to rank 0 (device to device, RCCL send/recv), "
-                              "max over ranks; not inside ms_per_step"}
-        del g, k_dev, d_dev
+                              "max over ranks; not inside ms_per_step",
+                      "value_incl_gather": total_kp_g / dtg_max,
+                      "ms_per_step_incl_gather": 1e3 * dtg_max / args.steps,
+                      "incl_note": "the same steps with every step's results gathered on rank 0 (snapshot in "
+                                   "HBM, RCCL send/recv overlapped with the next step), max over ranks"}
 
     pyr_gbs = st["pyramid_bytes"] / (st["pyramid_ms"] * 1e-3) / 1e9 if st["pyramid_ms"] > 0 else 0.0
     per_launch_bytes = st["pyramid_bytes"] / max(1, st["pyramid_launches"])
@@ -421,6 +447,7 @@ def main():
             "cpu_baseline_all_cores": cpu_all,
             "keypoint_stages": kp_stages,
             "gather": gather,
+            "value_incl_gather": gather["value_incl_gather"] if gather else None,
             "configs": configs,
         }
         print(json.dumps(out), flush=True)

@@ -456,11 +456,18 @@ __global__ __launch_bounds__(256, SIFT_ORIENT_MIN_WAVES) void k_orient(const Ori
             // the plane: a sample's four neighbours are one 32-bit offset plus
             // a uniform soffset (one or two rows) and an immediate (0, 4, 8
             // bytes); the clamped position keeps every access inside the plane.
-            const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(img - pitch - 1, (uint32_t)((H + 1) * pitch) * 4u);
+            // The resource starts at the row above the patch's first clamped
+            // row and spans only the patch's rows, so offsets stay small
+            // however large the plane (octave 0 of a 16384-px frame is 2^32
+            // bytes: a plane-based 32-bit offset would wrap).
+            const int rb = max(y - radius, 1);                    // first sample row (clamped)
+            const int re = min(max(y + radius, 1), H - 2);        // last sample row (clamped)
+            const __amdgpu_buffer_rsrc_t rs =
+                uniform_rsrc(img + (ptrdiff_t)(rb - 1) * pitch - 1, (uint32_t)(re - rb + 3) * (uint32_t)pitch * 4u);
             const int s1 = __builtin_amdgcn_readfirstlane(4 * pitch), s2 = 2 * s1;
             auto fetch = [&](int iy, int ix, float& l, float& r, float& u, float& d) {
                 const int yy = min(max(y + iy - radius, 1), H - 2), xx = min(max(x + ix - radius, 1), W - 2);
-                const int vo = (yy * pitch + xx) * 4;
+                const int vo = ((yy - rb) * pitch + xx) * 4;
                 r = buffer_load_f32(rs, vo + 8, s1);
                 l = buffer_load_f32(rs, vo, s1);
                 u = buffer_load_f32(rs, vo + 4, 0);
@@ -486,7 +493,7 @@ __global__ __launch_bounds__(256, SIFT_ORIENT_MIN_WAVES) void k_orient(const Ori
                 constexpr bool IN = decltype(in_tag)::value;
                 auto fetch_s = [&](int iy, int ix, float& l, float& r, float& u, float& d) {
                     if constexpr (IN) {
-                        const int vo = ((y + iy - radius) * pitch + (x + ix - radius)) * 4;
+                        const int vo = ((y + iy - radius - rb) * pitch + (x + ix - radius)) * 4;
                         r = buffer_load_f32(rs, vo + 8, s1);
                         l = buffer_load_f32(rs, vo, s1);
                         u = buffer_load_f32(rs, vo + 4, 0);

@@ -1506,9 +1506,15 @@ int sift_mi_create(int device_ordinal, sift_mi_profile profile, sift_mi_ctx** ou
 void sift_mi_destroy(sift_mi_ctx* c) {
     if (!c) return;
     (void)hipSetDevice(c->device);
-    if (c->stream) (void)hipStreamSynchronize(c->stream);
-    if (c->own2) (void)hipStreamSynchronize(c->own2);
-    if (c->cstream) (void)hipStreamSynchronize(c->cstream);
+    // every stream that may still run work on this context's buffers first:
+    // the caller's stream (sift_mi_set_stream), the context's own lane-0
+    // stream (it goes back to the pool below), lane 1, both aux streams
+    // (octave blurs 4, 5 and detection write the arenas) and the copy stream
+    {
+        const hipStream_t ss[] = {c->stream, c->own, c->own2, c->aux[0], c->aux[1], c->cstream};
+        for (hipStream_t s : ss)
+            if (s) (void)hipStreamSynchronize(s);
+    }
     c->plan.release();
     c->staging.release();
     c->jpeg.release();
@@ -1525,8 +1531,6 @@ void sift_mi_destroy(sift_mi_ctx* c) {
         if (S.copied) (void)hipEventDestroy(S.copied);
     }
     if (c->fork) (void)hipEventDestroy(c->fork);
-    for (auto& a : c->aux)
-        if (a) (void)hipStreamSynchronize(a);
     for (auto& lane : c->oct_ev)
         for (auto& e : lane)
             if (e) (void)hipEventDestroy(e);

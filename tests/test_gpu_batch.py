@@ -108,15 +108,23 @@ def test_random_noise(pkg, ctx, oracle):
     assert_parity(pkg, res, kp_o, desc_o, ext_o)
 
 
-@pytest.mark.parametrize("chunk", [0, 2])
+@pytest.mark.parametrize("chunk", [0, 2, -1, -2])
 def test_device_resident_results(pkg, ctx, chunk):
     """fetch=False keeps every frame's results in HBM (the bench's `value`
-    path); copied back they equal the host-fetched batch, chunked or not."""
+    path); copied back they equal the host-fetched batch, chunked or not.
+    chunk -1: the whole batch in one chunk, -2: a single frame -- one chunk,
+    whose results are handed out as the slot's own output buffers (no copy;
+    host.cpp res_slot), then a fetch=True call on the same context must
+    return its own results, not the slot's stale ones."""
     import torch
     fr = _frames()
+    if chunk == -2:
+        fr = fr[:1]
     t = torch.from_numpy(fr).cuda()
     c2 = pkg.Context(0)
-    if chunk:
+    if chunk == -1:
+        c2.set_chunk(len(fr))
+    elif chunk:
         c2.set_chunk(chunk)
     offs, res = c2.sift_batch_device(t.data_ptr(), t.shape[0], t.shape[2], t.shape[1], t.stride(1), t.stride(0),
                                      fetch=False)
@@ -136,6 +144,24 @@ def test_device_resident_results(pkg, ctx, chunk):
         a, b = int(offs[i]), int(offs[i + 1])
         assert np.array_equal(kp[a:b], ref[i].keypoints_array), i
         assert np.array_equal(desc[a:b], ref[i].descriptors), i
+    if chunk < 0:
+        # a fetched call after the direct-slot one: its own results
+        fr2 = np.ascontiguousarray(fr[:, ::-1])
+        t2 = torch.from_numpy(fr2).cuda()
+        offs2, res2 = c2.sift_batch_device(t2.data_ptr(), t2.shape[0], t2.shape[2], t2.shape[1], t2.stride(1),
+                                           t2.stride(0), fetch=True)
+        ref2 = ctx.sift_batch(fr2)
+        for i in range(len(fr2)):
+            a, b = int(offs2[i]), int(offs2[i + 1])
+            assert np.array_equal(res2.keypoints_array[a:b], ref2[i].keypoints_array), i
+            assert np.array_equal(res2.descriptors[a:b], ref2[i].descriptors), i
+        # and a device-resident call again
+        offs3, _ = c2.sift_batch_device(t.data_ptr(), t.shape[0], t.shape[2], t.shape[1], t.stride(1), t.stride(0),
+                                        fetch=False)
+        kp_ptr3, desc_ptr3, n3 = c2.device_results()
+        assert n3 == n
+        assert hip.hipMemcpy(kp.ctypes.data, kp_ptr3, kp.nbytes, 2) == 0
+        assert np.array_equal(kp[: int(offs[1])], ref[0].keypoints_array)
     c2.close()
 
 

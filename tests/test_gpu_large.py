@@ -4,10 +4,15 @@
   test_gpu_parity.assert_parity: identical keypoint count and emission order,
   |dx|,|dy| <= 1e-4, descriptors within +-1).  ~10 s of oracle time on the
   host.
-* 8192 x 8192 (config #5, 13 octaves, ~16 GB of pyramid): too slow for the
-  oracle, so size-independent properties: determinism, emission order
-  (keys strictly increasing), descriptor range, the single-frame and the
-  batch entry points agreeing, and octave coverage.
+* 8192 x 8192 (config #5, 13 octaves, ~16 GB of pyramid): full parity
+  against the C oracle (~1 min and ~20 GB of host memory), plus the
+  size-independent properties: determinism, emission order (keys strictly
+  increasing), descriptor range, the single-frame and the batch entry points
+  agreeing, and octave coverage.
+* 16384 x 9000: octave 0 (32768 x 18000 f32) is a plane over 2^31 bytes, so
+  every stage that addresses a plane must do it with offsets that do not
+  wrap (k_orient's buffer resource spans only the patch's rows); full parity
+  against the oracle (~2 min, ~40 GB of host memory).
 * Over 8192 px on one side (the 2x seed is then wider than 16384, which needs
   the 15-bit x/y fields of the emission key): narrow strips 8200 x 48,
   48 x 8400 and 16384 x 24 against the oracle, plus a banded merge of the
@@ -43,6 +48,31 @@ def test_large_4096_parity(pkg, ctx, oracle):
     kp_o, desc_o, ext_o = oracle.sift(img, internal=True)
     res = ctx.sift(img)
     assert len(res) > 10000
+    assert_parity(pkg, res, kp_o, desc_o, ext_o)
+
+
+@pytest.mark.timeout(900)
+def test_max_8192_parity(pkg, ctx, oracle):
+    """Config #5 against the oracle (src/lib.rs:131-143 has no size limit)."""
+    from test_gpu_parity import assert_parity
+    img = _tiled(8192, 47)
+    res = ctx.sift(img)
+    kp_o, desc_o, ext_o = oracle.sift(img, internal=True)
+    assert len(res) > 50000
+    assert_parity(pkg, res, kp_o, desc_o, ext_o)
+
+
+@pytest.mark.timeout(900)
+def test_plane_over_2gb_parity(pkg, ctx, oracle):
+    """Octave-0 planes above 2^31 bytes: 32-bit plane offsets would wrap
+    (k_orient reads gradients through a buffer resource)."""
+    from test_gpu_parity import assert_parity
+    img = np.ascontiguousarray(_tiled(16384, 53)[:9000])
+    res = ctx.sift(img)
+    kp_o, desc_o, ext_o = oracle.sift(img, internal=True)
+    assert len(res) > 50000
+    # keypoints from the rows whose octave-0 byte offsets pass 2^31
+    assert (res.keypoints_array[:, 1] * 2 * 32768 * 4 > 2 ** 31).sum() > 1000
     assert_parity(pkg, res, kp_o, desc_o, ext_o)
 
 

@@ -166,8 +166,10 @@ def test_golden_snapshots_gpu(pkg, ctx, oracle):
         g = load_golden(name)
         # default mode: measured on MI355X (round 3) at the exact mode's max |d|
         # of 1 and 98.35 % / 97.33 % identical rows (tree / bird; exact mode
-        # 98.35 / 97.78 %): its own +-1 does not stack on the oracle's here
-        for c, min_desc, max_d in ((ctx, 0.97, 1), (ex, MIN_DESC_EQUAL, 1)):
+        # 98.35 / 97.78 %): its own +-1 does not stack on the oracle's here.
+        # The bound leaves a few rows of slack (bird: 0.96 = 9 of 225 rows
+        # differing, measured 6) for the fast path's summation order.
+        for c, min_desc, max_d in ((ctx, 0.96, 1), (ex, MIN_DESC_EQUAL, 1)):
             res = c.sift(g["image"])
             assert len(res) == count
             order = pkg.stable_sort_xy_size(res.keypoints_array)
