@@ -520,7 +520,12 @@ uint32_t auto_chunk(const Plan& p_probe_w_h, uint32_t w, uint32_t h, uint32_t n)
     }
     const double per_frame = 44.0 * sum_p;
     uint32_t cmax = (uint32_t)std::max(1.0, std::floor(32e9 / per_frame));
-    cmax = std::min<uint32_t>(cmax, 64);
+    // and ~531 M seed pixels (64 frames at 1080p): smaller frames get more
+    // frames per chunk, so their octave launches are as large (VGA: 256
+    // frames in two chunks of 128 instead of four of 64)
+    const double seed_px = 4.0 * w * h;
+    cmax = std::min<uint32_t>(cmax, (uint32_t)std::max(1.0, std::floor(64.0 * 3840.0 * 2160.0 / seed_px)));
+    cmax = std::min<uint32_t>(cmax, 256);
     uint32_t k = std::max<uint32_t>((n + cmax - 1) / cmax, n >= 2 ? 2u : 1u);  // chunks
     return std::max<uint32_t>(1, (n + k - 1) / k);
 }
@@ -755,6 +760,37 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
         bytes = (uint64_t)b;
     }
     uint64_t launches = 0;
+    // blur s of octave o for frames [f0, f0 + nf)
+    auto blur_launch = [&](int o, int s, uint32_t f0, uint32_t nf) {
+        float* G = p.gauss(o, lane) + (size_t)f0 * p.gstride(o);
+        const size_t P = p.P[o];
+        BlurLaunch B{};
+        B.src = G + (size_t)(s - 1) * P;
+        B.src_img_stride = p.gstride(o);
+        B.dst = G + (size_t)s * P;
+        B.dst_img_stride = p.gstride(o);
+        if (s == 3 && o + 1 < p.n_oct) {
+            B.nxt = p.gauss(o + 1, lane) + (size_t)f0 * p.gstride(o + 1);
+            B.nxt_img_stride = p.gstride(o + 1);
+            B.pitch_n = p.opitch[o + 1];
+            B.wn = p.ow[o + 1];
+            B.hn = p.oh[o + 1];
+        }
+        B.W = p.ow[o];
+        B.H = p.oh[o];
+        B.pitch = p.opitch[o];
+        B.n_img = (int)nf;
+        B.taps = p.oct_taps[s];
+        B.profile = p.profile;
+        if (c->band_restricted) {
+            B.y0 = rlo[(size_t)o * kImagesPerOctave + s];
+            B.y1 = std::max(rhi[(size_t)o * kImagesPerOctave + s], B.y0 + 1);
+        }
+        return B;
+    };
+    // the seed and blur 1 ran as one pass (k_seed_pair): octave 0 continues
+    // at blur 2, as the (2, 3) pair
+    bool seed_pair = false;
     // frames [f0, f0 + nf): seed, octave chain, tail (and their detection) on
     // stream sm; ov: blurs 4, 5 of each octave on the aux stream
     auto seed = [&](uint32_t f0, uint32_t nf, hipStream_t sm) -> int {
@@ -776,6 +812,13 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
         S.taps = p.seed_taps;
         S.y0 = seed_y0;
         S.y1 = seed_y1;
+        // G_0 and G_1 in one pass where it applies (whole planes: not for a
+        // restricted row band); G_0 is then never read back from HBM
+        seed_pair = p.n_oct > 0 && launch_seed_pair(p.seed_r, p.oct_r[1], S, blur_launch(0, 1, f0, nf), sm) == 0;
+        if (seed_pair) {
+            launches++;
+            return 0;
+        }
         if (launch_seed(p.seed_r, S, sm)) return fail(SIFT_MI_EUNSUPPORTED, "seed blur radius");
         launches++;
         return 0;
@@ -787,41 +830,19 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
             float* G = p.gauss(o, lane) + (size_t)f0 * p.gstride(o);
             float* D = p.dog(o, lane) + (size_t)f0 * p.dstride(o);
             const size_t P = p.P[o];
-            auto blur_launch = [&](int s) {
-                BlurLaunch B{};
-                B.src = G + (size_t)(s - 1) * P;
-                B.src_img_stride = p.gstride(o);
-                B.dst = G + (size_t)s * P;
-                B.dst_img_stride = p.gstride(o);
-                if (s == 3 && o + 1 < p.n_oct) {
-                    B.nxt = p.gauss(o + 1, lane) + (size_t)f0 * p.gstride(o + 1);
-                    B.nxt_img_stride = p.gstride(o + 1);
-                    B.pitch_n = p.opitch[o + 1];
-                    B.wn = p.ow[o + 1];
-                    B.hn = p.oh[o + 1];
-                }
-                B.W = p.ow[o];
-                B.H = p.oh[o];
-                B.pitch = p.opitch[o];
-                B.n_img = (int)nf;
-                B.taps = p.oct_taps[s];
-                B.profile = p.profile;
-                if (c->band_restricted) {
-                    B.y0 = rlo[(size_t)o * kImagesPerOctave + s];
-                    B.y1 = std::max(rhi[(size_t)o * kImagesPerOctave + s], B.y0 + 1);
-                }
-                return B;
-            };
-            for (int s = 1; s < kImagesPerOctave; s++) {
+            // octave 0 after k_seed_pair starts at blur 2
+            for (int s = (o == 0 && seed_pair) ? 2 : 1; s < kImagesPerOctave; s++) {
                 if (s == 4 && ov) {
                     HIPCHK(hipEventRecord(c->oct_ev[lane][o], sm));
                     HIPCHK(hipStreamWaitEvent(aux, c->oct_ev[lane][o], 0));
                     s45 = aux;
                 }
-                const BlurLaunch B = blur_launch(s);
+                const BlurLaunch B = blur_launch(o, s, f0, nf);
                 // G_1, G_2 in one pass where the pair kernel applies
-                // (k_blur2_strip: G_1 never read back from HBM)
-                if (s == 1 && launch_blur_pair(p.oct_r[s], p.oct_r[s + 1], B, blur_launch(s + 1), sm) == 0) {
+                // (k_blur2_strip: G_1 never read back from HBM); after the
+                // seed pair, G_2, G_3 (and the next octave's base) instead
+                if ((s == 1 || (s == 2 && o == 0 && seed_pair)) &&
+                    launch_blur_pair(p.oct_r[s], p.oct_r[s + 1], B, blur_launch(o, s + 1, f0, nf), sm) == 0) {
                     launches++;
                     s++;
                     continue;
@@ -898,7 +919,7 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
 // (bc / be / bk); finalize_chunk detects a count above its bound and the chunk
 // is re-run with larger bounds.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kMaxChunk = 64;  // frames per chunk (one wave plans the output)
+constexpr uint32_t kMaxChunk = 256;  // frames per chunk (one workgroup plans the output: k_limit_plan)
 
 struct Bounds {
     uint32_t bc, be, bk;

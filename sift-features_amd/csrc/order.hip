@@ -68,30 +68,51 @@ void launch_frame_starts(const uint64_t* sorted_keys, const uint32_t* n, uint32_
     hipLaunchKernelGGL(k_frame_starts, dim3((bound + 255) / 256), dim3(256), 0, st, sorted_keys, n, bound, starts);
 }
 
-// One wave; frame f = lane (n_img <= 64).  cnt[f] = next non-empty start - start[f].
-__global__ void k_limit_plan(const uint32_t* __restrict__ starts, const uint32_t* __restrict__ n_kp, uint32_t bound,
-                             int n_img, int64_t limit, uint32_t* __restrict__ out_cnt, uint32_t* __restrict__ seg_off,
-                             uint32_t* __restrict__ out_off, uint8_t* __restrict__ use_resp,
-                             uint32_t* __restrict__ n_out) {
-    const int f = threadIdx.x;
+// One workgroup; frame f = thread (n_img <= kLimitPlanFrames).  cnt[f] =
+// next non-empty start - start[f] (starts are in sorted order, so that is
+// the end of frame f's segment), then exclusive prefix sums of the counts
+// and of the output counts over the block.
+constexpr int kLimitPlanFrames = 256;
+__global__ __launch_bounds__(kLimitPlanFrames) void k_limit_plan(const uint32_t* __restrict__ starts,
+                                                                 const uint32_t* __restrict__ n_kp, uint32_t bound,
+                                                                 int n_img, int64_t limit,
+                                                                 uint32_t* __restrict__ out_cnt,
+                                                                 uint32_t* __restrict__ seg_off,
+                                                                 uint32_t* __restrict__ out_off,
+                                                                 uint8_t* __restrict__ use_resp,
+                                                                 uint32_t* __restrict__ n_out) {
+    __shared__ uint32_t st[kLimitPlanFrames + 1];
+    __shared__ uint32_t wsum[2][kLimitPlanFrames / 64];
+    const int f = threadIdx.x, lane = f & 63, wv = f >> 6;
     const uint32_t n = min(*n_kp, bound);
     const uint32_t s = f < n_img ? starts[f] : 0xffffffffu;
     // end of frame f: the smallest start among later frames (suffix min), else n
+    st[f] = s;
+    __syncthreads();
     uint32_t nxt = 0xffffffffu;
-    for (int g = n_img - 1; g > f; g--) nxt = min(nxt, starts[g]);
+    for (int g = n_img - 1; g > f; g--) nxt = min(nxt, st[g]);
     const uint32_t end = nxt == 0xffffffffu ? n : nxt;
     const uint32_t cnt = s == 0xffffffffu ? 0u : end - s;
     const bool trunc = limit >= 0 && (uint64_t)limit < cnt;
     const uint32_t oc = trunc ? (uint32_t)limit : cnt;
-    // exclusive prefix sums over the wave (frames are in sorted order)
+    // inclusive scans within each wave, then the waves' totals
     uint32_t seg = cnt, out = oc;
 #pragma unroll
     for (int o = 1; o < 64; o <<= 1) {
         const uint32_t a = __shfl_up(seg, o), b = __shfl_up(out, o);
-        if (f >= o) {
+        if (lane >= o) {
             seg += a;
             out += b;
         }
+    }
+    if (lane == 63) {
+        wsum[0][wv] = seg;
+        wsum[1][wv] = out;
+    }
+    __syncthreads();
+    for (int w = 0; w < wv; w++) {
+        seg += wsum[0][w];
+        out += wsum[1][w];
     }
     if (f < n_img) {
         out_cnt[f] = oc;
@@ -99,14 +120,14 @@ __global__ void k_limit_plan(const uint32_t* __restrict__ starts, const uint32_t
         out_off[f] = out - oc;
         use_resp[f] = trunc ? 1 : 0;
     }
-    if (f == 63) *n_out = out;
+    if (f == kLimitPlanFrames - 1) *n_out = out;
 }
 
 void launch_limit_plan(const uint32_t* starts, const uint32_t* n_kp, uint32_t bound, int n_img, int64_t limit,
                        uint32_t* out_cnt, uint32_t* seg_off, uint32_t* out_off, uint8_t* use_resp, uint32_t* n_out,
                        hipStream_t st) {
-    hipLaunchKernelGGL(k_limit_plan, dim3(1), dim3(64), 0, st, starts, n_kp, bound, n_img, limit, out_cnt, seg_off,
-                       out_off, use_resp, n_out);
+    hipLaunchKernelGGL(k_limit_plan, dim3(1), dim3(kLimitPlanFrames), 0, st, starts, n_kp, bound, n_img, limit,
+                       out_cnt, seg_off, out_off, use_resp, n_out);
 }
 
 // key = (frame << 32) | ~bits(response)  (response >= 0, so bit order == value order)

@@ -470,16 +470,19 @@ __device__ __forceinline__ void strip_rowpass(float* slot, const BlurTaps& taps,
 // output row y - R) is row L of slot a for L < S, row L - S of slot b
 // otherwise -- a compile-time choice per row.  OpenCV's SymmColumnFilter
 // (centre product, fma of pair sums) / imageproc's unfused chain.
-template <class G, int P, int WV, bool NXT>
+// LOFF: the window starts LOFF rows into slot a (the seed pair's G_0 chunks
+// start one row above their column-pass windows; k_seed_pair).
+template <class G, int P, int WV, bool NXT, int LOFF = 0>
 __device__ __forceinline__ void strip_colpass(const float* sa, const float* sb, const BlurTaps& taps, int lane,
                                               int y, int ye, int x0, int W, int pitch, __amdgpu_buffer_rsrc_t rd,
                                               __amdgpu_buffer_rsrc_t rn, int pitch_n, int wn, int hn) {
     constexpr int R = G::R;
     constexpr int NR = G::VB + 2 * R;
+    static_assert(LOFF + G::NW * G::VB + 2 * R <= 2 * G::S, "the column-pass window lies in slots a and b");
     f2v v[NR];
 #pragma unroll
     for (int j = 0; j < NR; j++) {
-        const int L = WV * G::VB + j;  // window row: slot a or b
+        const int L = LOFF + WV * G::VB + j;  // window row: slot a or b
         const float* rp = L < G::S ? sa + L * G::IWP : sb + (L - G::S) * G::IWP;
         v[j] = *(const lds_f2v*)(rp + 2 * lane);
     }
@@ -534,8 +537,9 @@ __device__ __forceinline__ void strip_colpass(const float* sa, const float* sb, 
         // strip_segment_rows), so those are the even / odd o
         if (NXT && (o & 1) == (P == kProfileOpenCV ? 0 : 1)) {  // o: unrolled constant
             const uint32_t nrow_bad = (gy >> 1) < hn ? row_bad : kStoreDrop;  // uniform
-            const float val = P == kProfileOpenCV ? out[o].x : out[o].y;
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, val), rn,
+            const uint32_t val = P == kProfileOpenCV ? __builtin_bit_cast(u32x2, out[o]).x
+                                                     : __builtin_bit_cast(u32x2, out[o]).y;  // (see strip_colpass_clamped)
+            __builtin_amdgcn_raw_buffer_store_b32(val, rn,
                                                   ((uint32_t)((gy >> 1) * pitch_n * 4) + lane_ncol) | lane_nbad |
                                                       nrow_bad,
                                                   0, 0);
@@ -547,23 +551,28 @@ __device__ __forceinline__ void strip_colpass(const float* sa, const float* sb, 
 // imageproc pair kernel's border chunks, whose G_s rows outside the image
 // (computed from clamped input rows) are not copies of the edge rows as
 // clamp-to-edge needs -- so they are never read: each tap reads the clamped
-// row of the chunk window (window row 0 = G_s row y - R) instead.  Imageproc
-// chain (acc = acc + v * k from the first tap), dynamic LDS offsets.
-template <class G>
+// row of the chunk window (window row 0 = G_s row y - R - LOFF) instead.
+// Imageproc chain (acc = acc + v * k from the first tap), dynamic LDS offsets.
+// NXT: image's Nearest 1/2 (pixel (2x + 1, 2y + 1): the odd rows' odd
+// columns, as strip_colpass).
+template <class G, bool NXT = false, int LOFF = 0>
 __device__ __forceinline__ void strip_colpass_clamped(const float* sa, const float* sb, const BlurTaps& taps,
                                                       int lane, int wv, int y, int ye, int x0, int W, int H,
-                                                      int pitch, __amdgpu_buffer_rsrc_t rd) {
+                                                      int pitch, __amdgpu_buffer_rsrc_t rd,
+                                                      __amdgpu_buffer_rsrc_t rn, int pitch_n, int wn, int hn) {
     constexpr int R = G::R;
     const int y0 = y + wv * G::VB;
     const int nrow = min(G::VB, ye - y0);
     const int gx = x0 + 2 * lane;
     const uint32_t lane_col = (uint32_t)(gx * 4), lane_bad = gx < W ? 0u : kStoreDrop;
+    const uint32_t lane_ncol = (uint32_t)((gx >> 1) * 4);
+    const uint32_t lane_nbad = ((gx >> 1) < wn && gx + 1 < W) ? 0u : kStoreDrop;
     for (int o = 0; o < G::VB; o++) {
         const int gy = y0 + o;
         f2v acc = {0.0f, 0.0f};
 #pragma unroll
         for (int t = 0; t <= 2 * R; t++) {
-            const int L = min(max(gy - R + t, 0), H - 1) - (y - R);
+            const int L = min(max(gy - R + t, 0), H - 1) - (y - R - LOFF);
             const float* rp = L < G::S ? sa + L * G::IWP : sb + (L - G::S) * G::IWP;
             const f2v v = *(const lds_f2v*)(rp + 2 * lane);
             const float k = taps.k[t > R ? t - R : R - t];
@@ -574,6 +583,15 @@ __device__ __forceinline__ void strip_colpass_clamped(const float* sa, const flo
         __builtin_amdgcn_raw_buffer_store_b64(__builtin_bit_cast(u32x2, acc), rd,
                                               ((uint32_t)(gy * pitch * 4) + lane_col) | lane_bad | row_bad, 0,
                                               SIFT_STORE_CPOL);
+        if (NXT && (gy & 1) == 1) {
+            const uint32_t nrow_bad = (gy >> 1) < hn ? row_bad : kStoreDrop;
+            // (the element as u32x2(acc).y: hipcc 7.2 stores element 0 for
+            // bit_cast(uint32_t, acc.y) after the 64-bit store of acc here)
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(u32x2, acc).y, rn,
+                                                  ((uint32_t)((gy >> 1) * pitch_n * 4) + lane_ncol) | lane_nbad |
+                                                      nrow_bad,
+                                                  0, 0);
+        }
     }
 }
 
@@ -677,9 +695,9 @@ __global__ __launch_bounds__(256, (strip_minb<R, NXT>())) void k_blur_strip(
 // the image -- A's row pass is an FMA chain from the leftmost tap, not
 // symmetric -- are replaced by their reflect-101 sources before B's row pass.
 // ---------------------------------------------------------------------------
-template <int Ra, int Rb>
+template <int Ra, int Rb, int HA = -1>
 struct PairGeom {
-    using GA = StripGeom<Ra, 16>;
+    using GA = StripGeom<Ra, 16, HA>;              // HA: A's window halo (8 for the seed loader's 144 columns)
     using GB = StripGeom<Rb, 16>;
     static constexpr int HB = GB::HWL;             // G_s halo columns of B's window
     static constexpr int TWO = GA::TW - 2 * HB;   // output columns per strip
@@ -688,7 +706,7 @@ struct PairGeom {
     // passes share a phase)
     static constexpr int NBR = NBW + 1;
     static constexpr int LDS_FLOATS = 2 * GA::SLOT + NBR * GB::SLOT;
-    static constexpr int MINB = 163840 / (4 * LDS_FLOATS) < 4 ? 163840 / (4 * LDS_FLOATS) : 4;
+    static constexpr int MINB = 163840 / (4 * LDS_FLOATS + 2048) < 4 ? 163840 / (4 * LDS_FLOATS + 2048) : 4;
     static_assert(GA::HWL <= 8 && GA::NCW == 2, "A: radius <= 8");
     static_assert(NBW == 2, "B: radius <= 8 (two-chunk column windows)");
     static_assert(GB::IWV >= GA::TW, "B's window holds A's 128 columns");
@@ -756,42 +774,54 @@ __device__ __forceinline__ void pair_colpass_a(const float* sa, const float* sb,
     }
 }
 
-template <int Ra, int Rb, bool NXT, int P = kProfileOpenCV>
-__global__ __launch_bounds__(256, (PairGeom<Ra, Rb>::MINB)) void k_blur2_strip(
-    const float* __restrict__ src, size_t img_stride, float* __restrict__ dst_a, float* __restrict__ dst_b,
-    float* __restrict__ nxt, size_t nxt_img_stride, int pitch_n, int wn, int hn, int W, int H, int pitch,
-    const BlurTaps taps_a, const BlurTaps taps_b, int ya, int yb, int seg) {
-    using Q = PairGeom<Ra, Rb>;
+// A's input chunks from a G_{s-1} plane (k_blur2_strip): strip_load /
+// strip_store of 16-row chunks of A's 144-column window.
+template <int Ra, int P, class GA>
+struct PlaneIn {
+    float4 pre[GA::LPT];
+    __amdgpu_buffer_rsrc_t rs;
+    int voff[GA::LPT];
+    bool cols_in;
+    int xa, W, H, pitch;
+    __device__ __forceinline__ void init(const float* src, int xa_, int W_, int H_, int pitch_) {
+        xa = xa_, W = W_, H = H_, pitch = pitch_;
+        rs = uniform_rsrc(src, (uint32_t)H * (uint32_t)pitch * 4u);
+        cols_in = xa - GA::HWL >= 0 && xa + GA::TW + GA::HWL <= W;
+        const int tid = threadIdx.x;
+#pragma unroll
+        for (int j = 0; j < GA::LPT; j++) {
+            const int i = min(tid + 64 * GA::NW * j, GA::NLOAD4 - 1);
+            const int ly = i / GA::C4, c4 = i - ly * GA::C4;
+            voff[j] = (ly * pitch + xa - GA::HWL + 4 * c4) * 4;
+        }
+    }
+    __device__ __forceinline__ void prefetch(int r0) { strip_load<Ra, P, GA>(pre, rs, voff, cols_in, r0, xa, W, H, pitch); }
+    __device__ __forceinline__ void store(float* slot, int) { strip_store<GA>(pre, slot); }
+};
+
+// The two-blur streaming pass shared by k_blur2_strip and k_seed_pair (see
+// above): A-input chunks from `ain`, G_s (A's output) and G_{s+1} (B's) to
+// HBM through ra / rb; NXT / NXTB: the next octave's base from A's / B's
+// column pass.  LOFF: G_s chunk k starts LOFF rows above B's window of
+// output chunk k (A's input chunks start LOFF rows higher), so the seed
+// loader's chunks start at odd window rows (its two-source-row fast path)
+// while segments start at even rows.
+template <int Ra, int Rb, bool NXT, int P, bool NXTB, int LOFF, int HA, class AIn>
+__device__ __forceinline__ void blur2_body(AIn& ain, float* lds, __amdgpu_buffer_rsrc_t ra, __amdgpu_buffer_rsrc_t rb,
+                                           __amdgpu_buffer_rsrc_t rn, int pitch_n, int wn, int hn, int X, int ys,
+                                           int ye, int W, int H, int pitch, const BlurTaps& taps_a,
+                                           const BlurTaps& taps_b) {
+    using Q = PairGeom<Ra, Rb, HA>;
     using GA = typename Q::GA;
     using GB = typename Q::GB;
     constexpr int S = GA::S;
     constexpr int NBW = Q::NBW, NBR = Q::NBR;
-    static_assert(P == kProfileOpenCV || !NXT, "imageproc pairs: no next-octave output");
-    __shared__ __attribute__((aligned(16))) float lds[Q::LDS_FLOATS];
+    static_assert(!(NXT && NXTB), "one next-octave output");
     float* aslot = lds;                   // 2 x GA::SLOT: A's input chunks (row-filtered in place)
     float* bslot = lds + 2 * GA::SLOT;    // NBR x GB::SLOT: G_s chunks (row-filtered in place)
     const int tid = threadIdx.x, lane = tid & 63;
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const TileId tile = xcd_tile();
-    const int X = tile.x * Q::TWO;        // output columns [X, X + TWO)
     const int xa = X - Q::HB;             // A's 128 columns (= B's window) start here
-    const int ys = ya + tile.y * seg, ye = min(yb, ys + seg);
-    if (ys >= ye) return;
-    const size_t b = tile.z;
-    const uint32_t plane_bytes = (uint32_t)H * (uint32_t)pitch * 4u;
-    const __amdgpu_buffer_rsrc_t rs = uniform_rsrc(src + b * img_stride, plane_bytes);
-    const __amdgpu_buffer_rsrc_t ra = uniform_rsrc(dst_a + b * img_stride, plane_bytes);
-    const __amdgpu_buffer_rsrc_t rb = uniform_rsrc(dst_b + b * img_stride, plane_bytes);
-    __amdgpu_buffer_rsrc_t rn = ra;
-    if constexpr (NXT) rn = uniform_rsrc(nxt + b * nxt_img_stride, (uint32_t)hn * (uint32_t)pitch_n * 4u);
-    const bool cols_in = xa - GA::HWL >= 0 && xa + GA::TW + GA::HWL <= W;
-    int voff[GA::LPT];
-#pragma unroll
-    for (int j = 0; j < GA::LPT; j++) {
-        const int i = min(tid + 64 * GA::NW * j, GA::NLOAD4 - 1);
-        const int ly = i / GA::C4, c4 = i - ly * GA::C4;
-        voff[j] = (ly * pitch + xa - GA::HWL + 4 * c4) * 4;
-    }
     int prow, pq;  // row-pass lane map
     strip_rowpass_map(lane, wv, prow, pq);
     // G_s columns outside the image in a B slot row: replaced by their
@@ -826,18 +856,17 @@ __global__ __launch_bounds__(256, (PairGeom<Ra, Rb>::MINB)) void k_blur2_strip(
     // chunks past the last output chunk); A's input 0 .. ng + 1
     const int nout = (ye - ys + S - 1) / S;
     const int ng = nout + NBW - 2, na = ng + 1;
-    const int ga = ys - Rb - Ra;  // first A-input row (chunk 0)
-    float4 pre[GA::LPT];
-    strip_load<Ra, P, GA>(pre, rs, voff, cols_in, ga, xa, W, H, pitch);
-    strip_store<GA>(pre, aslot);
-    strip_load<Ra, P, GA>(pre, rs, voff, cols_in, ga + S, xa, W, H, pitch);
+    const int ga = ys - Rb - Ra - LOFF;  // first A-input row (chunk 0)
+    ain.prefetch(ga);
+    ain.store(aslot, ga);
+    ain.prefetch(ga + S);
     __syncthreads();
     strip_rowpass<GA, P>(aslot, taps_a, prow, pq);
     for (int k = 0; k <= nout + NBW - 1; k++) {
         __syncthreads();  // P1
         if (k + 1 <= na) {
-            strip_store<GA>(pre, aslot + ((k + 1) & 1) * GA::SLOT);
-            if (k + 2 <= na) strip_load<Ra, P, GA>(pre, rs, voff, cols_in, ga + (k + 2) * S, xa, W, H, pitch);
+            ain.store(aslot + ((k + 1) & 1) * GA::SLOT, ga + (k + 1) * S);
+            if (k + 2 <= na) ain.prefetch(ga + (k + 2) * S);
         }
         __syncthreads();  // P2
         if (k + 1 <= na) strip_rowpass<GA, P>(aslot + ((k + 1) & 1) * GA::SLOT, taps_a, prow, pq);
@@ -860,7 +889,8 @@ __global__ __launch_bounds__(256, (PairGeom<Ra, Rb>::MINB)) void k_blur2_strip(
                 const int y0 = y + wv * GB::VB;
                 if (y0 - Rb < 0 || y0 + GB::VB - 1 + Rb > H - 1) {
                     if (lane < Q::TWO / 2)
-                        strip_colpass_clamped<GB>(s0, s1, taps_b, lane, wv, y, ye, X, W, H, pitch, rb);
+                        strip_colpass_clamped<GB, NXTB, LOFF>(s0, s1, taps_b, lane, wv, y, ye, X, W, H, pitch, rb,
+                                                              rn, pitch_n, wn, hn);
                     return;
                 }
             }
@@ -870,7 +900,7 @@ __global__ __launch_bounds__(256, (PairGeom<Ra, Rb>::MINB)) void k_blur2_strip(
 #define COLB(w)                                                                                                  \
     case w:                                                                                                      \
         if (lane < Q::TWO / 2)                                                                                   \
-            strip_colpass<GB, P, w, false>(s0, s1, taps_b, lane, y, ye, X, W, pitch, rb, rb, 0, 0, 0);           \
+            strip_colpass<GB, P, w, NXTB, LOFF>(s0, s1, taps_b, lane, y, ye, X, W, pitch, rb, rn, pitch_n, wn, hn); \
         break;
                 COLB(0) COLB(1) COLB(2) COLB(3)
                 default:
@@ -883,7 +913,7 @@ __global__ __launch_bounds__(256, (PairGeom<Ra, Rb>::MINB)) void k_blur2_strip(
             const float* s0 = aslot + (k & 1) * GA::SLOT;
             const float* s1 = aslot + ((k + 1) & 1) * GA::SLOT;
             float* dstb = bslot + (k % NBR) * GB::SLOT;
-            const int y = ys - Rb + k * S;  // first G_s row of chunk k
+            const int y = ys - Rb - LOFF + k * S;  // first G_s row of chunk k
             switch (wv) {
 #define COLA(w)                                                                                                       \
     case w:                                                                                                           \
@@ -898,6 +928,30 @@ __global__ __launch_bounds__(256, (PairGeom<Ra, Rb>::MINB)) void k_blur2_strip(
         }
         colb();
     }
+}
+
+template <int Ra, int Rb, bool NXT, int P = kProfileOpenCV, bool NXTB = false>
+__global__ __launch_bounds__(256, (PairGeom<Ra, Rb>::MINB)) void k_blur2_strip(
+    const float* __restrict__ src, size_t img_stride, float* __restrict__ dst_a, float* __restrict__ dst_b,
+    float* __restrict__ nxt, size_t nxt_img_stride, int pitch_n, int wn, int hn, int W, int H, int pitch,
+    const BlurTaps taps_a, const BlurTaps taps_b, int ya, int yb, int seg) {
+    using Q = PairGeom<Ra, Rb>;
+    static_assert(P == kProfileOpenCV || !NXT, "imageproc pairs: no next-octave output from A");
+    __shared__ __attribute__((aligned(16))) float lds[Q::LDS_FLOATS];
+    const TileId tile = xcd_tile();
+    const int X = tile.x * Q::TWO;        // output columns [X, X + TWO)
+    const int ys = ya + tile.y * seg, ye = min(yb, ys + seg);
+    if (ys >= ye) return;
+    const size_t b = tile.z;
+    const uint32_t plane_bytes = (uint32_t)H * (uint32_t)pitch * 4u;
+    const __amdgpu_buffer_rsrc_t ra = uniform_rsrc(dst_a + b * img_stride, plane_bytes);
+    const __amdgpu_buffer_rsrc_t rb = uniform_rsrc(dst_b + b * img_stride, plane_bytes);
+    __amdgpu_buffer_rsrc_t rn = ra;
+    if constexpr (NXT || NXTB) rn = uniform_rsrc(nxt + b * nxt_img_stride, (uint32_t)hn * (uint32_t)pitch_n * 4u);
+    PlaneIn<Ra, P, typename Q::GA> ain;
+    ain.init(src + b * img_stride, X - Q::HB, W, H, pitch);
+    blur2_body<Ra, Rb, NXT, P, NXTB, 0, -1>(ain, lds, ra, rb, rn, pitch_n, wn, hn, X, ys, ye, W, H, pitch, taps_a,
+                                           taps_b);
 }
 
 // ---------------------------------------------------------------------------
@@ -1145,8 +1199,12 @@ template <class G, int P, bool NOLOAD = false>
 struct SeedLoader {
     static constexpr int CW = 12;              // window columns per item
     static constexpr int NCG = G::IWV / CW;    // column groups (12)
-    static constexpr int NPW = G::VB / 2;      // row pairs per wave (4 at S = 32, 2 at S = 16)
-    static_assert(G::NW == 4 && G::IWV == 144 && NCG * NPW <= 64 && (NPW & (NPW - 1)) == 0, "loader item map");
+    // row pairs per loading wave: 4 (48 of its lanes busy); S = 32: all four
+    // waves load, S = 16 (k_seed_pair): waves 0, 1 load and 2, 3 skip the
+    // loader (2 pairs on each of 4 waves left 40 of 64 lanes idle)
+    static constexpr int NPW = 4;
+    static constexpr int NLW = G::S / (2 * NPW);  // loading waves
+    static_assert(G::NW == 4 && G::IWV == 144 && NCG * NPW <= 64 && NLW * NPW * 2 == G::S, "loader item map");
     // border columns: per window column its source offset from the item's
     // first source byte (bits 0-3), single / two taps (bit 4), coefficients
     struct Tables {
@@ -1198,7 +1256,7 @@ struct SeedLoader {
         const uint32_t nbytes = (boff + (uint32_t)(sh - 1) * (uint32_t)row_stride + (uint32_t)sw + 3u) & ~3u;
         rs = uniform_rsrc(src - boff, nbytes);
         // this lane's item: row pair pr of the wave, column group cg
-        act = lane < NCG * NPW;
+        act = wv < NLW && lane < NCG * NPW;
         pr = wv * NPW + (lane & (NPW - 1));
         cg = lane / NPW;
         c0 = xw0 + CW * cg;  // first window column (even)
@@ -1395,6 +1453,47 @@ struct SeedLoader {
         }
     }
 };
+
+// A's input chunks computed from the u8 frame (k_seed_pair): the strip
+// seed's 2x upsample loader (SeedLoader), 144 window columns from xa - 8.
+template <class GA, int P>
+struct SeedIn {
+    SeedLoader<GA, P> ld;
+    __device__ __forceinline__ void prefetch(int r0) { ld.prefetch(r0); }
+    __device__ __forceinline__ void store(float* slot, int r0) { ld.store(slot, r0); }
+};
+
+// k_seed_pair: the seed blur and blur 1 of octave 0 in one pass -- A is the
+// strip seed (u8 -> 2x upsample in registers -> R_seed blur, k_seed_strip's
+// loader and arithmetic) writing G_0, B is blur 1 writing G_1: G_0 is written
+// once and never read back (blur 2 then starts from G_1).
+template <int Ra, int Rb, int P>
+__global__ __launch_bounds__(256, (PairGeom<Ra, Rb, 8>::MINB)) void k_seed_pair(
+    const uint8_t* __restrict__ frames, size_t frame_pitch, size_t row_stride, int sh, int sw,
+    float* __restrict__ dst_a, float* __restrict__ dst_b, size_t img_stride, int W, int H, int pitch,
+    const BlurTaps taps_a, const BlurTaps taps_b, int ya, int yb, int seg) {
+    using Q = PairGeom<Ra, Rb, 8>;
+    using GA = typename Q::GA;
+    using L = SeedLoader<GA, P>;
+    __shared__ __attribute__((aligned(16))) float lds[Q::LDS_FLOATS];
+    __shared__ typename L::Tables tabs;
+    const int tid = threadIdx.x, lane = tid & 63;
+    const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const TileId tile = xcd_tile();
+    const int X = tile.x * Q::TWO;
+    const int ys = ya + tile.y * seg, ye = min(yb, ys + seg);
+    if (ys >= ye) return;
+    const size_t b = tile.z;
+    const uint32_t plane_bytes = (uint32_t)H * (uint32_t)pitch * 4u;
+    const __amdgpu_buffer_rsrc_t ra = uniform_rsrc(dst_a + b * img_stride, plane_bytes);
+    const __amdgpu_buffer_rsrc_t rb = uniform_rsrc(dst_b + b * img_stride, plane_bytes);
+    const int xw0 = X - Q::HB - GA::HWL;  // A's window: 144 columns
+    L::tables(tabs, xw0, W, sw);
+    __syncthreads();
+    SeedIn<GA, P> ain;
+    ain.ld.init(frames + b * frame_pitch, row_stride, sh, sw, W, H, xw0, tabs, lane, wv);
+    blur2_body<Ra, Rb, false, P, false, 1, 8>(ain, lds, ra, rb, ra, 0, 0, 0, X, ys, ye, W, H, pitch, taps_a, taps_b);
+}
 
 // ABL: timing ablations for tools/ubench_kernels.hip only (the product
 // launches ABL = 0): 1 drops the plane stores (zero-size buffer), 2 the
@@ -1602,9 +1701,9 @@ static void launch_blur_strip_rp(const BlurLaunch& L, dim3 grid, int ya, int yb,
 
 // workgroups per strip launch the segment count aims for (SIFT_MI_STRIP_WG:
 // tuning knob, read per launch)
-static long strip_wg_target() {
+static long strip_wg_target(long dflt = 6144) {
     const char* e = getenv("SIFT_MI_STRIP_WG");
-    return e ? std::max(1L, atol(e)) : 6144L;
+    return e ? std::max(1L, atol(e)) : dflt;
 }
 
 // Row segments of a strip launch over `rows` rows with `per` strips x frames:
@@ -1615,9 +1714,9 @@ static long strip_wg_target() {
 // (measured, tools/ubench_kernels.hip segs: octave 1 of 64 1080p frames,
 // R = 13, 319 us at 13 segments of 84 rows vs 254 us at 3 of 360), while the
 // small octaves need the segments to fill the chip.  Returns the segment length.
-static int strip_segment_rows(int rows, long per) {
+static int strip_segment_rows(int rows, long per, long target = 6144) {
     const long few = std::min<long>((2048 + per - 1) / per, rows / 40);
-    long nseg = std::min<long>((strip_wg_target() + per - 1) / per, std::max<long>(rows / 320, few));
+    long nseg = std::min<long>((strip_wg_target(target) + per - 1) / per, std::max<long>(rows / 320, few));
     nseg = std::max(1L, nseg);
     // even: with an even first row every segment starts at an even row (the
     // strip kernels' next-octave rows are then the even / odd rows of each
@@ -1654,10 +1753,16 @@ template <int Ra, int Rb, int P = kProfileOpenCV>
 static void launch_blur2_rr(const BlurLaunch& A, const BlurLaunch& B, hipStream_t st) {
     using Q = PairGeom<Ra, Rb>;
     const int strips = (A.W + Q::TWO - 1) / Q::TWO;
-    const int seg = strip_segment_rows(A.H, (long)strips * A.n_img);
+    // the octave-0 (2, 3) pair (B.nxt) at ~8 k workgroups: measured against
+    // 3 k / 4 k / 6 k / 12 k on 64 1080p frames (tools/head_ab.sh)
+    const int seg = strip_segment_rows(A.H, (long)strips * A.n_img, B.nxt ? 8192 : 6144);
     const int nseg = (A.H + seg - 1) / seg;
     const dim3 grid(strips, nseg, A.n_img);
-    if constexpr (P == kProfileImageproc) {
+    if (B.nxt) {  // blurs 2, 3 of octave 0: B writes the next octave's base
+        hipLaunchKernelGGL((k_blur2_strip<Ra, Rb, false, P, true>), grid, dim3(256), 0, st, A.src, A.src_img_stride,
+                           A.dst, B.dst, B.nxt, B.nxt_img_stride, B.pitch_n, B.wn, B.hn, A.W, A.H, A.pitch, A.taps,
+                           B.taps, 0, A.H, seg);
+    } else if constexpr (P == kProfileImageproc) {
         hipLaunchKernelGGL((k_blur2_strip<Ra, Rb, false, P>), grid, dim3(256), 0, st, A.src, A.src_img_stride, A.dst,
                            B.dst, A.nxt, A.nxt_img_stride, A.pitch_n, A.wn, A.hn, A.W, A.H, A.pitch, A.taps, B.taps,
                            0, A.H, seg);
@@ -1672,7 +1777,7 @@ static void launch_blur2_rr(const BlurLaunch& A, const BlurLaunch& B, hipStream_
     }
 }
 
-// SIFT_MI_PAIR=0 disables the pair kernel (A/B and test knob, read per launch)
+// SIFT_MI_PAIR=0 disables the pair kernels (A/B and test knob, read per launch)
 static bool pair_blur_enabled() {
     const char* e = getenv("SIFT_MI_PAIR");
     return !(e && !strcmp(e, "0"));
@@ -1680,25 +1785,30 @@ static bool pair_blur_enabled() {
 
 int launch_blur_pair(int ra, int rb, const BlurLaunch& A, const BlurLaunch& B, hipStream_t st) {
     // A: G_{s-1} -> G_s, B: G_s -> G_{s+1} of one octave arena (same geometry
-    // and image stride); whole planes, no DoG / next-octave output
-    // (A may write the next octave's base: blur s = 3 of a pair (3, 4))
-    const bool ok = A.profile == B.profile && !A.dog && !B.dog && !B.nxt && A.y1 <= A.y0 && B.y1 <= B.y0 && A.dst && B.dst && B.src == A.dst && A.W == B.W &&
-                    A.H == B.H && A.pitch == B.pitch && A.src_img_stride == A.dst_img_stride &&
+    // and image stride); whole planes, no DoG; at most one of them writes the
+    // next octave's base (B: blurs 2, 3 of octave 0 after k_seed_pair)
+    const bool ok = A.profile == B.profile && !A.dog && !B.dog && !(A.nxt && B.nxt) && A.y1 <= A.y0 &&
+                    B.y1 <= B.y0 && A.dst && B.dst && B.src == A.dst && A.W == B.W && A.H == B.H &&
+                    A.pitch == B.pitch && A.src_img_stride == A.dst_img_stride &&
                     B.src_img_stride == A.src_img_stride && B.dst_img_stride == A.src_img_stride && A.W >= 64 &&
                     A.H >= 64 && (uint64_t)A.H * (uint64_t)A.pitch * 4 < (1ull << 31) && strip_blur_enabled() &&
                     pair_blur_enabled();
     if (!ok) return -1;
-    // only (5, 6) -- blurs 1, 2.  A (8, 10) pair for blurs 3, 4 (three-chunk
-    // column windows at 16-row chunks) was built, exact and slower than the
-    // two single launches (1.75 vs 1.62 ms per 64 frames of 3840x2160, round
-    // 2), and was removed.
+    // (5, 6): blurs 1, 2; (6, 8) with B.nxt: blurs 2, 3 of octave 0 (G_1 from
+    // k_seed_pair).  A (8, 10) pair for blurs 3, 4 (three-chunk column
+    // windows at 16-row chunks) was built, exact and slower than the two
+    // single launches (1.75 vs 1.62 ms per 64 frames of 3840x2160, round 2;
+    // DESIGN.md 3.10), and was removed.
     if (A.profile == kProfileImageproc) {
         // imageproc's clamp-to-edge chain: rows outside the image are read
-        // clamped (strip_colpass_clamped); blurs 1, 2 are radii 3, 4
-        if (ra == 3 && rb == 4 && !A.nxt) { launch_blur2_rr<3, 4, kProfileImageproc>(A, B, st); return 0; }
+        // clamped (strip_colpass_clamped); blurs 1, 2 are radii 3, 4; blurs
+        // 2, 3 radii 4, 4
+        if (ra == 3 && rb == 4 && !A.nxt && !B.nxt) { launch_blur2_rr<3, 4, kProfileImageproc>(A, B, st); return 0; }
+        if (ra == 4 && rb == 4 && !A.nxt && B.nxt) { launch_blur2_rr<4, 4, kProfileImageproc>(A, B, st); return 0; }
         return -1;
     }
-    if (ra == 5 && rb == 6) { launch_blur2_rr<5, 6>(A, B, st); return 0; }
+    if (ra == 5 && rb == 6 && !B.nxt) { launch_blur2_rr<5, 6>(A, B, st); return 0; }
+    if (ra == 6 && rb == 8 && !A.nxt && B.nxt) { launch_blur2_rr<6, 8>(A, B, st); return 0; }
     return -1;
 }
 
@@ -1797,6 +1907,42 @@ int launch_seed(int R, const SeedLaunch& L, hipStream_t st) {
     else
         launch_seed_r<5>(L, st);
     return 0;
+}
+
+// SIFT_MI_SEED_PAIR=0: the seed and blur 1 as separate launches (A/B and
+// test knob, read per launch)
+static bool seed_pair_enabled() {
+    const char* e = getenv("SIFT_MI_SEED_PAIR");
+    return !(e && !strcmp(e, "0"));
+}
+
+template <int Ra, int Rb, int P>
+static void launch_seed_pair_rr(const SeedLaunch& S, const BlurLaunch& B, hipStream_t st) {
+    using Q = PairGeom<Ra, Rb, 8>;
+    const int strips = (S.W + Q::TWO - 1) / Q::TWO;
+    const int seg = strip_segment_rows(S.H, (long)strips * S.n_img, 8192);  // as the (2, 3) pair
+    const int nseg = (S.H + seg - 1) / seg;
+    hipLaunchKernelGGL((k_seed_pair<Ra, Rb, P>), dim3(strips, nseg, S.n_img), dim3(256), 0, st, S.frames,
+                       S.frame_pitch, S.row_stride, S.sh, S.sw, S.dst, B.dst, S.dst_img_stride, S.W, S.H, S.pitch,
+                       S.taps, B.taps, 0, S.H, seg);
+}
+
+int launch_seed_pair(int rs, int rb, const SeedLaunch& S, const BlurLaunch& B, hipStream_t st) {
+    // the strip seed's geometry (exact 2x, one reflection per window) and the
+    // pair's (whole planes, B = blur 1 of the seed's plane, same arena)
+    const bool ok = S.W == 2 * S.sw && S.H == 2 * S.sh && S.W >= 160 && S.H >= 64 &&
+                    (uint64_t)S.H * (uint64_t)S.pitch * 4 < (1ull << 31) && S.y1 <= S.y0 && B.y1 <= B.y0 &&
+                    B.profile == S.profile && B.src == S.dst && B.dst && !B.dog && !B.nxt && B.W == S.W &&
+                    B.H == S.H && B.pitch == S.pitch && B.src_img_stride == S.dst_img_stride &&
+                    B.dst_img_stride == S.dst_img_stride && strip_blur_enabled() && pair_blur_enabled() &&
+                    seed_pair_enabled();
+    if (!ok) return -1;
+    if (S.profile == kProfileImageproc) {
+        if (rs == 3 && rb == 3) { launch_seed_pair_rr<3, 3, kProfileImageproc>(S, B, st); return 0; }
+        return -1;
+    }
+    if (rs == 5 && rb == 5) { launch_seed_pair_rr<5, 5, kProfileOpenCV>(S, B, st); return 0; }
+    return -1;
 }
 
 // ---------------------------------------------------------------------------

@@ -111,6 +111,9 @@ int launch_blur(int radius, const BlurLaunch& L, hipStream_t st);
 // -1 when the pair kernel does not apply (the caller launches them singly)
 int launch_blur_pair(int ra, int rb, const BlurLaunch& A, const BlurLaunch& B, hipStream_t st);
 int launch_seed(int radius, const SeedLaunch& L, hipStream_t st);
+// the seed (radius rs) and blur 1 (radius rb; B.src == L.dst) in one pass
+// (k_seed_pair: G_0 never read back); -1 when it does not apply
+int launch_seed_pair(int rs, int rb, const SeedLaunch& L, const BlurLaunch& B, hipStream_t st);
 // D_s = G_{s+1} - G_s (s < 5) of an octave's G stack, for n images
 void launch_dog(const float* gauss, size_t plane, size_t g_img_stride, float* dog, size_t dog_img_stride, int W, int H,
                 int pitch, int n_img, hipStream_t st);

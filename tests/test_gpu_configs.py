@@ -2,9 +2,12 @@
 
 * config #2: one 1920x1080 frame, `sift()` vs the oracle directly;
 * config #3: 256 x 640x480 frames through the device-resident batch path
-  (`sift_batch_device(..., fetch=False)`: 4 chunks of 64 over both pipeline
-  lanes), 6 frames spread over every chunk (the last included) vs the
-  oracle, every frame vs per-frame `sift()`;
+  (`sift_batch_device(..., fetch=False)`: 2 chunks of 128 -- chunks are
+  sized by seed pixels, ~531 M per chunk -- over both pipeline lanes),
+  frames spread over both chunks (the last included) vs the oracle, every
+  frame vs per-frame `sift()`;
+* chunks of more than 64 frames with a features_limit (the per-frame output
+  plan is one 256-thread workgroup, k_limit_plan);
 * config #4, one GPU's shard: bench.py's exact call (128 x 1920x1080, auto
   chunks, results kept in HBM), 2 frames vs the oracle, every frame vs
   per-frame `sift()`;
@@ -79,7 +82,7 @@ def test_config3_vga_256_device(pkg, ctx, oracle):
     assert st["frames"] == 256
     c.close()
     assert np.all(np.diff(offs) > 0)
-    for i in (0, 63, 64, 130, 200, 255):  # every 64-frame chunk, both lanes, the last frame
+    for i in (0, 63, 64, 127, 128, 200, 255):  # both 128-frame chunks (lanes), the last frame
         a, b = int(offs[i]), int(offs[i + 1])
         kp_o, desc_o = oracle.sift(host[i])
         _parity_rows(kp[a:b], desc[a:b], kp_o, desc_o)
@@ -110,6 +113,22 @@ def test_config4_bench_shard_1080p(pkg, ctx, oracle):
         r = ctx.sift(host[i])
         assert np.array_equal(kp[a:b].view(np.uint32), r.keypoints_array.view(np.uint32)), i
         assert np.array_equal(desc[a:b], r.descriptors), i
+
+
+@pytest.mark.parametrize("limit", [None, 0, 3, 40])
+def test_large_chunk_features_limit(pkg, ctx, limit):
+    """200 frames in one chunk: the output plan (per-frame counts, offsets,
+    response truncation) covers frames past the first 64."""
+    import synth
+    fr = synth.frames(200, 96, 64, seed0=7)
+    c = pkg.Context(0, pkg.OpenCVProcessing)
+    c.set_chunk(200)
+    got = c.sift_batch(fr, features_limit=limit)
+    c.close()
+    ref = [ctx.sift(f, features_limit=limit) for f in fr]
+    if limit is None:
+        assert sum(len(r) for r in ref) > 200
+    assert all(a == b for a, b in zip(got, ref))
 
 
 @pytest.mark.parametrize("lanes", [1, 2])

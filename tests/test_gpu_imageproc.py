@@ -70,17 +70,20 @@ def test_ip_batch_and_limit(pkg, ctx_ip, oracle):
         assert_parity(pkg, res, kp_o, desc_o, ext_o)
 
 
-@pytest.mark.parametrize("kernel", ["strip", "tile", "notail", "nopair"])
+@pytest.mark.parametrize("kernel", ["strip", "tile", "notail", "nopair", "noseedpair"])
 @pytest.mark.parametrize("name", ["synth_640x480", "synth_301x207", "synth_1000x333", "synth_90x700",
                                   "synth_2000x40", "synth_97x61"])
 def test_ip_pyramid_kernels(ctx_ip, oracle, monkeypatch, kernel, name):
     """The imageproc profile's kernel families bit for bit against the oracle:
-    "strip" (k_seed_strip<3, imageproc>: the Triangle 2x upsample, vertical then
-    horizontal, clamped, in the strip loader; the k_blur2_strip<3, 4>
-    imageproc pair for G_1, G_2, whose border chunks read clamped G_1 rows;
+    "strip" (k_seed_pair<3, 3, imageproc>: the Triangle 2x upsample, vertical
+    then horizontal, clamped, in the strip loader, then the seed blur and
+    blur 1; the k_blur2_strip<4, 4> pair for G_2, G_3 and the next octave's
+    base (image's Nearest: odd rows / columns) of octave 0 and the <3, 4>
+    pair for G_1, G_2 of the others, whose border chunks read clamped rows;
     clamp-to-edge strip blurs and the tail kernel), "tile" (k_seed_ip and the
     tile blurs), "notail" (per-blur launches for the small octaves), "nopair"
-    (single-blur strips for G_1, G_2)."""
+    (single-blur strips for G_1, G_2), "noseedpair" (k_seed_strip, then
+    octave 0 like the others)."""
     from test_gpu_parity import _KERNEL_ENV, _extra
     for k, v in _KERNEL_ENV[kernel].items():
         monkeypatch.setenv(k, v)

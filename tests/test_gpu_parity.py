@@ -86,6 +86,7 @@ _KERNEL_ENV = {
     "nopair": {"SIFT_MI_PAIR": "0"},
     "notail": {"SIFT_MI_TAIL": "0"},
     "single": {"SIFT_MI_PAIR": "0", "SIFT_MI_TAIL": "0"},
+    "noseedpair": {"SIFT_MI_SEED_PAIR": "0"},
 }
 
 
@@ -94,15 +95,18 @@ _KERNEL_ENV = {
                                   "synth_90x700", "synth_2000x40", "synth_33x17"])
 def test_pyramid_blur_kernels(ctx, oracle, monkeypatch, kernel, name):
     """Every blur kernel family against the oracle's blur chain, bit for bit:
-    "strip" (the default: k_seed_strip, the k_blur2_strip pair for G_1, G_2,
-    k_blur_strip for the rest -- 128-column strips streamed down in row
+    "strip" (the default: k_seed_pair for G_0, G_1 of octave 0 and the
+    k_blur2_strip (6, 8) pair for its G_2, G_3 and the next octave's base,
+    the (5, 6) pair for G_1, G_2 of the later octaves, k_blur_strip for the
+    rest -- 128-column strips streamed down in row
     chunks, many row segments per octave at these sizes, partial strips,
     reflect-101 at every border -- and k_octave_tail from the first octave that
     fits LDS; the tile kernels where a strip does not apply: tiny octaves, W
     or H <= R), "tile" (SIFT_MI_BLUR_KERNEL=tile: one 64-column tile per
     workgroup everywhere), "nopair" / "notail" / "single" (SIFT_MI_PAIR=0,
     SIFT_MI_TAIL=0: single-blur strips instead of the pair kernel, per-blur
-    launches for the small octaves)."""
+    launches for the small octaves), "noseedpair" (SIFT_MI_SEED_PAIR=0:
+    k_seed_strip, then octave 0 like the others)."""
     for k, v in _KERNEL_ENV[kernel].items():
         monkeypatch.setenv(k, v)
     img = INPUTS[name] if name in INPUTS else _extra(name)

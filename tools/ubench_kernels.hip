@@ -432,6 +432,193 @@ void bench_seed(int N, int sw, int sh, int stride) {
     CK(hipFree(dxo)); CK(hipFree(dxa)); CK(hipFree(dxb)); CK(hipFree(dyo)); CK(hipFree(dya)); CK(hipFree(dyb));
 }
 
+// octave-0 head of the bench (N frames of 1920x1080 -> 3840x2160, 6-plane
+// arena + the next octave's plane): seed, (5, 6) pair, blur 3 with the next
+// base (round 3) vs k_seed_pair then the (6, 8) pair with the next base
+// (round 4); G_0..G_3 and the next base compared bit for bit
+void bench_head(int N, int profile) {
+    const int sw = 1920, sh = 1080, W = 2 * sw, H = 2 * sh, pitch = (W + 63) & ~63;
+    const int wn = W / 2, hn = H / 2, pn = (wn + 63) & ~63;
+    std::vector<uint8_t> hf((size_t)N * sw * sh);
+    uint32_t x = 12345;
+    for (size_t i = 0; i < hf.size(); i++) {
+        const size_t px = i % ((size_t)sw * sh);
+        const int xx = (int)(px % sw), yy = (int)(px / sw);
+        x = x * 1664525u + 1013904223u;  // smooth field + noise
+        hf[i] = (uint8_t)(128 + 60 * std::sin(xx * 0.05) * std::cos(yy * 0.03) + (int)(x >> 29));
+    }
+    uint8_t* df;
+    CK(hipMalloc(&df, hf.size()));
+    CK(hipMemcpy(df, hf.data(), hf.size(), hipMemcpyHostToDevice));
+    std::vector<int> xo, yo;
+    std::vector<float> xa, xb, ya, yb;
+    int xmax, ymax;
+    cv_linear_tab(sw, W, xo, xa, xb, &xmax);
+    cv_linear_tab(sh, H, yo, ya, yb, &ymax);
+    int *dxo, *dyo;
+    float *dxa, *dxb, *dya, *dyb;
+    CK(hipMalloc(&dxo, W * 4)); CK(hipMalloc(&dxa, W * 4)); CK(hipMalloc(&dxb, W * 4));
+    CK(hipMalloc(&dyo, H * 4)); CK(hipMalloc(&dya, H * 4)); CK(hipMalloc(&dyb, H * 4));
+    CK(hipMemcpy(dxo, xo.data(), W * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dxa, xa.data(), W * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dxb, xb.data(), W * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dyo, yo.data(), H * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dya, ya.data(), H * 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dyb, yb.data(), H * 4, hipMemcpyHostToDevice));
+    const size_t plane = (size_t)pitch * H, nplane = (size_t)pn * hn;
+    const size_t stride = plane * 6;
+    float *g[2], *nx[2];
+    for (int v = 0; v < 2; v++) {
+        CK(hipMalloc(&g[v], stride * N * 4));
+        CK(hipMalloc(&nx[v], nplane * N * 4));
+        CK(hipMemset(g[v], 0, stride * N * 4));
+        CK(hipMemset(nx[v], 0, nplane * N * 4));
+    }
+    // taps: normalised Gaussians of the radii (the arithmetic, not the sigmas, matters here)
+    auto taps = [](int R) {
+        BlurTaps t{};
+        double s = 0;
+        for (int k = -R; k <= R; k++) s += std::exp(-(k * k) / (2.0 * (R / 4.0) * (R / 4.0)));
+        for (int k = 0; k <= R; k++) t.k[k] = (float)(std::exp(-(k * k) / (2.0 * (R / 4.0) * (R / 4.0))) / s);
+        return t;
+    };
+    const bool ip = profile == kProfileImageproc;
+    const int rs = ip ? 3 : 5, r1 = ip ? 3 : 5, r2 = ip ? 4 : 6, r3 = ip ? 4 : 8;
+    auto seedl = [&](int v) {
+        SeedLaunch L{};
+        L.frames = df;
+        L.frame_pitch = (size_t)sw * sh;
+        L.row_stride = sw;
+        L.sh = sh;
+        L.sw = sw;
+        L.tab = ResizeTab{dxo, dxa, dxb, dyo, dya, dyb, xmax};
+        L.profile = profile;
+        L.dst = g[v];
+        L.dst_img_stride = stride;
+        L.W = W;
+        L.H = H;
+        L.pitch = pitch;
+        L.n_img = N;
+        L.taps = taps(rs);
+        return L;
+    };
+    auto blurl = [&](int v, int s, int R) {
+        BlurLaunch L{};
+        L.src = g[v] + (s - 1) * plane;
+        L.dst = g[v] + s * plane;
+        L.src_img_stride = L.dst_img_stride = stride;
+        L.W = W;
+        L.H = H;
+        L.pitch = pitch;
+        L.n_img = N;
+        L.taps = taps(R);
+        L.profile = profile;
+        if (s == 3) {
+            L.nxt = nx[v];
+            L.nxt_img_stride = nplane;
+            L.pitch_n = pn;
+            L.wn = wn;
+            L.hn = hn;
+        }
+        return L;
+    };
+    auto timeit = [&](auto&& f) {
+        f();
+        hipEvent_t a, b;
+        CK(hipEventCreate(&a));
+        CK(hipEventCreate(&b));
+        CK(hipEventRecord(a));
+        for (int i = 0; i < 5; i++) f();
+        CK(hipEventRecord(b));
+        CK(hipEventSynchronize(b));
+        float ms;
+        CK(hipEventElapsedTime(&ms, a, b));
+        return ms / 5;
+    };
+    int rc = 0;
+    const float t_old = timeit([&] {
+        rc |= launch_seed(rs, seedl(0), 0);
+        rc |= launch_blur_pair(r1, r2, blurl(0, 1, r1), blurl(0, 2, r2), 0);
+        rc |= launch_blur(r3, blurl(0, 3, r3), 0);
+    });
+    const float ts = timeit([&] { launch_seed(rs, seedl(0), 0); });
+    const float tp = timeit([&] { launch_blur_pair(r1, r2, blurl(0, 1, r1), blurl(0, 2, r2), 0); });
+    const float t3 = timeit([&] { launch_blur(r3, blurl(0, 3, r3), 0); });
+    const float t_new = timeit([&] {
+        rc |= launch_seed_pair(rs, r1, seedl(1), blurl(1, 1, r1), 0);
+        rc |= launch_blur_pair(r2, r3, blurl(1, 2, r2), blurl(1, 3, r3), 0);
+    });
+    const float tsp = timeit([&] { launch_seed_pair(rs, r1, seedl(1), blurl(1, 1, r1), 0); });
+    const float tp23 = timeit([&] { launch_blur_pair(r2, r3, blurl(1, 2, r2), blurl(1, 3, r3), 0); });
+    CK(hipDeviceSynchronize());
+    std::vector<float> h0(stride * N), h1(stride * N), n0(nplane * N), n1(nplane * N);
+    CK(hipMemcpy(h0.data(), g[0], stride * N * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(h1.data(), g[1], stride * N * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(n0.data(), nx[0], nplane * N * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(n1.data(), nx[1], nplane * N * 4, hipMemcpyDeviceToHost));
+    size_t diff[5] = {0, 0, 0, 0, 0};
+    for (int b = 0; b < N; b++)
+        for (int s = 0; s < 4; s++)
+            for (int y = 0; y < H; y++)
+                diff[s] += std::memcmp(&h0[b * stride + s * plane + (size_t)y * pitch],
+                                       &h1[b * stride + s * plane + (size_t)y * pitch], W * 4) != 0;
+    for (int b = 0; b < N; b++)
+        for (int y = 0; y < hn; y++)
+            diff[4] += std::memcmp(&n0[b * nplane + (size_t)y * pn], &n1[b * nplane + (size_t)y * pn], wn * 4) != 0;
+    // each path's next base against its own G_3 (nearest 1/2: (2x, 2y) / (2x + 1, 2y + 1))
+    for (int v = 0; v < 2; v++) {
+        const std::vector<float>& gg = v ? h1 : h0;
+        const std::vector<float>& nn = v ? n1 : n0;
+        size_t bad = 0;
+        int fb = -1, fy = -1, fx = -1;
+        for (int b = 0; b < N; b++)
+            for (int yy = 0; yy < hn; yy++)
+                for (int xx = 0; xx < wn; xx++) {
+                    const float e = gg[b * stride + 3 * plane + (size_t)(2 * yy + ip) * pitch + 2 * xx + ip];
+                    if (std::memcmp(&e, &nn[b * nplane + (size_t)yy * pn + xx], 4)) {
+                        if (!bad) fb = b, fy = yy, fx = xx;
+                        bad++;
+                    }
+                }
+        std::printf("  %s path: next base vs its G_3: %zu px differ (first frame %d y %d x %d)\n", v ? "new" : "old",
+                    bad, fb, fy, fx);
+        if (bad) {
+            int rows[8], nr = 0;
+            for (int yy = 0; yy < hn && nr < 8; yy++) {
+                bool d = false;
+                for (int xx = 0; xx < wn; xx++) {
+                    const float e = gg[3 * plane + (size_t)(2 * yy + ip) * pitch + 2 * xx + ip];
+                    d |= std::memcmp(&e, &nn[(size_t)yy * pn + xx], 4) != 0;
+                }
+                if (d) rows[nr++] = yy;
+            }
+            std::printf("    frame 0 rows:");
+            for (int i = 0; i < nr; i++) std::printf(" %d", rows[i]);
+            std::printf("\n    next[y=%d][0..3] = %g %g %g %g, G3 = %g %g %g %g\n", fy, nn[(size_t)fy * pn],
+                        nn[(size_t)fy * pn + 1], nn[(size_t)fy * pn + 2], nn[(size_t)fy * pn + 3],
+                        gg[3 * plane + (size_t)(2 * fy + ip) * pitch + ip], gg[3 * plane + (size_t)(2 * fy + ip) * pitch + 2 + ip],
+                        gg[3 * plane + (size_t)(2 * fy + ip) * pitch + 4 + ip], gg[3 * plane + (size_t)(2 * fy + ip) * pitch + 6 + ip]);
+        }
+    }
+    const double px = (double)W * H * N;
+    std::printf("octave-0 head (%s), %d x %dx%d -> G_0..G_3 + next base: rc %d\n", ip ? "imageproc" : "opencv", N,
+                sw, sh, rc);
+    std::printf("  round 3: seed %7.1f + pair(1,2) %7.1f + blur3 %7.1f us = %7.1f us in sequence (%7.1f us), "
+                "%.2f TB/s of its %.2f B/px\n", 1e3 * ts, 1e3 * tp, 1e3 * t3, 1e3 * (ts + tp + t3), 1e3 * t_old,
+                (0.25 + 24.25) * px / (t_old * 1e-3) / 1e12, 0.25 + 24.25);
+    std::printf("  round 4: seed pair %7.1f + pair(2,3) %7.1f us = %7.1f us in sequence (%7.1f us), "
+                "%.2f TB/s of its %.2f B/px\n", 1e3 * tsp, 1e3 * tp23, 1e3 * (tsp + tp23), 1e3 * t_new,
+                (0.25 + 20.25) * px / (t_new * 1e-3) / 1e12, 0.25 + 20.25);
+    std::printf("  rows differing: G0 %zu G1 %zu G2 %zu G3 %zu next %zu\n", diff[0], diff[1], diff[2], diff[3],
+                diff[4]);
+    for (int v = 0; v < 2; v++) {
+        CK(hipFree(g[v]));
+        CK(hipFree(nx[v]));
+    }
+    CK(hipFree(df));
+    CK(hipFree(dxo)); CK(hipFree(dxa)); CK(hipFree(dxb)); CK(hipFree(dyo)); CK(hipFree(dya)); CK(hipFree(dyb));
+}
+
 // k_seed_strip timing ablations (ABL bits: 1 no plane stores, 2 no loads /
 // upsample, 4 no row pass), 64 frames of 1920x1080 -> 3840x2160
 template <int ABL>
@@ -537,6 +724,11 @@ void bench_stream(int N) {
 
 int main(int argc, char** argv) {
     const char* mode = argc > 1 ? argv[1] : "all";
+    if (!strcmp(mode, "head")) {
+        bench_head(argc > 2 ? atoi(argv[2]) : 64, kProfileOpenCV);
+        bench_head(argc > 2 ? atoi(argv[2]) : 64, kProfileImageproc);
+        return 0;
+    }
     if (!strcmp(mode, "segs")) {
         bench_segs(argc > 2 ? atoi(argv[2]) : 64);
         return 0;
