@@ -148,6 +148,15 @@ int sift_mi_set_keep_on_device(sift_mi_ctx* ctx, int keep);
  * (frame i at offsets[i] .. offsets[i+1]); valid until the next call. */
 int sift_mi_device_results(sift_mi_ctx* ctx, const sift_mi_keypoint** d_kps, const uint8_t** d_desc, size_t* n);
 
+/* Validation read-back (extension, not the crate): the Gaussian planes
+ * G_0..G_5 of octave `octave` of frame `frame` of the last batch / sift()
+ * call, as that call's pyramid left them in the context's arena -- (6, h, w)
+ * f32 like sift_mi_read_scale_space.  Valid only when the last call ran as
+ * one chunk (one frame, or sift_mi_set_chunk >= its frames) and until the
+ * next call; SIFT_MI_ESTATE otherwise.  Lets tests check the batch path's
+ * planes (which no DoG is materialised for) against precompute_images. */
+int sift_mi_read_batch_scale_space(sift_mi_ctx* ctx, uint32_t frame, size_t octave, float* out);
+
 /* ---- src/lib.rs:123-143 `precompute_images` / `PrecomputedImages` ------- */
 int sift_mi_precompute(sift_mi_ctx* ctx, const uint8_t* pixels, uint32_t width, uint32_t height,
                        size_t row_stride, size_t* n_octaves);

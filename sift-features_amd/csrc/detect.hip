@@ -1,3 +1,4 @@
+#include <string.h>
 // Keypoint detection on MI355X: DoG extrema + sub-pixel refinement + contrast
 // and edge rejection (k_detect_rows, k_refine), then 36-bin orientation histograms and
 // reference orientations (k_orient).
@@ -284,6 +285,265 @@ void launch_detect(DetectLaunch& L, hipStream_t st) {
     L.block0[k] = nb;
     if (nb == 0) return;
     hipLaunchKernelGGL(k_detect_rows, dim3(nb), dim3(256), 0, st, L);
+}
+
+// ---------------------------------------------------------------------------
+// k_blur_detect: the octave's last blur (G_4 -> G_5, radius R) and the
+// extremum scan of its three scales (point_is_local_extremum,
+// src/lib.rs:437-506) in one pass.  G_5 is produced on chip, so the scan
+// reads G_0..G_4 (G_4 from the blur's own LDS rows) and never reads G_4 /
+// G_5 back from HBM: ~26 B per octave pixel for blur 5 and detection
+// together instead of ~35 (blur 5: 8 + halo, k_detect_rows: 24 + halo).
+//
+// A wave owns k_detect_rows' strip geometry: 64 columns x = xb - 1 + lane
+// (62 outputs, the edge lanes are halo) by a segment of rows [ya, yb), and
+// walks down it one row of G_4 at a time:
+//   * the G_4 row's 64 + 2R columns [xb - 1 - R, xb + 63 + R) go to an LDS
+//     ring (BD_RING rows per wave; loaded two rows ahead), and each lane's
+//     row-filter output at its column is the FMA chain from the leftmost tap
+//     of OpenCV's RowFilter (imageproc: the unfused chain) over 2R + 1 ring
+//     values -- the same operations as the strip kernels (pyramid.hip);
+//   * the last 2R + 1 row-filter outputs are a register window, whose column
+//     filter (centre product + fma of the pair sums / imageproc's unfused
+//     chain) is G_5 at row r = q - R: stored (rows [ya, yb), lanes 1..62);
+//   * row r's D_0..D_4 are formed from G_0..G_3 (loaded two rows ahead),
+//     G_4 (its ring row, still resident) and G_5, and the 3x3x3 test of row
+//     r - 1 runs on the rolling row max / min exactly as k_detect_rows.
+// Rows and columns outside the image are reflect-101 (clamp-to-edge) like the
+// strip blur; only rows inside the image are stored or tested, so G_5 and the
+// candidates are those of launch_blur + k_detect_rows bit for bit.
+// ---------------------------------------------------------------------------
+constexpr int BD_RING = 16;  // raw G_4 rows per wave (the rows r .. r + R and the next)
+constexpr int BD_RP = 100;   // ring row pitch (floats): 64 + 2R columns, R <= 18
+
+template <int P>
+__device__ __forceinline__ int bd_index(int p, int n) {
+    if (P == kProfileOpenCV) p = p < 0 ? -p : (p >= n ? 2 * n - 2 - p : p);
+    return p < 0 ? 0 : (p >= n ? n - 1 : p);
+}
+
+// 1-D block id remapped so each XCD walks a contiguous range (neighbouring
+// strips of one row segment share their G_4 halo columns in that XCD's L2)
+__device__ __forceinline__ uint32_t xcd_block_1d() {
+    const uint32_t nwg = gridDim.x, orig = blockIdx.x;
+    const uint32_t q = nwg / 8, r = nwg % 8, xcd = orig % 8;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
+template <int R, int P>
+__global__ __launch_bounds__(256) void k_blur_detect(const BlurDetectLaunch L) {
+    static_assert(64 + 2 * R <= BD_RP && R + 3 <= BD_RING, "ring geometry");
+    __shared__ float ring[4][BD_RING * BD_RP];
+    __shared__ uint64_t lcand[DR_LCAP];
+    __shared__ uint32_t lcount, gbase;
+    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    const int W = L.W, H = L.H, pitch = L.pitch;
+    const uint32_t g = xcd_block_1d() * 4 + wave;  // strip index: frame-major, then row segment, then column
+    const uint32_t per = (uint32_t)(L.nsx * L.nsy);
+    const int b = (int)(g / per);
+    const uint32_t rem = g - (uint32_t)b * per;
+    const int sy = (int)(rem / (uint32_t)L.nsx), sx = (int)(rem % (uint32_t)L.nsx);
+    if (tid == 0) lcount = 0;
+    __syncthreads();
+    if (b < L.n_img) {
+        const size_t P_ = (size_t)pitch * H;
+        const uint32_t pb = (uint32_t)P_ * 4u;  // plane bytes (< 2^31: launch_blur_detect)
+        const float* gb = L.gauss + (size_t)b * L.img_stride;
+        const __amdgpu_buffer_rsrc_t rg0 = uniform_rsrc(gb, pb), rg1 = uniform_rsrc(gb + P_, pb),
+                                     rg2 = uniform_rsrc(gb + 2 * P_, pb), rg3 = uniform_rsrc(gb + 3 * P_, pb),
+                                     rg4 = uniform_rsrc(gb + 4 * P_, pb), rg5 = uniform_rsrc(gb + 5 * P_, pb);
+        const int xb = sx * DR_COLS;
+        const int x = xb - 1 + lane;  // this lane's column
+        const int xc = min(max(x, 0), W - 1);
+        const bool xout = lane >= 1 && lane <= DR_COLS && x >= kImageBorder && x < W - kImageBorder;
+        const bool xst = lane >= 1 && lane <= DR_COLS && x < W;
+        const int ya = sy * L.seg, yb = min(ya + L.seg, H);
+        // G_4 ring columns [xb - 1 - R, xb + 63 + R): lane -> column ca, and
+        // lanes < 2R also ca + 64
+        const int ca = xb - 1 - R + lane;
+        const int va = bd_index<P>(ca, W) * 4, vb = bd_index<P>(ca + 64, W) * 4, vx = xc * 4;
+        float* rg = ring[wave];
+        auto ld4 = [&](int q, float& a, float& c) {  // G_4 row q (reflected) into registers
+            const int so = bd_index<P>(q, H) * pitch * 4;
+            a = buffer_load_f32(rg4, va, so);
+            c = lane < 2 * R ? buffer_load_f32(rg4, vb, so) : 0.0f;
+        };
+        auto ld03 = [&](int r, float (&d)[4]) {  // G_0..G_3 at (row r clamped, column xc)
+            const int so = min(max(r, 0), H - 1) * pitch * 4;
+            d[0] = buffer_load_f32(rg0, vx, so);
+            d[1] = buffer_load_f32(rg1, vx, so);
+            d[2] = buffer_load_f32(rg2, vx, so);
+            d[3] = buffer_load_f32(rg3, vx, so);
+        };
+        // row filter of G_4 row q at this lane's column (q's ring row)
+        auto rowpass = [&](int q) -> float {
+            const float* p = rg + (q & (BD_RING - 1)) * BD_RP + lane;
+            float v[2 * R + 1];
+#pragma unroll
+            for (int t = 0; t <= 2 * R; t++) v[t] = p[t];
+            float acc = v[0] * L.taps.k[R];
+#pragma unroll
+            for (int t = 1; t <= 2 * R; t++) {
+                const float kt = L.taps.k[t > R ? t - R : R - t];
+                acc = P == kProfileOpenCV ? __builtin_fmaf(v[t], kt, acc) : acc + v[t] * kt;
+            }
+            return acc;
+        };
+        float win[2 * R + 1];  // row-filter outputs of rows r - R .. r + R
+        // rolling detection state (k_detect_rows): row max / min of rows r - 2,
+        // r - 1, r per DoG plane, the left / right max / min and centre of row r - 1
+        float hmx[kDogPerOctave][3], hmn[kDogPerOctave][3];
+        float lrx[kDogPerOctave], lrn[kDogPerOctave], ctr[kDogPerOctave];
+        const float threshold = floorf(0.5f * kContrastThreshold / (float)kScalesPerOctave);
+        const int q0 = ya - 1 - R, q1 = yb + R;  // G_4 rows filtered: [q0, q1]
+        float a0, c0, a1, c1;
+        float d0[4], d1[4];
+        ld4(q0, a0, c0);
+        ld4(q0 + 1, a1, c1);
+        ld03(ya - 1, d0);
+        ld03(ya, d1);
+        // G_4 row q arrived in (a, c); G_0..G_3 of row r = q - R in d (when r >= ya - 1)
+        auto step = [&](int q, float& a, float& c, float (&d)[4]) {
+            float* wp = rg + (q & (BD_RING - 1)) * BD_RP;
+            wp[lane] = a;
+            if (lane < 2 * R) wp[64 + lane] = c;
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+            __builtin_amdgcn_wave_barrier();
+            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+            if (q + 2 <= q1) ld4(q + 2, a, c);
+            win[2 * R] = rowpass(q);
+            const int r = q - R;
+            if (r >= ya - 1) {  // uniform
+                float g5;
+                if constexpr (P == kProfileOpenCV) {
+                    g5 = win[R] * L.taps.k[0];
+#pragma unroll
+                    for (int t = 1; t <= R; t++) g5 = __builtin_fmaf(win[R + t] + win[R - t], L.taps.k[t], g5);
+                } else {
+                    g5 = win[0] * L.taps.k[R];
+#pragma unroll
+                    for (int t = 1; t <= 2 * R; t++) g5 = g5 + win[t] * L.taps.k[t > R ? t - R : R - t];
+                }
+                if (xst && r >= ya && r < yb)
+                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, g5), rg5, vx,
+                                                          r * pitch * 4, 2 /* nt */);
+                // row r's DoG values (G_4 from the ring: row r is resident)
+                const float g4 = rg[(r & (BD_RING - 1)) * BD_RP + lane + R];
+                float cur[kDogPerOctave];
+                cur[0] = d[1] - d[0];
+                cur[1] = d[2] - d[1];
+                cur[2] = d[3] - d[2];
+                cur[3] = g4 - d[3];
+                cur[4] = g5 - g4;
+                if (r + 2 <= yb) ld03(r + 2, d);
+                float nlx[kDogPerOctave], nln[kDogPerOctave];
+#pragma unroll
+                for (int p = 0; p < kDogPerOctave; p++) {
+                    const float l = dpp_from_left(cur[p]), rr = dpp_from_right(cur[p]);
+                    nlx[p] = fmaxf(l, rr);
+                    nln[p] = fminf(l, rr);
+                    hmx[p][2] = fmaxf(nlx[p], cur[p]);
+                    hmn[p][2] = fminf(nln[p], cur[p]);
+                }
+                const int y = r - 1;  // tested row: rows r - 2, r - 1, r are in
+                if (y >= ya) {        // uniform
+                    const bool yin = xout && y >= kImageBorder && y < H - kImageBorder;
+                    float pmx[kDogPerOctave], pmn[kDogPerOctave];
+#pragma unroll
+                    for (int p = 0; p < kDogPerOctave; p++) {
+                        pmx[p] = fmaxf(fmaxf(hmx[p][0], hmx[p][1]), hmx[p][2]);
+                        pmn[p] = fminf(fminf(hmn[p][0], hmn[p][1]), hmn[p][2]);
+                    }
+                    uint32_t ok3 = 0;
+#pragma unroll
+                    for (int s_in = 1; s_in <= kScalesPerOctave; s_in++) {
+                        const float val = ctr[s_in];
+                        const float m8 = fmaxf(fmaxf(hmx[s_in][0], hmx[s_in][2]), lrx[s_in]);
+                        const float n8 = fminf(fminf(hmn[s_in][0], hmn[s_in][2]), lrn[s_in]);
+                        const float mx = fmaxf(fmaxf(pmx[s_in - 1], pmx[s_in + 1]), m8);
+                        const float mn = fminf(fminf(pmn[s_in - 1], pmn[s_in + 1]), n8);
+                        const bool ok = yin && fabsf(val) > threshold && (val > 0.0f ? val >= mx : val <= mn);
+                        ok3 |= (uint32_t)ok << (s_in - 1);
+                    }
+                    if (__ballot(ok3 != 0)) {  // wave-uniform: rare
+                        while (ok3) {
+                            const int bit = __builtin_ctz(ok3);
+                            ok3 &= ok3 - 1;
+                            const uint64_t key = make_key((uint32_t)(L.img_base + b), (uint32_t)L.octave,
+                                                          (uint32_t)(bit + 1), (uint32_t)y, (uint32_t)x);
+                            const uint32_t li = atomicAdd(&lcount, 1u);
+                            if (li < DR_LCAP) {
+                                lcand[li] = key;
+                            } else {
+                                const uint32_t slot = atomicAdd(L.counter, 1u);
+                                if (slot < L.cap) L.cand[slot] = key;
+                            }
+                        }
+                    }
+                }
+#pragma unroll
+                for (int p = 0; p < kDogPerOctave; p++) {
+                    hmx[p][0] = hmx[p][1];
+                    hmn[p][0] = hmn[p][1];
+                    hmx[p][1] = hmx[p][2];
+                    hmn[p][1] = hmn[p][2];
+                    lrx[p] = nlx[p];
+                    lrn[p] = nln[p];
+                    ctr[p] = cur[p];
+                }
+            }
+#pragma unroll
+            for (int j = 0; j < 2 * R; j++) win[j] = win[j + 1];
+        };
+        // two rows in flight in two alternating buffers (the loop is unrolled
+        // by two, so neither is copied while its loads are outstanding): G_4
+        // rows q0 + 2i and rows ya - 1 + 2i (r - (ya - 1) = q - q0 - 2R) in
+        // (a0, c0) / d0, the odd ones in (a1, c1) / d1
+        for (int q = q0; q <= q1; q += 2) {
+            step(q, a0, c0, d0);
+            if (q + 1 <= q1) step(q + 1, a1, c1, d1);
+        }
+    }
+    // one global atomic per block, then a coalesced copy of the block's list
+    __syncthreads();
+    const uint32_t nl = lcount < DR_LCAP ? lcount : DR_LCAP;
+    if (nl == 0) return;
+    if (tid == 0) gbase = atomicAdd(L.counter, nl);
+    __syncthreads();
+    for (uint32_t i = tid; i < nl; i += 256)
+        if (gbase + i < L.cap) L.cand[gbase + i] = lcand[i];
+}
+
+// SIFT_MI_FUSED_DETECT=0 keeps blur 5 and detection apart (A/B and test knob)
+int launch_blur_detect(int R, BlurDetectLaunch& L, hipStream_t st) {
+    {
+        const char* e = getenv("SIFT_MI_FUSED_DETECT");
+        if (e && !strcmp(e, "0")) return -1;
+    }
+    const bool ok = L.W > R + 1 && L.H > R + 1 && L.W >= 2 * kImageBorder && L.H >= 2 * kImageBorder &&
+                    (uint64_t)L.H * (uint64_t)L.pitch * 4 < (1ull << 31) && L.n_img > 0;
+    if (!ok) return -1;
+    const bool ocv = L.profile == kProfileOpenCV;
+    if (!((ocv && R == 13) || (!ocv && R == 7))) return -1;
+    L.nsx = (L.W + DR_COLS - 1) / DR_COLS;
+    // row segments: a segment re-filters 2R + 2 halo rows, so long ones, but
+    // enough waves to fill the chip (>= ~16 k)
+    int seg = 32;
+    for (int s : {256, 128, 64}) {
+        if ((long)L.nsx * ((L.H + s - 1) / s) * L.n_img >= 16384) {
+            seg = s;
+            break;
+        }
+    }
+    L.seg = seg;
+    L.nsy = (L.H + seg - 1) / seg;
+    const long waves = (long)L.nsx * L.nsy * L.n_img;
+    const dim3 grid((uint32_t)((waves + 3) / 4));
+    if (ocv)
+        hipLaunchKernelGGL((k_blur_detect<13, kProfileOpenCV>), grid, dim3(256), 0, st, L);
+    else
+        hipLaunchKernelGGL((k_blur_detect<7, kProfileImageproc>), grid, dim3(256), 0, st, L);
+    return 0;
 }
 
 // ---------------------------------------------------------------------------

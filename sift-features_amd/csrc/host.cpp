@@ -410,6 +410,7 @@ struct Slot {
     hipEvent_t copied = {};  // results copied to the host (copy stream)
     bool pending_copy = false;
     bool detected = false;  // this chunk's detection is enqueued (stage overlap: inside the pyramid)
+    uint32_t fused_mask = 0;  // octaves detected by k_blur_detect (with their blur 5) in the pyramid
     uint32_t m = 0, frame_base = 0, cap_frames = 0;
     uint32_t bc = 0, be = 0, bk = 0;  // candidate / extremum / keypoint bounds used by this chunk
     // detection / description buffers of this slot's lane (the slot's chunks
@@ -482,6 +483,8 @@ struct sift_mi_ctx {
     bool have_pyramid = false;  // single-frame precompute state
     size_t dev_result_n = 0;
     int res_slot = -1;  // >= 0: the last call's device results are that slot's outputs (one chunk, no copy)
+    int batch_arena = -1;     // >= 0: the last batch call ran as one chunk in this arena (read-back)
+    uint32_t batch_frames = 0;
     sift_mi_stats stats{};
 };
 
@@ -688,8 +691,11 @@ constexpr int kBandDrift = 24, kBandPatch = 41;
 // only octaves 0 .. k-1 (k = 1, 2, 3) on the aux stream.
 // detect_slot >= 0 (stage overlap): the detection of the chunk in that slot
 // is launched from here, each part's octaves as soon as their blurs are done.
+// cand_slot >= 0 (the keypoint stages follow): octaves whose blur 5 and
+// detection run as one pass (k_blur_detect) append their candidates to that
+// slot's buffer from here, whatever detect_slot is (Slot::fused_mask).
 int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_pitch, size_t row_stride,
-                uint32_t n, bool full, int detect_slot = -1) {
+                uint32_t n, bool full, int detect_slot = -1, int cand_slot = -1) {
     Plan& p = c->plan;
     hipStream_t st = lane_stream(c, lane);
     lane = arena_of(c, lane);
@@ -838,6 +844,30 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
                     s45 = aux;
                 }
                 const BlurLaunch B = blur_launch(o, s, f0, nf);
+                // blur 5 and the octave's detection in one pass (k_blur_detect:
+                // G_4 / G_5 never read back by the extremum scan)
+                if (s == kImagesPerOctave - 1 && cand_slot >= 0 && !full && c->band_n <= 1 && o < 32) {
+                    Slot& S = c->slot[cand_slot];
+                    BlurDetectLaunch F{};
+                    F.gauss = G;
+                    F.img_stride = p.gstride(o);
+                    F.W = p.ow[o];
+                    F.H = p.oh[o];
+                    F.pitch = p.opitch[o];
+                    F.octave = o;
+                    F.n_img = (int)nf;
+                    F.img_base = (int)f0;
+                    F.profile = p.profile;
+                    F.taps = p.oct_taps[s];
+                    F.cand = S.cand.p;
+                    F.counter = S.counters.p + 0;
+                    F.cap = S.bc;
+                    if (launch_blur_detect(p.oct_r[s], F, s45) == 0) {
+                        S.fused_mask |= 1u << o;
+                        launches++;
+                        continue;
+                    }
+                }
                 // G_1, G_2 in one pass where the pair kernel applies
                 // (k_blur2_strip: G_1 never read back from HBM); after the
                 // seed pair, G_2, G_3 (and the next octave's base) instead
@@ -1000,6 +1030,7 @@ int prepare_chunk(sift_mi_ctx* c, int si, uint32_t m, uint32_t frame_base, const
     S.be = B.be;
     S.bk = B.bk;
     S.detected = false;
+    S.fused_mask = 0;
     uint32_t* cnt = S.counters.p;
     // stage counters, frame starts (~0), descriptor work queues
     launch_chunk_init(cnt, (int)m, kDescWorkWords, st);
@@ -1019,6 +1050,7 @@ int launch_detection(sift_mi_ctx* c, int si, uint32_t f0, uint32_t nf, int o0, i
     int k = 0;
     for (int o = o0; o < o1; o++) {
         if (p.oh[o] < 2 * kImageBorder || p.ow[o] < 2 * kImageBorder) continue;  // src/lib.rs:315
+        if ((S.fused_mask >> o) & 1) continue;  // detected with its blur 5 (k_blur_detect)
         DetectOctave& d = D.oct[k++];
         d.gauss = p.gauss(o, arena_of(c, si)) + (size_t)f0 * p.gstride(o);
         d.img_stride = p.gstride(o);
@@ -1180,7 +1212,7 @@ int enqueue_chunk(sift_mi_ctx* c, int si, const uint8_t* d_frames, size_t frame_
     // detection starts inside the pyramid (run_pyramid), so ev[1]..ev[2] is
     // then only the refinement
     const bool fused = pyramid && c->lanes == 2 && c->stage_overlap;
-    if (pyramid) CHK(run_pyramid(c, si, d_frames, frame_pitch, stride, m, false, fused ? si : -1));
+    if (pyramid) CHK(run_pyramid(c, si, d_frames, frame_pitch, stride, m, false, fused ? si : -1, si));
     HIPCHK(hipEventRecord(S.ev[1], st));
     return enqueue_keypoints(c, si, m, limit, frame_base, B);
 }
@@ -1313,6 +1345,7 @@ int extract_device(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, 
     c->have_pyramid = false;
     c->n_result = 0;
     c->have_result = false;
+    c->batch_arena = -1;
     if (c->band_n > 1) {
         CHK(c->band_flag.ensure(1));
         HIPCHK(hipMemsetAsync(c->band_flag.p, 0, sizeof(uint32_t), c->stream));
@@ -1358,6 +1391,10 @@ int extract_device(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, 
     HIPCHK(hipStreamSynchronize(c->cstream));
     if (offsets) offsets[n] = c->n_result;
     c->have_result = true;
+    if (n_chunks == 1 && !c->band_restricted) {
+        c->batch_arena = arena_of(c, 0);
+        c->batch_frames = n;
+    }
     if (c->band_restricted) {
         // a refinement drifted past the computed rows: redo the band on the
         // whole-frame pyramid (exact; the rare case)
@@ -1736,6 +1773,18 @@ int sift_mi_read_scale_space(sift_mi_ctx* c, size_t o, float* out) {
     CHK(set_device(c));
     const Plan& p = c->plan;
     HIPCHK(hipMemcpy2D(out, (size_t)p.ow[o] * sizeof(float), c->plan.gauss((int)o), (size_t)p.opitch[o] * sizeof(float),
+                       (size_t)p.ow[o] * sizeof(float), (size_t)kImagesPerOctave * p.oh[o], hipMemcpyDeviceToHost));
+    return 0;
+}
+
+int sift_mi_read_batch_scale_space(sift_mi_ctx* c, uint32_t frame, size_t o, float* out) {
+    if (!c || !out || c->batch_arena < 0) return fail(SIFT_MI_ESTATE, "no single-chunk batch pyramid");
+    if (o >= (size_t)c->plan.n_oct || frame >= c->batch_frames) return fail(SIFT_MI_EINVAL, "frame / octave out of range");
+    CHK(set_device(c));
+    CHK(sync_lanes(c));
+    Plan& p = c->plan;
+    const float* g = p.gauss((int)o, c->batch_arena) + (size_t)frame * p.gstride((int)o);
+    HIPCHK(hipMemcpy2D(out, (size_t)p.ow[o] * sizeof(float), g, (size_t)p.opitch[o] * sizeof(float),
                        (size_t)p.ow[o] * sizeof(float), (size_t)kImagesPerOctave * p.oh[o], hipMemcpyDeviceToHost));
     return 0;
 }

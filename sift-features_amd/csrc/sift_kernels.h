@@ -145,6 +145,21 @@ struct DetectLaunch {
 };
 // octaves L.oct[0 .. n_oct) (block0 is filled here)
 void launch_detect(DetectLaunch& L, hipStream_t st);
+// The octave's blur 5 (G_4 -> G_5, radius R, whole planes) and its
+// detection in one pass (k_blur_detect); -1 when it does not apply (the
+// caller then runs launch_blur and the octave's k_detect_rows).  nsx, nsy,
+// seg are filled here.
+struct BlurDetectLaunch {
+    float* gauss;       // octave G_0 base of the launch's first frame
+    size_t img_stride;  // floats between frames
+    int W, H, pitch, octave, n_img, img_base, profile;
+    int nsx, nsy, seg;
+    BlurTaps taps;      // blur 5
+    uint64_t* cand;
+    uint32_t* counter;
+    uint32_t cap;
+};
+int launch_blur_detect(int R, BlurDetectLaunch& L, hipStream_t st);
 
 // Stage sizes live in device counters (no host round trip between stages):
 // every consumer reads its count from device memory, clamps it to the buffer

@@ -248,6 +248,16 @@ class Context:
         check(lib().sift_mi_device_results(self._h, ctypes.byref(kp), ctypes.byref(desc), ctypes.byref(n)))
         return kp.value, desc.value, n.value
 
+    def read_batch_scale_space(self, frame, octave, dims):
+        """(6, h, w) f32 Gaussians of `octave` of `frame` of the last call, as
+        its pyramid left them (valid when that call ran as one chunk; a
+        validation read-back, sift_mi_read_batch_scale_space).  dims = (w, h)
+        of the octave."""
+        w, h = dims
+        out = np.empty((6, h, w), np.float32)
+        check(lib().sift_mi_read_batch_scale_space(self._h, int(frame), int(octave), out.ctypes.data))
+        return out
+
     # -- precompute_images / sift_with_precomputed (src/lib.rs:123-177) ------
     def precompute_images(self, img):
         a = _u8_image(img)

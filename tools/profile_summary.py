@@ -1,6 +1,6 @@
 """Summarise a round profile (tools/round_profile.sh) into profiles/.
 
-    python3 tools/profile_summary.py <round> <out dir> <frames per call>
+    python3 tools/profile_summary.py <round> <out dir> <frames per call> [W H]
 
 Reads the passes under <out dir> (trace/, fetch/, write/, sq1/, sq2/; raw
 CSVs, optionally gzipped) and writes
@@ -32,11 +32,11 @@ import sys
 from collections import defaultdict
 
 ROUND, OUT, FRAMES = sys.argv[1], sys.argv[2], int(sys.argv[3])
+W, H = (int(sys.argv[4]), int(sys.argv[5])) if len(sys.argv) > 5 else (1920, 1080)
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 PROF = os.path.join(ROOT, "profiles")
 os.makedirs(PROF, exist_ok=True)
 PYR = ("k_seed", "k_blur", "k_octave_tail")
-W, H = 1920, 1080
 N_SIMD = 256 * 4
 
 
@@ -117,7 +117,8 @@ n_oct = int(round(math.log2(min(2 * W, 2 * H)) - 2)) + 1
 dims = [((2 * W) >> o, (2 * H) >> o) for o in range(n_oct)]
 sum_p = sum(w * h for w, h in dims)
 algo_pf = W * H + 44 * sum_p  # u8 read once, G_0..G_5 + D_0..D_4 written once
-cmax = min(64, max(1, int(32e9 // (44.0 * sum_p))))  # host auto_chunk
+cmax = min(256, max(1, int(32e9 // (44.0 * sum_p))),  # host auto_chunk
+           max(1, int(64.0 * 3840 * 2160 // (4.0 * W * H))))
 nck = max(-(-FRAMES // cmax), 2 if FRAMES >= 2 else 1)
 chunk = -(-FRAMES // nck)
 
@@ -139,7 +140,10 @@ busy_us = sum(d for v in pos.values() for _, d in v)
 
 
 def launch_blurs(k):
-    """Blurs of the chain a pyramid launch performs (seed: 0)."""
+    """Blurs of the chain a pyramid launch performs (seed: 0; the seed pair:
+    the seed and blur 1, counted as -1)."""
+    if k.startswith("k_seed_pair"):
+        return -1
     if k.startswith("k_seed"):
         return 0
     if k.startswith("k_blur2"):
@@ -160,6 +164,10 @@ def pos_info(seq):
         nb = launch_blurs(k)
         if nb == 0:
             out.append((0, "seed", chunk * (W * H + 4 * dims[0][0] * dims[0][1])))
+            continue
+        if nb == -1:  # k_seed_pair: u8 read, G_0 and G_1 written
+            out.append((0, "seed,1", chunk * (W * H + 8 * dims[0][0] * dims[0][1])))
+            done = 1
             continue
         o, s = done // 5, done % 5 + 1
         if nb is None:
@@ -205,7 +213,9 @@ if n_f and n_w:
           "fetch_bytes_per_launch": fetch / max(1, n_f), "write_bytes_per_launch": write / max(1, n_w),
           "algorithmic_bytes_per_frame": algo_pf,
           "source": f"profiles/{ROUND}_summary.md (rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes)"}
-    json.dump(tj, open(os.path.join(PROF, "pmc_traffic.json"), "w"), indent=1)
+    # bench.py reads pmc_traffic.json for its own (1080p) frame size
+    TJ = "pmc_traffic.json" if (W, H) == (1920, 1080) else f"pmc_traffic_{W}x{H}.json"
+    json.dump(tj, open(os.path.join(PROF, TJ), "w"), indent=1)
 
 # per-kernel SQ counters (sums over every dispatch of the kernel in the pass)
 sq = defaultdict(lambda: defaultdict(float))
@@ -221,7 +231,8 @@ for kind in ("sq1", "sq2", "fetch", "write"):
 
 out_md = os.path.join(PROF, f"{ROUND}_summary.md")
 with open(out_md, "w") as f:
-    f.write(f"# {ROUND} profile: `bench.py --frames {FRAMES} --steps {steps} --warmup 1 --no-configs` on one MI355X\n\n")
+    f.write(f"# {ROUND} profile: `bench.py --frames {FRAMES} --width {W} --height {H} --steps {steps} --warmup 1 "
+            f"--no-configs` on one MI355X\n\n")
     f.write("Command: `bash tools/round_profile.sh` (rocprofv3 --kernel-trace --stats; then separate "
             "--pmc passes: FETCH_SIZE; WRITE_SIZE; two SQ counter groups). Summarised by "
             "`tools/profile_summary.py`.\n\n")
@@ -293,7 +304,7 @@ with open(out_md, "w") as f:
 
 dst = os.path.join(OUT, "profiles")
 os.makedirs(dst, exist_ok=True)
-for name in (f"{ROUND}_summary.md", f"{ROUND}_kernel_stats.csv", "pmc_traffic.json"):
+for name in (f"{ROUND}_summary.md", f"{ROUND}_kernel_stats.csv", "pmc_traffic.json", f"pmc_traffic_{W}x{H}.json"):
     p = os.path.join(PROF, name)
     if os.path.exists(p):
         shutil.copy(p, os.path.join(dst, name))
