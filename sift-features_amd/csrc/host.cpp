@@ -9,6 +9,7 @@
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <chrono>
 #include <cmath>
 #include <cstdio>
 #include <cstring>
@@ -22,6 +23,21 @@
 #include "sift_kernels.h"
 
 using namespace siftmi;
+
+hipError_t siftmi::host_wait_event(hipEvent_t e) {
+    static const bool spin = [] {
+        const char* v = getenv("SIFT_MI_WAIT");
+        return v && !strcmp(v, "spin");
+    }();
+    if (spin) return hipEventSynchronize(e);
+    const auto t0 = std::chrono::steady_clock::now();
+    for (;;) {
+        const hipError_t r = hipEventQuery(e);
+        if (r != hipErrorNotReady) return r;
+        if (std::chrono::steady_clock::now() - t0 > std::chrono::microseconds(1000))
+            std::this_thread::sleep_for(std::chrono::microseconds(20));
+    }
+}
 
 namespace {
 
@@ -447,6 +463,7 @@ struct sift_mi_ctx {
     hipStream_t cstream = nullptr; // device->host result copies
     hipStream_t own2 = nullptr;    // compute stream of pipeline lane 1 (lane 0 runs on `stream`)
     hipStream_t aux[2] = {};       // per lane: blurs 4, 5 of each octave beside the next octave
+    hipStream_t dec = nullptr;     // JPEG batch decoding: a high-priority stream (its own hardware queue)
     hipEvent_t oct_ev[2][kTailMaxOct + 1] = {};  // per lane: octave o's G_3 done / aux joined
     int oct_overlap = 1;           // SIFT_MI_OCT_OVERLAP=0: one stream per lane (A/B, tests)
     bool lanes_busy = false;       // this call keeps both pipeline lanes busy (no octave overlap then)
@@ -937,6 +954,12 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
     CHK(part(0, n, st, c->oct_overlap && !c->lanes_busy && p.n_oct <= kTailMaxOct));
     HIPCHK(hipGetLastError());
     c->stats.pyramid_launches += launches;
+    // octaves whose detection ran inside the pyramid (k_blur_detect): the
+    // stage's yardstick adds what the reference's extremum scan reads, the
+    // five DoG planes once (20 B per octave pixel)
+    if (cand_slot >= 0)
+        for (int o = 0; o < p.n_oct && o < 32; o++)
+            if ((c->slot[cand_slot].fused_mask >> o) & 1) bytes += 20ull * p.px[o];
     c->stats.pyramid_bytes += bytes * n;
     return 0;
 }
@@ -1222,7 +1245,7 @@ int enqueue_chunk(sift_mi_ctx* c, int si, const uint8_t* d_frames, size_t frame_
 // its bound (the caller re-runs the chunk; the high-water marks now cover it).
 int finalize_chunk(sift_mi_ctx* c, int si, size_t* offsets, bool only_chunk = false) {
     Slot& S = c->slot[si];
-    HIPCHK(hipEventSynchronize(S.ev[6]));
+    HIPCHK(host_wait_event(S.ev[6]));
     const uint32_t* h = S.h_counts.p;
     const uint32_t m = S.m;
     const double fm = (double)m;
@@ -1569,7 +1592,7 @@ void sift_mi_destroy(sift_mi_ctx* c) {
     // stream (it goes back to the pool below), lane 1, both aux streams
     // (octave blurs 4, 5 and detection write the arenas) and the copy stream
     {
-        const hipStream_t ss[] = {c->stream, c->own, c->own2, c->aux[0], c->aux[1], c->cstream};
+        const hipStream_t ss[] = {c->stream, c->own, c->own2, c->aux[0], c->aux[1], c->cstream, c->dec};
         for (hipStream_t s : ss)
             if (s) (void)hipStreamSynchronize(s);
     }
@@ -1598,6 +1621,7 @@ void sift_mi_destroy(sift_mi_ctx* c) {
     c->h_kp.release();
     c->h_desc.release();
     c->h_key.release();
+    if (c->dec) (void)hipStreamDestroy(c->dec);
     if (c->own) {  // the streams go back to the pool (synchronised above)
         const hipStream_t ss[kCtxStreams] = {c->own, c->own2, c->aux[0], c->cstream, c->aux[1]};
         give_streams(c->device, ss);
@@ -2012,7 +2036,27 @@ int sift_mi_decode_jpeg_batch(sift_mi_ctx* c, const uint8_t* const* data, const 
     if (threads <= 0) threads = (int)std::min(16u, std::max(1u, std::thread::hardware_concurrency()));
     CHK(set_device(c));
     std::string err;
-    const int rc = jpeg_decode_batch(data, len, n, d_frames, frame_pitch, row_stride, threads, c->stream, c->jpeg, err);
+    // The reconstruction kernels run on a high-priority stream of their own
+    // (ordered after the context's stream): the runtime takes its hardware
+    // queue from the high-priority pool, so a decode pipelined beside another
+    // context's batch (bench.py configs.jpeg_e2e) does not queue behind that
+    // batch's kernels on a shared in-order queue -- normal-priority streams
+    // share GPU_MAX_HW_QUEUES (4) queues round robin.  A caller stream
+    // (sift_mi_set_stream) is used as is; SIFT_MI_DEC_STREAM=0: the context's
+    // stream (A/B knob).
+    hipStream_t st = c->stream;
+    const char* e = getenv("SIFT_MI_DEC_STREAM");
+    if (c->stream == c->own && !(e && !strcmp(e, "0"))) {
+        if (!c->dec) {
+            int least = 0, greatest = 0;
+            HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));
+            HIPCHK(hipStreamCreateWithPriority(&c->dec, hipStreamNonBlocking, greatest));
+        }
+        HIPCHK(hipEventRecord(c->fork, c->stream));
+        HIPCHK(hipStreamWaitEvent(c->dec, c->fork, 0));
+        st = c->dec;
+    }
+    const int rc = jpeg_decode_batch(data, len, n, d_frames, frame_pitch, row_stride, threads, st, c->jpeg, err);
     return rc ? fail(rc, err) : 0;
 }
 

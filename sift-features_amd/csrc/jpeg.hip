@@ -812,7 +812,7 @@ int jpeg_decode_batch(const uint8_t* const* data, const size_t* len, uint32_t n,
             ok = hipGetLastError() == hipSuccess;
         }
         // pinned buffer k is free for chunk ch + 2 once this upload is done
-        ok = ok && hipEventSynchronize(cache.up[k]) == hipSuccess;
+        ok = ok && host_wait_event(cache.up[k]) == hipSuccess;
         {
             std::lock_guard<std::mutex> lk(mu);
             if (ok)

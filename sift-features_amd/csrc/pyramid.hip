@@ -1961,7 +1961,9 @@ int launch_seed_pair(int rs, int rb, const SeedLaunch& S, const BlurLaunch& B, h
 // bound by LDS latency along each output's tap chain: the borders are
 // materialised instead of evaluated per tap (reflect-101 / clamp-to-edge halo
 // columns of the blur input, halo rows of the row-pass output, filled by a
-// pass of their own), so every tap read is a plain offset, and each thread
+// pass of their own where a halo row / column mirrors more than one image
+// row / column, else by the passes that compute the mirrored values), so every
+// tap read is a plain offset, and each thread
 // carries four independent chains (four outputs of a row / of a column).
 // LDS layout (floats), with Rm the largest radius of the octave's blurs:
 //   A, B  G_{s-1} / G_s:     H rows of pitch PA = (W + 2 Rm) | 1 (column halos), x at + Rm
@@ -2004,6 +2006,9 @@ __device__ __forceinline__ void tail_blur_r(float* __restrict__ A, float* __rest
                                             float* __restrict__ gn, int wn, int hn, int pn) {
     constexpr int Q = 4;
     const int PA = tail_pa(W, Rm), TP = tail_tp(W);
+    // halos written by the passes themselves where one mirror image suffices
+    const bool rows_direct = P != kProfileOpenCV || H > R;
+    const bool cols_direct = Rn > 0 && (P != kProfileOpenCV || W > Rn);
     // row pass (A's halo columns are in place): fma chain from the leftmost
     // tap (OpenCV) / unfused chain (imageproc); item = (row, 4 columns),
     // consecutive items down a column of items (lanes on distinct banks).
@@ -2030,15 +2035,36 @@ __device__ __forceinline__ void tail_blur_r(float* __restrict__ A, float* __rest
 #pragma unroll
         for (int q = 0; q < Q; q++)
             if (x0 + q < W) o[q] = acc[q];
+        // T's halo rows [-R, 0) and [H, H + R) that mirror row y, written
+        // here instead of by a pass of their own (one barrier less): one
+        // reflection (OpenCV, H > R) / the edge rows (imageproc)
+        if (rows_direct) {
+            auto mirror = [&](int p) {
+                float* h = T + (p + Rm) * TP + x0;
+#pragma unroll
+                for (int q = 0; q < Q; q++)
+                    if (x0 + q < W) h[q] = acc[q];
+            };
+            if constexpr (P == kProfileOpenCV) {
+                if (y >= 1 && y <= R) mirror(-y);
+                if (y >= H - 1 - R && y <= H - 2) mirror(2 * H - 2 - y);
+            } else {
+                if (y == 0)
+                    for (int p = -R; p < 0; p++) mirror(p);
+                if (y == H - 1)
+                    for (int p = H; p < H + R; p++) mirror(p);
+            }
+        }
     }
     __syncthreads();
-    // T's halo rows [-R, 0) and [H, H + R)
-    for (int i = threadIdx.x; i < 2 * R * W; i += 1024) {
-        const int j = i / W, x = i - j * W;
-        const int p = j < R ? j - R : H + j - R;
-        T[(p + Rm) * TP + x] = T[(tail_index<P>(p, H) + Rm) * TP + x];
+    if (!rows_direct) {  // T's halo rows [-R, 0) and [H, H + R)
+        for (int i = threadIdx.x; i < 2 * R * W; i += 1024) {
+            const int j = i / W, x = i - j * W;
+            const int p = j < R ? j - R : H + j - R;
+            T[(p + Rm) * TP + x] = T[(tail_index<P>(p, H) + Rm) * TP + x];
+        }
+        __syncthreads();
     }
-    __syncthreads();
     // column pass: centre product + fma of the (below + above) pair sums
     // (OpenCV) / the unfused chain from the first tap (imageproc); item =
     // (column, 4 consecutive rows), lanes along the row (coalesced stores)
@@ -2074,7 +2100,21 @@ __device__ __forceinline__ void tail_blur_r(float* __restrict__ A, float* __rest
         for (int q = 0; q < Q; q++) {
             const int y = y0 + q;
             if (y >= H) break;
-            B[y * PA + Rm + x] = acc[q];
+            float* brow = B + y * PA + Rm;
+            brow[x] = acc[q];
+            // B's halo columns for the next blur (radius Rn) that mirror
+            // column x (one reflection: OpenCV, W > Rn / imageproc's edges)
+            if (cols_direct) {
+                if constexpr (P == kProfileOpenCV) {
+                    if (x >= 1 && x <= Rn) brow[-x] = acc[q];
+                    if (x >= W - 1 - Rn && x <= W - 2) brow[2 * W - 2 - x] = acc[q];
+                } else {
+                    if (x == 0)
+                        for (int p = -Rn; p < 0; p++) brow[p] = acc[q];
+                    if (x == W - 1)
+                        for (int p = W; p < W + Rn; p++) brow[p] = acc[q];
+                }
+            }
             g[(size_t)y * pitch + x] = acc[q];
             if (nxt && (x & 1) == par && (y & 1) == par && (x >> 1) < wn && (y >> 1) < hn) {
                 N[(y >> 1) * wn + (x >> 1)] = acc[q];
@@ -2083,7 +2123,7 @@ __device__ __forceinline__ void tail_blur_r(float* __restrict__ A, float* __rest
         }
     }
     __syncthreads();
-    if (Rn > 0) {  // B's halo columns for the next blur
+    if (Rn > 0 && !cols_direct) {  // B's halo columns for the next blur
         tail_fill_cols<P>(B, W, H, Rm, Rn);
         __syncthreads();
     }

@@ -70,6 +70,11 @@ struct SeedLaunch {
 };
 
 
+// Host wait for an event (host.cpp): spins ~1 ms, then polls with short
+// sleeps, so a thread waiting for a multi-ms chunk does not hold a CPU the
+// decode threads (or a CPU quota) need.  SIFT_MI_WAIT=spin: hipEventSynchronize.
+hipError_t host_wait_event(hipEvent_t e);
+
 // jpeg.hip: baseline JPEG -> 8-bit luma (zune-jpeg + image::grayscale arithmetic)
 int jpeg_dims(const uint8_t* data, size_t len, uint32_t* w, uint32_t* h, std::string& err);
 int jpeg_decode_luma(const uint8_t* data, size_t len, uint8_t* out, size_t out_stride, bool out_on_device,
