@@ -194,7 +194,7 @@ __device__ __forceinline__ void blur_tile_compute(const float* __restrict__ tin,
                 nxt[(size_t)(gy >> 1) * pitch_n + (gx >> 1)] = acc.x;
         } else {
             if ((o & 1) == 1 && nxt && pair && (gx >> 1) < wn && (gy >> 1) < hn)
-                nxt[(size_t)(gy >> 1) * pitch_n + (gx >> 1)] = acc.y;
+                nxt[(size_t)(gy >> 1) * pitch_n + (gx >> 1)] = ip_unit_clamp(acc.y);
         }
     }
 }
@@ -537,8 +537,11 @@ __device__ __forceinline__ void strip_colpass(const float* sa, const float* sb, 
         // strip_segment_rows), so those are the even / odd o
         if (NXT && (o & 1) == (P == kProfileOpenCV ? 0 : 1)) {  // o: unrolled constant
             const uint32_t nrow_bad = (gy >> 1) < hn ? row_bad : kStoreDrop;  // uniform
-            const uint32_t val = P == kProfileOpenCV ? __builtin_bit_cast(u32x2, out[o]).x
-                                                     : __builtin_bit_cast(u32x2, out[o]).y;  // (see strip_colpass_clamped)
+            // (the element's bits as u32x2(out[o]).y: see strip_colpass_clamped)
+            const uint32_t odd = __builtin_bit_cast(u32x2, out[o]).y;
+            const uint32_t val = P == kProfileOpenCV
+                                     ? __builtin_bit_cast(u32x2, out[o]).x
+                                     : __builtin_bit_cast(uint32_t, ip_unit_clamp(__builtin_bit_cast(float, odd)));
             __builtin_amdgcn_raw_buffer_store_b32(val, rn,
                                                   ((uint32_t)((gy >> 1) * pitch_n * 4) + lane_ncol) | lane_nbad |
                                                       nrow_bad,
@@ -587,7 +590,8 @@ __device__ __forceinline__ void strip_colpass_clamped(const float* sa, const flo
             const uint32_t nrow_bad = (gy >> 1) < hn ? row_bad : kStoreDrop;
             // (the element as u32x2(acc).y: hipcc 7.2 stores element 0 for
             // bit_cast(uint32_t, acc.y) after the 64-bit store of acc here)
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(u32x2, acc).y, rn,
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, ip_unit_clamp(__builtin_bit_cast(
+                                                      float, __builtin_bit_cast(u32x2, acc).y))), rn,
                                                   ((uint32_t)((gy >> 1) * pitch_n * 4) + lane_ncol) | lane_nbad |
                                                       nrow_bad,
                                                   0, 0);
@@ -2117,8 +2121,9 @@ __device__ __forceinline__ void tail_blur_r(float* __restrict__ A, float* __rest
             }
             g[(size_t)y * pitch + x] = acc[q];
             if (nxt && (x & 1) == par && (y & 1) == par && (x >> 1) < wn && (y >> 1) < hn) {
-                N[(y >> 1) * wn + (x >> 1)] = acc[q];
-                gn[(size_t)(y >> 1) * pn + (x >> 1)] = acc[q];
+                const float nv = P == kProfileOpenCV ? acc[q] : ip_unit_clamp(acc[q]);
+                N[(y >> 1) * wn + (x >> 1)] = nv;
+                gn[(size_t)(y >> 1) * pn + (x >> 1)] = nv;
             }
         }
     }

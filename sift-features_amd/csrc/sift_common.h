@@ -152,6 +152,12 @@ __device__ __forceinline__ TileId xcd_tile() {
 
 __host__ __device__ __forceinline__ int clamp_idx(int p, int len) { return p < 0 ? 0 : (p >= len ? len - 1 : p); }
 
+// image 0.25.2 imageops::resize clamps every f32 output to [DEFAULT_MIN_VALUE,
+// DEFAULT_MAX_VALUE] = [0, 1] (horizontal_sample's clamp), its Nearest 1/2
+// included: the imageproc profile's next-octave base is the picked G_3 pixel
+// clamped (a blur of values in [0, 1] can round a hair past 1)
+__host__ __device__ __forceinline__ float ip_unit_clamp(float v) { return v < 0.0f ? 0.0f : (v > 1.0f ? 1.0f : v); }
+
 // Correctly rounded f32 transcendentals evaluated in f64 (the reference calls
 // glibc expf/sinf/cosf/powf, which are correctly rounded in all but rare
 // near-midpoint cases).
