@@ -94,3 +94,24 @@ def test_ip_pyramid_kernels(ctx_ip, oracle, monkeypatch, kernel, name):
     for o in range(opy.n_octaves):
         g, go = pre.scale_space_octave(o), opy.scale_space(o)
         assert np.array_equal(g, go), (o, np.argwhere(g != go)[:5])
+
+
+@pytest.mark.parametrize("kernel", ["strip", "tile", "notail", "nopair", "noseedpair"])
+@pytest.mark.parametrize("shape", [(640, 480), (301, 207)])
+def test_ip_saturated_next_octave_clamp(ctx_ip, oracle, monkeypatch, kernel, shape):
+    """Large saturated (255) regions: a blur of 1.0s can round a hair past 1,
+    and image's resize clamps its f32 output to [0, 1] -- the next octave's
+    base (Nearest 1/2 of G_3) is clamped in every kernel family (strip pair,
+    strip blur, tile blur, tail)."""
+    import synth
+    from test_gpu_parity import _KERNEL_ENV
+    for k, v in _KERNEL_ENV[kernel].items():
+        monkeypatch.setenv(k, v)
+    f = synth.frame(shape[0], shape[1], 9).astype(np.float32)
+    img = np.clip(f * 2.0 - 60.0, 0, 255).astype(np.uint8)
+    assert (img == 255).mean() > 0.1
+    pre = ctx_ip.precompute_images(img)
+    opy = oracle.Pyramid(img, PROFILE_IMAGEPROC)
+    for o in range(opy.n_octaves):
+        g, go = pre.scale_space_octave(o), opy.scale_space(o)
+        assert np.array_equal(g, go), (o, np.argwhere(g != go)[:5])
