@@ -336,7 +336,11 @@ __global__ __launch_bounds__(256) void k_blur_detect(const BlurDetectLaunch L) {
     __shared__ float ring[4][BD_RING * BD_RP];
     __shared__ uint64_t lcand[DR_LCAP];
     __shared__ uint32_t lcount, gbase;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
+    // the wave index through readfirstlane: everything derived from it (the
+    // strip, its rows, the buffer row offsets) is then known to be uniform
+    // and lives in SGPRs -- a soffset the compiler cannot prove uniform turns
+    // every buffer access into a readfirstlane waterfall loop
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
     const int W = L.W, H = L.H, pitch = L.pitch;
     const uint32_t g = xcd_block_1d() * 4 + wave;  // strip index: frame-major, then row segment, then column
     const uint32_t per = (uint32_t)(L.nsx * L.nsy);
@@ -365,8 +369,11 @@ __global__ __launch_bounds__(256) void k_blur_detect(const BlurDetectLaunch L) {
         float* rg = ring[wave];
         auto ld4 = [&](int q, float& a, float& c) {  // G_4 row q (reflected) into registers
             const int so = bd_index<P>(q, H) * pitch * 4;
+            // both loads on every lane (vb is clamped into the row): an
+            // exec-masked load sits behind a skip branch, which makes the
+            // compiler's load-counter waits conservative
             a = buffer_load_f32(rg4, va, so);
-            c = lane < 2 * R ? buffer_load_f32(rg4, vb, so) : 0.0f;
+            c = buffer_load_f32(rg4, vb, so);
         };
         auto ld03 = [&](int r, float (&d)[4]) {  // G_0..G_3 at (row r clamped, column xc)
             const int so = min(max(r, 0), H - 1) * pitch * 4;
@@ -396,25 +403,44 @@ __global__ __launch_bounds__(256) void k_blur_detect(const BlurDetectLaunch L) {
         float lrx[kDogPerOctave], lrn[kDogPerOctave], ctr[kDogPerOctave];
         const float threshold = floorf(0.5f * kContrastThreshold / (float)kScalesPerOctave);
         const int q0 = ya - 1 - R, q1 = yb + R;  // G_4 rows filtered: [q0, q1]
-        float a0, c0, a1, c1;
-        float d0[4], d1[4];
-        ld4(q0, a0, c0);
-        ld4(q0 + 1, a1, c1);
-        ld03(ya - 1, d0);
-        ld03(ya, d1);
-        // G_4 row q arrived in (a, c); G_0..G_3 of row r = q - R in d (when r >= ya - 1)
-        auto step = [&](int q, float& a, float& c, float (&d)[4]) {
-            float* wp = rg + (q & (BD_RING - 1)) * BD_RP;
-            wp[lane] = a;
-            if (lane < 2 * R) wp[64 + lane] = c;
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-            __builtin_amdgcn_wave_barrier();
-            __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-            if (q + 2 <= q1) ld4(q + 2, a, c);
-            win[2 * R] = rowpass(q);
+        // Row data of one G_4 row q: its ring columns (a, c) and G_0..G_3 of
+        // row r = q - R at this lane's column (the window-filling rows r <
+        // ya - 1 load rows ya - 1 / ya instead; rows past the end re-load
+        // the last one).  Four buffers: the two rows of a half-iteration are
+        // processed from one pair while the next two rows' loads, issued at the
+        // top of the half, are in flight into the other pair.  Every half
+        // issues the same memory operations (a G_5 row outside the segment is
+        // stored to an offset the buffer drops), so the compiler's load-counter
+        // waits are static: each waits for loads issued a half-iteration
+        // earlier, never for the ones just issued.
+        struct RowBuf {
+            float a, c, d[4];
+        };
+        auto load = [&](int q, RowBuf& B, int par) {
+            const int qq = min(q, q1), r = qq - R;
+            ld4(qq, B.a, B.c);
+            ld03(r >= ya - 1 ? min(r, yb) : ya - 1 + par, B.d);
+        };
+        auto shift = [&]() {
+#pragma unroll
+            for (int j = 0; j < 2 * R; j++) win[j] = win[j + 1];
+        };
+        // G_4 row q from B into the ring, row-filtered into win[2R]; once the
+        // window holds rows r - R .. r + R (r = q - R >= ya - 1): G_5 of row r,
+        // row r's DoG values, the test of row r - 1.  Steps past q1 only
+        // issue their (dropped) store.
+        auto step = [&](int q, const RowBuf& B) {
+            const bool on = q <= q1;  // uniform
             const int r = q - R;
-            if (r >= ya - 1) {  // uniform
-                float g5;
+            float g5 = 0.0f;
+            if (on) {
+                float* wp = rg + (q & (BD_RING - 1)) * BD_RP;
+                wp[lane] = B.a;
+                if (lane < 2 * R) wp[64 + lane] = B.c;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                win[2 * R] = rowpass(q);
                 if constexpr (P == kProfileOpenCV) {
                     g5 = win[R] * L.taps.k[0];
 #pragma unroll
@@ -424,84 +450,97 @@ __global__ __launch_bounds__(256) void k_blur_detect(const BlurDetectLaunch L) {
 #pragma unroll
                     for (int t = 1; t <= 2 * R; t++) g5 = g5 + win[t] * L.taps.k[t > R ? t - R : R - t];
                 }
-                if (xst && r >= ya && r < yb)
-                    __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, g5), rg5, vx,
-                                                          r * pitch * 4, 2 /* nt */);
-                // row r's DoG values (G_4 from the ring: row r is resident)
-                const float g4 = rg[(r & (BD_RING - 1)) * BD_RP + lane + R];
-                float cur[kDogPerOctave];
-                cur[0] = d[1] - d[0];
-                cur[1] = d[2] - d[1];
-                cur[2] = d[3] - d[2];
-                cur[3] = g4 - d[3];
-                cur[4] = g5 - g4;
-                if (r + 2 <= yb) ld03(r + 2, d);
-                float nlx[kDogPerOctave], nln[kDogPerOctave];
+            }
+            const uint32_t bad = (on && xst && r >= ya && r < yb) ? 0u : 0xfffffff0u;  // past every plane: dropped
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, g5), rg5,
+                                                  ((uint32_t)(r * pitch * 4) + (uint32_t)vx) | bad, 0, 2 /* nt */);
+            if (!(on && r >= ya - 1)) {  // uniform
+                shift();
+                return;
+            }
+            // row r's DoG values (G_4 from the ring: row r is resident)
+            const float g4 = rg[(r & (BD_RING - 1)) * BD_RP + lane + R];
+            float cur[kDogPerOctave];
+            cur[0] = B.d[1] - B.d[0];
+            cur[1] = B.d[2] - B.d[1];
+            cur[2] = B.d[3] - B.d[2];
+            cur[3] = g4 - B.d[3];
+            cur[4] = g5 - g4;
+            float nlx[kDogPerOctave], nln[kDogPerOctave];
+#pragma unroll
+            for (int p = 0; p < kDogPerOctave; p++) {
+                const float l = dpp_from_left(cur[p]), rr = dpp_from_right(cur[p]);
+                nlx[p] = fmaxf(l, rr);
+                nln[p] = fminf(l, rr);
+                hmx[p][2] = fmaxf(nlx[p], cur[p]);
+                hmn[p][2] = fminf(nln[p], cur[p]);
+            }
+            const int y = r - 1;  // tested row: rows r - 2, r - 1, r are in
+            if (y >= ya) {        // uniform
+                const bool yin = xout && y >= kImageBorder && y < H - kImageBorder;
+                float pmx[kDogPerOctave], pmn[kDogPerOctave];
 #pragma unroll
                 for (int p = 0; p < kDogPerOctave; p++) {
-                    const float l = dpp_from_left(cur[p]), rr = dpp_from_right(cur[p]);
-                    nlx[p] = fmaxf(l, rr);
-                    nln[p] = fminf(l, rr);
-                    hmx[p][2] = fmaxf(nlx[p], cur[p]);
-                    hmn[p][2] = fminf(nln[p], cur[p]);
+                    pmx[p] = fmaxf(fmaxf(hmx[p][0], hmx[p][1]), hmx[p][2]);
+                    pmn[p] = fminf(fminf(hmn[p][0], hmn[p][1]), hmn[p][2]);
                 }
-                const int y = r - 1;  // tested row: rows r - 2, r - 1, r are in
-                if (y >= ya) {        // uniform
-                    const bool yin = xout && y >= kImageBorder && y < H - kImageBorder;
-                    float pmx[kDogPerOctave], pmn[kDogPerOctave];
+                uint32_t ok3 = 0;
 #pragma unroll
-                    for (int p = 0; p < kDogPerOctave; p++) {
-                        pmx[p] = fmaxf(fmaxf(hmx[p][0], hmx[p][1]), hmx[p][2]);
-                        pmn[p] = fminf(fminf(hmn[p][0], hmn[p][1]), hmn[p][2]);
-                    }
-                    uint32_t ok3 = 0;
-#pragma unroll
-                    for (int s_in = 1; s_in <= kScalesPerOctave; s_in++) {
-                        const float val = ctr[s_in];
-                        const float m8 = fmaxf(fmaxf(hmx[s_in][0], hmx[s_in][2]), lrx[s_in]);
-                        const float n8 = fminf(fminf(hmn[s_in][0], hmn[s_in][2]), lrn[s_in]);
-                        const float mx = fmaxf(fmaxf(pmx[s_in - 1], pmx[s_in + 1]), m8);
-                        const float mn = fminf(fminf(pmn[s_in - 1], pmn[s_in + 1]), n8);
-                        const bool ok = yin && fabsf(val) > threshold && (val > 0.0f ? val >= mx : val <= mn);
-                        ok3 |= (uint32_t)ok << (s_in - 1);
-                    }
-                    if (__ballot(ok3 != 0)) {  // wave-uniform: rare
-                        while (ok3) {
-                            const int bit = __builtin_ctz(ok3);
-                            ok3 &= ok3 - 1;
-                            const uint64_t key = make_key((uint32_t)(L.img_base + b), (uint32_t)L.octave,
-                                                          (uint32_t)(bit + 1), (uint32_t)y, (uint32_t)x);
-                            const uint32_t li = atomicAdd(&lcount, 1u);
-                            if (li < DR_LCAP) {
-                                lcand[li] = key;
-                            } else {
-                                const uint32_t slot = atomicAdd(L.counter, 1u);
-                                if (slot < L.cap) L.cand[slot] = key;
-                            }
+                for (int s_in = 1; s_in <= kScalesPerOctave; s_in++) {
+                    const float val = ctr[s_in];
+                    const float m8 = fmaxf(fmaxf(hmx[s_in][0], hmx[s_in][2]), lrx[s_in]);
+                    const float n8 = fminf(fminf(hmn[s_in][0], hmn[s_in][2]), lrn[s_in]);
+                    const float mx = fmaxf(fmaxf(pmx[s_in - 1], pmx[s_in + 1]), m8);
+                    const float mn = fminf(fminf(pmn[s_in - 1], pmn[s_in + 1]), n8);
+                    const bool ok = yin && fabsf(val) > threshold && (val > 0.0f ? val >= mx : val <= mn);
+                    ok3 |= (uint32_t)ok << (s_in - 1);
+                }
+                if (__ballot(ok3 != 0)) {  // wave-uniform: rare
+                    while (ok3) {
+                        const int bit = __builtin_ctz(ok3);
+                        ok3 &= ok3 - 1;
+                        const uint64_t key = make_key((uint32_t)(L.img_base + b), (uint32_t)L.octave,
+                                                      (uint32_t)(bit + 1), (uint32_t)y, (uint32_t)x);
+                        const uint32_t li = atomicAdd(&lcount, 1u);
+                        if (li < DR_LCAP) {
+                            lcand[li] = key;
+                        } else {
+                            const uint32_t slot = atomicAdd(L.counter, 1u);
+                            if (slot < L.cap) L.cand[slot] = key;
                         }
                     }
                 }
-#pragma unroll
-                for (int p = 0; p < kDogPerOctave; p++) {
-                    hmx[p][0] = hmx[p][1];
-                    hmn[p][0] = hmn[p][1];
-                    hmx[p][1] = hmx[p][2];
-                    hmn[p][1] = hmn[p][2];
-                    lrx[p] = nlx[p];
-                    lrn[p] = nln[p];
-                    ctr[p] = cur[p];
-                }
             }
 #pragma unroll
-            for (int j = 0; j < 2 * R; j++) win[j] = win[j + 1];
+            for (int p = 0; p < kDogPerOctave; p++) {
+                hmx[p][0] = hmx[p][1];
+                hmn[p][0] = hmn[p][1];
+                hmx[p][1] = hmx[p][2];
+                hmn[p][1] = hmn[p][2];
+                lrx[p] = nlx[p];
+                lrn[p] = nln[p];
+                ctr[p] = cur[p];
+            }
+            shift();
         };
-        // two rows in flight in two alternating buffers (the loop is unrolled
-        // by two, so neither is copied while its loads are outstanding): G_4
-        // rows q0 + 2i and rows ya - 1 + 2i (r - (ya - 1) = q - q0 - 2R) in
-        // (a0, c0) / d0, the odd ones in (a1, c1) / d1
-        for (int q = q0; q <= q1; q += 2) {
-            step(q, a0, c0, d0);
-            if (q + 1 <= q1) step(q + 1, a1, c1, d1);
+        // rows q, q + 1 from (A0, A1) while q + 2, q + 3 load into (B0, B1),
+        // then the other way round (even / odd rows: par 0 / 1)
+        RowBuf A0, A1, B0, B1;
+        load(q0, A0, 0);
+        load(q0 + 1, A1, 1);
+        for (int q = q0; q <= q1; q += 4) {
+            load(q + 2, B0, 0);
+            load(q + 3, B1, 1);
+            __builtin_amdgcn_sched_barrier(0);
+            step(q, A0);
+            step(q + 1, A1);
+            __builtin_amdgcn_sched_barrier(0);
+            load(q + 4, A0, 0);
+            load(q + 5, A1, 1);
+            __builtin_amdgcn_sched_barrier(0);
+            step(q + 2, B0);
+            step(q + 3, B1);
+            __builtin_amdgcn_sched_barrier(0);
         }
     }
     // one global atomic per block, then a coalesced copy of the block's list
