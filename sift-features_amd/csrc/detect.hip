@@ -553,12 +553,12 @@ __global__ __launch_bounds__(256) void k_blur_detect(const BlurDetectLaunch L) {
         if (gbase + i < L.cap) L.cand[gbase + i] = lcand[i];
 }
 
-// SIFT_MI_FUSED_DETECT=0 keeps blur 5 and detection apart (A/B and test knob)
+// SIFT_MI_FUSED_DETECT=0 keeps blur 5 and detection apart, =force fuses
+// every octave it can at 32-row segments (A/B and test knobs)
 int launch_blur_detect(int R, BlurDetectLaunch& L, hipStream_t st) {
-    {
-        const char* e = getenv("SIFT_MI_FUSED_DETECT");
-        if (e && !strcmp(e, "0")) return -1;
-    }
+    const char* e = getenv("SIFT_MI_FUSED_DETECT");
+    if (e && !strcmp(e, "0")) return -1;
+    const bool force = e && !strcmp(e, "force");
     const bool ok = L.W > R + 1 && L.H > R + 1 && L.W >= 2 * kImageBorder && L.H >= 2 * kImageBorder &&
                     (uint64_t)L.H * (uint64_t)L.pitch * 4 < (1ull << 31) && L.n_img > 0;
     if (!ok) return -1;
@@ -566,14 +566,20 @@ int launch_blur_detect(int R, BlurDetectLaunch& L, hipStream_t st) {
     if (!((ocv && R == 13) || (!ocv && R == 7))) return -1;
     L.nsx = (L.W + DR_COLS - 1) / DR_COLS;
     // row segments: a segment re-filters 2R + 2 halo rows, so long ones, but
-    // enough waves to fill the chip (>= ~16 k)
-    int seg = 32;
+    // enough waves to fill the chip (>= ~16 k).  A wave walks its segment row
+    // after row, so an octave too small for that at >= 64-row segments (one
+    // 1080p frame's octaves, a batch's small octaves) is left to launch_blur +
+    // k_detect_rows: there the fused pass is a chain of latency-bound row
+    // steps (one frame's octave 4: 54 us against 10 us for its blur 5)
+    int seg = 0;
     for (int s : {256, 128, 64}) {
         if ((long)L.nsx * ((L.H + s - 1) / s) * L.n_img >= 16384) {
             seg = s;
             break;
         }
     }
+    if (force) seg = 32;  // many segment boundaries on test-sized frames
+    if (!seg) return -1;
     L.seg = seg;
     L.nsy = (L.H + seg - 1) / seg;
     const long waves = (long)L.nsx * L.nsy * L.n_img;

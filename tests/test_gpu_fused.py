@@ -30,14 +30,13 @@ def _frame(name, seed=7):
     return synth.frame(w, h, seed)
 
 
-@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("fused", ["force", "0"])
 @pytest.mark.parametrize("profile", [0, 1])
 @pytest.mark.parametrize("name", SHAPES)
 def test_batch_pyramid_bit_exact(pkg, oracle, monkeypatch, fused, profile, name):
     """Every Gaussian plane the batch path leaves in its arena (G_5 from
     k_blur_detect when fused) equals the oracle's, bit for bit."""
-    if not fused:
-        monkeypatch.setenv("SIFT_MI_FUSED_DETECT", "0")
+    monkeypatch.setenv("SIFT_MI_FUSED_DETECT", fused)
     img = _frame(name)
     c = pkg.Context(0, pkg.OpenCVProcessing if profile == 0 else pkg.ImageprocProcessing)
     c.sift(img)
@@ -50,15 +49,14 @@ def test_batch_pyramid_bit_exact(pkg, oracle, monkeypatch, fused, profile, name)
     c.close()
 
 
-@pytest.mark.parametrize("fused", [True, False])
+@pytest.mark.parametrize("fused", ["force", "0"])
 @pytest.mark.parametrize("profile", [0, 1])
 @pytest.mark.parametrize("name", SHAPES + ["noise"])
 def test_fused_detect_parity(pkg, oracle, monkeypatch, fused, profile, name):
     """Keypoints (count, emission order, values) and descriptors vs the
     oracle with and without the fused pass."""
     from test_gpu_parity import assert_parity
-    if not fused:
-        monkeypatch.setenv("SIFT_MI_FUSED_DETECT", "0")
+    monkeypatch.setenv("SIFT_MI_FUSED_DETECT", fused)
     img = _frame(name)
     c = pkg.Context(0, pkg.OpenCVProcessing if profile == 0 else pkg.ImageprocProcessing)
     res = c.sift(img)
@@ -67,10 +65,11 @@ def test_fused_detect_parity(pkg, oracle, monkeypatch, fused, profile, name):
     assert_parity(pkg, res, kp_o, desc_o, ext_o)
 
 
-def test_batch_pyramid_multi_frame(pkg, oracle):
+def test_batch_pyramid_multi_frame(pkg, oracle, monkeypatch):
     """Frames of one chunk (the fused pass's frame index and image stride):
     every frame's planes of a 5-frame single-chunk batch equal the oracle's."""
     import synth
+    monkeypatch.setenv("SIFT_MI_FUSED_DETECT", "force")
     fr = synth.frames(5, 320, 240, seed0=21)
     c = pkg.Context(0, pkg.OpenCVProcessing)
     c.set_chunk(5)
