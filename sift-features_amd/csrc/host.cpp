@@ -1178,38 +1178,45 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
     launch_orient(O, st);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(S.ev[3], st));
-    // emission order: radix sort of the keys (padding sorts last)
-    const int img_bits = img_bits_for(m);
-    const int end_bit = kKeyImgShift + img_bits;
-    const uint64_t pad = (end_bit >= 64) ? ~0ull : ((1ull << end_bit) - 1);
-    size_t tmp = sort_pairs_u64(nullptr, 0, S.keys_a.p, S.keys_b.p, S.vals_a.p, S.vals_b.p, B.bk, end_bit, st);
-    const int rb = 32 + img_bits;
-    const uint64_t rpad = (1ull << rb) - 1;
-    if (limit >= 0)
-        tmp = std::max(tmp, sort_pairs_u64(nullptr, 0, S.keys_a.p, S.keys_b.p, S.vals_a.p, S.fin.p, B.bk, rb, st));
-    if (!tmp) return fail(SIFT_MI_EHIP, "radix sort sizing failed");
-    if (tmp > S.sort_tmp.cap) {
-        HIPCHK(hipStreamSynchronize(st));
-        CHK(S.sort_tmp.ensure(tmp));
-    }
-    launch_make_sort_keys(S.kp.p, cnt + 2, B.bk, pad, S.keys_a.p, S.vals_a.p, st);
-    if (!sort_pairs_u64(S.sort_tmp.p, S.sort_tmp.cap, S.keys_a.p, S.keys_b.p, S.vals_a.p, S.vals_b.p, B.bk,
-                        end_bit, st))
-        return fail(SIFT_MI_EHIP, "radix sort failed");
+    // emission order: radix sort of the keys (padding sorts last); one frame
+    // without a limit: k_order_small (SIFT_MI_SMALL_ORDER=0: the general path)
+    const char* so_env = getenv("SIFT_MI_SMALL_ORDER");
     const uint32_t* order = S.vals_b.p;  // emission order -> kp index
-    launch_frame_starts(S.keys_b.p, cnt + 2, B.bk, starts, st);
-    // features_limit (src/lib.rs:156-161): per-frame plan on the device
-    launch_limit_plan(starts, cnt + 2, B.bk, (int)m, limit, out_cnt, S.seg_off.p, S.out_off.p, S.use_resp.p,
-                      cnt + 3, st);
-    if (limit >= 0) {
-        // stable sort: response-descending within each frame, emission order on ties
-        launch_make_resp_keys(S.kp.p, order, cnt + 2, B.bk, 0, rpad, S.keys_a.p, S.vals_a.p, st);
-        if (!sort_pairs_u64(S.sort_tmp.p, S.sort_tmp.cap, S.keys_a.p, S.keys_b.p, S.vals_a.p, S.fin.p, B.bk, rb,
-                            st))
-            return fail(SIFT_MI_EHIP, "response sort failed");
-        launch_select(order, S.fin.p, S.seg_off.p, S.out_off.p, S.use_resp.p, (int)m, cnt + 3, B.bk, S.vals_a.p,
-                      st);
-        order = S.vals_a.p;
+    if (m == 1 && limit < 0 && B.bk <= kSmallOrder && !(so_env && !strcmp(so_env, "0"))) {
+        launch_order_small(S.kp.p, cnt + 2, B.bk, S.vals_b.p, starts, out_cnt, S.seg_off.p, S.out_off.p, S.use_resp.p,
+                           cnt + 3, st);
+    } else {
+        const int img_bits = img_bits_for(m);
+        const int end_bit = kKeyImgShift + img_bits;
+        const uint64_t pad = (end_bit >= 64) ? ~0ull : ((1ull << end_bit) - 1);
+        size_t tmp = sort_pairs_u64(nullptr, 0, S.keys_a.p, S.keys_b.p, S.vals_a.p, S.vals_b.p, B.bk, end_bit, st);
+        const int rb = 32 + img_bits;
+        const uint64_t rpad = (1ull << rb) - 1;
+        if (limit >= 0)
+            tmp = std::max(tmp, sort_pairs_u64(nullptr, 0, S.keys_a.p, S.keys_b.p, S.vals_a.p, S.fin.p, B.bk, rb, st));
+        if (!tmp) return fail(SIFT_MI_EHIP, "radix sort sizing failed");
+        if (tmp > S.sort_tmp.cap) {
+            HIPCHK(hipStreamSynchronize(st));
+            CHK(S.sort_tmp.ensure(tmp));
+        }
+        launch_make_sort_keys(S.kp.p, cnt + 2, B.bk, pad, S.keys_a.p, S.vals_a.p, st);
+        if (!sort_pairs_u64(S.sort_tmp.p, S.sort_tmp.cap, S.keys_a.p, S.keys_b.p, S.vals_a.p, S.vals_b.p, B.bk,
+                            end_bit, st))
+            return fail(SIFT_MI_EHIP, "radix sort failed");
+        launch_frame_starts(S.keys_b.p, cnt + 2, B.bk, starts, st);
+        // features_limit (src/lib.rs:156-161): per-frame plan on the device
+        launch_limit_plan(starts, cnt + 2, B.bk, (int)m, limit, out_cnt, S.seg_off.p, S.out_off.p, S.use_resp.p,
+                          cnt + 3, st);
+        if (limit >= 0) {
+            // stable sort: response-descending within each frame, emission order on ties
+            launch_make_resp_keys(S.kp.p, order, cnt + 2, B.bk, 0, rpad, S.keys_a.p, S.vals_a.p, st);
+            if (!sort_pairs_u64(S.sort_tmp.p, S.sort_tmp.cap, S.keys_a.p, S.keys_b.p, S.vals_a.p, S.fin.p, B.bk, rb,
+                                st))
+                return fail(SIFT_MI_EHIP, "response sort failed");
+            launch_select(order, S.fin.p, S.seg_off.p, S.out_off.p, S.use_resp.p, (int)m, cnt + 3, B.bk, S.vals_a.p,
+                          st);
+            order = S.vals_a.p;
+        }
     }
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(S.ev[4], st));

@@ -179,6 +179,8 @@ def pos_info(seq):
             continue
         px = dims[o][0] * dims[o][1]
         by = (4 + 4 * nb) * px + (px if (s <= 3 < s + nb) and o + 1 < n_oct else 0)
+        if k.startswith("k_blur_detect"):  # blur 5 + the scan: G_0..G_4 read, G_5 written
+            by = 24 * px
         out.append((o, f"{s}" if nb == 1 else f"{s},{s + 1}", chunk * by))
         done += nb
     return out
