@@ -438,6 +438,14 @@ struct Slot {
     bool detected = false;  // this chunk's detection is enqueued (stage overlap: inside the pyramid)
     uint32_t fused_mask = 0;  // octaves detected by k_blur_detect (with their blur 5) in the pyramid
     bool graph_run = false;   // the chunk was a graph replay: only ev[0] / ev[6] were recorded
+    // single-chunk calls with octave overlap: refinement + orientation of the
+    // octaves below the tail run on the aux stream beside the tail (early),
+    // the tail octaves' candidates / extrema in their own region (cand_b,
+    // ext_b; counters at counters[4 + 2m + kDescWorkWords + 0 / 1])
+    bool early = false;
+    uint32_t bcb = 0;
+    DevBuf<uint64_t> cand_b;
+    DevBuf<ExtRec> ext_b;
     uint32_t m = 0, frame_base = 0, cap_frames = 0;
     uint32_t bc = 0, be = 0, bk = 0;  // candidate / extremum / keypoint bounds used by this chunk
     // detection / description buffers of this slot's lane (the slot's chunks
@@ -453,6 +461,8 @@ struct Slot {
     void release_bufs() {
         cand.release();
         ext.release();
+        cand_b.release();
+        ext_b.release();
         kp.release();
         keys_a.release();
         keys_b.release();
@@ -498,6 +508,7 @@ struct sift_mi_ctx {
     int last_slot = 0;
     // per-frame high-water marks that size the next chunk's bounds
     double pf_cand = 0, pf_ext = 0, pf_kp = 0;
+    double pf_cand_b = 0;  // the tail octaves' candidates / extrema (Slot::early)
     // device results of a whole batch (keep_on_device), concatenated in frame order
     DevBuf<OutKp> r_kp;
     DevBuf<uint8_t> r_desc;
@@ -519,7 +530,7 @@ struct sift_mi_ctx {
     struct GraphKey {
         const uint8_t* frames;
         size_t frame_pitch, stride;
-        uint32_t m, w, h, bc, be, bk;
+        uint32_t m, w, h, bc, be, bk, bcb;
         int64_t limit;
         uint64_t gen;
         int keep, exact, samples, lanes, prof, maxo;
@@ -528,6 +539,8 @@ struct sift_mi_ctx {
     };
     GraphKey gkey{}, gseen{};
     bool gkey_ok = false, gseen_ok = false;
+    bool g_early = false;      // the captured chunk's host-side flags
+    uint32_t g_fused = 0;
     hipGraph_t graph = nullptr;
     hipGraphExec_t gexec = nullptr;
     uint32_t batch_frames = 0;
@@ -607,6 +620,7 @@ int ensure_plan(sift_mi_ctx* c, uint32_t w, uint32_t h, uint32_t chunk) {
         p.release();
         // per-frame stage high-water marks belong to a frame size
         c->pf_cand = c->pf_ext = c->pf_kp = 0;
+        c->pf_cand_b = 0;
     }
     p.profile = (int)c->profile;
     const bool ip = c->profile == SIFT_MI_PROFILE_IMAGEPROC;
@@ -713,7 +727,14 @@ int ensure_plan(sift_mi_ctx* c, uint32_t w, uint32_t h, uint32_t chunk) {
 // Detection of octaves [o0, o1) of frames [f0, f0 + nf) of slot si's chunk:
 // one multi-octave k_detect_rows launch (candidates into the slot's buffer,
 // bounded by S.bc).
-int launch_detection(sift_mi_ctx* c, int si, uint32_t f0, uint32_t nf, int o0, int o1, hipStream_t st);
+int launch_detection(sift_mi_ctx* c, int si, uint32_t f0, uint32_t nf, int o0, int o1, hipStream_t st,
+                     uint64_t* cand = nullptr, uint32_t* counter = nullptr, uint32_t cap = 0);
+// refinement of the candidates (cand, *n_cand <= cand_cap) into ext (*counter,
+// cap), and orientation of those extrema into the slot's keypoints
+int launch_refine_stage(sift_mi_ctx* c, int si, const uint64_t* cand, const uint32_t* n_cand, uint32_t cand_cap,
+                        ExtRec* ext, uint32_t* counter, uint32_t cap, hipStream_t st);
+int launch_orient_stage(sift_mi_ctx* c, int si, const ExtRec* ext, const uint32_t* n_ext, uint32_t ext_cap,
+                        uint32_t kp_cap, hipStream_t st);
 
 // Row bands with a restricted pyramid: rows a refined keypoint may drift from
 // its detection row and still be exact without a re-run, and the rows its
@@ -964,7 +985,24 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
                                p.dog(o, lane) + (size_t)f0 * p.dstride(o), p.dstride(o), p.ow[o], p.oh[o],
                                p.opitch[o], (int)nf, sm);
         }
-        if (detect_slot >= 0) {
+        const char* ee = getenv("SIFT_MI_EARLY");
+        if (detect_slot >= 0 && ov && o_tail > 0 && o_tail < p.n_oct && c->slot[detect_slot].bcb &&
+            !(ee && !strcmp(ee, "0"))) {
+            // one chunk (octave overlap): the octaves below the tail are
+            // detected, refined and oriented on the aux stream beside the tail
+            // kernel; the tail octaves, after it, into a region of their own
+            // (Slot::early; SIFT_MI_EARLY=0: off)
+            Slot& S = c->slot[detect_slot];
+            uint32_t* cnt = S.counters.p;
+            uint32_t* cb = cnt + 4 + 2 * S.m + kDescWorkWords;
+            CHK(launch_detection(c, detect_slot, f0, nf, 0, o_tail, aux));
+            CHK(launch_refine_stage(c, detect_slot, S.cand.p, cnt + 0, S.bc, S.ext.p, cnt + 1, S.be, aux));
+            CHK(launch_orient_stage(c, detect_slot, S.ext.p, cnt + 1, S.be, S.bk, aux));
+            CHK(launch_detection(c, detect_slot, f0, nf, o_tail, p.n_oct, sm, S.cand_b.p, cb + 0, S.bcb));
+            CHK(launch_refine_stage(c, detect_slot, S.cand_b.p, cb + 0, S.bcb, S.ext_b.p, cb + 1, S.bcb, sm));
+            CHK(launch_orient_stage(c, detect_slot, S.ext_b.p, cb + 1, S.bcb, S.bk, sm));
+            S.early = true;
+        } else if (detect_slot >= 0) {
             // octaves [0, o_tail) are complete once their last blur is done:
             // with ov their detection runs on the aux stream beside the tail
             CHK(launch_detection(c, detect_slot, f0, nf, 0, o_tail, ov && o_tail > 0 ? aux : sm));
@@ -1039,14 +1077,22 @@ Bounds chunk_bounds(sift_mi_ctx* c, uint32_t m) {
 // buffer has to be reallocated).
 int reserve_chunk(sift_mi_ctx* c, int si, const Bounds& B, uint32_t frames) {
     Slot& S = c->slot[si];
+    const uint32_t bcb = std::max<uint32_t>(2048, (uint32_t)std::min<double>(std::ceil(c->pf_cand_b * 1.3 * frames) + 1024, 1e9));
     const bool grow = B.bc > S.cand.cap || B.be > S.ext.cap || B.bk > S.kp.cap || B.bk > S.keys_a.cap ||
-                      frames > S.seg_off.cap || B.bk > S.out_kp.cap || 4 + 2 * frames + kDescWorkWords > S.counters.cap;
+                      bcb > S.cand_b.cap || bcb > S.ext_b.cap ||
+                      frames > S.seg_off.cap || B.bk > S.out_kp.cap ||
+                      4 + 2 * frames + kDescWorkWords + 2 > S.counters.cap;
     if (grow) {
         HIPCHK(hipStreamSynchronize(lane_stream(c, si)));
         HIPCHK(hipStreamSynchronize(c->cstream));
     }
     CHK(S.cand.ensure(B.bc));
     CHK(S.ext.ensure(B.be));
+    // the tail octaves' own candidate / extremum region (Slot::early): a
+    // 1.3x per-frame high-water mark, at least 2048
+    S.bcb = std::max<uint32_t>(2048, (uint32_t)std::min<double>(std::ceil(c->pf_cand_b * 1.3 * frames) + 1024, 1e9));
+    CHK(S.cand_b.ensure(S.bcb));
+    CHK(S.ext_b.ensure(S.bcb));
     CHK(S.kp.ensure(B.bk));
     CHK(S.keys_a.ensure(B.bk));
     CHK(S.keys_b.ensure(B.bk));
@@ -1056,8 +1102,8 @@ int reserve_chunk(sift_mi_ctx* c, int si, const Bounds& B, uint32_t frames) {
     CHK(S.seg_off.ensure(frames));
     CHK(S.out_off.ensure(frames));
     CHK(S.use_resp.ensure(frames));
-    CHK(S.counters.ensure(4 + 2 * frames + kDescWorkWords));
-    CHK(S.h_counts.ensure(4 + 2 * frames));
+    CHK(S.counters.ensure(4 + 2 * frames + kDescWorkWords + 2));
+    CHK(S.h_counts.ensure(4 + 2 * frames + 2));
     CHK(S.out_kp.ensure(B.bk));
     CHK(S.out_desc.ensure((size_t)B.bk * kDescSize));
     CHK(S.out_key.ensure(B.bk));
@@ -1084,22 +1130,24 @@ int prepare_chunk(sift_mi_ctx* c, int si, uint32_t m, uint32_t frame_base, const
     S.detected = false;
     S.fused_mask = 0;
     S.graph_run = false;
+    S.early = false;
     uint32_t* cnt = S.counters.p;
     // stage counters, frame starts (~0), descriptor work queues
-    launch_chunk_init(cnt, (int)m, kDescWorkWords, st);
+    launch_chunk_init(cnt, (int)m, kDescWorkWords + 2, st);  // + the tail region's counters (Slot::early)
     HIPCHK(hipGetLastError());
     return 0;
 }
 
-int launch_detection(sift_mi_ctx* c, int si, uint32_t f0, uint32_t nf, int o0, int o1, hipStream_t st) {
+int launch_detection(sift_mi_ctx* c, int si, uint32_t f0, uint32_t nf, int o0, int o1, hipStream_t st,
+                     uint64_t* cand, uint32_t* counter, uint32_t cap) {
     Plan& p = c->plan;
     Slot& S = c->slot[si];
     DetectLaunch D{};
     D.n_img = (int)nf;
     D.img_base = (int)f0;  // frame index within the chunk (emission keys)
-    D.cand = S.cand.p;
-    D.counter = S.counters.p + 0;
-    D.cap = S.bc;
+    D.cand = cand ? cand : S.cand.p;
+    D.counter = cand ? counter : S.counters.p + 0;
+    D.cap = cand ? cap : S.bc;
     int k = 0;
     for (int o = o0; o < o1; o++) {
         if (p.oh[o] < 2 * kImageBorder || p.ow[o] < 2 * kImageBorder) continue;  // src/lib.rs:315
@@ -1124,22 +1172,13 @@ int launch_detection(sift_mi_ctx* c, int si, uint32_t f0, uint32_t nf, int o0, i
     return 0;
 }
 
-int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_t frame_base, const Bounds& B) {
+int launch_refine_stage(sift_mi_ctx* c, int si, const uint64_t* cand, const uint32_t* n_cand, uint32_t cand_cap,
+                        ExtRec* ext, uint32_t* counter, uint32_t cap, hipStream_t st) {
     Plan& p = c->plan;
-    Slot& S = c->slot[si];
-    hipStream_t st = lane_stream(c, si);
-    (void)frame_base;
-    uint32_t* cnt = S.counters.p;
-    uint32_t* starts = cnt + 4;
-    uint32_t* out_cnt = cnt + 4 + m;
-    uint32_t* work = cnt + 4 + 2 * m;  // descriptor work queues
-    (void)starts;
-    (void)work;
-    if (!S.detected) CHK(launch_detection(c, si, 0, m, 0, p.n_oct, st));
     RefineLaunch R{};
-    R.cand = S.cand.p;
-    R.n_cand = cnt + 0;
-    R.cand_cap = B.bc;
+    R.cand = cand;
+    R.n_cand = n_cand;
+    R.cand_cap = cand_cap;
     R.band_flag = c->band_restricted ? c->band_flag.p : nullptr;
     R.band_r = (int)c->band_r;
     R.band_n = (int)c->band_n;
@@ -1155,27 +1194,53 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
     R.oh = p.d_oh.p;
     R.opitch = p.d_opitch.p;
     R.img_base = 0;
-    R.out = S.ext.p;
-    R.counter = cnt + 1;
-    R.cap = B.be;
+    R.out = ext;
+    R.counter = counter;
+    R.cap = cap;
     launch_refine(R, st);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(S.ev[2], st));
+    return 0;
+}
+
+int launch_orient_stage(sift_mi_ctx* c, int si, const ExtRec* ext, const uint32_t* n_ext, uint32_t ext_cap,
+                        uint32_t kp_cap, hipStream_t st) {
+    Plan& p = c->plan;
+    Slot& S = c->slot[si];
     OrientLaunch O{};
-    O.ext = S.ext.p;
-    O.n_ext = cnt + 1;
-    O.ext_cap = B.be;
+    O.ext = ext;
+    O.n_ext = n_ext;
+    O.ext_cap = ext_cap;
     O.gauss = p.d_gauss[arena_of(c, si)].p;
     O.gauss_img_stride = p.d_gstride.p;
     O.ow = p.d_ow.p;
     O.oh = p.d_oh.p;
     O.opitch = p.d_opitch.p;
     O.out = S.kp.p;
-    O.counter = cnt + 2;
+    O.counter = S.counters.p + 2;
     O.img_base = 0;
-    O.cap = B.bk;
+    O.cap = kp_cap;
     O.samples = c->count_samples ? c->samples.p : nullptr;
     launch_orient(O, st);
+    HIPCHK(hipGetLastError());
+    return 0;
+}
+
+int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_t frame_base, const Bounds& B) {
+    Plan& p = c->plan;
+    Slot& S = c->slot[si];
+    hipStream_t st = lane_stream(c, si);
+    (void)frame_base;
+    uint32_t* cnt = S.counters.p;
+    uint32_t* starts = cnt + 4;
+    uint32_t* out_cnt = cnt + 4 + m;
+    uint32_t* work = cnt + 4 + 2 * m;  // descriptor work queues
+    (void)starts;
+    (void)work;
+    if (!S.detected) CHK(launch_detection(c, si, 0, m, 0, p.n_oct, st));
+    // (early: refinement and orientation were enqueued inside the pyramid)
+    if (!S.early) CHK(launch_refine_stage(c, si, S.cand.p, cnt + 0, B.bc, S.ext.p, cnt + 1, B.be, st));
+    HIPCHK(hipEventRecord(S.ev[2], st));
+    if (!S.early) CHK(launch_orient_stage(c, si, S.ext.p, cnt + 1, B.be, B.bk, st));
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(S.ev[3], st));
     // emission order: radix sort of the keys (padding sorts last); one frame
@@ -1244,6 +1309,9 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(S.ev[5], st));
     HIPCHK(hipMemcpyAsync(S.h_counts.p, cnt, (4 + 2 * m) * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
+    if (S.early)
+        HIPCHK(hipMemcpyAsync(S.h_counts.p + 4 + 2 * m, cnt + 4 + 2 * m + kDescWorkWords, 2 * sizeof(uint32_t),
+                              hipMemcpyDeviceToHost, st));
     HIPCHK(hipEventRecord(S.ev[6], st));
     return 0;
 }
@@ -1290,10 +1358,13 @@ int finalize_chunk(sift_mi_ctx* c, int si, size_t* offsets, bool only_chunk = fa
     const uint32_t* h = S.h_counts.p;
     const uint32_t m = S.m;
     const double fm = (double)m;
-    c->pf_cand = std::max(c->pf_cand, h[0] / fm);
-    c->pf_ext = std::max(c->pf_ext, h[1] / fm);
+    // the tail octaves' region (Slot::early): its counts follow the frame plan
+    const uint32_t hb0 = S.early ? h[4 + 2 * m] : 0, hb1 = S.early ? h[4 + 2 * m + 1] : 0;
+    c->pf_cand = std::max(c->pf_cand, (h[0] + hb0) / fm);
+    c->pf_ext = std::max(c->pf_ext, (h[1] + hb1) / fm);
     c->pf_kp = std::max(c->pf_kp, h[2] / fm);
-    if (h[0] > S.bc || h[1] > S.be || h[2] > S.bk) {
+    c->pf_cand_b = std::max(c->pf_cand_b, std::max(hb0, hb1) / fm);
+    if (h[0] > S.bc || h[1] > S.be || h[2] > S.bk || hb0 > S.bcb || hb1 > S.bcb) {
         c->stats.stage_reruns++;
         return 1;
     }
@@ -1354,7 +1425,7 @@ int finalize_chunk(sift_mi_ctx* c, int si, size_t* offsets, bool only_chunk = fa
         }
     }
     c->n_result = base + n_out;
-    c->stats.extrema += h[1];
+    c->stats.extrema += h[1] + hb1;
     c->stats.keypoints += n_out;
     c->stats.frames += m;
     return 0;
@@ -1414,6 +1485,7 @@ int enqueue_single_graph(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_p
     k.bc = B.bc;
     k.be = B.be;
     k.bk = B.bk;
+    k.bcb = S.bcb;
     k.limit = limit;
     k.gen = g_alloc_gen.load();
     k.keep = c->keep_on_device;
@@ -1452,6 +1524,8 @@ int enqueue_single_graph(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_p
         c->graph = g;
         c->gkey = k;
         c->gkey_ok = true;
+        c->g_early = S.early;
+        c->g_fused = S.fused_mask;
     }
     // the host-side chunk state prepare_chunk keeps (finalize_chunk reads it)
     S.m = m;
@@ -1462,6 +1536,8 @@ int enqueue_single_graph(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_p
     S.bk = B.bk;
     S.detected = true;
     S.graph_run = true;
+    S.early = c->g_early;
+    S.fused_mask = c->g_fused;
     HIPCHK(hipEventRecord(S.ev[0], st));
     HIPCHK(hipGraphLaunch(c->gexec, st));
     HIPCHK(hipEventRecord(S.ev[6], st));

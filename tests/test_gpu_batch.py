@@ -327,3 +327,25 @@ def test_single_chunk_graph_replay(pkg, ctx, oracle, monkeypatch, fetch):
     kp_o, desc_o, ext_o = oracle.sift(b, internal=True)
     assert_parity(pkg, res, kp_o, desc_o, ext_o)
     c.close()
+
+
+@pytest.mark.parametrize("knob", ["SIFT_MI_EARLY", "SIFT_MI_SMALL_ORDER"])
+@pytest.mark.parametrize("profile", [0, 1])
+def test_single_chunk_paths_equal(pkg, monkeypatch, knob, profile):
+    """One-chunk calls take two latency paths -- the octaves below the tail
+    refined and oriented beside the tail kernel with the tail octaves in a
+    region of their own (Slot::early), and the one-workgroup ordering stage
+    (k_order_small) -- whose results must equal the general path's
+    (SIFT_MI_EARLY=0 / SIFT_MI_SMALL_ORDER=0) bit for bit, incl. keys."""
+    import synth
+    frames = [synth.frame(640, 480, 3), synth.frame(1000, 333, 5),
+              np.random.default_rng(5).integers(0, 256, (96, 128), dtype=np.uint8)]
+    prof = pkg.OpenCVProcessing if profile == 0 else pkg.ImageprocProcessing
+    c = pkg.Context(0, prof)
+    got = [c.sift(f) for f in frames]
+    monkeypatch.setenv(knob, "0")
+    ref = [c.sift(f) for f in frames]
+    c.close()
+    for a, b in zip(got, ref):
+        assert a == b
+        assert np.array_equal(a.keys, b.keys)
