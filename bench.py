@@ -440,7 +440,9 @@ def main():
             "roofline": {"bound": "hbm", "achieved": pyr_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": pyr_gbs / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "kernel": "pyramid stage (k_seed_strip + k_blur2_strip + k_blur_strip<R> + k_octave_tail), rank 0",
+                         "kernel": "pyramid stage (k_seed_pair + k_blur2_strip + k_blur_strip<R> + k_octave_tail, and "
+                                   "k_blur_detect: blur 5 with the extremum scan of the octaves it fuses, whose "
+                                   "yardstick adds the 5 DoG planes the reference's scan reads), rank 0",
                          "algorithmic_bytes_per_launch": per_launch_bytes,
                          "avg_launch_ms": per_launch_ms},
             "cpu_baseline": cpu,
