@@ -426,23 +426,30 @@ struct Plan {
 // kernels run while the host waits for chunk k and copies its results out.
 struct Slot {
     // [0] candidates [1] extrema [2] keypoints [3] outputs [4..4+F) frame starts
-    // [4+F..4+2F) per-frame outputs [4+2F..4+2F+kDescWorkWords) descriptor work queues
+    // [4+F..4+2F) per-frame outputs [4+2F..4+2F+2) the tail region's counters
+    // (early) [4+2F+2..4+2F+2+kDescWorkWords) descriptor work queues
     DevBuf<uint32_t> counters;
     PinBuf<uint32_t> h_counts;
     DevBuf<OutKp> out_kp;
     DevBuf<uint8_t> out_desc;
     DevBuf<uint64_t> out_key;
+    DevBuf<uint8_t> desc_kp;  // one-frame calls: descriptors in keypoint index order (Slot::desc_first)
     hipEvent_t ev[7] = {};   // stage boundaries on the compute stream (ev[6] = chunk done)
     hipEvent_t copied = {};  // results copied to the host (copy stream)
+    hipEvent_t ordered = {};  // desc_first: the ordering stage done (lane 1's stream)
     bool pending_copy = false;
     bool detected = false;  // this chunk's detection is enqueued (stage overlap: inside the pyramid)
     uint32_t fused_mask = 0;  // octaves detected by k_blur_detect (with their blur 5) in the pyramid
     bool graph_run = false;   // the chunk was a graph replay: only ev[0] / ev[6] were recorded
     // single-chunk calls with octave overlap: refinement + orientation of the
-    // octaves below the tail run on the aux stream beside the tail (early),
-    // the tail octaves' candidates / extrema in their own region (cand_b,
-    // ext_b; counters at counters[4 + 2m + kDescWorkWords + 0 / 1])
+    // octaves below the tail run beside the tail (early; on lane 1's stream,
+    // else the aux stream), the tail octaves' candidates / extrema in their
+    // own region (cand_b, ext_b; counters at counters[4 + 2m + 0 / 1])
     bool early = false;
+    // one-frame early calls without a limit: the descriptors are computed in
+    // keypoint index order (desc_kp) while lane 1's stream orders the
+    // keypoints; k_gather_out then writes the outputs in emission order
+    bool desc_first = false;
     uint32_t bcb = 0;
     DevBuf<uint64_t> cand_b;
     DevBuf<ExtRec> ext_b;
@@ -485,7 +492,11 @@ struct sift_mi_ctx {
     hipStream_t own2 = nullptr;    // compute stream of pipeline lane 1 (lane 0 runs on `stream`)
     hipStream_t aux[2] = {};       // per lane: blurs 4, 5 of each octave beside the next octave
     hipStream_t dec = nullptr;     // JPEG batch decoding: a high-priority stream (its own hardware queue)
-    hipEvent_t oct_ev[2][kTailMaxOct + 1] = {};  // per lane: octave o's G_3 done / aux joined
+    // per lane: [o] octave o's G_3 done, [kTailMaxOct] aux joined,
+    // [kDetEv + o] octave o's G_5 done (detection stream), [kDetJoin] detection
+    // stream joined
+    static constexpr int kDetEv = kTailMaxOct + 1, kDetJoin = 2 * kTailMaxOct + 1;
+    hipEvent_t oct_ev[2][2 * kTailMaxOct + 2] = {};
     int oct_overlap = 1;           // SIFT_MI_OCT_OVERLAP=0: one stream per lane (A/B, tests)
     bool lanes_busy = false;       // this call keeps both pipeline lanes busy (no octave overlap then)
     int stage_overlap = 1;         // SIFT_MI_STAGE_OVERLAP=0: detection after the whole pyramid
@@ -864,6 +875,9 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
     // the seed and blur 1 ran as one pass (k_seed_pair): octave 0 continues
     // at blur 2, as the (2, 3) pair
     bool seed_pair = false;
+    // one-chunk calls (Slot::early): the stream that detects octaves [0, o_tail)
+    // one by one as each octave's G_5 lands on the aux stream (set in part())
+    hipStream_t det = nullptr;
     // frames [f0, f0 + nf): seed, octave chain, tail (and their detection) on
     // stream sm; ov: blurs 4, 5 of each octave on the aux stream
     auto seed = [&](uint32_t f0, uint32_t nf, hipStream_t sm) -> int {
@@ -951,10 +965,24 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
             // precompute_images: D_s = G_{s+1} - G_s, the same f32 subtraction
             // the keypoint stages form where they read the DoG
             if (full) launch_dog(G, P, p.gstride(o), D, p.dstride(o), p.ow[o], p.oh[o], p.opitch[o], (int)nf, s45);
+            if (det) {  // this octave's extremum scan, beside the next octaves' blurs
+                HIPCHK(hipEventRecord(c->oct_ev[lane][sift_mi_ctx::kDetEv + o], s45));
+                HIPCHK(hipStreamWaitEvent(det, c->oct_ev[lane][sift_mi_ctx::kDetEv + o], 0));
+                CHK(launch_detection(c, detect_slot, f0, nf, o, o + 1, det));
+            }
         }
         return 0;
     };
     auto part = [&](uint32_t f0, uint32_t nf, hipStream_t sm, bool ov) -> int {
+        const char* ee = getenv("SIFT_MI_EARLY");
+        const bool early = detect_slot >= 0 && ov && o_tail > 0 && o_tail < p.n_oct && c->slot[detect_slot].bcb &&
+                           !(ee && !strcmp(ee, "0"));
+        // lane 1's stream is idle in a one-chunk call on lane 0: it detects
+        // the octaves below the tail as they complete, then refines and
+        // orients them (SIFT_MI_DET_STREAM=0: all of that on the aux stream
+        // after its last blur)
+        const char* de = getenv("SIFT_MI_DET_STREAM");
+        det = (early && lane == 0 && c->lanes == 2 && !(de && !strcmp(de, "0"))) ? c->own2 : nullptr;
         CHK(seed(f0, nf, sm));
         CHK(octaves(f0, nf, 0, o_tail, sm, ov));
         if (o_tail < p.n_oct) {
@@ -985,19 +1013,19 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
                                p.dog(o, lane) + (size_t)f0 * p.dstride(o), p.dstride(o), p.ow[o], p.oh[o],
                                p.opitch[o], (int)nf, sm);
         }
-        const char* ee = getenv("SIFT_MI_EARLY");
-        if (detect_slot >= 0 && ov && o_tail > 0 && o_tail < p.n_oct && c->slot[detect_slot].bcb &&
-            !(ee && !strcmp(ee, "0"))) {
+        if (early) {
             // one chunk (octave overlap): the octaves below the tail are
-            // detected, refined and oriented on the aux stream beside the tail
-            // kernel; the tail octaves, after it, into a region of their own
-            // (Slot::early; SIFT_MI_EARLY=0: off)
+            // detected, refined and oriented beside the tail kernel (on the
+            // detection stream, else on the aux stream); the tail octaves,
+            // after it, into a region of their own (Slot::early;
+            // SIFT_MI_EARLY=0: off)
             Slot& S = c->slot[detect_slot];
             uint32_t* cnt = S.counters.p;
-            uint32_t* cb = cnt + 4 + 2 * S.m + kDescWorkWords;
-            CHK(launch_detection(c, detect_slot, f0, nf, 0, o_tail, aux));
-            CHK(launch_refine_stage(c, detect_slot, S.cand.p, cnt + 0, S.bc, S.ext.p, cnt + 1, S.be, aux));
-            CHK(launch_orient_stage(c, detect_slot, S.ext.p, cnt + 1, S.be, S.bk, aux));
+            uint32_t* cb = cnt + 4 + 2 * S.m;
+            hipStream_t below = det ? det : aux;
+            if (!det) CHK(launch_detection(c, detect_slot, f0, nf, 0, o_tail, aux));
+            CHK(launch_refine_stage(c, detect_slot, S.cand.p, cnt + 0, S.bc, S.ext.p, cnt + 1, S.be, below));
+            CHK(launch_orient_stage(c, detect_slot, S.ext.p, cnt + 1, S.be, S.bk, below));
             CHK(launch_detection(c, detect_slot, f0, nf, o_tail, p.n_oct, sm, S.cand_b.p, cb + 0, S.bcb));
             CHK(launch_refine_stage(c, detect_slot, S.cand_b.p, cb + 0, S.bcb, S.ext_b.p, cb + 1, S.bcb, sm));
             CHK(launch_orient_stage(c, detect_slot, S.ext_b.p, cb + 1, S.bcb, S.bk, sm));
@@ -1011,6 +1039,11 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
         if (ov && o_tail > 0) {  // join: the aux stream's work before what follows on sm
             HIPCHK(hipEventRecord(c->oct_ev[lane][kTailMaxOct], aux));
             HIPCHK(hipStreamWaitEvent(sm, c->oct_ev[lane][kTailMaxOct], 0));
+        }
+        if (det) {
+            HIPCHK(hipEventRecord(c->oct_ev[lane][sift_mi_ctx::kDetJoin], det));
+            HIPCHK(hipStreamWaitEvent(sm, c->oct_ev[lane][sift_mi_ctx::kDetJoin], 0));
+            det = nullptr;
         }
         return 0;
     };
@@ -1081,10 +1114,12 @@ int reserve_chunk(sift_mi_ctx* c, int si, const Bounds& B, uint32_t frames) {
     const bool grow = B.bc > S.cand.cap || B.be > S.ext.cap || B.bk > S.kp.cap || B.bk > S.keys_a.cap ||
                       bcb > S.cand_b.cap || bcb > S.ext_b.cap ||
                       frames > S.seg_off.cap || B.bk > S.out_kp.cap ||
-                      4 + 2 * frames + kDescWorkWords + 2 > S.counters.cap;
+                      4 + 2 * frames + kDescWorkWords + 2 > S.counters.cap ||
+                      (frames == 1 && (size_t)B.bk * kDescSize > S.desc_kp.cap);
     if (grow) {
         HIPCHK(hipStreamSynchronize(lane_stream(c, si)));
         HIPCHK(hipStreamSynchronize(c->cstream));
+        if (si == 0 && c->lanes == 2) HIPCHK(hipStreamSynchronize(c->own2));  // one-chunk calls' second stream
     }
     CHK(S.cand.ensure(B.bc));
     CHK(S.ext.ensure(B.be));
@@ -1107,6 +1142,7 @@ int reserve_chunk(sift_mi_ctx* c, int si, const Bounds& B, uint32_t frames) {
     CHK(S.out_kp.ensure(B.bk));
     CHK(S.out_desc.ensure((size_t)B.bk * kDescSize));
     CHK(S.out_key.ensure(B.bk));
+    if (frames == 1) CHK(S.desc_kp.ensure((size_t)B.bk * kDescSize));
     return 0;
 }
 
@@ -1233,7 +1269,7 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
     uint32_t* cnt = S.counters.p;
     uint32_t* starts = cnt + 4;
     uint32_t* out_cnt = cnt + 4 + m;
-    uint32_t* work = cnt + 4 + 2 * m;  // descriptor work queues
+    uint32_t* work = cnt + 4 + 2 * m + 2;  // descriptor work queues (after the tail region's counters)
     (void)starts;
     (void)work;
     if (!S.detected) CHK(launch_detection(c, si, 0, m, 0, p.n_oct, st));
@@ -1243,54 +1279,57 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
     if (!S.early) CHK(launch_orient_stage(c, si, S.ext.p, cnt + 1, B.be, B.bk, st));
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(S.ev[3], st));
-    // emission order: radix sort of the keys (padding sorts last); one frame
-    // without a limit: k_order_small (SIFT_MI_SMALL_ORDER=0: the general path)
-    const char* so_env = getenv("SIFT_MI_SMALL_ORDER");
+    // one frame, no limit, early detection: the descriptors are computed in
+    // keypoint index order beside the ordering stage, which runs on lane 1's
+    // idle stream; k_gather_out then writes the outputs in emission order
+    // (SIFT_MI_DESC_FIRST=0: order, then describe in emission order)
+    const char* dfe = getenv("SIFT_MI_DESC_FIRST");
+    S.desc_first = S.early && m == 1 && limit < 0 && si == 0 && c->lanes == 2 && !(dfe && !strcmp(dfe, "0"));
+    hipStream_t os = S.desc_first ? c->own2 : st;  // the ordering stage's stream
+    if (S.desc_first) HIPCHK(hipStreamWaitEvent(os, S.ev[3], 0));
+    // emission order: radix sort of the keys (padding sorts last)
     const uint32_t* order = S.vals_b.p;  // emission order -> kp index
-    if (m == 1 && limit < 0 && B.bk <= kSmallOrder && !(so_env && !strcmp(so_env, "0"))) {
-        launch_order_small(S.kp.p, cnt + 2, B.bk, S.vals_b.p, starts, out_cnt, S.seg_off.p, S.out_off.p, S.use_resp.p,
-                           cnt + 3, st);
-    } else {
-        const int img_bits = img_bits_for(m);
-        const int end_bit = kKeyImgShift + img_bits;
-        const uint64_t pad = (end_bit >= 64) ? ~0ull : ((1ull << end_bit) - 1);
-        size_t tmp = sort_pairs_u64(nullptr, 0, S.keys_a.p, S.keys_b.p, S.vals_a.p, S.vals_b.p, B.bk, end_bit, st);
-        const int rb = 32 + img_bits;
-        const uint64_t rpad = (1ull << rb) - 1;
-        if (limit >= 0)
-            tmp = std::max(tmp, sort_pairs_u64(nullptr, 0, S.keys_a.p, S.keys_b.p, S.vals_a.p, S.fin.p, B.bk, rb, st));
-        if (!tmp) return fail(SIFT_MI_EHIP, "radix sort sizing failed");
-        if (tmp > S.sort_tmp.cap) {
-            HIPCHK(hipStreamSynchronize(st));
-            CHK(S.sort_tmp.ensure(tmp));
-        }
-        launch_make_sort_keys(S.kp.p, cnt + 2, B.bk, pad, S.keys_a.p, S.vals_a.p, st);
-        if (!sort_pairs_u64(S.sort_tmp.p, S.sort_tmp.cap, S.keys_a.p, S.keys_b.p, S.vals_a.p, S.vals_b.p, B.bk,
-                            end_bit, st))
-            return fail(SIFT_MI_EHIP, "radix sort failed");
-        launch_frame_starts(S.keys_b.p, cnt + 2, B.bk, starts, st);
-        // features_limit (src/lib.rs:156-161): per-frame plan on the device
-        launch_limit_plan(starts, cnt + 2, B.bk, (int)m, limit, out_cnt, S.seg_off.p, S.out_off.p, S.use_resp.p,
-                          cnt + 3, st);
-        if (limit >= 0) {
-            // stable sort: response-descending within each frame, emission order on ties
-            launch_make_resp_keys(S.kp.p, order, cnt + 2, B.bk, 0, rpad, S.keys_a.p, S.vals_a.p, st);
-            if (!sort_pairs_u64(S.sort_tmp.p, S.sort_tmp.cap, S.keys_a.p, S.keys_b.p, S.vals_a.p, S.fin.p, B.bk, rb,
-                                st))
-                return fail(SIFT_MI_EHIP, "response sort failed");
-            launch_select(order, S.fin.p, S.seg_off.p, S.out_off.p, S.use_resp.p, (int)m, cnt + 3, B.bk, S.vals_a.p,
-                          st);
-            order = S.vals_a.p;
-        }
+    const int img_bits = img_bits_for(m);
+    const int end_bit = kKeyImgShift + img_bits;
+    const uint64_t pad = (end_bit >= 64) ? ~0ull : ((1ull << end_bit) - 1);
+    size_t tmp = sort_pairs_u64(nullptr, 0, S.keys_a.p, S.keys_b.p, S.vals_a.p, S.vals_b.p, B.bk, end_bit, os);
+    const int rb = 32 + img_bits;
+    const uint64_t rpad = (1ull << rb) - 1;
+    if (limit >= 0)
+        tmp = std::max(tmp, sort_pairs_u64(nullptr, 0, S.keys_a.p, S.keys_b.p, S.vals_a.p, S.fin.p, B.bk, rb, os));
+    if (!tmp) return fail(SIFT_MI_EHIP, "radix sort sizing failed");
+    if (tmp > S.sort_tmp.cap) {
+        HIPCHK(hipStreamSynchronize(st));
+        if (os != st) HIPCHK(hipStreamSynchronize(os));
+        CHK(S.sort_tmp.ensure(tmp));
+    }
+    launch_make_sort_keys(S.kp.p, cnt + 2, B.bk, pad, S.keys_a.p, S.vals_a.p, os);
+    if (!sort_pairs_u64(S.sort_tmp.p, S.sort_tmp.cap, S.keys_a.p, S.keys_b.p, S.vals_a.p, S.vals_b.p, B.bk,
+                        end_bit, os))
+        return fail(SIFT_MI_EHIP, "radix sort failed");
+    launch_frame_starts(S.keys_b.p, cnt + 2, B.bk, starts, os);
+    // features_limit (src/lib.rs:156-161): per-frame plan on the device
+    launch_limit_plan(starts, cnt + 2, B.bk, (int)m, limit, out_cnt, S.seg_off.p, S.out_off.p, S.use_resp.p,
+                      cnt + 3, os);
+    if (limit >= 0) {
+        // stable sort: response-descending within each frame, emission order on ties
+        launch_make_resp_keys(S.kp.p, order, cnt + 2, B.bk, 0, rpad, S.keys_a.p, S.vals_a.p, os);
+        if (!sort_pairs_u64(S.sort_tmp.p, S.sort_tmp.cap, S.keys_a.p, S.keys_b.p, S.vals_a.p, S.fin.p, B.bk, rb,
+                            os))
+            return fail(SIFT_MI_EHIP, "response sort failed");
+        launch_select(order, S.fin.p, S.seg_off.p, S.out_off.p, S.use_resp.p, (int)m, cnt + 3, B.bk, S.vals_a.p,
+                      os);
+        order = S.vals_a.p;
     }
     HIPCHK(hipGetLastError());
+    if (S.desc_first) HIPCHK(hipEventRecord(S.ordered, os));
     HIPCHK(hipEventRecord(S.ev[4], st));
     // descriptors into this slot's outputs, once its previous copy-out is done
     if (S.pending_copy) HIPCHK(hipStreamWaitEvent(st, S.copied, 0));
     DescLaunch DL{};
     DL.kp = S.kp.p;
-    DL.idx = order;
-    DL.n = cnt + 3;
+    DL.idx = S.desc_first ? nullptr : order;
+    DL.n = S.desc_first ? cnt + 2 : cnt + 3;
     DL.bound = B.bk;
     DL.work = work;
     DL.key_base = (uint64_t)frame_base << kKeyImgShift;
@@ -1300,18 +1339,22 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
     DL.oh = p.d_oh.p;
     DL.opitch = p.d_opitch.p;
     DL.img_base = 0;
-    DL.out_kp = S.out_kp.p;
-    DL.out_key = S.out_key.p;
-    DL.out_desc = S.out_desc.p;
+    DL.out_kp = S.desc_first ? nullptr : S.out_kp.p;
+    DL.out_key = S.desc_first ? nullptr : S.out_key.p;
+    DL.out_desc = S.desc_first ? S.desc_kp.p : S.out_desc.p;
     DL.exact = c->exact_descriptors;
     DL.samples = c->count_samples ? c->samples.p + 8 : nullptr;
     launch_describe(DL, st);
+    if (S.desc_first) {
+        HIPCHK(hipStreamWaitEvent(st, S.ordered, 0));
+        launch_gather_out(S.kp.p, order, cnt + 3, B.bk, S.desc_kp.p, S.out_desc.p, S.out_kp.p, S.out_key.p,
+                          DL.key_base, st);
+    }
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(S.ev[5], st));
-    HIPCHK(hipMemcpyAsync(S.h_counts.p, cnt, (4 + 2 * m) * sizeof(uint32_t), hipMemcpyDeviceToHost, st));
-    if (S.early)
-        HIPCHK(hipMemcpyAsync(S.h_counts.p + 4 + 2 * m, cnt + 4 + 2 * m + kDescWorkWords, 2 * sizeof(uint32_t),
-                              hipMemcpyDeviceToHost, st));
+    // the frame plan and the tail region's counters (Slot::early) in one copy
+    HIPCHK(hipMemcpyAsync(S.h_counts.p, cnt, (4 + 2 * m + (S.early ? 2 : 0)) * sizeof(uint32_t),
+                          hipMemcpyDeviceToHost, st));
     HIPCHK(hipEventRecord(S.ev[6], st));
     return 0;
 }
@@ -1781,6 +1824,7 @@ int sift_mi_create(int device_ordinal, sift_mi_profile profile, sift_mi_ctx** ou
     for (auto& S : c->slot) {
         for (auto& e : S.ev) ok = ok && hipEventCreate(&e) == hipSuccess;
         ok = ok && hipEventCreateWithFlags(&S.copied, hipEventDisableTiming) == hipSuccess;
+        ok = ok && hipEventCreateWithFlags(&S.ordered, hipEventDisableTiming) == hipSuccess;
     }
     if (!ok) {
         sift_mi_destroy(c);
@@ -1813,9 +1857,11 @@ void sift_mi_destroy(sift_mi_ctx* c) {
         S.out_kp.release();
         S.out_desc.release();
         S.out_key.release();
+        S.desc_kp.release();
         for (auto& e : S.ev)
             if (e) (void)hipEventDestroy(e);
         if (S.copied) (void)hipEventDestroy(S.copied);
+        if (S.ordered) (void)hipEventDestroy(S.ordered);
     }
     if (c->fork) (void)hipEventDestroy(c->fork);
     for (auto& lane : c->oct_ev)

@@ -182,55 +182,42 @@ void launch_select(const uint32_t* emis_order, const uint32_t* resp_order, const
                        use_resp, n_img, n_out, bound, final_idx);
 }
 
-// ---------------------------------------------------------------------------
-// The whole ordering stage of a one-frame chunk without a features_limit in
-// ONE workgroup: (key << 14 | index) packed in a u64 (a frame's emission keys
-// use 42 bits, the index < 2^14), bitonic-sorted in LDS, then the emission
-// order and the frame's output plan.  Replaces make_sort_keys, the radix sort
-// (five kernels), frame_starts and limit_plan -- eight dependent launches of
-// a few microseconds each on a single frame's critical path.
-// ---------------------------------------------------------------------------
-__global__ __launch_bounds__(1024) void k_order_small(const KpRec* __restrict__ kp, const uint32_t* __restrict__ n_kp,
-                                                      uint32_t bound, uint32_t* __restrict__ order,
-                                                      uint32_t* __restrict__ starts, uint32_t* __restrict__ out_cnt,
-                                                      uint32_t* __restrict__ seg_off, uint32_t* __restrict__ out_off,
-                                                      uint8_t* __restrict__ use_resp, uint32_t* __restrict__ n_out) {
-    __shared__ uint64_t sk[kSmallOrder];
-    const int tid = threadIdx.x;
-    const uint32_t n = min(min(*n_kp, bound), (uint32_t)kSmallOrder);
-    uint32_t N = 2;
-    while (N < n) N <<= 1;
-    for (uint32_t i = tid; i < N; i += 1024) sk[i] = i < n ? (kp[i].key << 14) | (uint64_t)i : ~0ull;
-    __syncthreads();
-    for (uint32_t k = 2; k <= N; k <<= 1) {
-        for (uint32_t j = k >> 1; j > 0; j >>= 1) {
-            for (uint32_t p = tid; p < N / 2; p += 1024) {
-                const uint32_t i = ((p & ~(j - 1)) << 1) | (p & (j - 1)), l = i + j;  // the pair (i, i ^ j)
-                const uint64_t a = sk[i], b = sk[l];
-                if ((a > b) == ((i & k) == 0)) {
-                    sk[i] = b;
-                    sk[l] = a;
-                }
-            }
-            __syncthreads();
-        }
-    }
-    for (uint32_t i = tid; i < n; i += 1024) order[i] = (uint32_t)(sk[i] & 0x3fffu);
-    if (tid == 0) {
-        starts[0] = n ? 0u : 0xffffffffu;
-        out_cnt[0] = n;
-        seg_off[0] = 0;
-        out_off[0] = 0;
-        use_resp[0] = 0;
-        *n_out = n;
+// Outputs of a call whose descriptors were computed in keypoint index order
+// (one-frame calls: k_describe runs beside the ordering stage): row j of the
+// outputs is keypoint order[j] -- its descriptor (16 bytes per thread), its
+// KeyPoint (src/lib.rs:163-176: x, y, size * DELTA_MIN) and its emission key.
+__global__ void k_gather_out(const KpRec* __restrict__ kp, const uint32_t* __restrict__ order,
+                             const uint32_t* __restrict__ n_out, uint32_t bound, const uint4* __restrict__ desc_in,
+                             uint4* __restrict__ desc_out, OutKp* __restrict__ out_kp, uint64_t* __restrict__ out_key,
+                             uint64_t key_base) {
+    constexpr uint32_t kParts = kDescSize / 16;
+    const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    const uint32_t j = t / kParts, part = t % kParts;
+    const uint32_t n = min(*n_out, bound);
+    if (j >= n) return;
+    const uint32_t i = order[j];
+    desc_out[(size_t)j * kParts + part] = desc_in[(size_t)i * kParts + part];
+    if (part == 0) {
+        const KpRec r = kp[i];
+        OutKp k;
+        k.x = r.x * 0.5f;
+        k.y = r.y * 0.5f;
+        k.size = r.size * 0.5f;
+        k.angle = r.angle;
+        k.response = r.response;
+        out_kp[j] = k;
+        out_key[j] = r.key + key_base;
     }
 }
 
-void launch_order_small(const KpRec* kp, const uint32_t* n_kp, uint32_t bound, uint32_t* order, uint32_t* starts,
-                        uint32_t* out_cnt, uint32_t* seg_off, uint32_t* out_off, uint8_t* use_resp, uint32_t* n_out,
-                        hipStream_t st) {
-    hipLaunchKernelGGL(k_order_small, dim3(1), dim3(1024), 0, st, kp, n_kp, bound, order, starts, out_cnt, seg_off,
-                       out_off, use_resp, n_out);
+void launch_gather_out(const KpRec* kp, const uint32_t* order, const uint32_t* n_out, uint32_t bound,
+                       const uint8_t* desc_in, uint8_t* desc_out, OutKp* out_kp, uint64_t* out_key, uint64_t key_base,
+                       hipStream_t st) {
+    if (!bound) return;
+    const uint64_t threads = (uint64_t)bound * (kDescSize / 16);
+    hipLaunchKernelGGL(k_gather_out, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, kp, order, n_out,
+                       bound, reinterpret_cast<const uint4*>(desc_in), reinterpret_cast<uint4*>(desc_out), out_kp,
+                       out_key, key_base);
 }
 
 }  // namespace siftmi

@@ -227,18 +227,16 @@ void launch_frame_starts(const uint64_t* sorted_keys, const uint32_t* n, uint32_
 void launch_limit_plan(const uint32_t* starts, const uint32_t* n_kp, uint32_t bound, int n_img, int64_t limit,
                        uint32_t* out_cnt, uint32_t* seg_off, uint32_t* out_off, uint8_t* use_resp, uint32_t* n_out,
                        hipStream_t st);
-// One frame, no features_limit, bound <= kSmallOrder keypoints: the whole
-// ordering stage (emission order + the frame's output plan) in one
-// workgroup (k_order_small), instead of make_sort_keys .. limit_plan
-constexpr uint32_t kSmallOrder = 16384;
-void launch_order_small(const KpRec* kp, const uint32_t* n_kp, uint32_t bound, uint32_t* order, uint32_t* starts,
-                        uint32_t* out_cnt, uint32_t* seg_off, uint32_t* out_off, uint8_t* use_resp, uint32_t* n_out,
-                        hipStream_t st);
 // key = (frame << 32) | ~bits(response) over the emission order; padded beyond *n
 void launch_make_resp_keys(const KpRec* kp, const uint32_t* order, const uint32_t* n, uint32_t bound, int img_base,
                            uint64_t pad, uint64_t* keys, uint32_t* vals, hipStream_t st);
 // final[i] = src index for i < *n_out: for frame f, if use_resp[f] the
 // response order, else the emission order
+// one-frame calls: descriptors computed in keypoint index order (desc_in),
+// then row j of the outputs = keypoint order[j] (descriptor, KeyPoint, key)
+void launch_gather_out(const KpRec* kp, const uint32_t* order, const uint32_t* n_out, uint32_t bound,
+                       const uint8_t* desc_in, uint8_t* desc_out, OutKp* out_kp, uint64_t* out_key, uint64_t key_base,
+                       hipStream_t st);
 void launch_select(const uint32_t* emis_order, const uint32_t* resp_order, const uint32_t* seg_off,
                    const uint32_t* out_off, const uint8_t* use_resp, int n_img, const uint32_t* n_out, uint32_t bound,
                    uint32_t* final_idx, hipStream_t st);

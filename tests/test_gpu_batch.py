@@ -329,22 +329,24 @@ def test_single_chunk_graph_replay(pkg, ctx, oracle, monkeypatch, fetch):
     c.close()
 
 
-@pytest.mark.parametrize("knob", ["SIFT_MI_EARLY", "SIFT_MI_SMALL_ORDER"])
+@pytest.mark.parametrize("knob", ["SIFT_MI_EARLY", "SIFT_MI_DET_STREAM", "SIFT_MI_DESC_FIRST"])
 @pytest.mark.parametrize("profile", [0, 1])
 def test_single_chunk_paths_equal(pkg, monkeypatch, knob, profile):
-    """One-chunk calls take two latency paths -- the octaves below the tail
-    refined and oriented beside the tail kernel with the tail octaves in a
-    region of their own (Slot::early), and the one-workgroup ordering stage
-    (k_order_small) -- whose results must equal the general path's
-    (SIFT_MI_EARLY=0 / SIFT_MI_SMALL_ORDER=0) bit for bit, incl. keys."""
+    """One-chunk calls take latency paths of their own -- the octaves below
+    the tail detected (one by one, on lane 1's stream), refined and oriented
+    beside the tail kernel with the tail octaves in a region of their own
+    (Slot::early), and the descriptors computed in keypoint index order beside
+    the ordering stage, then gathered (Slot::desc_first) -- whose results must
+    equal the general path's (the knob = 0) bit for bit, incl. keys.  Each
+    frame runs twice: the second call uses the bounds the first one learned."""
     import synth
     frames = [synth.frame(640, 480, 3), synth.frame(1000, 333, 5),
               np.random.default_rng(5).integers(0, 256, (96, 128), dtype=np.uint8)]
     prof = pkg.OpenCVProcessing if profile == 0 else pkg.ImageprocProcessing
     c = pkg.Context(0, prof)
-    got = [c.sift(f) for f in frames]
+    got = [c.sift(f) for f in frames for _ in range(2)]
     monkeypatch.setenv(knob, "0")
-    ref = [c.sift(f) for f in frames]
+    ref = [c.sift(f) for f in frames for _ in range(2)]
     c.close()
     for a, b in zip(got, ref):
         assert a == b
