@@ -1108,14 +1108,15 @@ Bounds chunk_bounds(sift_mi_ctx* c, uint32_t m) {
 
 // Grows the shared buffers for bounds B (waits for in-flight work first when a
 // buffer has to be reallocated).
-int reserve_chunk(sift_mi_ctx* c, int si, const Bounds& B, uint32_t frames) {
+// frames: the slot's frame capacity (the plan's chunk); m: this chunk's frames
+int reserve_chunk(sift_mi_ctx* c, int si, const Bounds& B, uint32_t frames, uint32_t m) {
     Slot& S = c->slot[si];
     const uint32_t bcb = std::max<uint32_t>(2048, (uint32_t)std::min<double>(std::ceil(c->pf_cand_b * 1.3 * frames) + 1024, 1e9));
     const bool grow = B.bc > S.cand.cap || B.be > S.ext.cap || B.bk > S.kp.cap || B.bk > S.keys_a.cap ||
                       bcb > S.cand_b.cap || bcb > S.ext_b.cap ||
                       frames > S.seg_off.cap || B.bk > S.out_kp.cap ||
                       4 + 2 * frames + kDescWorkWords + 2 > S.counters.cap ||
-                      (frames == 1 && (size_t)B.bk * kDescSize > S.desc_kp.cap);
+                      (m == 1 && (size_t)B.bk * kDescSize > S.desc_kp.cap);
     if (grow) {
         HIPCHK(hipStreamSynchronize(lane_stream(c, si)));
         HIPCHK(hipStreamSynchronize(c->cstream));
@@ -1142,7 +1143,7 @@ int reserve_chunk(sift_mi_ctx* c, int si, const Bounds& B, uint32_t frames) {
     CHK(S.out_kp.ensure(B.bk));
     CHK(S.out_desc.ensure((size_t)B.bk * kDescSize));
     CHK(S.out_key.ensure(B.bk));
-    if (frames == 1) CHK(S.desc_kp.ensure((size_t)B.bk * kDescSize));
+    if (m == 1) CHK(S.desc_kp.ensure((size_t)B.bk * kDescSize));  // Slot::desc_first
     return 0;
 }
 
@@ -1284,7 +1285,8 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
     // idle stream; k_gather_out then writes the outputs in emission order
     // (SIFT_MI_DESC_FIRST=0: order, then describe in emission order)
     const char* dfe = getenv("SIFT_MI_DESC_FIRST");
-    S.desc_first = S.early && m == 1 && limit < 0 && si == 0 && c->lanes == 2 && !(dfe && !strcmp(dfe, "0"));
+    S.desc_first = S.early && m == 1 && limit < 0 && si == 0 && c->lanes == 2 &&
+                   S.desc_kp.cap >= (size_t)B.bk * kDescSize && !(dfe && !strcmp(dfe, "0"));
     hipStream_t os = S.desc_first ? c->own2 : st;  // the ordering stage's stream
     if (S.desc_first) HIPCHK(hipStreamWaitEvent(os, S.ev[3], 0));
     // emission order: radix sort of the keys (padding sorts last)
@@ -1379,7 +1381,7 @@ int enqueue_chunk(sift_mi_ctx* c, int si, const uint8_t* d_frames, size_t frame_
     Slot& S = c->slot[si];
     const Bounds B = chunk_bounds(c, m);
     CHK(ensure_lane(c, arena_of(c, si)));
-    CHK(reserve_chunk(c, si, B, c->plan.chunk));
+    CHK(reserve_chunk(c, si, B, c->plan.chunk, m));
     hipStream_t st = lane_stream(c, si);
     HIPCHK(hipEventRecord(S.ev[0], st));
     CHK(prepare_chunk(c, si, m, frame_base, B));
@@ -1515,7 +1517,7 @@ int enqueue_single_graph(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_p
     if (!on || c->band_n > 1 || c->lanes != 2 || S.pending_copy) return 0;
     const Bounds B = chunk_bounds(c, m);
     CHK(ensure_lane(c, arena_of(c, 0)));
-    CHK(reserve_chunk(c, 0, B, c->plan.chunk));
+    CHK(reserve_chunk(c, 0, B, c->plan.chunk, m));
     hipStream_t st = lane_stream(c, 0);
     sift_mi_ctx::GraphKey k;
     std::memset(&k, 0, sizeof k);
