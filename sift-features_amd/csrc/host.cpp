@@ -753,6 +753,11 @@ int launch_orient_stage(sift_mi_ctx* c, int si, const ExtRec* ext, const uint32_
 // gradient's neighbour row).
 constexpr int kBandDrift = 24, kBandPatch = 41;
 
+// One-chunk calls: octaves below the tail with at least this many pixels
+// per frame are detected on their own stream as soon as they complete
+// (smaller ones are latency-bound launches: they join the tail's detection)
+constexpr size_t kDetStreamPx = size_t(1) << 20;
+
 // ---------------------------------------------------------------------------
 // Stage 1: Gaussian scale space + DoG for n frames (device-resident u8)
 // ---------------------------------------------------------------------------
@@ -875,9 +880,10 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
     // the seed and blur 1 ran as one pass (k_seed_pair): octave 0 continues
     // at blur 2, as the (2, 3) pair
     bool seed_pair = false;
-    // one-chunk calls (Slot::early): the stream that detects octaves [0, o_tail)
+    // one-chunk calls (Slot::early): the stream that detects octaves [0, k_det)
     // one by one as each octave's G_5 lands on the aux stream (set in part())
     hipStream_t det = nullptr;
+    int k_det = 0;
     // frames [f0, f0 + nf): seed, octave chain, tail (and their detection) on
     // stream sm; ov: blurs 4, 5 of each octave on the aux stream
     auto seed = [&](uint32_t f0, uint32_t nf, hipStream_t sm) -> int {
@@ -965,7 +971,7 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
             // precompute_images: D_s = G_{s+1} - G_s, the same f32 subtraction
             // the keypoint stages form where they read the DoG
             if (full) launch_dog(G, P, p.gstride(o), D, p.dstride(o), p.ow[o], p.oh[o], p.opitch[o], (int)nf, s45);
-            if (det) {  // this octave's extremum scan, beside the next octaves' blurs
+            if (det && o < k_det) {  // this octave's extremum scan, beside the next octaves' blurs
                 HIPCHK(hipEventRecord(c->oct_ev[lane][sift_mi_ctx::kDetEv + o], s45));
                 HIPCHK(hipStreamWaitEvent(det, c->oct_ev[lane][sift_mi_ctx::kDetEv + o], 0));
                 CHK(launch_detection(c, detect_slot, f0, nf, o, o + 1, det));
@@ -978,11 +984,18 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
         const bool early = detect_slot >= 0 && ov && o_tail > 0 && o_tail < p.n_oct && c->slot[detect_slot].bcb &&
                            !(ee && !strcmp(ee, "0"));
         // lane 1's stream is idle in a one-chunk call on lane 0: it detects
-        // the octaves below the tail as they complete, then refines and
-        // orients them (SIFT_MI_DET_STREAM=0: all of that on the aux stream
-        // after its last blur)
+        // the large octaves below the tail (>= kDetStreamPx pixels) one by one
+        // as they complete, then refines and orients them while the tail
+        // kernel runs; the smaller octaves join the tail's detection on the
+        // main stream (SIFT_MI_DET_STREAM=0: every octave below the tail
+        // detected, refined and oriented on the aux stream after its last blur)
         const char* de = getenv("SIFT_MI_DET_STREAM");
-        det = (early && lane == 0 && c->lanes == 2 && !(de && !strcmp(de, "0"))) ? c->own2 : nullptr;
+        det = nullptr;
+        k_det = 0;
+        if (early && lane == 0 && c->lanes == 2 && !(de && !strcmp(de, "0"))) {
+            while (k_det < o_tail && p.px[k_det] >= kDetStreamPx) k_det++;
+            if (k_det > 0) det = c->own2;
+        }
         CHK(seed(f0, nf, sm));
         CHK(octaves(f0, nf, 0, o_tail, sm, ov));
         if (o_tail < p.n_oct) {
@@ -1022,11 +1035,20 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
             Slot& S = c->slot[detect_slot];
             uint32_t* cnt = S.counters.p;
             uint32_t* cb = cnt + 4 + 2 * S.m;
-            hipStream_t below = det ? det : aux;
-            if (!det) CHK(launch_detection(c, detect_slot, f0, nf, 0, o_tail, aux));
-            CHK(launch_refine_stage(c, detect_slot, S.cand.p, cnt + 0, S.bc, S.ext.p, cnt + 1, S.be, below));
-            CHK(launch_orient_stage(c, detect_slot, S.ext.p, cnt + 1, S.be, S.bk, below));
-            CHK(launch_detection(c, detect_slot, f0, nf, o_tail, p.n_oct, sm, S.cand_b.p, cb + 0, S.bcb));
+            if (det) {
+                // octaves [0, k_det): detected on det inside octaves()
+                CHK(launch_refine_stage(c, detect_slot, S.cand.p, cnt + 0, S.bc, S.ext.p, cnt + 1, S.be, det));
+                CHK(launch_orient_stage(c, detect_slot, S.ext.p, cnt + 1, S.be, S.bk, det));
+                // the smaller octaves' G_5 (aux) before their detection on sm
+                HIPCHK(hipEventRecord(c->oct_ev[lane][kTailMaxOct], aux));
+                HIPCHK(hipStreamWaitEvent(sm, c->oct_ev[lane][kTailMaxOct], 0));
+            } else {
+                CHK(launch_detection(c, detect_slot, f0, nf, 0, o_tail, aux));
+                CHK(launch_refine_stage(c, detect_slot, S.cand.p, cnt + 0, S.bc, S.ext.p, cnt + 1, S.be, aux));
+                CHK(launch_orient_stage(c, detect_slot, S.ext.p, cnt + 1, S.be, S.bk, aux));
+            }
+            const int ob = det ? k_det : o_tail;  // first octave of the main stream's region
+            CHK(launch_detection(c, detect_slot, f0, nf, ob, p.n_oct, sm, S.cand_b.p, cb + 0, S.bcb));
             CHK(launch_refine_stage(c, detect_slot, S.cand_b.p, cb + 0, S.bcb, S.ext_b.p, cb + 1, S.bcb, sm));
             CHK(launch_orient_stage(c, detect_slot, S.ext_b.p, cb + 1, S.bcb, S.bk, sm));
             S.early = true;
@@ -1036,7 +1058,7 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
             CHK(launch_detection(c, detect_slot, f0, nf, 0, o_tail, ov && o_tail > 0 ? aux : sm));
             CHK(launch_detection(c, detect_slot, f0, nf, o_tail, p.n_oct, sm));
         }
-        if (ov && o_tail > 0) {  // join: the aux stream's work before what follows on sm
+        if (ov && o_tail > 0 && !det) {  // join: the aux stream's work before what follows on sm
             HIPCHK(hipEventRecord(c->oct_ev[lane][kTailMaxOct], aux));
             HIPCHK(hipStreamWaitEvent(sm, c->oct_ev[lane][kTailMaxOct], 0));
         }
