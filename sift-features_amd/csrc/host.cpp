@@ -946,9 +946,12 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
                     F.img_base = (int)f0;
                     F.profile = p.profile;
                     F.taps = p.oct_taps[s];
-                    F.cand = S.cand.p;
-                    F.counter = S.counters.p + 0;
-                    F.cap = S.bc;
+                    // with a detection stream, octaves from k_det on belong to
+                    // the main stream's region (Slot::early), fused or not
+                    const bool to_b = det && o >= k_det;
+                    F.cand = to_b ? S.cand_b.p : S.cand.p;
+                    F.counter = to_b ? S.counters.p + 4 + 2 * S.m : S.counters.p + 0;
+                    F.cap = to_b ? S.bcb : S.bc;
                     if (launch_blur_detect(p.oct_r[s], F, s45) == 0) {
                         S.fused_mask |= 1u << o;
                         launches++;
