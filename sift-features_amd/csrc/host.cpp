@@ -441,6 +441,10 @@ struct Slot {
     bool detected = false;  // this chunk's detection is enqueued (stage overlap: inside the pyramid)
     uint32_t fused_mask = 0;  // octaves detected by k_blur_detect (with their blur 5) in the pyramid
     bool graph_run = false;   // the chunk was a graph replay: only ev[0] / ev[6] were recorded
+    // ev[0..5] recorded: the one-lane mode times the stages (a marker packet
+    // costs ~7 us of the stream's timeline; two-lane calls record only ev[6])
+    bool staged = false;
+    hipEvent_t oriented = {};  // desc_first: the keypoints are oriented (fork to lane 1's stream)
     // single-chunk calls with octave overlap: refinement + orientation of the
     // octaves below the tail run beside the tail (early; on lane 1's stream,
     // else the aux stream), the tail octaves' candidates / extrema in their
@@ -1301,10 +1305,10 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
     if (!S.detected) CHK(launch_detection(c, si, 0, m, 0, p.n_oct, st));
     // (early: refinement and orientation were enqueued inside the pyramid)
     if (!S.early) CHK(launch_refine_stage(c, si, S.cand.p, cnt + 0, B.bc, S.ext.p, cnt + 1, B.be, st));
-    HIPCHK(hipEventRecord(S.ev[2], st));
+    if (S.staged) HIPCHK(hipEventRecord(S.ev[2], st));
     if (!S.early) CHK(launch_orient_stage(c, si, S.ext.p, cnt + 1, B.be, B.bk, st));
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(S.ev[3], st));
+    if (S.staged) HIPCHK(hipEventRecord(S.ev[3], st));
     // one frame, no limit, early detection: the descriptors are computed in
     // keypoint index order beside the ordering stage, which runs on lane 1's
     // idle stream; k_gather_out then writes the outputs in emission order
@@ -1313,7 +1317,10 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
     S.desc_first = S.early && m == 1 && limit < 0 && si == 0 && c->lanes == 2 &&
                    S.desc_kp.cap >= (size_t)B.bk * kDescSize && !(dfe && !strcmp(dfe, "0"));
     hipStream_t os = S.desc_first ? c->own2 : st;  // the ordering stage's stream
-    if (S.desc_first) HIPCHK(hipStreamWaitEvent(os, S.ev[3], 0));
+    if (S.desc_first) {
+        HIPCHK(hipEventRecord(S.oriented, st));
+        HIPCHK(hipStreamWaitEvent(os, S.oriented, 0));
+    }
     // emission order: radix sort of the keys (padding sorts last)
     const uint32_t* order = S.vals_b.p;  // emission order -> kp index
     const int img_bits = img_bits_for(m);
@@ -1350,7 +1357,7 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
     }
     HIPCHK(hipGetLastError());
     if (S.desc_first) HIPCHK(hipEventRecord(S.ordered, os));
-    HIPCHK(hipEventRecord(S.ev[4], st));
+    if (S.staged) HIPCHK(hipEventRecord(S.ev[4], st));
     // descriptors into this slot's outputs, once its previous copy-out is done
     if (S.pending_copy) HIPCHK(hipStreamWaitEvent(st, S.copied, 0));
     DescLaunch DL{};
@@ -1378,7 +1385,7 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
                           DL.key_base, st);
     }
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(S.ev[5], st));
+    if (S.staged) HIPCHK(hipEventRecord(S.ev[5], st));
     // the frame plan and the tail region's counters (Slot::early) in one copy
     HIPCHK(hipMemcpyAsync(S.h_counts.p, cnt, (4 + 2 * m + (S.early ? 2 : 0)) * sizeof(uint32_t),
                           hipMemcpyDeviceToHost, st));
@@ -1392,6 +1399,7 @@ void accumulate_times(sift_mi_ctx* c, Slot& S) {
         if (hipEventElapsedTime(&ms, S.ev[0], S.ev[6]) == hipSuccess) c->stats.total_ms += ms;
         return;
     }
+    if (!S.staged) return;
     if (hipEventElapsedTime(&ms, S.ev[0], S.ev[1]) == hipSuccess) c->stats.pyramid_ms += ms;
     if (hipEventElapsedTime(&ms, S.ev[1], S.ev[2]) == hipSuccess) c->stats.detect_ms += ms;
     if (hipEventElapsedTime(&ms, S.ev[2], S.ev[3]) == hipSuccess) c->stats.orient_ms += ms;
@@ -1408,14 +1416,15 @@ int enqueue_chunk(sift_mi_ctx* c, int si, const uint8_t* d_frames, size_t frame_
     CHK(ensure_lane(c, arena_of(c, si)));
     CHK(reserve_chunk(c, si, B, c->plan.chunk, m));
     hipStream_t st = lane_stream(c, si);
-    HIPCHK(hipEventRecord(S.ev[0], st));
+    S.staged = c->lanes == 1;
+    if (S.staged) HIPCHK(hipEventRecord(S.ev[0], st));
     CHK(prepare_chunk(c, si, m, frame_base, B));
     // stage overlap (two-lane mode; the one-lane mode times the stages apart):
     // detection starts inside the pyramid (run_pyramid), so ev[1]..ev[2] is
     // then only the refinement
     const bool fused = pyramid && c->lanes == 2 && c->stage_overlap;
     if (pyramid) CHK(run_pyramid(c, si, d_frames, frame_pitch, stride, m, false, fused ? si : -1, si));
-    HIPCHK(hipEventRecord(S.ev[1], st));
+    if (S.staged) HIPCHK(hipEventRecord(S.ev[1], st));
     return enqueue_keypoints(c, si, m, limit, frame_base, B);
 }
 
@@ -1852,6 +1861,7 @@ int sift_mi_create(int device_ordinal, sift_mi_profile profile, sift_mi_ctx** ou
         for (auto& e : S.ev) ok = ok && hipEventCreate(&e) == hipSuccess;
         ok = ok && hipEventCreateWithFlags(&S.copied, hipEventDisableTiming) == hipSuccess;
         ok = ok && hipEventCreateWithFlags(&S.ordered, hipEventDisableTiming) == hipSuccess;
+        ok = ok && hipEventCreateWithFlags(&S.oriented, hipEventDisableTiming) == hipSuccess;
     }
     if (!ok) {
         sift_mi_destroy(c);
@@ -1889,6 +1899,7 @@ void sift_mi_destroy(sift_mi_ctx* c) {
             if (e) (void)hipEventDestroy(e);
         if (S.copied) (void)hipEventDestroy(S.copied);
         if (S.ordered) (void)hipEventDestroy(S.ordered);
+        if (S.oriented) (void)hipEventDestroy(S.oriented);
     }
     if (c->fork) (void)hipEventDestroy(c->fork);
     for (auto& lane : c->oct_ev)
