@@ -446,9 +446,9 @@ struct Slot {
     bool staged = false;
     hipEvent_t oriented = {};  // desc_first: the keypoints are oriented (fork to lane 1's stream)
     // single-chunk calls with octave overlap: refinement + orientation of the
-    // octaves below the tail run beside the tail (early; on lane 1's stream,
-    // else the aux stream), the tail octaves' candidates / extrema in their
-    // own region (cand_b, ext_b; counters at counters[4 + 2m + 0 / 1])
+    // octaves below the tail run on the aux stream beside the tail (early),
+    // the tail octaves' candidates / extrema in their own region (cand_b,
+    // ext_b; counters at counters[4 + 2m + 0 / 1])
     bool early = false;
     // one-frame early calls without a limit: the descriptors are computed in
     // keypoint index order (desc_kp) while lane 1's stream orders the
@@ -496,11 +496,7 @@ struct sift_mi_ctx {
     hipStream_t own2 = nullptr;    // compute stream of pipeline lane 1 (lane 0 runs on `stream`)
     hipStream_t aux[2] = {};       // per lane: blurs 4, 5 of each octave beside the next octave
     hipStream_t dec = nullptr;     // JPEG batch decoding: a high-priority stream (its own hardware queue)
-    // per lane: [o] octave o's G_3 done, [kTailMaxOct] aux joined,
-    // [kDetEv + o] octave o's G_5 done (detection stream), [kDetJoin] detection
-    // stream joined
-    static constexpr int kDetEv = kTailMaxOct + 1, kDetJoin = 2 * kTailMaxOct + 1;
-    hipEvent_t oct_ev[2][2 * kTailMaxOct + 2] = {};
+    hipEvent_t oct_ev[2][kTailMaxOct + 1] = {};  // per lane: octave o's G_3 done / aux joined
     int oct_overlap = 1;           // SIFT_MI_OCT_OVERLAP=0: one stream per lane (A/B, tests)
     bool lanes_busy = false;       // this call keeps both pipeline lanes busy (no octave overlap then)
     int stage_overlap = 1;         // SIFT_MI_STAGE_OVERLAP=0: detection after the whole pyramid
@@ -757,10 +753,7 @@ int launch_orient_stage(sift_mi_ctx* c, int si, const ExtRec* ext, const uint32_
 // gradient's neighbour row).
 constexpr int kBandDrift = 24, kBandPatch = 41;
 
-// One-chunk calls: octaves below the tail with at least this many pixels
-// per frame are detected on their own stream as soon as they complete
-// (smaller ones are latency-bound launches: they join the tail's detection)
-constexpr size_t kDetStreamPx = size_t(1) << 20;
+
 
 // ---------------------------------------------------------------------------
 // Stage 1: Gaussian scale space + DoG for n frames (device-resident u8)
@@ -884,10 +877,6 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
     // the seed and blur 1 ran as one pass (k_seed_pair): octave 0 continues
     // at blur 2, as the (2, 3) pair
     bool seed_pair = false;
-    // one-chunk calls (Slot::early): the stream that detects octaves [0, k_det)
-    // one by one as each octave's G_5 lands on the aux stream (set in part())
-    hipStream_t det = nullptr;
-    int k_det = 0;
     // frames [f0, f0 + nf): seed, octave chain, tail (and their detection) on
     // stream sm; ov: blurs 4, 5 of each octave on the aux stream
     auto seed = [&](uint32_t f0, uint32_t nf, hipStream_t sm) -> int {
@@ -950,12 +939,9 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
                     F.img_base = (int)f0;
                     F.profile = p.profile;
                     F.taps = p.oct_taps[s];
-                    // with a detection stream, octaves from k_det on belong to
-                    // the main stream's region (Slot::early), fused or not
-                    const bool to_b = det && o >= k_det;
-                    F.cand = to_b ? S.cand_b.p : S.cand.p;
-                    F.counter = to_b ? S.counters.p + 4 + 2 * S.m : S.counters.p + 0;
-                    F.cap = to_b ? S.bcb : S.bc;
+                    F.cand = S.cand.p;
+                    F.counter = S.counters.p + 0;
+                    F.cap = S.bc;
                     if (launch_blur_detect(p.oct_r[s], F, s45) == 0) {
                         S.fused_mask |= 1u << o;
                         launches++;
@@ -978,11 +964,6 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
             // precompute_images: D_s = G_{s+1} - G_s, the same f32 subtraction
             // the keypoint stages form where they read the DoG
             if (full) launch_dog(G, P, p.gstride(o), D, p.dstride(o), p.ow[o], p.oh[o], p.opitch[o], (int)nf, s45);
-            if (det && o < k_det) {  // this octave's extremum scan, beside the next octaves' blurs
-                HIPCHK(hipEventRecord(c->oct_ev[lane][sift_mi_ctx::kDetEv + o], s45));
-                HIPCHK(hipStreamWaitEvent(det, c->oct_ev[lane][sift_mi_ctx::kDetEv + o], 0));
-                CHK(launch_detection(c, detect_slot, f0, nf, o, o + 1, det));
-            }
         }
         return 0;
     };
@@ -990,19 +971,6 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
         const char* ee = getenv("SIFT_MI_EARLY");
         const bool early = detect_slot >= 0 && ov && o_tail > 0 && o_tail < p.n_oct && c->slot[detect_slot].bcb &&
                            !(ee && !strcmp(ee, "0"));
-        // lane 1's stream is idle in a one-chunk call on lane 0: it detects
-        // the large octaves below the tail (>= kDetStreamPx pixels) one by one
-        // as they complete, then refines and orients them while the tail
-        // kernel runs; the smaller octaves join the tail's detection on the
-        // main stream (SIFT_MI_DET_STREAM=0: every octave below the tail
-        // detected, refined and oriented on the aux stream after its last blur)
-        const char* de = getenv("SIFT_MI_DET_STREAM");
-        det = nullptr;
-        k_det = 0;
-        if (early && lane == 0 && c->lanes == 2 && !(de && !strcmp(de, "0"))) {
-            while (k_det < o_tail && p.px[k_det] >= kDetStreamPx) k_det++;
-            if (k_det > 0) det = c->own2;
-        }
         CHK(seed(f0, nf, sm));
         CHK(octaves(f0, nf, 0, o_tail, sm, ov));
         if (o_tail < p.n_oct) {
@@ -1035,27 +1003,20 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
         }
         if (early) {
             // one chunk (octave overlap): the octaves below the tail are
-            // detected, refined and oriented beside the tail kernel (on the
-            // detection stream, else on the aux stream); the tail octaves,
-            // after it, into a region of their own (Slot::early;
-            // SIFT_MI_EARLY=0: off)
+            // detected, refined and oriented on the aux stream beside the tail
+            // kernel; the tail octaves, after it, into a region of their own
+            // (Slot::early; SIFT_MI_EARLY=0: off).  Tried and dropped: the
+            // large octaves detected on lane 1's stream as each one's G_5
+            // lands (0.634 vs 0.613-0.624 ms per 1080p frame: the scan then
+            // competes with the blur chain for HBM instead of filling the
+            // idle chip beside the one-workgroup tail kernel)
             Slot& S = c->slot[detect_slot];
             uint32_t* cnt = S.counters.p;
             uint32_t* cb = cnt + 4 + 2 * S.m;
-            if (det) {
-                // octaves [0, k_det): detected on det inside octaves()
-                CHK(launch_refine_stage(c, detect_slot, S.cand.p, cnt + 0, S.bc, S.ext.p, cnt + 1, S.be, det));
-                CHK(launch_orient_stage(c, detect_slot, S.ext.p, cnt + 1, S.be, S.bk, det));
-                // the smaller octaves' G_5 (aux) before their detection on sm
-                HIPCHK(hipEventRecord(c->oct_ev[lane][kTailMaxOct], aux));
-                HIPCHK(hipStreamWaitEvent(sm, c->oct_ev[lane][kTailMaxOct], 0));
-            } else {
-                CHK(launch_detection(c, detect_slot, f0, nf, 0, o_tail, aux));
-                CHK(launch_refine_stage(c, detect_slot, S.cand.p, cnt + 0, S.bc, S.ext.p, cnt + 1, S.be, aux));
-                CHK(launch_orient_stage(c, detect_slot, S.ext.p, cnt + 1, S.be, S.bk, aux));
-            }
-            const int ob = det ? k_det : o_tail;  // first octave of the main stream's region
-            CHK(launch_detection(c, detect_slot, f0, nf, ob, p.n_oct, sm, S.cand_b.p, cb + 0, S.bcb));
+            CHK(launch_detection(c, detect_slot, f0, nf, 0, o_tail, aux));
+            CHK(launch_refine_stage(c, detect_slot, S.cand.p, cnt + 0, S.bc, S.ext.p, cnt + 1, S.be, aux));
+            CHK(launch_orient_stage(c, detect_slot, S.ext.p, cnt + 1, S.be, S.bk, aux));
+            CHK(launch_detection(c, detect_slot, f0, nf, o_tail, p.n_oct, sm, S.cand_b.p, cb + 0, S.bcb));
             CHK(launch_refine_stage(c, detect_slot, S.cand_b.p, cb + 0, S.bcb, S.ext_b.p, cb + 1, S.bcb, sm));
             CHK(launch_orient_stage(c, detect_slot, S.ext_b.p, cb + 1, S.bcb, S.bk, sm));
             S.early = true;
@@ -1065,14 +1026,9 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
             CHK(launch_detection(c, detect_slot, f0, nf, 0, o_tail, ov && o_tail > 0 ? aux : sm));
             CHK(launch_detection(c, detect_slot, f0, nf, o_tail, p.n_oct, sm));
         }
-        if (ov && o_tail > 0 && !det) {  // join: the aux stream's work before what follows on sm
+        if (ov && o_tail > 0) {  // join: the aux stream's work before what follows on sm
             HIPCHK(hipEventRecord(c->oct_ev[lane][kTailMaxOct], aux));
             HIPCHK(hipStreamWaitEvent(sm, c->oct_ev[lane][kTailMaxOct], 0));
-        }
-        if (det) {
-            HIPCHK(hipEventRecord(c->oct_ev[lane][sift_mi_ctx::kDetJoin], det));
-            HIPCHK(hipStreamWaitEvent(sm, c->oct_ev[lane][sift_mi_ctx::kDetJoin], 0));
-            det = nullptr;
         }
         return 0;
     };

@@ -329,12 +329,12 @@ def test_single_chunk_graph_replay(pkg, ctx, oracle, monkeypatch, fetch):
     c.close()
 
 
-@pytest.mark.parametrize("knob", ["SIFT_MI_EARLY", "SIFT_MI_DET_STREAM", "SIFT_MI_DESC_FIRST"])
+@pytest.mark.parametrize("knob", ["SIFT_MI_EARLY", "SIFT_MI_DESC_FIRST"])
 @pytest.mark.parametrize("profile", [0, 1])
 def test_single_chunk_paths_equal(pkg, monkeypatch, knob, profile):
     """One-chunk calls take latency paths of their own -- the octaves below
-    the tail detected (one by one, on lane 1's stream), refined and oriented
-    beside the tail kernel with the tail octaves in a region of their own
+    the tail detected, refined and oriented on the aux stream beside the tail
+    kernel with the tail octaves in a region of their own
     (Slot::early), and the descriptors computed in keypoint index order beside
     the ordering stage, then gathered (Slot::desc_first) -- whose results must
     equal the general path's (the knob = 0) bit for bit, incl. keys.  Each
