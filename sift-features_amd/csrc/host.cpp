@@ -826,6 +826,10 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
         const char* e = getenv("SIFT_MI_TAIL");
         if (!(e && !strcmp(e, "0")) && p.n_oct <= kTailMaxOct)
             o_tail = tail_octave_start(p.ow.data(), p.oh.data(), p.n_oct, p.oct_r);
+        // SIFT_MI_TAIL_SHIFT=k (A/B knob): the tail starts k octaves later
+        // (smaller tail octaves fit as well; the octaves before run per blur)
+        if (const char* ts = getenv("SIFT_MI_TAIL_SHIFT"))
+            o_tail = std::min(p.n_oct, o_tail + std::max(0, atoi(ts)));
     }
     uint64_t bytes = p.algo_bytes_per_frame;  // per frame, SURVEY.md 8(d)
     if (c->band_restricted) {
@@ -910,28 +914,6 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
         return 0;
     };
     // octaves [o0, o1) of frames [f0, f0 + nf)
-    // SIFT_MI_FUSED_DEFER=1 (A/B knob): octave o's fused blur 5 + detection is
-    // enqueued on the aux stream after octave o + 1's G_3 is done, so its
-    // long-running waves do not hold the CUs the main stream's next blur needs
-    const char* fde = getenv("SIFT_MI_FUSED_DEFER");
-    const bool defer = fde && !strcmp(fde, "1");
-    struct Deferred {
-        bool on = false;
-        int o = 0;
-        BlurDetectLaunch F{};
-        BlurLaunch B{};
-    } pend;
-    auto flush = [&]() -> int {  // the deferred blur 5 on the aux stream (unfused if the pass declines)
-        if (!pend.on) return 0;
-        pend.on = false;
-        launches++;
-        if (launch_blur_detect(p.oct_r[kImagesPerOctave - 1], pend.F, aux) == 0) {
-            c->slot[cand_slot].fused_mask |= 1u << pend.o;
-            return 0;
-        }
-        if (launch_blur(p.oct_r[kImagesPerOctave - 1], pend.B, aux)) return fail(SIFT_MI_EUNSUPPORTED, "octave blur radius");
-        return 0;
-    };
     auto octaves = [&](uint32_t f0, uint32_t nf, int o0, int o1, hipStream_t sm, bool ov) -> int {
         hipStream_t s45 = sm;
         for (int o = o0; o < o1; o++) {
@@ -944,7 +926,6 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
                     HIPCHK(hipEventRecord(c->oct_ev[lane][o], sm));
                     HIPCHK(hipStreamWaitEvent(aux, c->oct_ev[lane][o], 0));
                     s45 = aux;
-                    CHK(flush());  // the previous octave's deferred blur 5
                 }
                 const BlurLaunch B = blur_launch(o, s, f0, nf);
                 // blur 5 and the octave's detection in one pass (k_blur_detect:
@@ -965,13 +946,6 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
                     F.cand = S.cand.p;
                     F.counter = S.counters.p + 0;
                     F.cap = S.bc;
-                    if (defer && ov && o + 1 < o1) {
-                        pend.on = true;
-                        pend.o = o;
-                        pend.F = F;
-                        pend.B = B;
-                        continue;
-                    }
                     if (launch_blur_detect(p.oct_r[s], F, s45) == 0) {
                         S.fused_mask |= 1u << o;
                         launches++;
@@ -995,7 +969,6 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
             // the keypoint stages form where they read the DoG
             if (full) launch_dog(G, P, p.gstride(o), D, p.dstride(o), p.ow[o], p.oh[o], p.opitch[o], (int)nf, s45);
         }
-        CHK(flush());
         return 0;
     };
     auto part = [&](uint32_t f0, uint32_t nf, hipStream_t sm, bool ov) -> int {
@@ -1792,16 +1765,8 @@ bool take_streams(int dev, hipStream_t (&out)[kCtxStreams]) {
             return true;
         }
     }
-    // SIFT_MI_LANE_PRIO=high (A/B knob): the two lane streams at the greatest
-    // priority, so a lane's blur chain is dispatched ahead of its aux stream's
-    // long-running blur 5 + detection waves
-    int least = 0, greatest = 0;
-    const char* lp = getenv("SIFT_MI_LANE_PRIO");
-    const bool lane_hi = lp && !strcmp(lp, "high") && hipDeviceGetStreamPriorityRange(&least, &greatest) == hipSuccess;
     for (int i = 0; i < kCtxStreams; i++) {
-        const hipError_t e = (lane_hi && i < 2) ? hipStreamCreateWithPriority(&out[i], hipStreamNonBlocking, greatest)
-                                                : hipStreamCreateWithFlags(&out[i], hipStreamNonBlocking);
-        if (e != hipSuccess) {
+        if (hipStreamCreateWithFlags(&out[i], hipStreamNonBlocking) != hipSuccess) {
             for (int k = 0; k < i; k++) (void)hipStreamDestroy(out[k]);
             return false;
         }

@@ -30,21 +30,13 @@ def _frame(name, seed=7):
     return synth.frame(w, h, seed)
 
 
-def _set_fused(monkeypatch, fused):
-    """"force" / "0": SIFT_MI_FUSED_DETECT; "defer": forced and enqueued after
-    the next octave's G_3 (SIFT_MI_FUSED_DEFER=1)."""
-    monkeypatch.setenv("SIFT_MI_FUSED_DETECT", "force" if fused == "defer" else fused)
-    if fused == "defer":
-        monkeypatch.setenv("SIFT_MI_FUSED_DEFER", "1")
-
-
-@pytest.mark.parametrize("fused", ["force", "0", "defer"])
+@pytest.mark.parametrize("fused", ["force", "0"])
 @pytest.mark.parametrize("profile", [0, 1])
 @pytest.mark.parametrize("name", SHAPES)
 def test_batch_pyramid_bit_exact(pkg, oracle, monkeypatch, fused, profile, name):
     """Every Gaussian plane the batch path leaves in its arena (G_5 from
     k_blur_detect when fused) equals the oracle's, bit for bit."""
-    _set_fused(monkeypatch, fused)
+    monkeypatch.setenv("SIFT_MI_FUSED_DETECT", fused)
     img = _frame(name)
     c = pkg.Context(0, pkg.OpenCVProcessing if profile == 0 else pkg.ImageprocProcessing)
     c.sift(img)
@@ -57,14 +49,14 @@ def test_batch_pyramid_bit_exact(pkg, oracle, monkeypatch, fused, profile, name)
     c.close()
 
 
-@pytest.mark.parametrize("fused", ["force", "0", "defer"])
+@pytest.mark.parametrize("fused", ["force", "0"])
 @pytest.mark.parametrize("profile", [0, 1])
 @pytest.mark.parametrize("name", SHAPES + ["noise"])
 def test_fused_detect_parity(pkg, oracle, monkeypatch, fused, profile, name):
     """Keypoints (count, emission order, values) and descriptors vs the
     oracle with and without the fused pass."""
     from test_gpu_parity import assert_parity
-    _set_fused(monkeypatch, fused)
+    monkeypatch.setenv("SIFT_MI_FUSED_DETECT", fused)
     img = _frame(name)
     c = pkg.Context(0, pkg.OpenCVProcessing if profile == 0 else pkg.ImageprocProcessing)
     res = c.sift(img)
