@@ -914,16 +914,21 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
         return 0;
     };
     // octaves [o0, o1) of frames [f0, f0 + nf)
+    // the launch that writes an octave's G_3 signals the aux stream's event
+    // itself (SIFT_MI_EXT_EVENTS=0: a separate event record after it)
+    const char* xe = getenv("SIFT_MI_EXT_EVENTS");
+    const bool ext_events = !(xe && !strcmp(xe, "0"));
     auto octaves = [&](uint32_t f0, uint32_t nf, int o0, int o1, hipStream_t sm, bool ov) -> int {
         hipStream_t s45 = sm;
         for (int o = o0; o < o1; o++) {
+            bool g3_signalled = false;
             float* G = p.gauss(o, lane) + (size_t)f0 * p.gstride(o);
             float* D = p.dog(o, lane) + (size_t)f0 * p.dstride(o);
             const size_t P = p.P[o];
             // octave 0 after k_seed_pair starts at blur 2
             for (int s = (o == 0 && seed_pair) ? 2 : 1; s < kImagesPerOctave; s++) {
                 if (s == 4 && ov) {
-                    HIPCHK(hipEventRecord(c->oct_ev[lane][o], sm));
+                    if (!g3_signalled) HIPCHK(hipEventRecord(c->oct_ev[lane][o], sm));
                     HIPCHK(hipStreamWaitEvent(aux, c->oct_ev[lane][o], 0));
                     s45 = aux;
                 }
@@ -955,14 +960,28 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
                 // G_1, G_2 in one pass where the pair kernel applies
                 // (k_blur2_strip: G_1 never read back from HBM); after the
                 // seed pair, G_2, G_3 (and the next octave's base) instead
-                if ((s == 1 || (s == 2 && o == 0 && seed_pair)) &&
-                    launch_blur_pair(p.oct_r[s], p.oct_r[s + 1], B, blur_launch(o, s + 1, f0, nf), sm) == 0) {
+                // (the launch that writes G_3: blur 3, or the octave-0 (2, 3) pair)
+                const bool g3 = ov && ext_events && (s == 3 || (s == 2 && o == 0 && seed_pair));
+                if (g3) set_launch_done_event(c->oct_ev[lane][o]);
+                int rc = 1;
+                if (s == 1 || (s == 2 && o == 0 && seed_pair))
+                    rc = launch_blur_pair(p.oct_r[s], p.oct_r[s + 1], B, blur_launch(o, s + 1, f0, nf), sm);
+                if (rc == 0) {
+                    g3_signalled = g3 && !launch_done_pending();
+                    set_launch_done_event(nullptr);
                     launches++;
                     s++;
                     continue;
                 }
-                if (launch_blur(p.oct_r[s], B, s >= 4 ? s45 : sm))
+                // a declined pair launched nothing: the event is still pending
+                // for blur s itself only if that is blur 3
+                if (g3 && s != 3) set_launch_done_event(nullptr);
+                if (launch_blur(p.oct_r[s], B, s >= 4 ? s45 : sm)) {
+                    set_launch_done_event(nullptr);
                     return fail(SIFT_MI_EUNSUPPORTED, "octave blur radius");
+                }
+                g3_signalled = g3_signalled || (g3 && s == 3 && !launch_done_pending());
+                set_launch_done_event(nullptr);
                 launches++;
             }
             // precompute_images: D_s = G_{s+1} - G_s, the same f32 subtraction

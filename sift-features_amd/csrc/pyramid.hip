@@ -24,6 +24,8 @@
 //                 (nearest 1/2 = pixel (2x, 2y)).
 // The stage is HBM-bound: per octave pixel the reference materialises 6 G + 5 D
 // images (44 B); see DESIGN.md for the roofline accounting.
+#include <hip/hip_ext.h>
+
 #include "sift_common.h"
 #include "sift_kernels.h"
 
@@ -32,6 +34,37 @@
 #include <cstring>
 
 namespace siftmi {
+
+// The next kernel a launcher below enqueues from this host thread signals
+// t_done on completion (hipExtLaunchKernel's stop event, no marker packet of
+// its own: a marker between two kernels costs ~7 us of the stream's
+// timeline).
+static thread_local hipEvent_t t_done = nullptr;
+void set_launch_done_event(hipEvent_t e) { t_done = e; }
+bool launch_done_pending() { return t_done != nullptr; }
+
+template <class F, class... A>
+static void klaunch(F kernel, dim3 grid, dim3 block, hipStream_t st, A... args) {
+    if (t_done) {
+        hipEvent_t e = t_done;
+        t_done = nullptr;
+        // hipExtLaunchKernelGGL's packing, with its status checked: on failure
+        // the kernel goes out plainly and e is recorded after it
+        auto tup_ = std::tuple<A...>{args...};
+        auto tup = validateArgsCountType(kernel, tup_);
+        void* kargs[sizeof...(A) > 0 ? sizeof...(A) : 1];
+        pArgs<0>(tup, kargs);
+        if (hipExtLaunchKernel(reinterpret_cast<void*>(kernel), grid, block, kargs, 0, st, nullptr, e, 0) !=
+            hipSuccess) {
+            (void)hipGetLastError();
+            hipLaunchKernelGGL(kernel, grid, block, 0, st, args...);
+            (void)hipEventRecord(e, st);
+        }
+    } else {
+        hipLaunchKernelGGL(kernel, grid, block, 0, st, args...);
+    }
+}
+
 
 // ---------------------------------------------------------------------------
 // Tile geometry.  Input window columns [x0 - HWL, x0 + TW + HWL) with
@@ -1681,11 +1714,11 @@ static void launch_blur_r(const BlurLaunch& L, hipStream_t st) {
     if (ty1 <= ty0) return;
     dim3 grid((L.W + G::TW - 1) / G::TW, ty1 - ty0, L.n_img);
     if (L.profile == kProfileImageproc)
-        hipLaunchKernelGGL((k_blur<R, TH, kProfileImageproc>), grid, dim3(256), 0, st, L.src, L.src_img_stride, L.dst,
+        klaunch((k_blur<R, TH, kProfileImageproc>), grid, dim3(256), st, L.src, L.src_img_stride, L.dst,
                            L.dst_img_stride, L.dog, L.dog_img_stride, L.nxt, L.nxt_img_stride, L.pitch_n, L.wn, L.hn,
                            L.W, L.H, L.pitch, L.taps, ty0);
     else
-        hipLaunchKernelGGL((k_blur<R, TH, kProfileOpenCV>), grid, dim3(256), 0, st, L.src, L.src_img_stride, L.dst,
+        klaunch((k_blur<R, TH, kProfileOpenCV>), grid, dim3(256), st, L.src, L.src_img_stride, L.dst,
                            L.dst_img_stride, L.dog, L.dog_img_stride, L.nxt, L.nxt_img_stride, L.pitch_n, L.wn, L.hn,
                            L.W, L.H, L.pitch, L.taps, ty0);
 }
@@ -1694,11 +1727,11 @@ template <int R, int P>
 static void launch_blur_strip_rp(const BlurLaunch& L, dim3 grid, int ya, int yb, int seg, hipStream_t st) {
     using G = StripGeom<R>;
     if (L.nxt)
-        hipLaunchKernelGGL((k_blur_strip<R, P, true>), grid, dim3(64 * G::NW), 0, st, L.src, L.src_img_stride, L.dst,
+        klaunch((k_blur_strip<R, P, true>), grid, dim3(64 * G::NW), st, L.src, L.src_img_stride, L.dst,
                            L.dst_img_stride, L.nxt, L.nxt_img_stride, L.pitch_n, L.wn, L.hn, L.W, L.H, L.pitch,
                            L.taps, ya, yb, seg);
     else
-        hipLaunchKernelGGL((k_blur_strip<R, P, false>), grid, dim3(64 * G::NW), 0, st, L.src, L.src_img_stride,
+        klaunch((k_blur_strip<R, P, false>), grid, dim3(64 * G::NW), st, L.src, L.src_img_stride,
                            L.dst, L.dst_img_stride, L.nxt, L.nxt_img_stride, L.pitch_n, L.wn, L.hn, L.W, L.H,
                            L.pitch, L.taps, ya, yb, seg);
 }
@@ -1763,19 +1796,19 @@ static void launch_blur2_rr(const BlurLaunch& A, const BlurLaunch& B, hipStream_
     const int nseg = (A.H + seg - 1) / seg;
     const dim3 grid(strips, nseg, A.n_img);
     if (B.nxt) {  // blurs 2, 3 of octave 0: B writes the next octave's base
-        hipLaunchKernelGGL((k_blur2_strip<Ra, Rb, false, P, true>), grid, dim3(256), 0, st, A.src, A.src_img_stride,
+        klaunch((k_blur2_strip<Ra, Rb, false, P, true>), grid, dim3(256), st, A.src, A.src_img_stride,
                            A.dst, B.dst, B.nxt, B.nxt_img_stride, B.pitch_n, B.wn, B.hn, A.W, A.H, A.pitch, A.taps,
                            B.taps, 0, A.H, seg);
     } else if constexpr (P == kProfileImageproc) {
-        hipLaunchKernelGGL((k_blur2_strip<Ra, Rb, false, P>), grid, dim3(256), 0, st, A.src, A.src_img_stride, A.dst,
+        klaunch((k_blur2_strip<Ra, Rb, false, P>), grid, dim3(256), st, A.src, A.src_img_stride, A.dst,
                            B.dst, A.nxt, A.nxt_img_stride, A.pitch_n, A.wn, A.hn, A.W, A.H, A.pitch, A.taps, B.taps,
                            0, A.H, seg);
     } else if (A.nxt) {
-        hipLaunchKernelGGL((k_blur2_strip<Ra, Rb, true>), grid, dim3(256), 0, st, A.src, A.src_img_stride, A.dst,
+        klaunch((k_blur2_strip<Ra, Rb, true>), grid, dim3(256), st, A.src, A.src_img_stride, A.dst,
                            B.dst, A.nxt, A.nxt_img_stride, A.pitch_n, A.wn, A.hn, A.W, A.H, A.pitch, A.taps, B.taps,
                            0, A.H, seg);
     } else {
-        hipLaunchKernelGGL((k_blur2_strip<Ra, Rb, false>), grid, dim3(256), 0, st, A.src, A.src_img_stride, A.dst,
+        klaunch((k_blur2_strip<Ra, Rb, false>), grid, dim3(256), st, A.src, A.src_img_stride, A.dst,
                            B.dst, A.nxt, A.nxt_img_stride, A.pitch_n, A.wn, A.hn, A.W, A.H, A.pitch, A.taps, B.taps,
                            0, A.H, seg);
     }
@@ -1863,7 +1896,7 @@ static void launch_seed_r(const SeedLaunch& L, hipStream_t st) {
     const int ty1 = L.y1 > L.y0 ? std::min(tiles_y, (L.y1 + G::TH - 1) / G::TH) : tiles_y;
     if (ty1 <= ty0) return;
     dim3 grid((L.W + G::TW - 1) / G::TW, ty1 - ty0, L.n_img);
-    hipLaunchKernelGGL((k_seed<R, TH>), grid, dim3(256), 0, st, L.frames, L.frame_pitch, L.row_stride, L.sh, L.sw, L.tab,
+    klaunch((k_seed<R, TH>), grid, dim3(256), st, L.frames, L.frame_pitch, L.row_stride, L.sh, L.sw, L.tab,
                        L.dst, L.dst_img_stride, L.W, L.H, L.pitch, L.taps, ty0);
 }
 
@@ -1872,7 +1905,7 @@ static void launch_seed_ip_r(const SeedLaunch& L, hipStream_t st) {
     constexpr int TH = 32;
     using G = BlurGeom<R, TH>;
     dim3 grid((L.W + G::TW - 1) / G::TW, (L.H + G::TH - 1) / G::TH, L.n_img);
-    hipLaunchKernelGGL((k_seed_ip<R, TH>), grid, dim3(256), 0, st, L.frames, L.frame_pitch, L.row_stride, L.sh, L.sw,
+    klaunch((k_seed_ip<R, TH>), grid, dim3(256), st, L.frames, L.frame_pitch, L.row_stride, L.sh, L.sw,
                        L.iptab, L.dst, L.dst_img_stride, L.W, L.H, L.pitch, L.taps);
 }
 
@@ -1897,11 +1930,11 @@ int launch_seed(int R, const SeedLaunch& L, hipStream_t st) {
         const int nseg = (rows + seg - 1) / seg;
         const dim3 grid(strips, nseg, L.n_img);
         if (ip)
-            hipLaunchKernelGGL((k_seed_strip<3, kProfileImageproc>), grid, dim3(256), 0, st, L.frames, L.frame_pitch,
+            klaunch((k_seed_strip<3, kProfileImageproc>), grid, dim3(256), st, L.frames, L.frame_pitch,
                                L.row_stride, L.sh, L.sw, L.dst, L.dst_img_stride, L.W, L.H, L.pitch, L.taps, ya, yb,
                                seg);
         else
-            hipLaunchKernelGGL((k_seed_strip<5, kProfileOpenCV>), grid, dim3(256), 0, st, L.frames, L.frame_pitch,
+            klaunch((k_seed_strip<5, kProfileOpenCV>), grid, dim3(256), st, L.frames, L.frame_pitch,
                                L.row_stride, L.sh, L.sw, L.dst, L.dst_img_stride, L.W, L.H, L.pitch, L.taps, ya, yb,
                                seg);
         return 0;
@@ -1926,7 +1959,7 @@ static void launch_seed_pair_rr(const SeedLaunch& S, const BlurLaunch& B, hipStr
     const int strips = (S.W + Q::TWO - 1) / Q::TWO;
     const int seg = strip_segment_rows(S.H, (long)strips * S.n_img, 8192);  // as the (2, 3) pair
     const int nseg = (S.H + seg - 1) / seg;
-    hipLaunchKernelGGL((k_seed_pair<Ra, Rb, P>), dim3(strips, nseg, S.n_img), dim3(256), 0, st, S.frames,
+    klaunch((k_seed_pair<Ra, Rb, P>), dim3(strips, nseg, S.n_img), dim3(256), st, S.frames,
                        S.frame_pitch, S.row_stride, S.sh, S.sw, S.dst, B.dst, S.dst_img_stride, S.W, S.H, S.pitch,
                        S.taps, B.taps, 0, S.H, seg);
 }
@@ -2234,9 +2267,9 @@ int tail_octave_start(const int* ow, const int* oh, int n_oct, const int* radii)
 void launch_octave_tail(const TailLaunch& L, hipStream_t st) {
     if (L.o0 >= L.n_oct || L.n_img <= 0) return;
     if (L.profile == kProfileImageproc)
-        hipLaunchKernelGGL(k_octave_tail<kProfileImageproc>, dim3(L.n_img), dim3(1024), 0, st, L);
+        klaunch(k_octave_tail<kProfileImageproc>, dim3(L.n_img), dim3(1024), st, L);
     else
-        hipLaunchKernelGGL(k_octave_tail<kProfileOpenCV>, dim3(L.n_img), dim3(1024), 0, st, L);
+        klaunch(k_octave_tail<kProfileOpenCV>, dim3(L.n_img), dim3(1024), st, L);
 }
 
 // ---------------------------------------------------------------------------
@@ -2259,7 +2292,7 @@ void launch_dog(const float* gauss, size_t plane, size_t g_img_stride, float* do
                 int pitch, int n_img, hipStream_t st) {
     (void)W;
     const size_t n4 = (size_t)pitch * H / 4;  // pitch: a multiple of 64 floats
-    hipLaunchKernelGGL(k_dog, dim3((unsigned)((n4 + 255) / 256), kDogPerOctave, n_img), dim3(256), 0, st, gauss,
+    klaunch(k_dog, dim3((unsigned)((n4 + 255) / 256), kDogPerOctave, n_img), dim3(256), st, gauss,
                        plane, g_img_stride, dog, dog_img_stride, n4);
 }
 
@@ -2295,13 +2328,13 @@ __global__ void k_resize_nearest_f32(const float* __restrict__ src, int sw, cons
 void launch_resize_linear_f32(const float* src, int sw, int sh, const ResizeTab& tab, float* dst, int dw, int dh,
                               hipStream_t st) {
     dim3 grid((dw + 63) / 64, (dh + 3) / 4, 1);
-    hipLaunchKernelGGL(k_resize_linear_f32, grid, dim3(256), 0, st, src, sw, sh, tab, dst, dw, dh);
+    klaunch(k_resize_linear_f32, grid, dim3(256), st, src, sw, sh, tab, dst, dw, dh);
 }
 
 void launch_resize_nearest_f32(const float* src, int sw, const int* xofs, const int* yofs, float* dst, int dw, int dh,
                                hipStream_t st) {
     dim3 grid((dw + 63) / 64, (dh + 3) / 4, 1);
-    hipLaunchKernelGGL(k_resize_nearest_f32, grid, dim3(256), 0, st, src, sw, xofs, yofs, dst, dw, dh);
+    klaunch(k_resize_nearest_f32, grid, dim3(256), st, src, sw, xofs, yofs, dst, dw, dh);
 }
 
 // image::imageops::resize (Imageproc profile): vertical_sample into tmp
@@ -2331,9 +2364,9 @@ __global__ void k_ip_hsample(const float* __restrict__ tmp, int sw, const int* _
 
 void launch_ip_resize_f32(const float* src, int sw, int sh, const int* xl, const float* xw, int xtaps, const int* yl,
                           const float* yw, int ytaps, float* tmp, float* dst, int dw, int dh, hipStream_t st) {
-    hipLaunchKernelGGL(k_ip_vsample, dim3((sw + 63) / 64, (dh + 3) / 4, 1), dim3(256), 0, st, src, sw, sh, yl, yw,
+    klaunch(k_ip_vsample, dim3((sw + 63) / 64, (dh + 3) / 4, 1), dim3(256), st, src, sw, sh, yl, yw,
                        ytaps, tmp, dh);
-    hipLaunchKernelGGL(k_ip_hsample, dim3((dw + 63) / 64, (dh + 3) / 4, 1), dim3(256), 0, st, tmp, sw, xl, xw, xtaps,
+    klaunch(k_ip_hsample, dim3((dw + 63) / 64, (dh + 3) / 4, 1), dim3(256), st, tmp, sw, xl, xw, xtaps,
                        dst, dw, dh);
 }
 

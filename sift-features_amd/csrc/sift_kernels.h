@@ -111,6 +111,11 @@ int tail_octave_start(const int* ow, const int* oh, int n_oct, const int* radii)
 void launch_octave_tail(const TailLaunch& L, hipStream_t st);
 
 // pyramid.hip
+// The next kernel a pyramid launcher enqueues from this host thread signals
+// e on completion (no marker packet of its own); launch_done_pending() is
+// true while no launch has taken it (the caller then clears it and records e)
+void set_launch_done_event(hipEvent_t e);
+bool launch_done_pending();
 int launch_blur(int radius, const BlurLaunch& L, hipStream_t st);
 // two consecutive blurs of an octave (A then B, B.src == A.dst) in one pass;
 // -1 when the pair kernel does not apply (the caller launches them singly)
