@@ -916,8 +916,12 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
     // octaves [o0, o1) of frames [f0, f0 + nf)
     // SIFT_MI_EXT_EVENTS=1: the launch that writes an octave's G_3 signals
     // the aux stream's event itself (default: a separate event record after it)
+    // (not under stream capture: a kernel's stop event does not become a
+    // graph dependency, so the captured aux work would not wait)
     const char* xe = getenv("SIFT_MI_EXT_EVENTS");
-    const bool ext_events = xe && !strcmp(xe, "1");
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    const bool ext_events = xe && !strcmp(xe, "1") && hipStreamIsCapturing(st, &cap) == hipSuccess &&
+                            cap == hipStreamCaptureStatusNone;
     auto octaves = [&](uint32_t f0, uint32_t nf, int o0, int o1, hipStream_t sm, bool ov) -> int {
         hipStream_t s45 = sm;
         for (int o = o0; o < o1; o++) {
