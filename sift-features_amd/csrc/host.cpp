@@ -826,10 +826,6 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
         const char* e = getenv("SIFT_MI_TAIL");
         if (!(e && !strcmp(e, "0")) && p.n_oct <= kTailMaxOct)
             o_tail = tail_octave_start(p.ow.data(), p.oh.data(), p.n_oct, p.oct_r);
-        // SIFT_MI_TAIL_SHIFT=k (A/B knob): the tail starts k octaves later
-        // (smaller tail octaves fit as well; the octaves before run per blur)
-        if (const char* ts = getenv("SIFT_MI_TAIL_SHIFT"))
-            o_tail = std::min(p.n_oct, o_tail + std::max(0, atoi(ts)));
     }
     uint64_t bytes = p.algo_bytes_per_frame;  // per frame, SURVEY.md 8(d)
     if (c->band_restricted) {
@@ -914,13 +910,15 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
         return 0;
     };
     // octaves [o0, o1) of frames [f0, f0 + nf)
-    // SIFT_MI_EXT_EVENTS=1: the launch that writes an octave's G_3 signals
-    // the aux stream's event itself (default: a separate event record after it)
+    // the launch that writes an octave's G_3 signals the aux stream's event
+    // itself: no marker packet on the main stream (SIFT_MI_EXT_EVENTS=0: a
+    // separate event record after it; 0.626 / 0.629 vs 0.616 / 0.619 ms per
+    // 1080p frame)
     // (not under stream capture: a kernel's stop event does not become a
     // graph dependency, so the captured aux work would not wait)
     const char* xe = getenv("SIFT_MI_EXT_EVENTS");
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    const bool ext_events = xe && !strcmp(xe, "1") && hipStreamIsCapturing(st, &cap) == hipSuccess &&
+    const bool ext_events = !(xe && !strcmp(xe, "0")) && hipStreamIsCapturing(st, &cap) == hipSuccess &&
                             cap == hipStreamCaptureStatusNone;
     auto octaves = [&](uint32_t f0, uint32_t nf, int o0, int o1, hipStream_t sm, bool ov) -> int {
         hipStream_t s45 = sm;
