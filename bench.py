@@ -19,14 +19,18 @@ for 1080p), not the "5 octaves" wording of configs[1].
 
 `value` = keypoints (each with its descriptor) produced by all ranks per
 second, max-over-ranks wall time between barriers.
-`roofline` = the pyramid stage (seed + blur/DoG kernels; HBM-bound): its
-algorithmic bytes W*H + 44*sum(P_o) per frame (u8 read once,
-G_0..G_5 and D_0..D_4 written once; the batch path writes only G_0..G_5 and
-forms D where detection reads it -- its kernels' actual HBM traffic is the
-PMC `traffic` field) / its HIP-event time on the
+`roofline` = the pyramid stage (seed + blur kernels; HBM-bound): SURVEY.md
+8(d)'s algorithmic bytes W*H + 44*sum(P_o) per frame (u8 read once, G_0..G_5
+and D_0..D_4 written once -- nothing else; the batch path writes only
+G_0..G_5 and forms D where detection reads it, and its kernels' actual HBM
+traffic is the PMC `traffic` field) / the stage's HIP-event time on the
 kernels' stream, vs 8 TB/s, from a second pass of the same steps with the
 chunks serialised (one pipeline lane) so the stage runs alone;
-`stage_ms_per_step` comes from that pass too.  `cpu_baseline` = the CPU oracle (a C port of
+`stage_ms_per_step` comes from that pass too.  The stage's time includes the
+extremum scan of the octaves detected with their blur 5 (k_blur_detect);
+`roofline_fused_stage` states the same time against the yardstick plus what
+the reference's scan reads for those octaves (20 B per octave pixel), a
+separately labelled figure.  `cpu_baseline` = the CPU oracle (a C port of
 src/lib.rs, 1 thread) on a bounded sample of the same frames, rank 0 at N=1;
 `cpu_baseline_all_cores` the same with one frame per thread on the host's
 CPU share (OMP_NUM_THREADS, 16 per GPU on the GPU pool).
@@ -315,6 +319,8 @@ def main():
     pyr_gbs = st["pyramid_bytes"] / (st["pyramid_ms"] * 1e-3) / 1e9 if st["pyramid_ms"] > 0 else 0.0
     per_launch_bytes = st["pyramid_bytes"] / max(1, st["pyramid_launches"])
     per_launch_ms = st["pyramid_ms"] / max(1, st["pyramid_launches"])
+    fused_bytes = st["pyramid_bytes"] + st["pyramid_scan_bytes"]
+    fused_gbs = fused_bytes / (st["pyramid_ms"] * 1e-3) / 1e9 if st["pyramid_ms"] > 0 else 0.0
 
     # the same steps with the results copied to host arrays (PCIe-inclusive)
     host_fetch = None
@@ -440,11 +446,19 @@ def main():
             "roofline": {"bound": "hbm", "achieved": pyr_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                          "frac": pyr_gbs / HBM_PEAK_GBS, "traffic": traffic,
                          "traffic_source": traffic_src,
-                         "kernel": "pyramid stage (k_seed_pair + k_blur2_strip + k_blur_strip<R> + k_octave_tail, and "
-                                   "k_blur_detect: blur 5 with the extremum scan of the octaves it fuses, whose "
-                                   "yardstick adds the 5 DoG planes the reference's scan reads), rank 0",
+                         "kernel": "pyramid stage (k_seed_pair + k_blur2_strip + k_blur_strip<R> + k_octave_tail + "
+                                   "k_blur_detect, whose time includes the extremum scan of the octaves it fuses), "
+                                   "rank 0; yardstick SURVEY.md 8(d) W*H + 44*sum(P_o) per frame",
+                         "algorithmic_bytes_per_frame": st["pyramid_bytes"] / max(1, st["frames"]),
                          "algorithmic_bytes_per_launch": per_launch_bytes,
+                         "launches": st["pyramid_launches"],
                          "avg_launch_ms": per_launch_ms},
+            "roofline_fused_stage": {"achieved": fused_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
+                                     "frac": fused_gbs / HBM_PEAK_GBS,
+                                     "bytes_per_launch": fused_bytes / max(1, st["pyramid_launches"]),
+                                     "note": "the same stage time against the 8(d) yardstick plus what the "
+                                             "reference's extremum scan reads for the octaves k_blur_detect "
+                                             "scans inside the stage (5 DoG planes, 20 B per octave pixel)"},
             "cpu_baseline": cpu,
             "cpu_baseline_all_cores": cpu_all,
             "keypoint_stages": kp_stages,

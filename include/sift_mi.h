@@ -151,11 +151,38 @@ int sift_mi_device_results(sift_mi_ctx* ctx, const sift_mi_keypoint** d_kps, con
 /* Validation read-back (extension, not the crate): the Gaussian planes
  * G_0..G_5 of octave `octave` of frame `frame` of the last batch / sift()
  * call, as that call's pyramid left them in the context's arena -- (6, h, w)
- * f32 like sift_mi_read_scale_space.  Valid only when the last call ran as
+ * f32 like sift_mi_read_scale_space, with (w, h) from
+ * sift_mi_batch_octave_dims; `out_floats` is the capacity of `out`
+ * (SIFT_MI_EINVAL below 6 * w * h).  Valid only when the last call ran as
  * one chunk (one frame, or sift_mi_set_chunk >= its frames) and until the
- * next call; SIFT_MI_ESTATE otherwise.  Lets tests check the batch path's
- * planes (which no DoG is materialised for) against precompute_images. */
-int sift_mi_read_batch_scale_space(sift_mi_ctx* ctx, uint32_t frame, size_t octave, float* out);
+ * next call of any kind (precompute included); SIFT_MI_ESTATE otherwise.
+ * Lets tests check the batch path's planes (which no DoG is materialised
+ * for) against precompute_images. */
+int sift_mi_batch_octave_dims(sift_mi_ctx* ctx, size_t octave, uint32_t* width, uint32_t* height);
+int sift_mi_read_batch_scale_space(sift_mi_ctx* ctx, uint32_t frame, size_t octave, float* out, size_t out_floats);
+
+/* Kernel-path switches (test / diagnostic, not configuration).  The default
+ * of every option is the product path; each alternative computes the same
+ * bits through a different kernel family, so the tests can hold every family
+ * against the oracle.  Per context (no environment variables, no process-wide
+ * state); waits for the context's work in flight.  SIFT_MI_EINVAL for an
+ * unknown option or a value out of range. */
+typedef enum {
+    SIFT_MI_PATH_TILE_BLUR = 0,    /* 1: one-tile-per-workgroup blurs everywhere (default 0) */
+    SIFT_MI_PATH_PAIR_BLUR = 1,    /* 0: no two-blur kernels (default 1) */
+    SIFT_MI_PATH_SEED_PAIR = 2,    /* 0: seed and blur 1 as two launches (default 1) */
+    SIFT_MI_PATH_TAIL = 3,         /* 0: per-blur launches for the small octaves (default 1) */
+    SIFT_MI_PATH_FUSED_DETECT = 4, /* 0: blur 5 and the extremum scan apart; 2: fused wherever it
+                                      applies, at 32-row segments (default 1: where it fills the chip) */
+    SIFT_MI_PATH_EARLY = 5,        /* 0: one-chunk calls detect every octave after the tail (default 1) */
+    SIFT_MI_PATH_DESC_FIRST = 6,   /* 0: one-frame calls order, then describe (default 1) */
+    SIFT_MI_PATH_GRAPH = 7,        /* 1: identical single-chunk calls replayed as a HIP graph (default 0) */
+    SIFT_MI_PATH_BAND_DRIFT = 8,   /* row bands: accepted refinement drift, -41..24 rows (default 24;
+                                      smaller values force the whole-pyramid re-run) */
+    SIFT_MI_PATH_BOUND_SHRINK = 9  /* k >= 1: first-chunk stage bounds / k (default 1; > 1 forces the
+                                      bound-overflow re-run) */
+} sift_mi_path_option;
+int sift_mi_set_path_option(sift_mi_ctx* ctx, int option, int value);
 
 /* ---- src/lib.rs:123-143 `precompute_images` / `PrecomputedImages` ------- */
 int sift_mi_precompute(sift_mi_ctx* ctx, const uint8_t* pixels, uint32_t width, uint32_t height,
@@ -218,9 +245,16 @@ int sift_mi_decode_jpeg_batch(sift_mi_ctx* ctx, const uint8_t* const* data, cons
                               uint8_t* d_frames, size_t frame_pitch, size_t row_stride, int threads);
 
 /* ---- measurement ---------------------------------------------------------
- * Cumulative since the last reset, from HIP events on the context stream.
- * pyramid_* covers the seed + octave blur/DoG kernels (the HBM-bound stage);
- * pyramid_bytes is the algorithmic byte count W*H + 44*sum(P_o) per frame. */
+ * Cumulative since the last reset.  The stage times (pyramid_ms ..
+ * descriptor_ms, total_ms) come from HIP events that only the one-lane mode
+ * records (sift_mi_set_pipeline_lanes(ctx, 1): the stage-timing mode; a
+ * marker costs ~7 us of a stream's timeline, so the two-lane throughput mode
+ * records none and leaves them at 0).  pyramid_* covers the seed + octave
+ * blur kernels (the HBM-bound stage), which include the extremum scan of the
+ * octaves detected with their last blur (k_blur_detect); pyramid_bytes is
+ * SURVEY.md 8(d)'s algorithmic byte count W*H + 44*sum(P_o) per frame, and
+ * pyramid_scan_bytes what the reference's scan reads for those fused
+ * octaves (the five DoG planes once, 20 B per octave pixel), apart. */
 typedef struct {
     double pyramid_ms;
     double detect_ms;
@@ -241,6 +275,7 @@ typedef struct {
      * rotated 4x4 region that compute_descriptor (src/lib.rs:785-990) enumerates */
     uint64_t orient_samples;
     uint64_t desc_samples;
+    uint64_t pyramid_scan_bytes;
 } sift_mi_stats;
 int sift_mi_get_stats(sift_mi_ctx* ctx, sift_mi_stats* out);
 int sift_mi_reset_stats(sift_mi_ctx* ctx);
@@ -250,6 +285,10 @@ int sift_mi_reset_stats(sift_mi_ctx* ctx);
 int sift_mi_set_sample_counting(sift_mi_ctx* ctx, int on);
 
 /* Library version string and last error (thread-local).
+ * 0.4.0: sift_mi_set_path_option (replaces the environment knobs),
+ *        sift_mi_batch_octave_dims, sift_mi_read_batch_scale_space takes the
+ *        output capacity, sift_mi_stats gained pyramid_scan_bytes (pyramid_bytes
+ *        no longer includes it).
  * 0.3.0: no ABI change from 0.2.
  * 0.2.0: emission keys (sift_mi_fetch_keys) widened x / y to 15 bits -- image
  *        field moved from bit 40 to bit 42; sift_mi_stats gained band_reruns,

@@ -19,7 +19,7 @@ EXPORTS = [
     "sift_mi_extract_batch_device", "sift_mi_set_exact_descriptors", "sift_mi_set_max_octaves", "sift_mi_set_sample_counting", "sift_mi_set_keep_on_device", "sift_mi_device_results",
     "sift_mi_set_pipeline_lanes", "sift_mi_set_row_band",
     "sift_mi_precompute", "sift_mi_octave_dims", "sift_mi_read_scale_space", "sift_mi_read_dog",
-    "sift_mi_read_batch_scale_space",
+    "sift_mi_read_batch_scale_space", "sift_mi_batch_octave_dims", "sift_mi_set_path_option",
     "sift_mi_sift_with_precomputed", "sift_mi_compute_descriptor", "sift_mi_gaussian_blur",
     "sift_mi_resize_linear", "sift_mi_resize_nearest", "sift_mi_match_descriptors", "sift_mi_jpeg_dims",
     "sift_mi_decode_jpeg", "sift_mi_decode_jpeg_batch", "sift_mi_get_stats",
@@ -49,7 +49,7 @@ class Stats(ctypes.Structure):
                 ("frames", ctypes.c_uint64), ("extrema", ctypes.c_uint64),
                 ("keypoints", ctypes.c_uint64), ("band_reruns", ctypes.c_uint64),
                 ("stage_reruns", ctypes.c_uint64), ("orient_samples", ctypes.c_uint64),
-                ("desc_samples", ctypes.c_uint64)]
+                ("desc_samples", ctypes.c_uint64), ("pyramid_scan_bytes", ctypes.c_uint64)]
 
     def as_dict(self):
         return {k: getattr(self, k) for k, _ in self._fields_}
@@ -97,7 +97,9 @@ def lib():
         "sift_mi_precompute": [vp, vp, u32, u32, sz, P(sz)],
         "sift_mi_octave_dims": [vp, sz, P(u32), P(u32)],
         "sift_mi_read_scale_space": [vp, sz, vp],
-        "sift_mi_read_batch_scale_space": [vp, ctypes.c_uint32, sz, vp],
+        "sift_mi_read_batch_scale_space": [vp, ctypes.c_uint32, sz, vp, sz],
+        "sift_mi_batch_octave_dims": [vp, sz, P(u32), P(u32)],
+        "sift_mi_set_path_option": [vp, i32, i32],
         "sift_mi_read_dog": [vp, sz, vp],
         "sift_mi_sift_with_precomputed": [vp, i64, P(sz)],
         "sift_mi_compute_descriptor": [vp, vp, u32, u32, f32, f32, f32, f32, vp],

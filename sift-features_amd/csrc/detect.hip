@@ -1,4 +1,3 @@
-#include <string.h>
 // Keypoint detection on MI355X: DoG extrema + sub-pixel refinement + contrast
 // and edge rejection (k_detect_rows, k_refine), then 36-bin orientation histograms and
 // reference orientations (k_orient).
@@ -29,34 +28,61 @@ namespace siftmi {
 // formed where it is read, with the same single f32 subtraction the blur
 // epilogue uses when it does write D (pyramid.hip), so every value is
 // bit-identical to the stored plane.
-struct DogView {
-    const gfloat* g;  // G_0 of one frame's octave
-    size_t P;         // floats per plane
-    __device__ __forceinline__ float operator()(int s, size_t off) const {
-        return g[(size_t)(s + 1) * P + off] - g[(size_t)s * P + off];
-    }
+//
+// One Newton step reads the 3x3x3 DoG neighbourhood of (s, y, x): the four
+// Gaussians G_{s-1} .. G_{s+2} at rows y-1 .. y+1, columns x-1 .. x+1, i.e.
+// twelve 12-byte row segments.  They are fetched as twelve 3-dword loads (one
+// instruction each) instead of the 28 distinct single floats the expressions
+// name: the kernel is bound by the address rate of its scattered loads (one
+// candidate per lane, every lane a different row), not by arithmetic.  The
+// unused corner values of the outer planes cost no extra cache line.
+typedef float f3a __attribute__((ext_vector_type(3), aligned(4)));
+typedef __attribute__((address_space(1))) const f3a gf3a;
+
+struct Nbhd {
+    float d[3][3][3];  // [prev / curr / next][row y-1 .. y+1][column x-1 .. x+1]
 };
 
-__device__ __forceinline__ bool interpolate(const DogView& dv, int W, int H, int pitch, int& scale, int& x, int& y,
-                                            float& os, float& ox, float& oy, uint32_t* band_flag, int vlo, int vhi) {
+__device__ __forceinline__ void load_nbhd(const gfloat* g0, size_t P, int pitch, int s, int y, int x, Nbhd& n) {
+    f3a g[4][3];
+#pragma unroll
+    for (int k = 0; k < 4; k++)
+#pragma unroll
+        for (int r = 0; r < 3; r++)
+            g[k][r] = *(const gf3a*)(g0 + (size_t)(s - 1 + k) * P + (size_t)(y - 1 + r) * pitch + (x - 1));
+#pragma unroll
+    for (int j = 0; j < 3; j++)
+#pragma unroll
+        for (int r = 0; r < 3; r++) {
+            n.d[j][r][0] = g[j + 1][r].x - g[j][r].x;
+            n.d[j][r][1] = g[j + 1][r].y - g[j][r].y;
+            n.d[j][r][2] = g[j + 1][r].z - g[j][r].z;
+        }
+}
+
+// On success n holds the neighbourhood of the converged point (scale, y, x),
+// which extremum_contrast / extremum_is_on_edge read next.
+__device__ __forceinline__ bool interpolate(const gfloat* g0, size_t P, int W, int H, int pitch, int& scale, int& x,
+                                            int& y, float& os, float& ox, float& oy, Nbhd& n, uint32_t* band_flag,
+                                            int vlo, int vhi) {
     for (int it = 0; it < kMaxInterpSteps; it++) {
         // row bands with a restricted pyramid (host.cpp run_pyramid): the
         // rows read here must be computed ones, else the host recomputes the
         // band on the whole-frame pyramid
         if (band_flag && (y - 1 < vlo || y + 1 >= vhi)) atomicOr(band_flag, 1u);
-        const int prev = scale - 1, curr = scale, next = scale + 1;
-#define AT(a, yy, xx) dv(a, (size_t)(yy) * pitch + (xx))
-        const float g1 = (AT(next, y, x) - AT(prev, y, x)) / 2.f;
-        const float g2 = (AT(curr, y + 1, x) - AT(curr, y - 1, x)) / 2.f;
-        const float g3 = (AT(curr, y, x + 1) - AT(curr, y, x - 1)) / 2.f;
-        const float v2 = AT(curr, y, x) * 2.f;
-        const float h11 = AT(next, y, x) + AT(prev, y, x) - v2;
-        const float h12 = (AT(next, y + 1, x) - AT(next, y - 1, x) - AT(prev, y + 1, x) + AT(prev, y - 1, x)) / 4.f;
-        const float h13 = (AT(next, y, x + 1) - AT(next, y, x - 1) - AT(prev, y, x + 1) + AT(prev, y, x - 1)) / 4.f;
-        const float h22 = AT(curr, y + 1, x) + AT(curr, y - 1, x) - v2;
-        const float h33 = AT(curr, y, x + 1) + AT(curr, y, x - 1) - v2;
-        const float h23 =
-            (AT(curr, y + 1, x + 1) - AT(curr, y + 1, x - 1) - AT(curr, y - 1, x + 1) + AT(curr, y - 1, x - 1)) / 4.f;
+        load_nbhd(g0, P, pitch, scale, y, x, n);
+        // AT(plane, dy, dx): plane 0 / 1 / 2 = prev / curr / next
+#define AT(a, dy, dx) n.d[a][(dy) + 1][(dx) + 1]
+        const float g1 = (AT(2, 0, 0) - AT(0, 0, 0)) / 2.f;
+        const float g2 = (AT(1, 1, 0) - AT(1, -1, 0)) / 2.f;
+        const float g3 = (AT(1, 0, 1) - AT(1, 0, -1)) / 2.f;
+        const float v2 = AT(1, 0, 0) * 2.f;
+        const float h11 = AT(2, 0, 0) + AT(0, 0, 0) - v2;
+        const float h12 = (AT(2, 1, 0) - AT(2, -1, 0) - AT(0, 1, 0) + AT(0, -1, 0)) / 4.f;
+        const float h13 = (AT(2, 0, 1) - AT(2, 0, -1) - AT(0, 0, 1) + AT(0, 0, -1)) / 4.f;
+        const float h22 = AT(1, 1, 0) + AT(1, -1, 0) - v2;
+        const float h33 = AT(1, 0, 1) + AT(1, 0, -1) - v2;
+        const float h23 = (AT(1, 1, 1) - AT(1, 1, -1) - AT(1, -1, 1) + AT(1, -1, -1)) / 4.f;
 #undef AT
         const float det =
             h11 * h22 * h33 - h11 * h23 * h23 - h12 * h12 * h33 + 2.f * h12 * h13 * h23 - h13 * h13 * h22;
@@ -553,12 +579,11 @@ __global__ __launch_bounds__(256) void k_blur_detect(const BlurDetectLaunch L) {
         if (gbase + i < L.cap) L.cand[gbase + i] = lcand[i];
 }
 
-// SIFT_MI_FUSED_DETECT=0 keeps blur 5 and detection apart, =force fuses
-// every octave it can at 32-row segments (A/B and test knobs)
-int launch_blur_detect(int R, BlurDetectLaunch& L, hipStream_t st) {
-    const char* e = getenv("SIFT_MI_FUSED_DETECT");
-    if (e && !strcmp(e, "0")) return -1;
-    const bool force = e && !strcmp(e, "force");
+// PathOpts::fused_detect: 0 keeps blur 5 and detection apart, 2 fuses every
+// octave it can at 32-row segments (test paths)
+int launch_blur_detect(int R, BlurDetectLaunch& L, hipStream_t st, const PathOpts& o) {
+    if (o.fused_detect == 0) return -1;
+    const bool force = o.fused_detect == 2;
     const bool ok = L.W > R + 1 && L.H > R + 1 && L.W >= 2 * kImageBorder && L.H >= 2 * kImageBorder &&
                     (uint64_t)L.H * (uint64_t)L.pitch * 4 < (1ull << 31) && L.n_img > 0;
     if (!ok) return -1;
@@ -603,31 +628,36 @@ __device__ __forceinline__ bool refine_one(const RefineLaunch& L, uint64_t key, 
     const int y = (int)((key >> kKeyYShift) & kKeyCoordMask);
     const int x = (int)((key >> kKeyXShift) & kKeyCoordMask);
     const int W = L.ow[o], H = L.oh[o], pitch = L.opitch[o];
-    const DogView dv{as_global(L.gauss[o]) + (size_t)(b - L.img_base) * L.g_img_stride[o], (size_t)pitch * H};
+    const gfloat* g0 = as_global(L.gauss[o]) + (size_t)(b - L.img_base) * L.g_img_stride[o];
+    const size_t P = (size_t)pitch * H;
     int sc = s_in, xi = x, yi = y;
     float os, ox, oy;
+    Nbhd n;
     int vlo = 0, vhi = H;  // rows of this octave's Gaussians that are exact
     if (L.band_flag) {
         vlo = max(0, (int)((uint64_t)H * L.band_r / L.band_n) - 1 - L.band_margin);
         vhi = min(H, (int)((uint64_t)H * (L.band_r + 1) / L.band_n) + 1 + L.band_margin);
     }
-    if (!interpolate(dv, W, H, pitch, sc, xi, yi, os, ox, oy, L.band_flag, vlo, vhi)) return false;
-    const size_t c = (size_t)yi * pitch + xi;
-    auto prev = [&](size_t off) { return dv(sc - 1, off); };
-    auto curr = [&](size_t off) { return dv(sc, off); };
-    auto next = [&](size_t off) { return dv(sc + 1, off); };
+    if (!interpolate(g0, P, W, H, pitch, sc, xi, yi, os, ox, oy, n, L.band_flag, vlo, vhi)) return false;
+    // the converged point's neighbourhood is n (the last step did not move)
+#define PREV(dy, dx) n.d[0][(dy) + 1][(dx) + 1]
+#define CURR(dy, dx) n.d[1][(dy) + 1][(dx) + 1]
+#define NEXT(dy, dx) n.d[2][(dy) + 1][(dx) + 1]
     // extremum_contrast (src/lib.rs:606-626)
-    const float g1 = (next(c) - prev(c)) / 2.f;
-    const float g2 = (curr(c + pitch) - curr(c - pitch)) / 2.f;
-    const float g3 = (curr(c + 1) - curr(c - 1)) / 2.f;
+    const float g1 = (NEXT(0, 0) - PREV(0, 0)) / 2.f;
+    const float g2 = (CURR(1, 0) - CURR(-1, 0)) / 2.f;
+    const float g3 = (CURR(0, 1) - CURR(0, -1)) / 2.f;
     const float interp = os * g1 + oy * g2 + ox * g3;
-    const float contrast = fabsf(curr(c) + interp / 2.f);
+    const float contrast = fabsf(CURR(0, 0) + interp / 2.f);
     if (contrast * (float)kScalesPerOctave <= kContrastThreshold) return false;
     // extremum_is_on_edge (src/lib.rs:630-653)
-    const float v2 = curr(c) * 2.0f;
-    const float h11 = curr(c + pitch) + curr(c - pitch) - v2;
-    const float d22 = curr(c + 1) + curr(c - 1) - v2;
-    const float h12 = (curr(c + pitch + 1) - curr(c + pitch - 1) - curr(c - pitch + 1) + curr(c - pitch - 1)) / 4.f;
+    const float v2 = CURR(0, 0) * 2.0f;
+    const float h11 = CURR(1, 0) + CURR(-1, 0) - v2;
+    const float d22 = CURR(0, 1) + CURR(0, -1) - v2;
+    const float h12 = (CURR(1, 1) - CURR(1, -1) - CURR(-1, 1) + CURR(-1, -1)) / 4.f;
+#undef PREV
+#undef CURR
+#undef NEXT
     const float tr = d22 + h11;
     const float det = d22 * h11 - h12 * h12;
     if (det <= 0.f) return false;

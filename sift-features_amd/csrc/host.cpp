@@ -26,11 +26,6 @@
 using namespace siftmi;
 
 hipError_t siftmi::host_wait_event(hipEvent_t e) {
-    static const bool spin = [] {
-        const char* v = getenv("SIFT_MI_WAIT");
-        return v && !strcmp(v, "spin");
-    }();
-    if (spin) return hipEventSynchronize(e);
     const auto t0 = std::chrono::steady_clock::now();
     for (;;) {
         const hipError_t r = hipEventQuery(e);
@@ -497,9 +492,8 @@ struct sift_mi_ctx {
     hipStream_t aux[2] = {};       // per lane: blurs 4, 5 of each octave beside the next octave
     hipStream_t dec = nullptr;     // JPEG batch decoding: a high-priority stream (its own hardware queue)
     hipEvent_t oct_ev[2][kTailMaxOct + 1] = {};  // per lane: octave o's G_3 done / aux joined
-    int oct_overlap = 1;           // SIFT_MI_OCT_OVERLAP=0: one stream per lane (A/B, tests)
     bool lanes_busy = false;       // this call keeps both pipeline lanes busy (no octave overlap then)
-    int stage_overlap = 1;         // SIFT_MI_STAGE_OVERLAP=0: detection after the whole pyramid
+    PathOpts opts;                 // kernel-path switches (sift_mi_set_path_option)
     hipEvent_t fork = nullptr;     // orders lane 1 after / before the caller's stream
     int lanes = 2;                 // pipeline lanes (sift_mi_set_pipeline_lanes)
     uint32_t chunk_override = 0;
@@ -534,11 +528,12 @@ struct sift_mi_ctx {
     size_t dev_result_n = 0;
     int res_slot = -1;  // >= 0: the last call's device results are that slot's outputs (one chunk, no copy)
     int batch_arena = -1;     // >= 0: the last batch call ran as one chunk in this arena (read-back)
-    // Single-chunk calls as a HIP graph (SIFT_MI_GRAPH=1): the call's ~40
+    // Single-chunk calls as a HIP graph (PathOpts::graph): the call's ~40
     // launches are captured the second time an identical call (same frames
     // pointer, geometry, bounds, modes, buffers) is seen, then replayed with
     // one hipGraphLaunch.
     struct GraphKey {
+        PathOpts opts;  // the switches decide what is captured
         const uint8_t* frames;
         size_t frame_pitch, stride;
         uint32_t m, w, h, bc, be, bk, bcb;
@@ -627,6 +622,7 @@ int ensure_plan(sift_mi_ctx* c, uint32_t w, uint32_t h, uint32_t chunk) {
     if (p.w == w && p.h == h && p.chunk >= chunk && p.arena[0].p && p.profile == (int)c->profile &&
         p.max_oct == c->max_octaves)
         return 0;
+    c->batch_arena = -1;  // the arenas are re-sized or re-planned: no batch read-back
     if (!(p.w == w && p.h == h && p.profile == (int)c->profile && p.max_oct == c->max_octaves)) {
         p.release();
         // per-frame stage high-water marks belong to a frame size
@@ -764,8 +760,9 @@ constexpr int kBandDrift = 24, kBandPatch = 41;
 // the DoG planes and reading them back.
 // Octave overlap: octave o + 1 needs only G_3 of octave o (its G_0 is
 // written by blur 3), so blurs 4, 5 of each octave run on the lane's aux
-// stream beside the next octave's blurs (SIFT_MI_OCT_OVERLAP=0: off).  Tried
-// and measured slower or no faster (round 3): the chunk's
+// stream beside the next octave's blurs (without: 0.779 vs 0.62 ms per 1080p
+// frame, round 4).  Tried and measured slower or no faster (round 3, DESIGN.md
+// 3.10): the chunk's
 // frames split in two halves on the two streams; seed + octave 0 in
 // sub-batches of 2-32 frames for Infinity Cache reuse; a second aux stream;
 // only octaves 0 .. k-1 (k = 1, 2, 3) on the aux stream.
@@ -820,13 +817,10 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
         seed_y1 = std::max(rhi[0], rlo[0] + 1);
     }
     // the small octaves from o_tail on: one k_octave_tail launch
-    // (SIFT_MI_TAIL=0: per-blur launches for every octave; A/B and test knob)
+    // (PathOpts::tail = 0: per-blur launches for every octave)
+    const PathOpts& po = c->opts;
     int o_tail = p.n_oct;
-    {
-        const char* e = getenv("SIFT_MI_TAIL");
-        if (!(e && !strcmp(e, "0")) && p.n_oct <= kTailMaxOct)
-            o_tail = tail_octave_start(p.ow.data(), p.oh.data(), p.n_oct, p.oct_r);
-    }
+    if (po.tail && p.n_oct <= kTailMaxOct) o_tail = tail_octave_start(p.ow.data(), p.oh.data(), p.n_oct, p.oct_r);
     uint64_t bytes = p.algo_bytes_per_frame;  // per frame, SURVEY.md 8(d)
     if (c->band_restricted) {
         // the same yardstick over the rows this band computes: 4 B per pixel
@@ -900,26 +894,23 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
         S.y1 = seed_y1;
         // G_0 and G_1 in one pass where it applies (whole planes: not for a
         // restricted row band); G_0 is then never read back from HBM
-        seed_pair = p.n_oct > 0 && launch_seed_pair(p.seed_r, p.oct_r[1], S, blur_launch(0, 1, f0, nf), sm) == 0;
+        seed_pair = p.n_oct > 0 && launch_seed_pair(p.seed_r, p.oct_r[1], S, blur_launch(0, 1, f0, nf), sm, po) == 0;
         if (seed_pair) {
             launches++;
             return 0;
         }
-        if (launch_seed(p.seed_r, S, sm)) return fail(SIFT_MI_EUNSUPPORTED, "seed blur radius");
+        if (launch_seed(p.seed_r, S, sm, po)) return fail(SIFT_MI_EUNSUPPORTED, "seed blur radius");
         launches++;
         return 0;
     };
     // octaves [o0, o1) of frames [f0, f0 + nf)
     // the launch that writes an octave's G_3 signals the aux stream's event
-    // itself: no marker packet on the main stream (SIFT_MI_EXT_EVENTS=0: a
-    // separate event record after it; 0.626 / 0.629 vs 0.616 / 0.619 ms per
-    // 1080p frame)
+    // itself: no marker packet on the main stream (a separate event record
+    // after it: 0.626 / 0.629 vs 0.616 / 0.619 ms per 1080p frame, round 4)
     // (not under stream capture: a kernel's stop event does not become a
     // graph dependency, so the captured aux work would not wait)
-    const char* xe = getenv("SIFT_MI_EXT_EVENTS");
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
-    const bool ext_events = !(xe && !strcmp(xe, "0")) && hipStreamIsCapturing(st, &cap) == hipSuccess &&
-                            cap == hipStreamCaptureStatusNone;
+    const bool ext_events = hipStreamIsCapturing(st, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone;
     auto octaves = [&](uint32_t f0, uint32_t nf, int o0, int o1, hipStream_t sm, bool ov) -> int {
         hipStream_t s45 = sm;
         for (int o = o0; o < o1; o++) {
@@ -953,7 +944,7 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
                     F.cand = S.cand.p;
                     F.counter = S.counters.p + 0;
                     F.cap = S.bc;
-                    if (launch_blur_detect(p.oct_r[s], F, s45) == 0) {
+                    if (launch_blur_detect(p.oct_r[s], F, s45, po) == 0) {
                         S.fused_mask |= 1u << o;
                         launches++;
                         continue;
@@ -967,7 +958,7 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
                 if (g3) set_launch_done_event(c->oct_ev[lane][o]);
                 int rc = 1;
                 if (s == 1 || (s == 2 && o == 0 && seed_pair))
-                    rc = launch_blur_pair(p.oct_r[s], p.oct_r[s + 1], B, blur_launch(o, s + 1, f0, nf), sm);
+                    rc = launch_blur_pair(p.oct_r[s], p.oct_r[s + 1], B, blur_launch(o, s + 1, f0, nf), sm, po);
                 if (rc == 0) {
                     g3_signalled = g3 && !launch_done_pending();
                     set_launch_done_event(nullptr);
@@ -978,7 +969,7 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
                 // a declined pair launched nothing: the event is still pending
                 // for blur s itself only if that is blur 3
                 if (g3 && s != 3) set_launch_done_event(nullptr);
-                if (launch_blur(p.oct_r[s], B, s >= 4 ? s45 : sm)) {
+                if (launch_blur(p.oct_r[s], B, s >= 4 ? s45 : sm, po)) {
                     set_launch_done_event(nullptr);
                     return fail(SIFT_MI_EUNSUPPORTED, "octave blur radius");
                 }
@@ -993,9 +984,8 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
         return 0;
     };
     auto part = [&](uint32_t f0, uint32_t nf, hipStream_t sm, bool ov) -> int {
-        const char* ee = getenv("SIFT_MI_EARLY");
-        const bool early = detect_slot >= 0 && ov && o_tail > 0 && o_tail < p.n_oct && c->slot[detect_slot].bcb &&
-                           !(ee && !strcmp(ee, "0"));
+        const bool early =
+            detect_slot >= 0 && ov && o_tail > 0 && o_tail < p.n_oct && c->slot[detect_slot].bcb && po.early;
         CHK(seed(f0, nf, sm));
         CHK(octaves(f0, nf, 0, o_tail, sm, ov));
         if (o_tail < p.n_oct) {
@@ -1030,7 +1020,7 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
             // one chunk (octave overlap): the octaves below the tail are
             // detected, refined and oriented on the aux stream beside the tail
             // kernel; the tail octaves, after it, into a region of their own
-            // (Slot::early; SIFT_MI_EARLY=0: off).  Tried and dropped: the
+            // (Slot::early; PathOpts::early = 0: off).  Tried and dropped: the
             // large octaves detected on lane 1's stream as each one's G_5
             // lands (0.634 vs 0.613-0.624 ms per 1080p frame: the scan then
             // competes with the blur chain for HBM instead of filling the
@@ -1061,16 +1051,20 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
     // flight the other lane's kernels already fill the chip, and the extra
     // stream costs ~2% of batch throughput (30.4 vs 29.8 M keypoints/s,
     // 128 1080p frames, three A/B pairs)
-    CHK(part(0, n, st, c->oct_overlap && !c->lanes_busy && p.n_oct <= kTailMaxOct));
+    CHK(part(0, n, st, !c->lanes_busy && p.n_oct <= kTailMaxOct));
     HIPCHK(hipGetLastError());
     c->stats.pyramid_launches += launches;
-    // octaves whose detection ran inside the pyramid (k_blur_detect): the
-    // stage's yardstick adds what the reference's extremum scan reads, the
-    // five DoG planes once (20 B per octave pixel)
+    // pyramid_bytes is SURVEY.md 8(d)'s yardstick alone (W*H + 44*sum P_o per
+    // frame).  The octaves whose extremum scan ran inside the stage
+    // (k_blur_detect) are reported apart: what the reference's scan reads for
+    // them, the five DoG planes once (20 B per octave pixel), so a caller can
+    // state the fused stage's figure without mixing the two yardsticks.
+    uint64_t scan = 0;
     if (cand_slot >= 0)
         for (int o = 0; o < p.n_oct && o < 32; o++)
-            if ((c->slot[cand_slot].fused_mask >> o) & 1) bytes += 20ull * p.px[o];
+            if ((c->slot[cand_slot].fused_mask >> o) & 1) scan += 20ull * p.px[o];
     c->stats.pyramid_bytes += bytes * n;
+    c->stats.pyramid_scan_bytes += scan * n;
     return 0;
 }
 
@@ -1097,11 +1091,10 @@ Bounds chunk_bounds(sift_mi_ctx* c, uint32_t m) {
     };
     Bounds B;
     // first chunk: one candidate per 256 octave pixels; later chunks: 1.3x
-    // the per-frame high-water mark.  SIFT_MI_BOUND_SHRINK=k (test knob)
+    // the per-frame high-water mark.  PathOpts::bound_shrink = k (test path)
     // divides the first-chunk estimates by k and drops the slack, so every
     // chunk enqueued before a high-water mark exists overflows and re-runs.
-    double shrink = 1.0;
-    if (const char* e = getenv("SIFT_MI_BOUND_SHRINK")) shrink = std::max(1.0, atof(e));
+    const double shrink = std::max(1, c->opts.bound_shrink);
     if (shrink > 1.0 && c->pf_cand == 0) {
         auto tiny = [&](double per) { return (uint32_t)std::max(1.0, std::ceil(per / shrink * m)); };
         B.bc = tiny(sum_p / 256.0);
@@ -1231,10 +1224,10 @@ int launch_refine_stage(sift_mi_ctx* c, int si, const uint64_t* cand, const uint
     R.band_n = (int)c->band_n;
     R.band_patch = kBandPatch;
     R.band_margin = kBandDrift + 1 + kBandPatch;
-    // SIFT_MI_BAND_DRIFT narrows the rows the check accepts (down to -kBandPatch:
-    // patches may not cross the band edge; tests force the re-run path)
-    if (const char* e = getenv("SIFT_MI_BAND_DRIFT"))
-        R.band_margin = kBandPatch + 1 + std::min(kBandDrift, std::max(-kBandPatch, atoi(e)));
+    // PathOpts::band_drift narrows the rows the check accepts (down to
+    // -kBandPatch: patches may not cross the band edge; tests force the re-run
+    // path)
+    R.band_margin = kBandPatch + 1 + std::min(kBandDrift, std::max(-kBandPatch, c->opts.band_drift));
     R.gauss = p.d_gauss[arena_of(c, si)].p;
     R.g_img_stride = p.d_gstride.p;
     R.ow = p.d_ow.p;
@@ -1293,10 +1286,9 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
     // one frame, no limit, early detection: the descriptors are computed in
     // keypoint index order beside the ordering stage, which runs on lane 1's
     // idle stream; k_gather_out then writes the outputs in emission order
-    // (SIFT_MI_DESC_FIRST=0: order, then describe in emission order)
-    const char* dfe = getenv("SIFT_MI_DESC_FIRST");
+    // (PathOpts::desc_first = 0: order, then describe in emission order)
     S.desc_first = S.early && m == 1 && limit < 0 && si == 0 && c->lanes == 2 &&
-                   S.desc_kp.cap >= (size_t)B.bk * kDescSize && !(dfe && !strcmp(dfe, "0"));
+                   S.desc_kp.cap >= (size_t)B.bk * kDescSize && c->opts.desc_first;
     hipStream_t os = S.desc_first ? c->own2 : st;  // the ordering stage's stream
     if (S.desc_first) {
         HIPCHK(hipEventRecord(S.oriented, st));
@@ -1403,7 +1395,7 @@ int enqueue_chunk(sift_mi_ctx* c, int si, const uint8_t* d_frames, size_t frame_
     // stage overlap (two-lane mode; the one-lane mode times the stages apart):
     // detection starts inside the pyramid (run_pyramid), so ev[1]..ev[2] is
     // then only the refinement
-    const bool fused = pyramid && c->lanes == 2 && c->stage_overlap;
+    const bool fused = pyramid && c->lanes == 2;
     if (pyramid) CHK(run_pyramid(c, si, d_frames, frame_pitch, stride, m, false, fused ? si : -1, si));
     if (S.staged) HIPCHK(hipEventRecord(S.ev[1], st));
     return enqueue_keypoints(c, si, m, limit, frame_base, B);
@@ -1517,7 +1509,7 @@ int check_frame_args(uint32_t w, uint32_t h, size_t stride) {
     return 0;
 }
 
-// A single-chunk call replayed as a HIP graph (SIFT_MI_GRAPH=1): the first
+// A single-chunk call replayed as a HIP graph (PathOpts::graph): the first
 // call with a given key runs normally (it also sizes every buffer), the
 // second identical one is captured (relaxed stream capture of enqueue_chunk:
 // the fork / join with the aux stream becomes graph edges) and launched, later
@@ -1526,16 +1518,15 @@ int check_frame_args(uint32_t w, uint32_t h, size_t stride) {
 // here, 0 when the caller must enqueue it.
 int enqueue_single_graph(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, size_t stride, uint32_t m,
                          int64_t limit) {
-    const char* genv = getenv("SIFT_MI_GRAPH");  // read per call (tests toggle it)
-    const bool on = genv && !strcmp(genv, "1");
     Slot& S = c->slot[0];
-    if (!on || c->band_n > 1 || c->lanes != 2 || S.pending_copy) return 0;
+    if (!c->opts.graph || c->band_n > 1 || c->lanes != 2 || S.pending_copy) return 0;
     const Bounds B = chunk_bounds(c, m);
     CHK(ensure_lane(c, arena_of(c, 0)));
     CHK(reserve_chunk(c, 0, B, c->plan.chunk, m));
     hipStream_t st = lane_stream(c, 0);
     sift_mi_ctx::GraphKey k;
     std::memset(&k, 0, sizeof k);
+    k.opts = c->opts;
     k.frames = d_frames;
     k.frame_pitch = frame_pitch;
     k.stride = stride;
@@ -1803,7 +1794,7 @@ void give_streams(int dev, const hipStream_t (&in)[kCtxStreams]) {
 
 extern "C" {
 
-const char* sift_mi_version(void) { return "sift_mi 0.3.0 (gfx950)"; }
+const char* sift_mi_version(void) { return "sift_mi 0.4.0 (gfx950)"; }
 const char* sift_mi_last_error(void) { return g_err.c_str(); }
 
 int sift_mi_create(int device_ordinal, sift_mi_profile profile, sift_mi_ctx** out) {
@@ -1836,8 +1827,6 @@ int sift_mi_create(int device_ordinal, sift_mi_profile profile, sift_mi_ctx** ou
     bool ok = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) == hipSuccess;
     for (auto& lane : c->oct_ev)
         for (auto& e : lane) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
-    if (const char* e = getenv("SIFT_MI_OCT_OVERLAP")) c->oct_overlap = strcmp(e, "0") != 0;
-    if (const char* e = getenv("SIFT_MI_STAGE_OVERLAP")) c->stage_overlap = strcmp(e, "0") != 0;
     for (auto& S : c->slot) {
         for (auto& e : S.ev) ok = ok && hipEventCreate(&e) == hipSuccess;
         ok = ok && hipEventCreateWithFlags(&S.copied, hipEventDisableTiming) == hipSuccess;
@@ -1944,6 +1933,28 @@ int sift_mi_set_row_band(sift_mi_ctx* c, uint32_t band, uint32_t n_bands) {
     return 0;
 }
 
+int sift_mi_set_path_option(sift_mi_ctx* c, int option, int value) {
+    if (!c) return fail(SIFT_MI_EINVAL, "ctx is null");
+    CHK(set_device(c));
+    CHK(sync_lanes(c));  // no chunk in flight sees a half-changed path
+    PathOpts& o = c->opts;
+    const bool b = value == 0 || value == 1;
+    switch (option) {
+        case SIFT_MI_PATH_TILE_BLUR: if (!b) break; o.tile_blur = value; return 0;
+        case SIFT_MI_PATH_PAIR_BLUR: if (!b) break; o.pair = value; return 0;
+        case SIFT_MI_PATH_SEED_PAIR: if (!b) break; o.seed_pair = value; return 0;
+        case SIFT_MI_PATH_TAIL: if (!b) break; o.tail = value; return 0;
+        case SIFT_MI_PATH_FUSED_DETECT: if (value < 0 || value > 2) break; o.fused_detect = value; return 0;
+        case SIFT_MI_PATH_EARLY: if (!b) break; o.early = value; return 0;
+        case SIFT_MI_PATH_DESC_FIRST: if (!b) break; o.desc_first = value; return 0;
+        case SIFT_MI_PATH_GRAPH: if (!b) break; o.graph = value; return 0;
+        case SIFT_MI_PATH_BAND_DRIFT: if (value < -kBandPatch || value > kBandDrift) break; o.band_drift = value; return 0;
+        case SIFT_MI_PATH_BOUND_SHRINK: if (value < 1) break; o.bound_shrink = value; return 0;
+        default: return fail(SIFT_MI_EINVAL, "unknown path option");
+    }
+    return fail(SIFT_MI_EINVAL, "path option value out of range");
+}
+
 int sift_mi_set_keep_on_device(sift_mi_ctx* c, int keep) {
     if (!c) return fail(SIFT_MI_EINVAL, "ctx is null");
     c->keep_on_device = keep ? 1 : 0;
@@ -2046,6 +2057,7 @@ int sift_mi_precompute(sift_mi_ctx* c, const uint8_t* pixels, uint32_t w, uint32
     CHK(check_frame_args(w, h, stride));
     CHK(set_device(c));
     const uint8_t* frames[1] = {pixels};
+    c->batch_arena = -1;  // arena 0 is rewritten: the last batch's planes are gone
     CHK(upload_frames(c, frames, 1, w, h, stride));
     CHK(ensure_plan(c, w, h, 1));
     CHK(run_pyramid(c, 0, c->staging.p, (size_t)w * h, w, 1, true));
@@ -2074,12 +2086,23 @@ int sift_mi_read_scale_space(sift_mi_ctx* c, size_t o, float* out) {
     return 0;
 }
 
-int sift_mi_read_batch_scale_space(sift_mi_ctx* c, uint32_t frame, size_t o, float* out) {
+int sift_mi_batch_octave_dims(sift_mi_ctx* c, size_t o, uint32_t* w, uint32_t* h) {
+    if (!c || c->batch_arena < 0) return fail(SIFT_MI_ESTATE, "no single-chunk batch pyramid");
+    if (o >= (size_t)c->plan.n_oct) return fail(SIFT_MI_EINVAL, "octave out of range");
+    if (w) *w = (uint32_t)c->plan.ow[o];
+    if (h) *h = (uint32_t)c->plan.oh[o];
+    return 0;
+}
+
+int sift_mi_read_batch_scale_space(sift_mi_ctx* c, uint32_t frame, size_t o, float* out, size_t out_floats) {
     if (!c || !out || c->batch_arena < 0) return fail(SIFT_MI_ESTATE, "no single-chunk batch pyramid");
-    if (o >= (size_t)c->plan.n_oct || frame >= c->batch_frames) return fail(SIFT_MI_EINVAL, "frame / octave out of range");
+    Plan& p = c->plan;
+    if (o >= (size_t)p.n_oct || frame >= c->batch_frames || frame >= p.chunk)
+        return fail(SIFT_MI_EINVAL, "frame / octave out of range");
+    if (out_floats < (size_t)kImagesPerOctave * p.ow[o] * p.oh[o])
+        return fail(SIFT_MI_EINVAL, "out_floats < 6 * width * height of the octave (sift_mi_batch_octave_dims)");
     CHK(set_device(c));
     CHK(sync_lanes(c));
-    Plan& p = c->plan;
     const float* g = p.gauss((int)o, c->batch_arena) + (size_t)frame * p.gstride((int)o);
     HIPCHK(hipMemcpy2D(out, (size_t)p.ow[o] * sizeof(float), g, (size_t)p.opitch[o] * sizeof(float),
                        (size_t)p.ow[o] * sizeof(float), (size_t)kImagesPerOctave * p.oh[o], hipMemcpyDeviceToHost));
@@ -2099,6 +2122,7 @@ int sift_mi_read_dog(sift_mi_ctx* c, size_t o, float* out) {
 int sift_mi_sift_with_precomputed(sift_mi_ctx* c, int64_t limit, size_t* n_keypoints) {
     if (!c || !c->have_pyramid) return fail(SIFT_MI_ESTATE, "no precomputed pyramid");
     CHK(set_device(c));
+    c->batch_arena = -1;  // a later call: the batch read-back is no longer valid
     const int keep = c->keep_on_device;
     c->keep_on_device = 0;
     size_t offs[2];
@@ -2163,7 +2187,7 @@ int sift_mi_gaussian_blur(sift_mi_ctx* c, const float* src, uint32_t w, uint32_t
     L.profile = ip ? kProfileImageproc : kProfileOpenCV;
     if (hipMemcpy2DAsync(a.p, pitch * 4, src, (size_t)w * 4, (size_t)w * 4, h, hipMemcpyHostToDevice, c->stream) !=
             hipSuccess ||
-        launch_blur(r, L, c->stream) != 0 ||
+        launch_blur(r, L, c->stream, c->opts) != 0 ||
         hipMemcpy2DAsync(dst, (size_t)w * 4, b.p, pitch * 4, (size_t)w * 4, h, hipMemcpyDeviceToHost, c->stream) !=
             hipSuccess ||
         hipStreamSynchronize(c->stream) != hipSuccess)
@@ -2315,11 +2339,11 @@ int sift_mi_decode_jpeg_batch(sift_mi_ctx* c, const uint8_t* const* data, const 
     // context's batch (bench.py configs.jpeg_e2e) does not queue behind that
     // batch's kernels on a shared in-order queue -- normal-priority streams
     // share GPU_MAX_HW_QUEUES (4) queues round robin.  A caller stream
-    // (sift_mi_set_stream) is used as is; SIFT_MI_DEC_STREAM=0: the context's
-    // stream (A/B knob).
+    // (sift_mi_set_stream) is used as is.  Measured (round 4), with the
+    // polling host wait (host_wait_event): 2337 -> 3063 frames/s JPEG ->
+    // keypoints, pipelined beside sift().
     hipStream_t st = c->stream;
-    const char* e = getenv("SIFT_MI_DEC_STREAM");
-    if (c->stream == c->own && !(e && !strcmp(e, "0"))) {
+    if (c->stream == c->own) {
         if (!c->dec) {
             int least = 0, greatest = 0;
             HIPCHK(hipDeviceGetStreamPriorityRange(&least, &greatest));

@@ -1736,13 +1736,6 @@ static void launch_blur_strip_rp(const BlurLaunch& L, dim3 grid, int ya, int yb,
                            L.pitch, L.taps, ya, yb, seg);
 }
 
-// workgroups per strip launch the segment count aims for (SIFT_MI_STRIP_WG:
-// tuning knob, read per launch)
-static long strip_wg_target(long dflt = 6144) {
-    const char* e = getenv("SIFT_MI_STRIP_WG");
-    return e ? std::max(1L, atol(e)) : dflt;
-}
-
 // Row segments of a strip launch over `rows` rows with `per` strips x frames:
 // ~strip_wg_target() workgroups, but no segment shorter than ~320 rows unless
 // the launch would then have fewer than ~2048 workgroups (then down to ~40
@@ -1753,7 +1746,7 @@ static long strip_wg_target(long dflt = 6144) {
 // small octaves need the segments to fill the chip.  Returns the segment length.
 static int strip_segment_rows(int rows, long per, long target = 6144) {
     const long few = std::min<long>((2048 + per - 1) / per, rows / 40);
-    long nseg = std::min<long>((strip_wg_target(target) + per - 1) / per, std::max<long>(rows / 320, few));
+    long nseg = std::min<long>((target + per - 1) / per, std::max<long>(rows / 320, few));
     nseg = std::max(1L, nseg);
     // even: with an even first row every segment starts at an even row (the
     // strip kernels' next-octave rows are then the even / odd rows of each
@@ -1784,8 +1777,6 @@ static void launch_blur_strip_r(const BlurLaunch& L, hipStream_t st) {
         launch_blur_strip_rp<R, kProfileOpenCV>(L, grid, ya, yb, seg, st);
 }
 
-static bool strip_blur_enabled();
-
 template <int Ra, int Rb, int P = kProfileOpenCV>
 static void launch_blur2_rr(const BlurLaunch& A, const BlurLaunch& B, hipStream_t st) {
     using Q = PairGeom<Ra, Rb>;
@@ -1814,13 +1805,7 @@ static void launch_blur2_rr(const BlurLaunch& A, const BlurLaunch& B, hipStream_
     }
 }
 
-// SIFT_MI_PAIR=0 disables the pair kernels (A/B and test knob, read per launch)
-static bool pair_blur_enabled() {
-    const char* e = getenv("SIFT_MI_PAIR");
-    return !(e && !strcmp(e, "0"));
-}
-
-int launch_blur_pair(int ra, int rb, const BlurLaunch& A, const BlurLaunch& B, hipStream_t st) {
+int launch_blur_pair(int ra, int rb, const BlurLaunch& A, const BlurLaunch& B, hipStream_t st, const PathOpts& o) {
     // A: G_{s-1} -> G_s, B: G_s -> G_{s+1} of one octave arena (same geometry
     // and image stride); whole planes, no DoG; at most one of them writes the
     // next octave's base (B: blurs 2, 3 of octave 0 after k_seed_pair)
@@ -1828,8 +1813,7 @@ int launch_blur_pair(int ra, int rb, const BlurLaunch& A, const BlurLaunch& B, h
                     B.y1 <= B.y0 && A.dst && B.dst && B.src == A.dst && A.W == B.W && A.H == B.H &&
                     A.pitch == B.pitch && A.src_img_stride == A.dst_img_stride &&
                     B.src_img_stride == A.src_img_stride && B.dst_img_stride == A.src_img_stride && A.W >= 64 &&
-                    A.H >= 64 && (uint64_t)A.H * (uint64_t)A.pitch * 4 < (1ull << 31) && strip_blur_enabled() &&
-                    pair_blur_enabled();
+                    A.H >= 64 && (uint64_t)A.H * (uint64_t)A.pitch * 4 < (1ull << 31) && !o.tile_blur && o.pair;
     if (!ok) return -1;
     // (5, 6): blurs 1, 2; (6, 8) with B.nxt: blurs 2, 3 of octave 0 (G_1 from
     // k_seed_pair).  A (8, 10) pair for blurs 3, 4 (three-chunk column
@@ -1849,18 +1833,11 @@ int launch_blur_pair(int ra, int rb, const BlurLaunch& A, const BlurLaunch& B, h
     return -1;
 }
 
-// SIFT_MI_BLUR_KERNEL=tile forces the one-tile-per-workgroup kernels (A/B
-// and test knob, read per launch)
-static bool strip_blur_enabled() {
-    const char* e = getenv("SIFT_MI_BLUR_KERNEL");
-    return !(e && !strcmp(e, "tile"));
-}
-
-int launch_blur(int R, const BlurLaunch& L, hipStream_t st) {
+int launch_blur(int R, const BlurLaunch& L, hipStream_t st, const PathOpts& o) {
     // the strip kernel: materialised G_s, no DoG plane (the batch path), one
     // reflection per border (W, H > R), planes addressable by 32-bit offsets
     if (L.dst && !L.dog && R <= kStripMaxR && L.W > R && L.H > R &&
-        (uint64_t)L.H * (uint64_t)L.pitch * 4 < (1ull << 31) && strip_blur_enabled()) {
+        (uint64_t)L.H * (uint64_t)L.pitch * 4 < (1ull << 31) && !o.tile_blur) {
         switch (R) {
 #define CASE(r) \
     case r:     \
@@ -1909,7 +1886,7 @@ static void launch_seed_ip_r(const SeedLaunch& L, hipStream_t st) {
                        L.iptab, L.dst, L.dst_img_stride, L.W, L.H, L.pitch, L.taps);
 }
 
-int launch_seed(int R, const SeedLaunch& L, hipStream_t st) {
+int launch_seed(int R, const SeedLaunch& L, hipStream_t st, const PathOpts& o) {
     // the seed sigma is a constant: OpenCV cvRound(1.249 * 8 + 1) | 1 = 11
     // taps (R = 5); imageproc ceil(2 * 1.249) = 3
     const bool ip = L.profile == kProfileImageproc;
@@ -1917,7 +1894,7 @@ int launch_seed(int R, const SeedLaunch& L, hipStream_t st) {
     // the strip seed: exact 2x geometry, frames wide / tall enough for one
     // reflection of every window (else the tile kernels)
     if (L.W == 2 * L.sw && L.H == 2 * L.sh && L.W >= 160 && L.H >= 64 &&
-        (uint64_t)L.H * (uint64_t)L.pitch * 4 < (1ull << 31) && strip_blur_enabled()) {
+        (uint64_t)L.H * (uint64_t)L.pitch * 4 < (1ull << 31) && !o.tile_blur) {
         using G = StripGeom<5>;
         // segments start at even rows: the loader's row pairs then share their
         // two source rows (k_seed_strip); an extra row above a band is exact
@@ -1946,13 +1923,6 @@ int launch_seed(int R, const SeedLaunch& L, hipStream_t st) {
     return 0;
 }
 
-// SIFT_MI_SEED_PAIR=0: the seed and blur 1 as separate launches (A/B and
-// test knob, read per launch)
-static bool seed_pair_enabled() {
-    const char* e = getenv("SIFT_MI_SEED_PAIR");
-    return !(e && !strcmp(e, "0"));
-}
-
 template <int Ra, int Rb, int P>
 static void launch_seed_pair_rr(const SeedLaunch& S, const BlurLaunch& B, hipStream_t st) {
     using Q = PairGeom<Ra, Rb, 8>;
@@ -1964,15 +1934,14 @@ static void launch_seed_pair_rr(const SeedLaunch& S, const BlurLaunch& B, hipStr
                        S.taps, B.taps, 0, S.H, seg);
 }
 
-int launch_seed_pair(int rs, int rb, const SeedLaunch& S, const BlurLaunch& B, hipStream_t st) {
+int launch_seed_pair(int rs, int rb, const SeedLaunch& S, const BlurLaunch& B, hipStream_t st, const PathOpts& o) {
     // the strip seed's geometry (exact 2x, one reflection per window) and the
     // pair's (whole planes, B = blur 1 of the seed's plane, same arena)
     const bool ok = S.W == 2 * S.sw && S.H == 2 * S.sh && S.W >= 160 && S.H >= 64 &&
                     (uint64_t)S.H * (uint64_t)S.pitch * 4 < (1ull << 31) && S.y1 <= S.y0 && B.y1 <= B.y0 &&
                     B.profile == S.profile && B.src == S.dst && B.dst && !B.dog && !B.nxt && B.W == S.W &&
                     B.H == S.H && B.pitch == S.pitch && B.src_img_stride == S.dst_img_stride &&
-                    B.dst_img_stride == S.dst_img_stride && strip_blur_enabled() && pair_blur_enabled() &&
-                    seed_pair_enabled();
+                    B.dst_img_stride == S.dst_img_stride && !o.tile_blur && o.pair && o.seed_pair;
     if (!ok) return -1;
     if (S.profile == kProfileImageproc) {
         if (rs == 3 && rb == 3) { launch_seed_pair_rr<3, 3, kProfileImageproc>(S, B, st); return 0; }

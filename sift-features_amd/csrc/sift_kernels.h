@@ -36,6 +36,24 @@ struct IpResizeTab {
 // Arithmetic profile of the Processing backend (src/lib.rs:86-90).
 enum : int { kProfileOpenCV = 0, kProfileImageproc = 1 };
 
+// Kernel-path switches of one context (sift_mi_set_path_option).  The
+// defaults are the product path; every alternative computes the same bits and
+// exists so the tests can hold each kernel family against the oracle.  They
+// live in the context (no process-wide state, nothing read from the
+// environment).
+struct PathOpts {
+    int tile_blur = 0;     // 1: one-tile-per-workgroup blurs everywhere (no strip / pair kernels)
+    int pair = 1;          // 0: no pair kernels (k_blur2_strip, k_seed_pair)
+    int seed_pair = 1;     // 0: k_seed_strip, then blur 1 like the other octaves
+    int tail = 1;          // 0: per-blur launches for the small octaves (no k_octave_tail)
+    int fused_detect = 1;  // 0: blur 5 and the extremum scan apart; 2: fused at 32-row segments wherever it applies
+    int early = 1;         // one-chunk calls: detection of the octaves below the tail beside the tail kernel
+    int desc_first = 1;    // one-frame calls: descriptors beside the ordering stage
+    int graph = 0;         // 1: single-chunk calls captured once and replayed as a HIP graph
+    int band_drift = 24;   // row bands: refinement drift accepted without a re-run (< 24 forces re-runs)
+    int bound_shrink = 1;  // > 1: first-chunk stage bounds divided by it (forces the overflow re-run)
+};
+
 // Image planes are row-pitched: element (y, x) at plane[y * pitch + x].
 struct BlurLaunch {
     const float* src;
@@ -72,7 +90,7 @@ struct SeedLaunch {
 
 // Host wait for an event (host.cpp): spins ~1 ms, then polls with short
 // sleeps, so a thread waiting for a multi-ms chunk does not hold a CPU the
-// decode threads (or a CPU quota) need.  SIFT_MI_WAIT=spin: hipEventSynchronize.
+// decode threads (or a CPU quota) need.
 hipError_t host_wait_event(hipEvent_t e);
 
 // jpeg.hip: baseline JPEG -> 8-bit luma (zune-jpeg + image::grayscale arithmetic)
@@ -116,14 +134,16 @@ void launch_octave_tail(const TailLaunch& L, hipStream_t st);
 // true while no launch has taken it (the caller then clears it and records e)
 void set_launch_done_event(hipEvent_t e);
 bool launch_done_pending();
-int launch_blur(int radius, const BlurLaunch& L, hipStream_t st);
+int launch_blur(int radius, const BlurLaunch& L, hipStream_t st, const PathOpts& o = PathOpts{});
 // two consecutive blurs of an octave (A then B, B.src == A.dst) in one pass;
 // -1 when the pair kernel does not apply (the caller launches them singly)
-int launch_blur_pair(int ra, int rb, const BlurLaunch& A, const BlurLaunch& B, hipStream_t st);
-int launch_seed(int radius, const SeedLaunch& L, hipStream_t st);
+int launch_blur_pair(int ra, int rb, const BlurLaunch& A, const BlurLaunch& B, hipStream_t st,
+                     const PathOpts& o = PathOpts{});
+int launch_seed(int radius, const SeedLaunch& L, hipStream_t st, const PathOpts& o = PathOpts{});
 // the seed (radius rs) and blur 1 (radius rb; B.src == L.dst) in one pass
 // (k_seed_pair: G_0 never read back); -1 when it does not apply
-int launch_seed_pair(int rs, int rb, const SeedLaunch& L, const BlurLaunch& B, hipStream_t st);
+int launch_seed_pair(int rs, int rb, const SeedLaunch& L, const BlurLaunch& B, hipStream_t st,
+                     const PathOpts& o = PathOpts{});
 // D_s = G_{s+1} - G_s (s < 5) of an octave's G stack, for n images
 void launch_dog(const float* gauss, size_t plane, size_t g_img_stride, float* dog, size_t dog_img_stride, int W, int H,
                 int pitch, int n_img, hipStream_t st);
@@ -169,7 +189,7 @@ struct BlurDetectLaunch {
     uint32_t* counter;
     uint32_t cap;
 };
-int launch_blur_detect(int R, BlurDetectLaunch& L, hipStream_t st);
+int launch_blur_detect(int R, BlurDetectLaunch& L, hipStream_t st, const PathOpts& o = PathOpts{});
 
 // Stage sizes live in device counters (no host round trip between stages):
 // every consumer reads its count from device memory, clamps it to the buffer

@@ -21,6 +21,7 @@ in DESIGN.md:
     reference's `sort_unstable_by` leaves their order unspecified).
   * errors raise SiftMiError where the reference panics.
 """
+import contextlib
 import ctypes
 import threading
 from dataclasses import dataclass
@@ -248,15 +249,42 @@ class Context:
         check(lib().sift_mi_device_results(self._h, ctypes.byref(kp), ctypes.byref(desc), ctypes.byref(n)))
         return kp.value, desc.value, n.value
 
-    def read_batch_scale_space(self, frame, octave, dims):
+    def read_batch_scale_space(self, frame, octave, dims=None):
         """(6, h, w) f32 Gaussians of `octave` of `frame` of the last call, as
         its pyramid left them (valid when that call ran as one chunk; a
-        validation read-back, sift_mi_read_batch_scale_space).  dims = (w, h)
-        of the octave."""
-        w, h = dims
-        out = np.empty((6, h, w), np.float32)
-        check(lib().sift_mi_read_batch_scale_space(self._h, int(frame), int(octave), out.ctypes.data))
+        validation read-back, sift_mi_read_batch_scale_space).  The octave's
+        (w, h) come from the library (sift_mi_batch_octave_dims); `dims`, if
+        given, must equal them."""
+        w, h = ctypes.c_uint32(), ctypes.c_uint32()
+        check(lib().sift_mi_batch_octave_dims(self._h, int(octave), ctypes.byref(w), ctypes.byref(h)))
+        if dims is not None and tuple(dims) != (w.value, h.value):
+            raise ValueError(f"dims {tuple(dims)} != the batch octave's {(w.value, h.value)}")
+        out = np.empty((6, h.value, w.value), np.float32)
+        check(lib().sift_mi_read_batch_scale_space(self._h, int(frame), int(octave), out.ctypes.data, out.size))
         return out
+
+    # kernel-path switches (include/sift_mi.h sift_mi_path_option): test /
+    # diagnostic only; the defaults are the product path
+    PATH_OPTIONS = {"tile_blur": (0, 0), "pair_blur": (1, 1), "seed_pair": (2, 1), "tail": (3, 1),
+                    "fused_detect": (4, 1), "early": (5, 1), "desc_first": (6, 1), "graph": (7, 0),
+                    "band_drift": (8, 24), "bound_shrink": (9, 1)}
+
+    def set_path_option(self, name, value):
+        """One kernel-path switch (sift_mi_set_path_option), e.g.
+        set_path_option("pair_blur", 0)."""
+        check(lib().sift_mi_set_path_option(self._h, self.PATH_OPTIONS[name][0], int(value)))
+
+    @contextlib.contextmanager
+    def path_options(self, **opts):
+        """Kernel-path switches for the duration of a with-block, then the
+        defaults again."""
+        try:
+            for k, v in opts.items():
+                self.set_path_option(k, v)
+            yield self
+        finally:
+            for k in opts:
+                self.set_path_option(k, self.PATH_OPTIONS[k][1])
 
     # -- precompute_images / sift_with_precomputed (src/lib.rs:123-177) ------
     def precompute_images(self, img):

@@ -52,6 +52,19 @@ def test_version_and_errors_without_device(pkg):
     assert L.sift_mi_set_chunk(None, 4) == -1
     assert L.sift_mi_fetch(None, None, None, 0) == -1
     assert L.sift_mi_reset_stats(None) == -1
+    assert L.sift_mi_set_path_option(None, 0, 1) == -1
+
+
+def test_library_reads_no_environment(pkg):
+    """Path switches are per context (sift_mi_set_path_option): no product
+    source reads the environment (no process-global knobs).
+    (The binary's one getenv import comes from rocPRIM's headers in
+    order.hip's radix sort, not from this code.)"""
+    src = os.path.join(ROOT, "sift-features_amd", "csrc")
+    for fn in sorted(os.listdir(src)):
+        if fn.endswith((".hip", ".cpp", ".h")):
+            txt = open(os.path.join(src, fn)).read()
+            assert not re.search(r"\bgetenv\s*\(", txt), fn
 
 
 def test_no_cpu_fallback_in_product(pkg):

@@ -132,17 +132,17 @@ def test_world2_row_bands_allgather(pkg):
     assert all(r[3] for r in res)
 
 
-def test_band_rerun_path_is_exact(pkg, ctx, monkeypatch):
+def test_band_rerun_path_is_exact(pkg, ctx):
     """A band computes only its rows of the pyramid (plus the margins the
     keypoint stages read); a refinement that drifts further sets a device
     flag and the band is re-run on the whole-frame pyramid.  With the check's
-    margin narrowed to the band edge (SIFT_MI_BAND_DRIFT=-40) every band with
-    a keypoint near its edge takes that path: the result must still be the
-    exact whole-frame partition."""
+    margin narrowed to the band edge (path option band_drift = -40) every
+    band with a keypoint near its edge takes that path: the result must still
+    be the exact whole-frame partition."""
     import synth
     img = synth.frame(1920, 1080, 11)
     whole = ctx.sift(img)
-    monkeypatch.setenv("SIFT_MI_BAND_DRIFT", "-40")
     ctx.reset_stats()
-    _assert_whole(_bands(ctx, img, 4), whole)
+    with ctx.path_options(band_drift=-40):
+        _assert_whole(_bands(ctx, img, 4), whole)
     assert ctx.stats()["band_reruns"] > 0

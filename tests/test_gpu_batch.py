@@ -273,7 +273,7 @@ def test_world2_gather_device_results(pkg):
 
 
 @pytest.mark.gpu
-def test_batch_fused_kernels_equal_single_launches(pkg, monkeypatch):
+def test_batch_fused_kernels_equal_single_launches(pkg):
     """The batch path (no DoG planes) with the pair and tail kernels equals the
     batch path with single-blur launches only, bit for bit (1080p frames:
     the pair covers octaves 0-4, the tail octaves 5-9)."""
@@ -282,9 +282,8 @@ def test_batch_fused_kernels_equal_single_launches(pkg, monkeypatch):
     c = pkg.Context(0, pkg.OpenCVProcessing)
     try:
         fused = c.sift_batch(frames)
-        monkeypatch.setenv("SIFT_MI_PAIR", "0")
-        monkeypatch.setenv("SIFT_MI_TAIL", "0")
-        single = c.sift_batch(frames)
+        with c.path_options(pair_blur=0, tail=0):
+            single = c.sift_batch(frames)
     finally:
         c.close()
     for a, b in zip(fused, single):
@@ -294,21 +293,22 @@ def test_batch_fused_kernels_equal_single_launches(pkg, monkeypatch):
 
 
 @pytest.mark.parametrize("fetch", [False, True])
-def test_single_chunk_graph_replay(pkg, ctx, oracle, monkeypatch, fetch):
-    """SIFT_MI_GRAPH=1: identical single-frame calls are captured once (the
-    second call) and replayed as a HIP graph; every call's results equal the
-    normal path's and the oracle's, also after the frame contents change in
-    place (the graph reads the frame buffer anew) and when the frame pointer
-    changes (a new capture)."""
+def test_single_chunk_graph_replay(pkg, ctx, oracle, fetch):
+    """Path option graph = 1: identical single-frame calls are captured once
+    (the second call) and replayed as a HIP graph; every call's results equal
+    the normal path's and the oracle's, also after the frame contents change
+    in place (the graph reads the frame buffer anew), when the frame pointer
+    changes (a new capture) and when a path option changes between calls (the
+    options are part of the graph's key: ADVICE r04)."""
     import torch
     import synth
     from test_gpu_parity import assert_parity
-    monkeypatch.setenv("SIFT_MI_GRAPH", "1")
     a = synth.frame(640, 480, 3)
     b = synth.frame(640, 480, 4)
     ref = {0: ctx.sift(a), 1: ctx.sift(b)}
     t = torch.from_numpy(a).cuda()
     c = pkg.Context(0)
+    c.set_path_option("graph", 1)
     for i in range(5):
         src = a if i < 3 else b
         if i == 3:
@@ -326,12 +326,18 @@ def test_single_chunk_graph_replay(pkg, ctx, oracle, monkeypatch, fetch):
         assert res == ref[1], i
     kp_o, desc_o, ext_o = oracle.sift(b, internal=True)
     assert_parity(pkg, res, kp_o, desc_o, ext_o)
+    for opts in ({"early": 0}, {"fused_detect": 0, "desc_first": 0}, {}):
+        with c.path_options(**opts):
+            for i in range(3):
+                offs, res = c.sift_batch_device(t2.data_ptr(), 1, 640, 480, t2.stride(0), t2.numel(), fetch=True)
+                assert res == ref[1], (opts, i)
+                assert np.array_equal(res.keys, ref[1].keys), (opts, i)
     c.close()
 
 
-@pytest.mark.parametrize("knob", ["SIFT_MI_EARLY", "SIFT_MI_DESC_FIRST"])
+@pytest.mark.parametrize("knob", ["early", "desc_first"])
 @pytest.mark.parametrize("profile", [0, 1])
-def test_single_chunk_paths_equal(pkg, monkeypatch, knob, profile):
+def test_single_chunk_paths_equal(pkg, knob, profile):
     """One-chunk calls take latency paths of their own -- the octaves below
     the tail detected, refined and oriented on the aux stream beside the tail
     kernel with the tail octaves in a region of their own
@@ -345,7 +351,7 @@ def test_single_chunk_paths_equal(pkg, monkeypatch, knob, profile):
     prof = pkg.OpenCVProcessing if profile == 0 else pkg.ImageprocProcessing
     c = pkg.Context(0, prof)
     got = [c.sift(f) for f in frames for _ in range(2)]
-    monkeypatch.setenv(knob, "0")
+    c.set_path_option(knob, 0)
     ref = [c.sift(f) for f in frames for _ in range(2)]
     c.close()
     for a, b in zip(got, ref):

@@ -12,7 +12,7 @@
   chunks, results kept in HBM), 2 frames vs the oracle, every frame vs
   per-frame `sift()`;
 * the stage-bound overflow re-run (host.cpp finalize_chunk rc == 1): with
-  SIFT_MI_BOUND_SHRINK every chunk enqueued before a high-water mark exists
+  path option bound_shrink every chunk enqueued before a high-water mark exists
   overflows; the re-run chunks must equal per-frame results.
 Configs #1 (bird_small) and #5 (8192^2) are covered by test_gpu_parity /
 test_oracle_golden and test_gpu_large.
@@ -132,12 +132,12 @@ def test_large_chunk_features_limit(pkg, ctx, limit):
 
 
 @pytest.mark.parametrize("lanes", [1, 2])
-def test_stage_bound_overflow_rerun(pkg, ctx, monkeypatch, lanes):
+def test_stage_bound_overflow_rerun(pkg, ctx, lanes):
     import synth
     fr = synth.frames(7, 320, 240, seed0=40)
     ref = [ctx.sift(f) for f in fr]
-    monkeypatch.setenv("SIFT_MI_BOUND_SHRINK", "1000")
     c = pkg.Context(0, pkg.OpenCVProcessing)  # no high-water marks yet
+    c.set_path_option("bound_shrink", 1000)
     c.set_chunk(2)
     c.set_pipeline_lanes(lanes)
     got = c.sift_batch(fr)

@@ -9,7 +9,8 @@ pin both of its outputs:
     (sift_mi_read_batch_scale_space), bit-identical to the oracle's
     build_gaussian_scale_space (src/lib.rs:213-267);
   * the keypoints of the same calls against the oracle with the fused pass
-    on (the default) and off (SIFT_MI_FUSED_DETECT=0: launch_blur +
+    on (forced onto every octave it applies to, at 32-row segments:
+    path option fused_detect = 2) and off (fused_detect = 0: launch_blur +
     k_detect_rows), across frame shapes that exercise partial strips, short
     row segments, reflect-101 / clamp-to-edge borders and both profiles, and
     white noise (dense extrema, plateaus).
@@ -30,15 +31,15 @@ def _frame(name, seed=7):
     return synth.frame(w, h, seed)
 
 
-@pytest.mark.parametrize("fused", ["force", "0"])
+@pytest.mark.parametrize("fused", [2, 0])
 @pytest.mark.parametrize("profile", [0, 1])
 @pytest.mark.parametrize("name", SHAPES)
-def test_batch_pyramid_bit_exact(pkg, oracle, monkeypatch, fused, profile, name):
+def test_batch_pyramid_bit_exact(pkg, oracle, fused, profile, name):
     """Every Gaussian plane the batch path leaves in its arena (G_5 from
     k_blur_detect when fused) equals the oracle's, bit for bit."""
-    monkeypatch.setenv("SIFT_MI_FUSED_DETECT", fused)
     img = _frame(name)
     c = pkg.Context(0, pkg.OpenCVProcessing if profile == 0 else pkg.ImageprocProcessing)
+    c.set_path_option("fused_detect", fused)
     c.sift(img)
     opy = oracle.Pyramid(img, profile)
     for o in range(opy.n_octaves):
@@ -49,29 +50,29 @@ def test_batch_pyramid_bit_exact(pkg, oracle, monkeypatch, fused, profile, name)
     c.close()
 
 
-@pytest.mark.parametrize("fused", ["force", "0"])
+@pytest.mark.parametrize("fused", [2, 0])
 @pytest.mark.parametrize("profile", [0, 1])
 @pytest.mark.parametrize("name", SHAPES + ["noise"])
-def test_fused_detect_parity(pkg, oracle, monkeypatch, fused, profile, name):
+def test_fused_detect_parity(pkg, oracle, fused, profile, name):
     """Keypoints (count, emission order, values) and descriptors vs the
     oracle with and without the fused pass."""
     from test_gpu_parity import assert_parity
-    monkeypatch.setenv("SIFT_MI_FUSED_DETECT", fused)
     img = _frame(name)
     c = pkg.Context(0, pkg.OpenCVProcessing if profile == 0 else pkg.ImageprocProcessing)
+    c.set_path_option("fused_detect", fused)
     res = c.sift(img)
     c.close()
     kp_o, desc_o, ext_o = oracle.sift(img, profile=profile, internal=True)
     assert_parity(pkg, res, kp_o, desc_o, ext_o)
 
 
-def test_batch_pyramid_multi_frame(pkg, oracle, monkeypatch):
+def test_batch_pyramid_multi_frame(pkg, oracle):
     """Frames of one chunk (the fused pass's frame index and image stride):
     every frame's planes of a 5-frame single-chunk batch equal the oracle's."""
     import synth
-    monkeypatch.setenv("SIFT_MI_FUSED_DETECT", "force")
     fr = synth.frames(5, 320, 240, seed0=21)
     c = pkg.Context(0, pkg.OpenCVProcessing)
+    c.set_path_option("fused_detect", 2)
     c.set_chunk(5)
     got = c.sift_batch(fr)
     for i in (0, 2, 4):
@@ -86,7 +87,9 @@ def test_batch_pyramid_multi_frame(pkg, oracle, monkeypatch):
 
 
 def test_read_batch_scale_space_state(pkg):
-    """The read-back is refused when the last call ran as several chunks."""
+    """The read-back is refused when the last call ran as several chunks, and
+    after any later call (a precompute rewrites the arena: ADVICE r04); a
+    frame past the chunk and dims that are not the octave's are rejected."""
     import synth
     fr = synth.frames(4, 96, 64, seed0=3)
     c = pkg.Context(0, pkg.OpenCVProcessing)
@@ -95,4 +98,19 @@ def test_read_batch_scale_space_state(pkg):
         c.read_batch_scale_space(0, 0, (192, 128))
     c.sift(fr[0])
     assert c.read_batch_scale_space(0, 0, (192, 128)).shape == (6, 128, 192)
+    assert c.read_batch_scale_space(0, 1).shape == (6, 64, 96)
+    with pytest.raises(ValueError):
+        c.read_batch_scale_space(0, 0, (96, 64))
+    with pytest.raises(pkg.SiftMiError):
+        c.read_batch_scale_space(1, 0)
+    c.set_chunk(4)
+    c.sift_batch(fr)  # one chunk of 4 frames
+    assert c.read_batch_scale_space(3, 0).shape == (6, 128, 192)
+    c.precompute_images(synth.frame(48, 40, 1))  # other size: the plan is rebuilt
+    with pytest.raises(pkg.SiftMiError):
+        c.read_batch_scale_space(3, 0)
+    c.sift_batch(fr)
+    c.precompute_images(fr[1])  # same size: arena 0 rewritten in place
+    with pytest.raises(pkg.SiftMiError):
+        c.read_batch_scale_space(0, 0)
     c.close()

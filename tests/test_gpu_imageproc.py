@@ -73,7 +73,7 @@ def test_ip_batch_and_limit(pkg, ctx_ip, oracle):
 @pytest.mark.parametrize("kernel", ["strip", "tile", "notail", "nopair", "noseedpair"])
 @pytest.mark.parametrize("name", ["synth_640x480", "synth_301x207", "synth_1000x333", "synth_90x700",
                                   "synth_2000x40", "synth_97x61"])
-def test_ip_pyramid_kernels(ctx_ip, oracle, monkeypatch, kernel, name):
+def test_ip_pyramid_kernels(ctx_ip, oracle, kernel, name):
     """The imageproc profile's kernel families bit for bit against the oracle:
     "strip" (k_seed_pair<3, 3, imageproc>: the Triangle 2x upsample, vertical
     then horizontal, clamped, in the strip loader, then the seed blur and
@@ -84,34 +84,32 @@ def test_ip_pyramid_kernels(ctx_ip, oracle, monkeypatch, kernel, name):
     tile blurs), "notail" (per-blur launches for the small octaves), "nopair"
     (single-blur strips for G_1, G_2), "noseedpair" (k_seed_strip, then
     octave 0 like the others)."""
-    from test_gpu_parity import _KERNEL_ENV, _extra
-    for k, v in _KERNEL_ENV[kernel].items():
-        monkeypatch.setenv(k, v)
+    from test_gpu_parity import _KERNEL_OPTS, _extra
     img = INPUTS[name] if name in INPUTS else _extra(name)
-    pre = ctx_ip.precompute_images(img)
-    opy = oracle.Pyramid(img, PROFILE_IMAGEPROC)
-    assert pre.n_octaves == opy.n_octaves
-    for o in range(opy.n_octaves):
-        g, go = pre.scale_space_octave(o), opy.scale_space(o)
-        assert np.array_equal(g, go), (o, np.argwhere(g != go)[:5])
+    with ctx_ip.path_options(**_KERNEL_OPTS[kernel]):
+        pre = ctx_ip.precompute_images(img)
+        opy = oracle.Pyramid(img, PROFILE_IMAGEPROC)
+        assert pre.n_octaves == opy.n_octaves
+        for o in range(opy.n_octaves):
+            g, go = pre.scale_space_octave(o), opy.scale_space(o)
+            assert np.array_equal(g, go), (o, np.argwhere(g != go)[:5])
 
 
 @pytest.mark.parametrize("kernel", ["strip", "tile", "notail", "nopair", "noseedpair"])
 @pytest.mark.parametrize("shape", [(640, 480), (301, 207)])
-def test_ip_saturated_next_octave_clamp(ctx_ip, oracle, monkeypatch, kernel, shape):
+def test_ip_saturated_next_octave_clamp(ctx_ip, oracle, kernel, shape):
     """Large saturated (255) regions: a blur of 1.0s can round a hair past 1,
     and image's resize clamps its f32 output to [0, 1] -- the next octave's
     base (Nearest 1/2 of G_3) is clamped in every kernel family (strip pair,
     strip blur, tile blur, tail)."""
     import synth
-    from test_gpu_parity import _KERNEL_ENV
-    for k, v in _KERNEL_ENV[kernel].items():
-        monkeypatch.setenv(k, v)
+    from test_gpu_parity import _KERNEL_OPTS
     f = synth.frame(shape[0], shape[1], 9).astype(np.float32)
     img = np.clip(f * 2.0 - 60.0, 0, 255).astype(np.uint8)
     assert (img == 255).mean() > 0.1
-    pre = ctx_ip.precompute_images(img)
-    opy = oracle.Pyramid(img, PROFILE_IMAGEPROC)
-    for o in range(opy.n_octaves):
-        g, go = pre.scale_space_octave(o), opy.scale_space(o)
-        assert np.array_equal(g, go), (o, np.argwhere(g != go)[:5])
+    with ctx_ip.path_options(**_KERNEL_OPTS[kernel]):
+        pre = ctx_ip.precompute_images(img)
+        opy = oracle.Pyramid(img, PROFILE_IMAGEPROC)
+        for o in range(opy.n_octaves):
+            g, go = pre.scale_space_octave(o), opy.scale_space(o)
+            assert np.array_equal(g, go), (o, np.argwhere(g != go)[:5])

@@ -80,20 +80,20 @@ def test_pyramid_bit_exact(ctx, oracle, name):
         assert np.array_equal(d, do), (o, np.abs(d - do).max())
 
 
-_KERNEL_ENV = {
-    "strip": {"SIFT_MI_BLUR_KERNEL": "strip"},
-    "tile": {"SIFT_MI_BLUR_KERNEL": "tile"},
-    "nopair": {"SIFT_MI_PAIR": "0"},
-    "notail": {"SIFT_MI_TAIL": "0"},
-    "single": {"SIFT_MI_PAIR": "0", "SIFT_MI_TAIL": "0"},
-    "noseedpair": {"SIFT_MI_SEED_PAIR": "0"},
+_KERNEL_OPTS = {
+    "strip": {},
+    "tile": {"tile_blur": 1},
+    "nopair": {"pair_blur": 0},
+    "notail": {"tail": 0},
+    "single": {"pair_blur": 0, "tail": 0},
+    "noseedpair": {"seed_pair": 0},
 }
 
 
-@pytest.mark.parametrize("kernel", sorted(_KERNEL_ENV))
+@pytest.mark.parametrize("kernel", sorted(_KERNEL_OPTS))
 @pytest.mark.parametrize("name", ["synth_640x480", "synth_301x207", "synth_97x61", "synth_1000x333",
                                   "synth_90x700", "synth_2000x40", "synth_33x17"])
-def test_pyramid_blur_kernels(ctx, oracle, monkeypatch, kernel, name):
+def test_pyramid_blur_kernels(ctx, oracle, kernel, name):
     """Every blur kernel family against the oracle's blur chain, bit for bit:
     "strip" (the default: k_seed_pair for G_0, G_1 of octave 0 and the
     k_blur2_strip (6, 8) pair for its G_2, G_3 and the next octave's base,
@@ -102,22 +102,21 @@ def test_pyramid_blur_kernels(ctx, oracle, monkeypatch, kernel, name):
     chunks, many row segments per octave at these sizes, partial strips,
     reflect-101 at every border -- and k_octave_tail from the first octave that
     fits LDS; the tile kernels where a strip does not apply: tiny octaves, W
-    or H <= R), "tile" (SIFT_MI_BLUR_KERNEL=tile: one 64-column tile per
-    workgroup everywhere), "nopair" / "notail" / "single" (SIFT_MI_PAIR=0,
-    SIFT_MI_TAIL=0: single-blur strips instead of the pair kernel, per-blur
-    launches for the small octaves), "noseedpair" (SIFT_MI_SEED_PAIR=0:
+    or H <= R), "tile" (path option tile_blur: one 64-column tile per
+    workgroup everywhere), "nopair" / "notail" / "single" (pair_blur = 0,
+    tail = 0: single-blur strips instead of the pair kernel, per-blur
+    launches for the small octaves), "noseedpair" (seed_pair = 0:
     k_seed_strip, then octave 0 like the others)."""
-    for k, v in _KERNEL_ENV[kernel].items():
-        monkeypatch.setenv(k, v)
     img = INPUTS[name] if name in INPUTS else _extra(name)
-    pre = ctx.precompute_images(img)
-    opy = oracle.Pyramid(img)
-    assert pre.n_octaves == opy.n_octaves
-    for o in range(opy.n_octaves):
-        g, go = pre.scale_space_octave(o), opy.scale_space(o)
-        assert np.array_equal(g, go), (o, np.argwhere(g != go)[:5])
-        d, do = pre.dog_octave(o), opy.dog(o)
-        assert np.array_equal(d, do), (o, np.argwhere(d != do)[:5])
+    with ctx.path_options(**_KERNEL_OPTS[kernel]):
+        pre = ctx.precompute_images(img)
+        opy = oracle.Pyramid(img)
+        assert pre.n_octaves == opy.n_octaves
+        for o in range(opy.n_octaves):
+            g, go = pre.scale_space_octave(o), opy.scale_space(o)
+            assert np.array_equal(g, go), (o, np.argwhere(g != go)[:5])
+            d, do = pre.dog_octave(o), opy.dog(o)
+            assert np.array_equal(d, do), (o, np.argwhere(d != do)[:5])
 
 
 def _extra(name):
@@ -171,9 +170,10 @@ def test_golden_snapshots_gpu(pkg, ctx, oracle):
         # default mode: measured on MI355X (round 3) at the exact mode's max |d|
         # of 1 and 98.35 % / 97.33 % identical rows (tree / bird; exact mode
         # 98.35 / 97.78 %): its own +-1 does not stack on the oracle's here.
-        # The bound leaves a few rows of slack (bird: 0.96 = 9 of 225 rows
-        # differing, measured 6) for the fast path's summation order.
-        for c, min_desc, max_d in ((ctx, 0.96, 1), (ex, MIN_DESC_EQUAL, 1)):
+        # Bound 0.97 (bird: 219 / 225 rows measured = 0.9733; the round-4
+        # pre-emptive 0.96 is withdrawn): a change of the fast path's
+        # summation order that costs rows shows up.
+        for c, min_desc, max_d in ((ctx, 0.97, 1), (ex, MIN_DESC_EQUAL, 1)):
             res = c.sift(g["image"])
             assert len(res) == count
             order = pkg.stable_sort_xy_size(res.keypoints_array)
