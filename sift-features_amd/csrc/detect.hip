@@ -117,506 +117,6 @@ __device__ __forceinline__ bool interpolate(const gfloat* g0, size_t P, int W, i
 }
 
 // ---------------------------------------------------------------------------
-// k_detect_rows: point_is_local_extremum (src/lib.rs:437-506) over all three
-// scale triples of an octave, with no LDS staging.  A wave owns a strip of 64
-// columns (62 outputs: lanes 1..62, the edge lanes are halo) and DR_SH rows;
-// it walks down the strip, loading one row of the 5 DoG planes per step (one
-// coalesced 256-B load per plane), forming the 3-wide row max / min with DPP
-// wave shifts and keeping the last 3 rows in registers.  Every DoG byte is
-// read ~1.1x, there are no barriers, and the loads of the next row are in
-// flight while a row is tested.  (A 64x16-tile kernel staging the 5 planes
-// in LDS ran 1.8x longer: latency-bound, 62% of wave cycles waiting.)
-// Extrema are appended as packed emission keys for k_refine.
-// ---------------------------------------------------------------------------
-constexpr int DR_SH = 32;       // rows per strip
-constexpr int DR_COLS = 62;     // output columns per wave
-constexpr int DR_LCAP = 256;    // per-block LDS candidate list
-
-__device__ __forceinline__ float dpp_from_left(float v) {  // lane i <- lane i - 1 (wave_shr:1)
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x138, 0xf, 0xf, false));
-}
-__device__ __forceinline__ float dpp_from_right(float v) {  // lane i <- lane i + 1 (wave_shl:1)
-    return __int_as_float(__builtin_amdgcn_update_dpp(0, __float_as_int(v), 0x130, 0xf, 0xf, false));
-}
-
-// 73 VGPRs, 6 waves per SIMD; forcing 7 spills in the row loop (+30% time)
-#ifndef SIFT_DETECT_WPE
-#define SIFT_DETECT_WPE 1
-#endif
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_DETECT_WPE))) void k_detect_rows(const DetectLaunch ML) {
-    __shared__ uint64_t lcand[DR_LCAP];
-    __shared__ uint32_t lcount, gbase;
-    // this block's octave (block-uniform: a scan of <= 16 block offsets)
-    int oi = 0;
-    while (oi + 1 < ML.n_oct && blockIdx.x >= ML.block0[oi + 1]) oi++;
-    const DetectOctave& L = ML.oct[oi];
-    const int W = L.W, H = L.H, pitch = L.pitch;
-    const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int nsx = (W + DR_COLS - 1) / DR_COLS, nsy = (L.y_hi - L.y_lo + DR_SH - 1) / DR_SH;
-    const uint32_t g = (blockIdx.x - ML.block0[oi]) * 4 + wave;  // strip index: frame-major, then row band, then column
-    const uint32_t per = (uint32_t)(nsx * nsy);
-    const int b = (int)(g / per);
-    const uint32_t rem = g - (uint32_t)b * per;
-    const int sy = (int)(rem / nsx), sx = (int)(rem % nsx);
-    if (tid == 0) lcount = 0;
-    __syncthreads();
-    if (b < ML.n_img) {
-        const float* gb = L.gauss + (size_t)b * L.img_stride;
-        const size_t P = (size_t)pitch * H;
-        const int x = sx * DR_COLS - 1 + lane;  // this lane's column
-        const int xc = min(max(x, 0), W - 1);
-        const bool xout = lane >= 1 && lane <= DR_COLS && x >= kImageBorder && x < W - kImageBorder;
-        const int y0 = L.y_lo + sy * DR_SH, y1 = min(y0 + DR_SH, L.y_hi);
-        // rolling state per plane: row max / min of rows y - 1, y, y + 1
-        float hmx[kDogPerOctave][3], hmn[kDogPerOctave][3];
-        float lrx[kDogPerOctave], lrn[kDogPerOctave], ctr[kDogPerOctave];  // row y (middle planes used)
-        float nv[kImagesPerOctave], nlx[kDogPerOctave], nln[kDogPerOctave];
-        // one row of G_0..G_5; the loads of row y + 2 stay in flight as raw
-        // Gaussians and become D values (to_dog) when the row is consumed
-        auto load_row = [&](int yy, float (&g)[kImagesPerOctave]) {
-            const gfloat* rp = as_global(gb) + (size_t)min(max(yy, 0), H - 1) * pitch + xc;
-#pragma unroll
-            for (int p = 0; p < kImagesPerOctave; p++) g[p] = rp[(size_t)p * P];
-        };
-        auto to_dog = [&](const float (&g)[kImagesPerOctave], float (&v)[kDogPerOctave]) {
-#pragma unroll
-            for (int p = 0; p < kDogPerOctave; p++) v[p] = g[p + 1] - g[p];
-        };
-        auto row_stats = [&](const float (&v)[kDogPerOctave], float (&mx)[kDogPerOctave], float (&mn)[kDogPerOctave],
-                             float (&lx)[kDogPerOctave], float (&ln)[kDogPerOctave]) {
-#pragma unroll
-            for (int p = 0; p < kDogPerOctave; p++) {
-                const float l = dpp_from_left(v[p]), r = dpp_from_right(v[p]);
-                lx[p] = fmaxf(l, r);
-                ln[p] = fminf(l, r);
-                mx[p] = fmaxf(lx[p], v[p]);
-                mn[p] = fminf(ln[p], v[p]);
-            }
-        };
-        float v[kDogPerOctave], m0[kDogPerOctave], n0[kDogPerOctave];
-        // rows y0 - 1 and y0
-        load_row(y0 - 1, nv);
-        to_dog(nv, v);
-        row_stats(v, m0, n0, nlx, nln);
-#pragma unroll
-        for (int p = 0; p < kDogPerOctave; p++) {
-            hmx[p][0] = m0[p];
-            hmn[p][0] = n0[p];
-        }
-        load_row(y0, nv);
-        to_dog(nv, v);
-        row_stats(v, m0, n0, lrx, lrn);
-#pragma unroll
-        for (int p = 0; p < kDogPerOctave; p++) {
-            hmx[p][1] = m0[p];
-            hmn[p][1] = n0[p];
-            ctr[p] = v[p];
-        }
-        const float threshold = floorf(0.5f * kContrastThreshold / (float)kScalesPerOctave);
-        // Two rows in flight (rows y + 1 and y + 2 while row y is tested) in
-        // two alternating buffers -- the loop is unrolled by two so neither
-        // buffer is copied while its loads are outstanding.
-        float nv2[kImagesPerOctave];
-        load_row(y0 + 1, nv);
-        load_row(y0 + 2, nv2);
-        auto step = [&](int y, float (&buf)[kImagesPerOctave]) {
-            // row y + 1 arrived in buf; row y + 3 goes in flight into it
-            float cur[kDogPerOctave];
-            to_dog(buf, cur);
-            if (y + 2 < y1) load_row(y + 3, buf);
-            row_stats(cur, m0, n0, nlx, nln);
-#pragma unroll
-            for (int p = 0; p < kDogPerOctave; p++) {
-                hmx[p][2] = m0[p];
-                hmn[p][2] = n0[p];
-            }
-            // point_is_local_extremum for row y, scales 1..3
-            const bool yin = xout && y >= kImageBorder && y < H - kImageBorder;
-            float pmx[kDogPerOctave], pmn[kDogPerOctave];
-#pragma unroll
-            for (int p = 0; p < kDogPerOctave; p++) {
-                pmx[p] = fmaxf(fmaxf(hmx[p][0], hmx[p][1]), hmx[p][2]);
-                pmn[p] = fminf(fminf(hmn[p][0], hmn[p][1]), hmn[p][2]);
-            }
-            uint32_t ok3 = 0;
-#pragma unroll
-            for (int s_in = 1; s_in <= kScalesPerOctave; s_in++) {
-                const float val = ctr[s_in];
-                const float m8 = fmaxf(fmaxf(hmx[s_in][0], hmx[s_in][2]), lrx[s_in]);
-                const float n8 = fminf(fminf(hmn[s_in][0], hmn[s_in][2]), lrn[s_in]);
-                const float mx = fmaxf(fmaxf(pmx[s_in - 1], pmx[s_in + 1]), m8);
-                const float mn = fminf(fminf(pmn[s_in - 1], pmn[s_in + 1]), n8);
-                const bool ok = yin && fabsf(val) > threshold && (val > 0.0f ? val >= mx : val <= mn);
-                ok3 |= (uint32_t)ok << (s_in - 1);
-            }
-            if (__ballot(ok3 != 0)) {  // wave-uniform: rare
-                while (ok3) {
-                    const int bit = __builtin_ctz(ok3);
-                    ok3 &= ok3 - 1;
-                    const uint64_t key = make_key((uint32_t)(ML.img_base + b), (uint32_t)L.octave,
-                                                  (uint32_t)(bit + 1), (uint32_t)y, (uint32_t)x);
-                    const uint32_t li = atomicAdd(&lcount, 1u);
-                    if (li < DR_LCAP) {
-                        lcand[li] = key;
-                    } else {
-                        const uint32_t slot = atomicAdd(ML.counter, 1u);
-                        if (slot < ML.cap) ML.cand[slot] = key;
-                    }
-                }
-            }
-            // shift rows: y + 1 becomes the centre row
-#pragma unroll
-            for (int p = 0; p < kDogPerOctave; p++) {
-                hmx[p][0] = hmx[p][1];
-                hmn[p][0] = hmn[p][1];
-                hmx[p][1] = hmx[p][2];
-                hmn[p][1] = hmn[p][2];
-                lrx[p] = nlx[p];
-                lrn[p] = nln[p];
-                ctr[p] = cur[p];
-            }
-        };
-        for (int y = y0; y < y1; y += 2) {
-            step(y, nv);
-            if (y + 1 < y1) step(y + 1, nv2);
-        }
-    }
-    // one global atomic per block, then a coalesced copy of the block's list
-    __syncthreads();
-    const uint32_t nl = lcount < DR_LCAP ? lcount : DR_LCAP;
-    if (nl == 0) return;
-    if (tid == 0) gbase = atomicAdd(ML.counter, nl);
-    __syncthreads();
-    for (uint32_t i = tid; i < nl; i += 256)
-        if (gbase + i < ML.cap) ML.cand[gbase + i] = lcand[i];
-}
-
-void launch_detect(DetectLaunch& L, hipStream_t st) {
-    // drop empty octaves, then lay the octaves' blocks end to end
-    int k = 0;
-    for (int i = 0; i < L.n_oct; i++) {
-        const DetectOctave& d = L.oct[i];
-        if (d.y_lo < 0 || d.y_hi > d.H || d.y_hi <= d.y_lo) continue;
-        L.oct[k++] = d;
-    }
-    L.n_oct = k;
-    uint32_t nb = 0;
-    for (int i = 0; i < k; i++) {
-        const DetectOctave& d = L.oct[i];
-        L.block0[i] = nb;
-        const uint32_t strips =
-            (uint32_t)((d.W + DR_COLS - 1) / DR_COLS) * ((d.y_hi - d.y_lo + DR_SH - 1) / DR_SH) * L.n_img;
-        nb += (strips + 3) / 4;
-    }
-    L.block0[k] = nb;
-    if (nb == 0) return;
-    hipLaunchKernelGGL(k_detect_rows, dim3(nb), dim3(256), 0, st, L);
-}
-
-// ---------------------------------------------------------------------------
-// k_blur_detect: the octave's last blur (G_4 -> G_5, radius R) and the
-// extremum scan of its three scales (point_is_local_extremum,
-// src/lib.rs:437-506) in one pass.  G_5 is produced on chip, so the scan
-// reads G_0..G_4 (G_4 from the blur's own LDS rows) and never reads G_4 /
-// G_5 back from HBM: ~26 B per octave pixel for blur 5 and detection
-// together instead of ~35 (blur 5: 8 + halo, k_detect_rows: 24 + halo).
-//
-// A wave owns k_detect_rows' strip geometry: 64 columns x = xb - 1 + lane
-// (62 outputs, the edge lanes are halo) by a segment of rows [ya, yb), and
-// walks down it one row of G_4 at a time:
-//   * the G_4 row's 64 + 2R columns [xb - 1 - R, xb + 63 + R) go to an LDS
-//     ring (BD_RING rows per wave; loaded two rows ahead), and each lane's
-//     row-filter output at its column is the FMA chain from the leftmost tap
-//     of OpenCV's RowFilter (imageproc: the unfused chain) over 2R + 1 ring
-//     values -- the same operations as the strip kernels (pyramid.hip);
-//   * the last 2R + 1 row-filter outputs are a register window, whose column
-//     filter (centre product + fma of the pair sums / imageproc's unfused
-//     chain) is G_5 at row r = q - R: stored (rows [ya, yb), lanes 1..62);
-//   * row r's D_0..D_4 are formed from G_0..G_3 (loaded two rows ahead),
-//     G_4 (its ring row, still resident) and G_5, and the 3x3x3 test of row
-//     r - 1 runs on the rolling row max / min exactly as k_detect_rows.
-// Rows and columns outside the image are reflect-101 (clamp-to-edge) like the
-// strip blur; only rows inside the image are stored or tested, so G_5 and the
-// candidates are those of launch_blur + k_detect_rows bit for bit.
-// ---------------------------------------------------------------------------
-constexpr int BD_RING = 16;  // raw G_4 rows per wave (the rows r .. r + R and the next)
-constexpr int BD_RP = 100;   // ring row pitch (floats): 64 + 2R columns, R <= 18
-
-template <int P>
-__device__ __forceinline__ int bd_index(int p, int n) {
-    if (P == kProfileOpenCV) p = p < 0 ? -p : (p >= n ? 2 * n - 2 - p : p);
-    return p < 0 ? 0 : (p >= n ? n - 1 : p);
-}
-
-// 1-D block id remapped so each XCD walks a contiguous range (neighbouring
-// strips of one row segment share their G_4 halo columns in that XCD's L2)
-__device__ __forceinline__ uint32_t xcd_block_1d() {
-    const uint32_t nwg = gridDim.x, orig = blockIdx.x;
-    const uint32_t q = nwg / 8, r = nwg % 8, xcd = orig % 8;
-    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
-}
-
-template <int R, int P>
-__global__ __launch_bounds__(256) void k_blur_detect(const BlurDetectLaunch L) {
-    static_assert(64 + 2 * R <= BD_RP && R + 3 <= BD_RING, "ring geometry");
-    __shared__ float ring[4][BD_RING * BD_RP];
-    __shared__ uint64_t lcand[DR_LCAP];
-    __shared__ uint32_t lcount, gbase;
-    // the wave index through readfirstlane: everything derived from it (the
-    // strip, its rows, the buffer row offsets) is then known to be uniform
-    // and lives in SGPRs -- a soffset the compiler cannot prove uniform turns
-    // every buffer access into a readfirstlane waterfall loop
-    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
-    const int W = L.W, H = L.H, pitch = L.pitch;
-    const uint32_t g = xcd_block_1d() * 4 + wave;  // strip index: frame-major, then row segment, then column
-    const uint32_t per = (uint32_t)(L.nsx * L.nsy);
-    const int b = (int)(g / per);
-    const uint32_t rem = g - (uint32_t)b * per;
-    const int sy = (int)(rem / (uint32_t)L.nsx), sx = (int)(rem % (uint32_t)L.nsx);
-    if (tid == 0) lcount = 0;
-    __syncthreads();
-    if (b < L.n_img) {
-        const size_t P_ = (size_t)pitch * H;
-        const uint32_t pb = (uint32_t)P_ * 4u;  // plane bytes (< 2^31: launch_blur_detect)
-        const float* gb = L.gauss + (size_t)b * L.img_stride;
-        const __amdgpu_buffer_rsrc_t rg0 = uniform_rsrc(gb, pb), rg1 = uniform_rsrc(gb + P_, pb),
-                                     rg2 = uniform_rsrc(gb + 2 * P_, pb), rg3 = uniform_rsrc(gb + 3 * P_, pb),
-                                     rg4 = uniform_rsrc(gb + 4 * P_, pb), rg5 = uniform_rsrc(gb + 5 * P_, pb);
-        const int xb = sx * DR_COLS;
-        const int x = xb - 1 + lane;  // this lane's column
-        const int xc = min(max(x, 0), W - 1);
-        const bool xout = lane >= 1 && lane <= DR_COLS && x >= kImageBorder && x < W - kImageBorder;
-        const bool xst = lane >= 1 && lane <= DR_COLS && x < W;
-        const int ya = sy * L.seg, yb = min(ya + L.seg, H);
-        // G_4 ring columns [xb - 1 - R, xb + 63 + R): lane -> column ca, and
-        // lanes < 2R also ca + 64
-        const int ca = xb - 1 - R + lane;
-        const int va = bd_index<P>(ca, W) * 4, vb = bd_index<P>(ca + 64, W) * 4, vx = xc * 4;
-        float* rg = ring[wave];
-        auto ld4 = [&](int q, float& a, float& c) {  // G_4 row q (reflected) into registers
-            const int so = bd_index<P>(q, H) * pitch * 4;
-            // both loads on every lane (vb is clamped into the row): an
-            // exec-masked load sits behind a skip branch, which makes the
-            // compiler's load-counter waits conservative
-            a = buffer_load_f32(rg4, va, so);
-            c = buffer_load_f32(rg4, vb, so);
-        };
-        auto ld03 = [&](int r, float (&d)[4]) {  // G_0..G_3 at (row r clamped, column xc)
-            const int so = min(max(r, 0), H - 1) * pitch * 4;
-            d[0] = buffer_load_f32(rg0, vx, so);
-            d[1] = buffer_load_f32(rg1, vx, so);
-            d[2] = buffer_load_f32(rg2, vx, so);
-            d[3] = buffer_load_f32(rg3, vx, so);
-        };
-        // row filter of G_4 row q at this lane's column (q's ring row)
-        auto rowpass = [&](int q) -> float {
-            const float* p = rg + (q & (BD_RING - 1)) * BD_RP + lane;
-            float v[2 * R + 1];
-#pragma unroll
-            for (int t = 0; t <= 2 * R; t++) v[t] = p[t];
-            float acc = v[0] * L.taps.k[R];
-#pragma unroll
-            for (int t = 1; t <= 2 * R; t++) {
-                const float kt = L.taps.k[t > R ? t - R : R - t];
-                acc = P == kProfileOpenCV ? __builtin_fmaf(v[t], kt, acc) : acc + v[t] * kt;
-            }
-            return acc;
-        };
-        float win[2 * R + 1];  // row-filter outputs of rows r - R .. r + R
-        // rolling detection state (k_detect_rows): row max / min of rows r - 2,
-        // r - 1, r per DoG plane, the left / right max / min and centre of row r - 1
-        float hmx[kDogPerOctave][3], hmn[kDogPerOctave][3];
-        float lrx[kDogPerOctave], lrn[kDogPerOctave], ctr[kDogPerOctave];
-        const float threshold = floorf(0.5f * kContrastThreshold / (float)kScalesPerOctave);
-        const int q0 = ya - 1 - R, q1 = yb + R;  // G_4 rows filtered: [q0, q1]
-        // Row data of one G_4 row q: its ring columns (a, c) and G_0..G_3 of
-        // row r = q - R at this lane's column (the window-filling rows r <
-        // ya - 1 load rows ya - 1 / ya instead; rows past the end re-load
-        // the last one).  Four buffers: the two rows of a half-iteration are
-        // processed from one pair while the next two rows' loads, issued at the
-        // top of the half, are in flight into the other pair.  Every half
-        // issues the same memory operations (a G_5 row outside the segment is
-        // stored to an offset the buffer drops), so the compiler's load-counter
-        // waits are static: each waits for loads issued a half-iteration
-        // earlier, never for the ones just issued.
-        struct RowBuf {
-            float a, c, d[4];
-        };
-        auto load = [&](int q, RowBuf& B, int par) {
-            const int qq = min(q, q1), r = qq - R;
-            ld4(qq, B.a, B.c);
-            ld03(r >= ya - 1 ? min(r, yb) : ya - 1 + par, B.d);
-        };
-        auto shift = [&]() {
-#pragma unroll
-            for (int j = 0; j < 2 * R; j++) win[j] = win[j + 1];
-        };
-        // G_4 row q from B into the ring, row-filtered into win[2R]; once the
-        // window holds rows r - R .. r + R (r = q - R >= ya - 1): G_5 of row r,
-        // row r's DoG values, the test of row r - 1.  Steps past q1 only
-        // issue their (dropped) store.
-        auto step = [&](int q, const RowBuf& B) {
-            const bool on = q <= q1;  // uniform
-            const int r = q - R;
-            float g5 = 0.0f;
-            if (on) {
-                float* wp = rg + (q & (BD_RING - 1)) * BD_RP;
-                wp[lane] = B.a;
-                if (lane < 2 * R) wp[64 + lane] = B.c;
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-                win[2 * R] = rowpass(q);
-                if constexpr (P == kProfileOpenCV) {
-                    g5 = win[R] * L.taps.k[0];
-#pragma unroll
-                    for (int t = 1; t <= R; t++) g5 = __builtin_fmaf(win[R + t] + win[R - t], L.taps.k[t], g5);
-                } else {
-                    g5 = win[0] * L.taps.k[R];
-#pragma unroll
-                    for (int t = 1; t <= 2 * R; t++) g5 = g5 + win[t] * L.taps.k[t > R ? t - R : R - t];
-                }
-            }
-            const uint32_t bad = (on && xst && r >= ya && r < yb) ? 0u : 0xfffffff0u;  // past every plane: dropped
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, g5), rg5,
-                                                  ((uint32_t)(r * pitch * 4) + (uint32_t)vx) | bad, 0, 2 /* nt */);
-            if (!(on && r >= ya - 1)) {  // uniform
-                shift();
-                return;
-            }
-            // row r's DoG values (G_4 from the ring: row r is resident)
-            const float g4 = rg[(r & (BD_RING - 1)) * BD_RP + lane + R];
-            float cur[kDogPerOctave];
-            cur[0] = B.d[1] - B.d[0];
-            cur[1] = B.d[2] - B.d[1];
-            cur[2] = B.d[3] - B.d[2];
-            cur[3] = g4 - B.d[3];
-            cur[4] = g5 - g4;
-            float nlx[kDogPerOctave], nln[kDogPerOctave];
-#pragma unroll
-            for (int p = 0; p < kDogPerOctave; p++) {
-                const float l = dpp_from_left(cur[p]), rr = dpp_from_right(cur[p]);
-                nlx[p] = fmaxf(l, rr);
-                nln[p] = fminf(l, rr);
-                hmx[p][2] = fmaxf(nlx[p], cur[p]);
-                hmn[p][2] = fminf(nln[p], cur[p]);
-            }
-            const int y = r - 1;  // tested row: rows r - 2, r - 1, r are in
-            if (y >= ya) {        // uniform
-                const bool yin = xout && y >= kImageBorder && y < H - kImageBorder;
-                float pmx[kDogPerOctave], pmn[kDogPerOctave];
-#pragma unroll
-                for (int p = 0; p < kDogPerOctave; p++) {
-                    pmx[p] = fmaxf(fmaxf(hmx[p][0], hmx[p][1]), hmx[p][2]);
-                    pmn[p] = fminf(fminf(hmn[p][0], hmn[p][1]), hmn[p][2]);
-                }
-                uint32_t ok3 = 0;
-#pragma unroll
-                for (int s_in = 1; s_in <= kScalesPerOctave; s_in++) {
-                    const float val = ctr[s_in];
-                    const float m8 = fmaxf(fmaxf(hmx[s_in][0], hmx[s_in][2]), lrx[s_in]);
-                    const float n8 = fminf(fminf(hmn[s_in][0], hmn[s_in][2]), lrn[s_in]);
-                    const float mx = fmaxf(fmaxf(pmx[s_in - 1], pmx[s_in + 1]), m8);
-                    const float mn = fminf(fminf(pmn[s_in - 1], pmn[s_in + 1]), n8);
-                    const bool ok = yin && fabsf(val) > threshold && (val > 0.0f ? val >= mx : val <= mn);
-                    ok3 |= (uint32_t)ok << (s_in - 1);
-                }
-                if (__ballot(ok3 != 0)) {  // wave-uniform: rare
-                    while (ok3) {
-                        const int bit = __builtin_ctz(ok3);
-                        ok3 &= ok3 - 1;
-                        const uint64_t key = make_key((uint32_t)(L.img_base + b), (uint32_t)L.octave,
-                                                      (uint32_t)(bit + 1), (uint32_t)y, (uint32_t)x);
-                        const uint32_t li = atomicAdd(&lcount, 1u);
-                        if (li < DR_LCAP) {
-                            lcand[li] = key;
-                        } else {
-                            const uint32_t slot = atomicAdd(L.counter, 1u);
-                            if (slot < L.cap) L.cand[slot] = key;
-                        }
-                    }
-                }
-            }
-#pragma unroll
-            for (int p = 0; p < kDogPerOctave; p++) {
-                hmx[p][0] = hmx[p][1];
-                hmn[p][0] = hmn[p][1];
-                hmx[p][1] = hmx[p][2];
-                hmn[p][1] = hmn[p][2];
-                lrx[p] = nlx[p];
-                lrn[p] = nln[p];
-                ctr[p] = cur[p];
-            }
-            shift();
-        };
-        // rows q, q + 1 from (A0, A1) while q + 2, q + 3 load into (B0, B1),
-        // then the other way round (even / odd rows: par 0 / 1)
-        RowBuf A0, A1, B0, B1;
-        load(q0, A0, 0);
-        load(q0 + 1, A1, 1);
-        for (int q = q0; q <= q1; q += 4) {
-            load(q + 2, B0, 0);
-            load(q + 3, B1, 1);
-            __builtin_amdgcn_sched_barrier(0);
-            step(q, A0);
-            step(q + 1, A1);
-            __builtin_amdgcn_sched_barrier(0);
-            load(q + 4, A0, 0);
-            load(q + 5, A1, 1);
-            __builtin_amdgcn_sched_barrier(0);
-            step(q + 2, B0);
-            step(q + 3, B1);
-            __builtin_amdgcn_sched_barrier(0);
-        }
-    }
-    // one global atomic per block, then a coalesced copy of the block's list
-    __syncthreads();
-    const uint32_t nl = lcount < DR_LCAP ? lcount : DR_LCAP;
-    if (nl == 0) return;
-    if (tid == 0) gbase = atomicAdd(L.counter, nl);
-    __syncthreads();
-    for (uint32_t i = tid; i < nl; i += 256)
-        if (gbase + i < L.cap) L.cand[gbase + i] = lcand[i];
-}
-
-// PathOpts::fused_detect: 0 keeps blur 5 and detection apart, 2 fuses every
-// octave it can at 32-row segments (test paths)
-int launch_blur_detect(int R, BlurDetectLaunch& L, hipStream_t st, const PathOpts& o) {
-    if (o.fused_detect == 0) return -1;
-    const bool force = o.fused_detect == 2;
-    const bool ok = L.W > R + 1 && L.H > R + 1 && L.W >= 2 * kImageBorder && L.H >= 2 * kImageBorder &&
-                    (uint64_t)L.H * (uint64_t)L.pitch * 4 < (1ull << 31) && L.n_img > 0;
-    if (!ok) return -1;
-    const bool ocv = L.profile == kProfileOpenCV;
-    if (!((ocv && R == 13) || (!ocv && R == 7))) return -1;
-    L.nsx = (L.W + DR_COLS - 1) / DR_COLS;
-    // row segments: a segment re-filters 2R + 2 halo rows, so long ones, but
-    // enough waves to fill the chip (>= ~16 k).  A wave walks its segment row
-    // after row, so an octave too small for that at >= 64-row segments (one
-    // 1080p frame's octaves, a batch's small octaves) is left to launch_blur +
-    // k_detect_rows: there the fused pass is a chain of latency-bound row
-    // steps (one frame's octave 4: 54 us against 10 us for its blur 5)
-    int seg = 0;
-    for (int s : {256, 128, 64}) {
-        if ((long)L.nsx * ((L.H + s - 1) / s) * L.n_img >= 16384) {
-            seg = s;
-            break;
-        }
-    }
-    if (force) seg = 32;  // many segment boundaries on test-sized frames
-    if (!seg) return -1;
-    L.seg = seg;
-    L.nsy = (L.H + seg - 1) / seg;
-    const long waves = (long)L.nsx * L.nsy * L.n_img;
-    const dim3 grid((uint32_t)((waves + 3) / 4));
-    if (ocv)
-        hipLaunchKernelGGL((k_blur_detect<13, kProfileOpenCV>), grid, dim3(256), 0, st, L);
-    else
-        hipLaunchKernelGGL((k_blur_detect<7, kProfileImageproc>), grid, dim3(256), 0, st, L);
-    return 0;
-}
-
-// ---------------------------------------------------------------------------
 // k_refine: one thread per candidate extremum -- interpolate_extremum,
 // extremum_contrast, extremum_is_on_edge (src/lib.rs:334-367); accepted
 // extrema are appended with one atomic per wave.

@@ -1,0 +1,377 @@
+// Detection-stage micro-benchmarks (performance experiments only; not part of
+// libsift_mi.so): blur 4 / blur 5 strips, k_detect_rows, k_blur_detect and
+// k_refine on octave 0 of N 1080p frames (3840x2160 seed planes) of smooth
+// synthetic content, each launch timed alone with HIP events.  Build:
+//   hipcc --offload-arch=gfx950 -O3 -std=c++17 -ffp-contract=off -fno-honor-nans \
+//         tools/ubench_detect.hip -o tools/ubench_detect
+// (the scan kernels' flags; the refine kernels here do not depend on NaN
+// semantics for the timing A/B)
+#include "../sift-features_amd/csrc/detect.hip"
+#include "../sift-features_amd/csrc/scan.hip"
+#include "../sift-features_amd/csrc/pyramid.hip"
+
+#include <algorithm>
+#include <cmath>
+#include <cstring>
+#include <cstdio>
+#include <cstdlib>
+#include <vector>
+
+using namespace siftmi;
+
+// the round-4 k_refine (single-float DoG reads), for A/B
+namespace siftmi {
+struct DogViewOld {
+    const gfloat* g;  // G_0 of one frame's octave
+    size_t P;         // floats per plane
+    __device__ __forceinline__ float operator()(int s, size_t off) const {
+        return g[(size_t)(s + 1) * P + off] - g[(size_t)s * P + off];
+    }
+};
+
+__device__ __forceinline__ bool interpolate_old(const DogViewOld& dv, int W, int H, int pitch, int& scale, int& x, int& y,
+                                            float& os, float& ox, float& oy, uint32_t* band_flag, int vlo, int vhi) {
+    for (int it = 0; it < kMaxInterpSteps; it++) {
+        // row bands with a restricted pyramid (host.cpp run_pyramid): the
+        // rows read here must be computed ones, else the host recomputes the
+        // band on the whole-frame pyramid
+        if (band_flag && (y - 1 < vlo || y + 1 >= vhi)) atomicOr(band_flag, 1u);
+        const int prev = scale - 1, curr = scale, next = scale + 1;
+#define AT(a, yy, xx) dv(a, (size_t)(yy) * pitch + (xx))
+        const float g1 = (AT(next, y, x) - AT(prev, y, x)) / 2.f;
+        const float g2 = (AT(curr, y + 1, x) - AT(curr, y - 1, x)) / 2.f;
+        const float g3 = (AT(curr, y, x + 1) - AT(curr, y, x - 1)) / 2.f;
+        const float v2 = AT(curr, y, x) * 2.f;
+        const float h11 = AT(next, y, x) + AT(prev, y, x) - v2;
+        const float h12 = (AT(next, y + 1, x) - AT(next, y - 1, x) - AT(prev, y + 1, x) + AT(prev, y - 1, x)) / 4.f;
+        const float h13 = (AT(next, y, x + 1) - AT(next, y, x - 1) - AT(prev, y, x + 1) + AT(prev, y, x - 1)) / 4.f;
+        const float h22 = AT(curr, y + 1, x) + AT(curr, y - 1, x) - v2;
+        const float h33 = AT(curr, y, x + 1) + AT(curr, y, x - 1) - v2;
+        const float h23 =
+            (AT(curr, y + 1, x + 1) - AT(curr, y + 1, x - 1) - AT(curr, y - 1, x + 1) + AT(curr, y - 1, x - 1)) / 4.f;
+#undef AT
+        const float det =
+            h11 * h22 * h33 - h11 * h23 * h23 - h12 * h12 * h33 + 2.f * h12 * h13 * h23 - h13 * h13 * h22;
+        const float i11 = (h22 * h33 - h23 * h23) / det;
+        const float i12 = (h13 * h23 - h12 * h33) / det;
+        const float i13 = (h12 * h23 - h13 * h22) / det;
+        const float i22 = (h11 * h33 - h13 * h13) / det;
+        const float i23 = (h12 * h13 - h11 * h23) / det;
+        const float i33 = (h11 * h22 - h12 * h12) / det;
+        const float s_ = -(i11 * g1 + i12 * g2 + i13 * g3);
+        const float x_ = -(i13 * g1 + i23 * g2 + i33 * g3);
+        const float y_ = -(i12 * g1 + i22 * g2 + i23 * g3);
+        if (fabsf(s_) < 0.5f && fabsf(x_) < 0.5f && fabsf(y_) < 0.5f) {
+            os = s_;
+            ox = x_;
+            oy = y_;
+            return true;
+        }
+        // `x as isize + offset.round() as isize` (saturating), then bounds
+        const int64_t LIM = (int64_t)1 << 40;
+        const int64_t rx = sat_i64(roundf(x_)), ry = sat_i64(roundf(y_)), rs = sat_i64(roundf(s_));
+        if (rx > LIM || rx < -LIM || ry > LIM || ry < -LIM || rs > LIM || rs < -LIM) return false;
+        const int64_t nx = x + rx, ny = y + ry, ns = scale + rs;
+        if (!(ns >= 1 && ns <= kScalesPerOctave) || nx < kImageBorder || nx >= W - kImageBorder ||
+            ny < kImageBorder || ny >= H - kImageBorder)
+            return false;
+        x = (int)nx;
+        y = (int)ny;
+        scale = (int)ns;
+    }
+    return false;
+}
+
+__device__ __forceinline__ bool refine_one_old(const RefineLaunch& L, uint64_t key, ExtRec& e) {
+    const int b = (int)(key >> kKeyImgShift);
+    const int o = (int)((key >> kKeyOctShift) & 15);
+    const int s_in = (int)((key >> kKeyScaleShift) & 3);
+    const int y = (int)((key >> kKeyYShift) & kKeyCoordMask);
+    const int x = (int)((key >> kKeyXShift) & kKeyCoordMask);
+    const int W = L.ow[o], H = L.oh[o], pitch = L.opitch[o];
+    const DogViewOld dv{as_global(L.gauss[o]) + (size_t)(b - L.img_base) * L.g_img_stride[o], (size_t)pitch * H};
+    int sc = s_in, xi = x, yi = y;
+    float os, ox, oy;
+    int vlo = 0, vhi = H;  // rows of this octave's Gaussians that are exact
+    if (L.band_flag) {
+        vlo = max(0, (int)((uint64_t)H * L.band_r / L.band_n) - 1 - L.band_margin);
+        vhi = min(H, (int)((uint64_t)H * (L.band_r + 1) / L.band_n) + 1 + L.band_margin);
+    }
+    if (!interpolate_old(dv, W, H, pitch, sc, xi, yi, os, ox, oy, L.band_flag, vlo, vhi)) return false;
+    const size_t c = (size_t)yi * pitch + xi;
+    auto prev = [&](size_t off) { return dv(sc - 1, off); };
+    auto curr = [&](size_t off) { return dv(sc, off); };
+    auto next = [&](size_t off) { return dv(sc + 1, off); };
+    // extremum_contrast (src/lib.rs:606-626)
+    const float g1 = (next(c) - prev(c)) / 2.f;
+    const float g2 = (curr(c + pitch) - curr(c - pitch)) / 2.f;
+    const float g3 = (curr(c + 1) - curr(c - 1)) / 2.f;
+    const float interp = os * g1 + oy * g2 + ox * g3;
+    const float contrast = fabsf(curr(c) + interp / 2.f);
+    if (contrast * (float)kScalesPerOctave <= kContrastThreshold) return false;
+    // extremum_is_on_edge (src/lib.rs:630-653)
+    const float v2 = curr(c) * 2.0f;
+    const float h11 = curr(c + pitch) + curr(c - pitch) - v2;
+    const float d22 = curr(c + 1) + curr(c - 1) - v2;
+    const float h12 = (curr(c + pitch + 1) - curr(c + pitch - 1) - curr(c - pitch + 1) + curr(c - pitch - 1)) / 4.f;
+    const float tr = d22 + h11;
+    const float det = d22 * h11 - h12 * h12;
+    if (det <= 0.f) return false;
+    if ((tr * tr * kEdgeThreshold) > (kEdgeThreshold + 1.0f) * (kEdgeThreshold + 1.0f) * det) return false;
+    // an accepted keypoint's orientation / descriptor patch must be exact too
+    // (at the image's own top / bottom rows the patch reads clamp, so no limit)
+    if (L.band_flag && ((vlo > 0 && yi - L.band_patch < vlo) || (vhi < H && yi + L.band_patch >= vhi)))
+        atomicOr(L.band_flag, 1u);
+    e.key = key;
+    e.img = b;
+    e.octave = o;
+    e.scale = sc;
+    e.x = xi;
+    e.y = yi;
+    e.off_s = os;
+    e.off_x = ox;
+    e.off_y = oy;
+    e.response = contrast;
+    e.pad = 0;
+    return true;
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_REFINE_WPE))) void k_refine_old(const RefineLaunch L) {
+    const uint32_t n = min(*L.n_cand, L.cand_cap);
+    const int lane = threadIdx.x & 63;
+    for (uint32_t base = blockIdx.x * 256; base < n; base += gridDim.x * 256) {
+        const uint32_t i = base + threadIdx.x;
+        ExtRec e;
+        const bool keep = i < n && refine_one_old(L, L.cand[i], e);
+        const uint64_t mask = __ballot(keep);
+        if (!mask) continue;
+        const int leader = __ffsll((unsigned long long)mask) - 1;
+        uint32_t b = 0;
+        if (lane == leader) b = atomicAdd(L.counter, (uint32_t)__popcll(mask));
+        b = __shfl(b, leader);
+        const uint32_t slot = b + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+        if (keep && slot < L.cap) L.out[slot] = e;
+    }
+}
+
+}  // namespace siftmi
+
+#define CK(x)                                                                    \
+    do {                                                                         \
+        hipError_t e = (x);                                                      \
+        if (e != hipSuccess) {                                                   \
+            std::fprintf(stderr, "%s: %s\n", #x, hipGetErrorString(e));          \
+            std::exit(1);                                                        \
+        }                                                                        \
+    } while (0)
+
+// smooth blobs + a little noise, values in [0, 1]
+__global__ void k_fill_smooth(float* p, int W, int H, int pitch, size_t stride, int n) {
+    const size_t tot = (size_t)n * H * W;
+    for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < tot; i += (size_t)gridDim.x * 256) {
+        const int f = (int)(i / ((size_t)H * W));
+        const size_t r = i - (size_t)f * H * W;
+        const int y = (int)(r / W), x = (int)(r - (size_t)y * W);
+        uint32_t h = (uint32_t)i * 2654435761u;
+        h ^= h >> 15;
+        h *= 2246822519u;
+        h ^= h >> 13;
+        const float fx = x * 0.021f + f, fy = y * 0.017f - f;
+        float v = 0.5f + 0.2f * sinf(fx) * cosf(fy) + 0.1f * sinf(0.37f * fx + 1.3f * fy);
+        v += ((float)(h & 0xff) / 255.0f - 0.5f) * 0.02f;
+        p[(size_t)f * stride + (size_t)y * pitch + x] = fminf(fmaxf(v, 0.0f), 1.0f);
+    }
+}
+
+template <class F>
+float timeit(F f, int reps = 5) {
+    f();
+    CK(hipDeviceSynchronize());
+    hipEvent_t a, b;
+    CK(hipEventCreate(&a));
+    CK(hipEventCreate(&b));
+    CK(hipEventRecord(a));
+    for (int i = 0; i < reps; i++) f();
+    CK(hipEventRecord(b));
+    CK(hipEventSynchronize(b));
+    float ms;
+    CK(hipEventElapsedTime(&ms, a, b));
+    return ms / reps;
+}
+
+int main(int argc, char** argv) {
+    const int n = argc > 1 ? atoi(argv[1]) : 16;
+    const int W = 3840, H = 2160, pitch = 3840;
+    const size_t P = (size_t)pitch * H, stride = 6 * P;
+    float* g = nullptr;
+    CK(hipMalloc(&g, stride * n * sizeof(float)));
+    hipLaunchKernelGGL(k_fill_smooth, dim3(8192), dim3(256), 0, 0, g, W, H, pitch, stride, n);
+    // OpenCV octave sigmas (host.cpp octave_sigmas / cv_blur_taps): radii 5, 6, 8, 10, 13
+    const double sig[6] = {0, 1.2262735, 1.5450078, 1.9465878, 2.4525469, 3.0900155};
+    BlurTaps taps[6]{};
+    int rad[6]{};
+    for (int s = 1; s < 6; s++) {
+        const int nn = ((int)std::lrint(sig[s] * 8 + 1)) | 1, r = nn / 2;
+        const double scale2X = -0.125 / (sig[s] * sig[s]);
+        double vals[64], sum = 0;
+        for (int i = 0, x = 1 - nn; i < (nn - 1) / 2; i++, x += 2) {
+            vals[i] = std::exp((double)(x * x) * scale2X);
+            sum += vals[i];
+        }
+        sum = sum * 2 + 1;
+        taps[s].k[0] = (float)(1.0 / sum);
+        for (int i = 0; i < (nn - 1) / 2; i++) taps[s].k[r - i] = (float)(vals[i] / sum);
+        rad[s] = r;
+    }
+    auto blur = [&](int s) {
+        BlurLaunch B{};
+        B.src = g + (size_t)(s - 1) * P;
+        B.src_img_stride = stride;
+        B.dst = g + (size_t)s * P;
+        B.dst_img_stride = stride;
+        B.W = W;
+        B.H = H;
+        B.pitch = pitch;
+        B.n_img = n;
+        B.taps = taps[s];
+        B.profile = kProfileOpenCV;
+        return B;
+    };
+    for (int s = 1; s < 6; s++) CK((hipError_t)launch_blur(rad[s], blur(s), 0));
+    CK(hipDeviceSynchronize());
+    const double px = (double)W * H * n;
+    uint64_t* cand = nullptr;
+    uint32_t* cnt = nullptr;
+    const uint32_t cap = 1u << 26;
+    CK(hipMalloc(&cand, cap * sizeof(uint64_t)));
+    CK(hipMalloc(&cnt, 64));
+    const float t4 = timeit([&] { launch_blur(rad[4], blur(4), 0); });
+    const float t5 = timeit([&] { launch_blur(rad[5], blur(5), 0); });
+    DetectLaunch D{};
+    D.n_img = n;
+    D.cand = cand;
+    D.counter = cnt;
+    D.cap = cap;
+    D.n_oct = 1;
+    D.oct[0].gauss = g;
+    D.oct[0].img_stride = stride;
+    D.oct[0].W = W;
+    D.oct[0].H = H;
+    D.oct[0].pitch = pitch;
+    D.oct[0].y_lo = 0;
+    D.oct[0].y_hi = H;
+    const float td = timeit([&] {
+        CK(hipMemsetAsync(cnt, 0, 4, 0));
+        DetectLaunch d = D;
+        launch_detect(d, 0);
+    });
+    uint32_t nc_rows = 0;
+    CK(hipMemcpy(&nc_rows, cnt, 4, hipMemcpyDeviceToHost));
+    std::vector<uint64_t> c_rows(nc_rows);
+    CK(hipMemcpy(c_rows.data(), cand, nc_rows * 8, hipMemcpyDeviceToHost));
+    std::sort(c_rows.begin(), c_rows.end());
+    // G_5 of the strip blur (frame 0 and the last), to compare with k_blur_detect's
+    std::vector<float> g5a(P), g5b(P), g5c(P), g5d(P);
+    CK(hipMemcpy(g5a.data(), g + 5 * P, P * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(g5b.data(), g + (size_t)(n - 1) * stride + 5 * P, P * 4, hipMemcpyDeviceToHost));
+    BlurDetectLaunch F{};
+    F.gauss = g;
+    F.img_stride = stride;
+    F.W = W;
+    F.H = H;
+    F.pitch = pitch;
+    F.n_img = n;
+    F.profile = kProfileOpenCV;
+    F.taps = taps[5];
+    F.cand = cand;
+    F.counter = cnt;
+    F.cap = cap;
+    const float tbd = timeit([&] {
+        CK(hipMemsetAsync(cnt, 0, 4, 0));
+        BlurDetectLaunch f = F;
+        launch_blur_detect(rad[5], f, 0);
+    });
+    uint32_t nc = 0;
+    CK(hipMemcpy(&nc, cnt, 4, hipMemcpyDeviceToHost));
+    std::vector<uint64_t> c_bd(nc);
+    CK(hipMemcpy(c_bd.data(), cand, nc * 8, hipMemcpyDeviceToHost));
+    std::sort(c_bd.begin(), c_bd.end());
+    CK(hipMemcpy(g5c.data(), g + 5 * P, P * 4, hipMemcpyDeviceToHost));
+    CK(hipMemcpy(g5d.data(), g + (size_t)(n - 1) * stride + 5 * P, P * 4, hipMemcpyDeviceToHost));
+    const bool same_g5 = std::memcmp(g5a.data(), g5c.data(), P * 4) == 0 && std::memcmp(g5b.data(), g5d.data(), P * 4) == 0;
+    const bool same_cand = c_rows == c_bd;
+    // the candidates must be refined from a consistent order: restore k_detect_rows' list
+    CK(hipMemcpy(cand, c_rows.data(), nc_rows * 8, hipMemcpyHostToDevice));
+    CK(hipMemcpy(cnt, &nc_rows, 4, hipMemcpyHostToDevice));
+    nc = nc_rows;
+    // refine the candidates
+    const float** dg = nullptr;
+    size_t* dgs = nullptr;
+    int *dw = nullptr, *dh = nullptr, *dp = nullptr;
+    CK(hipMalloc(&dg, sizeof(float*)));
+    CK(hipMalloc(&dgs, sizeof(size_t)));
+    CK(hipMalloc(&dw, 4));
+    CK(hipMalloc(&dh, 4));
+    CK(hipMalloc(&dp, 4));
+    const float* g0 = g;
+    CK(hipMemcpy(dg, &g0, sizeof(float*), hipMemcpyHostToDevice));
+    CK(hipMemcpy(dgs, &stride, sizeof(size_t), hipMemcpyHostToDevice));
+    CK(hipMemcpy(dw, &W, 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dh, &H, 4, hipMemcpyHostToDevice));
+    CK(hipMemcpy(dp, &pitch, 4, hipMemcpyHostToDevice));
+    ExtRec* ext = nullptr;
+    CK(hipMalloc(&ext, (size_t)nc * sizeof(ExtRec) + 64));
+    RefineLaunch R{};
+    R.cand = cand;
+    R.n_cand = cnt;
+    R.cand_cap = nc;
+    R.gauss = dg;
+    R.g_img_stride = dgs;
+    R.ow = dw;
+    R.oh = dh;
+    R.opitch = dp;
+    R.out = ext;
+    R.counter = cnt + 1;
+    R.cap = nc;
+    R.band_n = 1;
+    const float tr = timeit([&] {
+        CK(hipMemsetAsync(cnt + 1, 0, 4, 0));
+        launch_refine(R, 0);
+    });
+    uint32_t ne = 0;
+    CK(hipMemcpy(&ne, cnt + 1, 4, hipMemcpyDeviceToHost));
+    std::vector<ExtRec> e_new(ne);
+    CK(hipMemcpy(e_new.data(), ext, ne * sizeof(ExtRec), hipMemcpyDeviceToHost));
+    const float tro = timeit([&] {
+        CK(hipMemsetAsync(cnt + 1, 0, 4, 0));
+        hipLaunchKernelGGL(k_refine_old, dim3(std::min<uint32_t>((R.cand_cap + 255) / 256, 2048)), dim3(256), 0, 0, R);
+    });
+    uint32_t ne_old = 0;
+    CK(hipMemcpy(&ne_old, cnt + 1, 4, hipMemcpyDeviceToHost));
+    std::vector<ExtRec> e_old(ne_old);
+    CK(hipMemcpy(e_old.data(), ext, ne_old * sizeof(ExtRec), hipMemcpyDeviceToHost));
+    // the same extrema (the append order differs run to run): sort by key
+    auto by_key = [](std::vector<ExtRec>& v) {
+        std::sort(v.begin(), v.end(), [](const ExtRec& a, const ExtRec& b) { return a.key < b.key; });
+    };
+    by_key(e_new);
+    by_key(e_old);
+    const bool same = ne == ne_old && std::memcmp(e_new.data(), e_old.data(), ne * sizeof(ExtRec)) == 0;
+    const double mb = px * 4 / 1e6;  // MB per plane over the batch
+    std::printf("octave 0 of %d 1080p frames (%.0f M px)\n", n, px / 1e6);
+    std::printf("blur4 strip R=%d     %8.1f us  %5.2f TB/s (8 B/px)\n", rad[4], t4 * 1e3, 2 * mb / t4 / 1e6);
+    std::printf("blur5 strip R=%d     %8.1f us  %5.2f TB/s (8 B/px)\n", rad[5], t5 * 1e3, 2 * mb / t5 / 1e6);
+    std::printf("k_detect_rows        %8.1f us  %5.2f TB/s (24 B/px)  %u candidates\n", td * 1e3,
+                6 * mb / td / 1e6, nc_rows);
+    std::printf("k_blur_detect        %8.1f us  %5.2f TB/s (24 B/px)  %u candidates\n", tbd * 1e3,
+                6 * mb / tbd / 1e6, nc);
+    std::printf("blur5 + detect_rows  %8.1f us\n", (t5 + td) * 1e3);
+    std::printf("k_blur_detect vs strip blur 5 + k_detect_rows: G_5 %s, candidates %s\n",
+                same_g5 ? "bit-identical" : "DIFFER", same_cand ? "identical" : "DIFFER");
+    if (!same_g5 || !same_cand) return 4;
+    std::printf("k_refine             %8.1f us  %u candidates -> %u extrema\n", tr * 1e3, nc, ne);
+    std::printf("k_refine (round 4)   %8.1f us  %u extrema; identical records: %s\n", tro * 1e3, ne_old,
+                same ? "yes" : "NO");
+    return same ? 0 : 3;
+    return 0;
+}
