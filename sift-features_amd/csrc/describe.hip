@@ -224,15 +224,15 @@ __device__ __forceinline__ void describe_normalize(float acc0, float acc1, uint8
 template <int kAblate = 0>
 __device__ __forceinline__ void describe_wave_exact(const float* __restrict__ img, int pitch, int width, int height,
                                                     float xf, float yf, float scale, float orientation,
-                                                    DescScratch& sc, uint8_t* __restrict__ out, int lane) {
+                                                    float sin_ori, float cos_ori, DescScratch& sc,
+                                                    uint8_t* __restrict__ out, int lane) {
     const int32_t x = (int32_t)sat_u32(roundf(xf));
     const int32_t y = (int32_t)sat_u32(roundf(yf));
     const float BIN_ANGLE_STEP = (float)kDescBins / 360.0f;
     const float hist_width = kLambdaDescr * scale;
     int radius = sat_i32(roundf(kLambdaDescr * scale * 1.41421356237309504880f * (float)(kDescHist + 1) * 0.5f));
     radius = radius < 0 ? 0 : (radius > (ROWS_MAX - 2) / 2 ? (ROWS_MAX - 2) / 2 : radius);
-    const float rad = orientation * (3.14159265358979323846f / 180.0f);  // f32::to_radians
-    const float sin_ori = (float)sin((double)rad), cos_ori = (float)cos((double)rad);
+    // (sin_ori, cos_ori): orientation_rotation(orientation), src/lib.rs:800-801
     const float sin_s = sin_ori / hist_width, cos_s = cos_ori / hist_width;
     const int n = 2 * radius + 1;
     // 1. per-row candidate column interval of the whole 4x4 region
@@ -430,8 +430,9 @@ struct NoHook {
 template <int kShare, int kAblate = 0, class Mid = NoHook>
 __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img, int pitch, int width, int height,
                                                    float xf, float yf, float scale, float orientation,
-                                                   DescScratchFast<kShare>& sc, uint8_t* __restrict__ out, int lane,
-                                                   Mid mid = Mid(), uint32_t* n_samples = nullptr) {
+                                                   float sin_ori, float cos_ori, DescScratchFast<kShare>& sc,
+                                                   uint8_t* __restrict__ out, int lane, Mid mid = Mid(),
+                                                   uint32_t* n_samples = nullptr) {
     constexpr int NS = 64 / kShare;  // slices
     const int32_t x = (int32_t)sat_u32(roundf(xf));
     const int32_t y = (int32_t)sat_u32(roundf(yf));
@@ -439,9 +440,7 @@ __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img
     const float hist_width = kLambdaDescr * scale;
     int radius = sat_i32(roundf(kLambdaDescr * scale * 1.41421356237309504880f * (float)(kDescHist + 1) * 0.5f));
     radius = radius < 0 ? 0 : (radius > (ROWS_MAX - 2) / 2 ? (ROWS_MAX - 2) / 2 : radius);
-    const float rad = orientation * (3.14159265358979323846f / 180.0f);  // f32::to_radians
-    const float sin_ori = (kAblate & 128) ? __sinf(rad) : (float)sin((double)rad);
-    const float cos_ori = (kAblate & 128) ? __cosf(rad) : (float)cos((double)rad);
+    // (sin_ori, cos_ori): orientation_rotation(orientation), src/lib.rs:800-801
     const float sin_s = sin_ori / hist_width, cos_s = cos_ori / hist_width;
     const int n = 2 * radius + 1;
     // bin b of lane l's slice lives at h[b * 64 + l]: every lane's read-add-write
@@ -462,18 +461,27 @@ __device__ __forceinline__ void describe_wave_fast(const float* __restrict__ img
     // chains for the ~2 waves per SIMD the LDS footprint allows -- and the
     // gradient loads of the next two are in flight meanwhile.
     int row = 0;
-    const gfloat* gimg = as_global(img);
     auto locate = [&](int k, int& xi, int& yi) {
         while (sc.rowpre[row + 1] <= k) row++;
         yi = row - radius;
         xi = sc.rowlo[row] + (k - sc.rowpre[row]);
     };
+    // The gradient reads of a sample (yy, xx) = (y + yi, x + xi): rows yy - 1
+    // .. yy + 1 of the window's clipped rows [rb, re] (1 <= rb, re <= H - 2).
+    // A buffer resource based one row above rb and one column left of 0:
+    // voffset ((yy - rb) * pitch + xx) * 4 (32-bit, < 2^24 products), the row
+    // in a uniform soffset and the column in the immediate -- no 64-bit
+    // address arithmetic per sample.
+    const int rb = max(y - radius, 1), re = min(y + radius, height - 2);
+    const __amdgpu_buffer_rsrc_t rs =
+        uniform_rsrc(img + (ptrdiff_t)(rb - 1) * pitch - 1, (uint32_t)max(re - rb + 3, 0) * (uint32_t)pitch * 4u);
+    const int s1 = __builtin_amdgcn_readfirstlane(4 * pitch), s2 = 2 * s1;
     auto fetch = [&](int xi, int yi, float& l, float& r, float& u, float& d) {
-        const gfloat* rw = gimg + (size_t)(y + yi) * pitch + (x + xi);
-        r = rw[1];
-        l = rw[-1];
-        u = rw[-pitch];
-        d = rw[pitch];
+        const int vo = ((int)__umul24((uint32_t)(yi + y - rb), (uint32_t)pitch) + x + xi) * 4;
+        r = buffer_load_f32(rs, vo + 8, s1);
+        l = buffer_load_f32(rs, vo, s1);
+        u = buffer_load_f32(rs, vo + 4, 0);
+        d = buffer_load_f32(rs, vo + 4, s2);
     };
     f2v sink = {0.f, 0.f};  // kAblate bit 0: register sink instead of the slice updates
     int nxi[2] = {0, 0}, nyi[2] = {0, 0};
@@ -691,7 +699,7 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kMode == 0 ?
                                             L.gauss_img_stride[o] +
                            (size_t)__builtin_amdgcn_readfirstlane(kp.scale) * pitch * H;
         // compute_descriptors (src/lib.rs:759-782)
-        const float angle = 360.0f - kp.angle;
+        const float angle = 360.0f - kp.angle;  // orientation (src/lib.rs:771); kp.sin_d / cos_d its rotation
         const float osf = 1.0f / (float)(1u << o);  // 2_f32.powi(-octave)
         const float kp_size = kp.size * osf;
         uint8_t* out = L.out_desc + (size_t)i * kDescSize;
@@ -702,11 +710,13 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kMode == 0 ?
             nkp = record(ni);
         };
         if constexpr (kExact) {
-            describe_wave_exact<kAblate>(img, pitch, W, H, kp.x * osf, kp.y * osf, kp_size, angle, scr, out, lane);
+            describe_wave_exact<kAblate>(img, pitch, W, H, kp.x * osf, kp.y * osf, kp_size, angle, kp.sin_d, kp.cos_d,
+                                         scr, out, lane);
             next();
         } else {
             describe_wave_fast<kExact ? 1 : kMode, kAblate>(img, pitch, W, H, kp.x * osf, kp.y * osf, kp_size, angle,
-                                                            scr, out, lane, next, L.samples ? &nsamp : nullptr);
+                                                            kp.sin_d, kp.cos_d, scr, out, lane, next,
+                                                            L.samples ? &nsamp : nullptr);
         }
         if (lane == 0) {
             if (L.out_kp) {
@@ -746,7 +756,9 @@ void launch_describe(const DescLaunch& L, hipStream_t st) {
 __global__ __launch_bounds__(64) void k_describe_one(const float* img, int w, int h, float x, float y, float scale,
                                                      float orientation, uint8_t* out) {
     __shared__ __attribute__((aligned(16))) DescScratch scr;
-    describe_wave_exact(img, w, w, h, x, y, scale, orientation, scr, out, threadIdx.x);
+    float sn, cs;
+    orientation_rotation(orientation, sn, cs);
+    describe_wave_exact(img, w, w, h, x, y, scale, orientation, sn, cs, scr, out, threadIdx.x);
 }
 
 void launch_describe_one(const float* img, int w, int h, float x, float y, float scale, float orientation,

@@ -480,13 +480,13 @@ __global__ __launch_bounds__(256, SIFT_ORIENT_MIN_WAVES) void k_orient(const Ori
         kp.img = e.img;
         kp.octave = e.octave;
         kp.scale = e.scale;
-        kp.pad = 0;
+
         kp.x = kp_x;
         kp.y = kp_y;
         kp.size = kp_scale * osf;
         kp.angle = 360.0f - (360.0f / (float)kOriBins) * bin;
         kp.response = e.response;
-        kp.pad2 = 0.f;
+        desc_rotation(kp.angle, kp.sin_d, kp.cos_d);
         L.out[slot] = kp;
     }
 }

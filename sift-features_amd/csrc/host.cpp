@@ -490,6 +490,8 @@ struct sift_mi_ctx {
     hipStream_t cstream = nullptr; // device->host result copies
     hipStream_t own2 = nullptr;    // compute stream of pipeline lane 1 (lane 0 runs on `stream`)
     hipStream_t aux[2] = {};       // per lane: blurs 4, 5 of each octave beside the next octave
+    hipStream_t aux2 = nullptr;    // lane 0: blurs 4, 5 of octaves >= 1 while octave 0's fused pass runs
+    hipEvent_t aux2_join = nullptr;
     hipStream_t dec = nullptr;     // JPEG batch decoding: a high-priority stream (its own hardware queue)
     hipEvent_t oct_ev[2][kTailMaxOct + 1] = {};  // per lane: octave o's G_3 done / aux joined
     bool lanes_busy = false;       // this call keeps both pipeline lanes busy (no octave overlap then)
@@ -563,6 +565,7 @@ int sync_lanes(sift_mi_ctx* c) {
     HIPCHK(hipStreamSynchronize(c->stream));
     HIPCHK(hipStreamSynchronize(c->own2));
     for (auto& a : c->aux) HIPCHK(hipStreamSynchronize(a));
+    if (c->aux2) HIPCHK(hipStreamSynchronize(c->aux2));
     return 0;
 }
 
@@ -777,6 +780,7 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
     hipStream_t st = lane_stream(c, lane);
     lane = arena_of(c, lane);
     hipStream_t aux = c->aux[lane];
+    hipStream_t aux2 = lane == 0 ? c->aux2 : nullptr;
     // row bands (sift_mi_set_row_band): the rows of every Gaussian the band's
     // keypoint stages read, propagated back through the blur chain and the
     // octave downsampling.  Detection covers octave rows [H*r/n, H*(r+1)/n);
@@ -911,6 +915,14 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
     // graph dependency, so the captured aux work would not wait)
     hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
     const bool ext_events = hipStreamIsCapturing(st, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone;
+    // Octave 0's fused blur 5 + scan (k_blur_detect, the stage's longest
+    // launch) is deferred until octave 1's G_3 is written, and the blurs 4, 5
+    // of octaves >= 1 go to a second aux stream: octave 1's blur 3 then does
+    // not run starved beside it (round 4: 3.4 ms at 0.35 TB/s), and the small
+    // octaves' chain runs beside the long pass instead of after it.
+    bool defer0 = false;           // octave 0's blur 5 is pending (deferral)
+    BlurDetectLaunch defer_f{};
+    bool used_aux2 = false;
     auto octaves = [&](uint32_t f0, uint32_t nf, int o0, int o1, hipStream_t sm, bool ov) -> int {
         hipStream_t s45 = sm;
         for (int o = o0; o < o1; o++) {
@@ -922,8 +934,17 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
             for (int s = (o == 0 && seed_pair) ? 2 : 1; s < kImagesPerOctave; s++) {
                 if (s == 4 && ov) {
                     if (!g3_signalled) HIPCHK(hipEventRecord(c->oct_ev[lane][o], sm));
-                    HIPCHK(hipStreamWaitEvent(aux, c->oct_ev[lane][o], 0));
-                    s45 = aux;
+                    if (o >= 1 && defer0) {
+                        // octave 1's G_3 is on its way: octave 0's fused pass
+                        // now, the octaves from here on on the second aux stream
+                        HIPCHK(hipStreamWaitEvent(aux, c->oct_ev[lane][o], 0));
+                        if (launch_blur_detect(p.oct_r[5], defer_f, aux, po) != 0)
+                            return fail(SIFT_MI_EHIP, "deferred blur-detect launch declined");
+                        defer0 = false;
+                    }
+                    hipStream_t a = (o >= 1 && used_aux2) ? aux2 : aux;
+                    HIPCHK(hipStreamWaitEvent(a, c->oct_ev[lane][o], 0));
+                    s45 = a;
                 }
                 const BlurLaunch B = blur_launch(o, s, f0, nf);
                 // blur 5 and the octave's detection in one pass (k_blur_detect:
@@ -944,6 +965,16 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
                     F.cand = S.cand.p;
                     F.counter = S.counters.p + 0;
                     F.cap = S.bc;
+                    // defer octave 0's pass (see above) when it is fused and a
+                    // later octave will take the second aux stream
+                    if (o == 0 && ov && aux2 && o1 > 1 && blur_detect_applies(p.oct_r[s], F, po)) {
+                        defer_f = F;
+                        defer0 = true;
+                        used_aux2 = true;
+                        S.fused_mask |= 1u << o;
+                        launches++;
+                        continue;
+                    }
                     if (launch_blur_detect(p.oct_r[s], F, s45, po) == 0) {
                         S.fused_mask |= 1u << o;
                         launches++;
@@ -988,6 +1019,16 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
             detect_slot >= 0 && ov && o_tail > 0 && o_tail < p.n_oct && c->slot[detect_slot].bcb && po.early;
         CHK(seed(f0, nf, sm));
         CHK(octaves(f0, nf, 0, o_tail, sm, ov));
+        if (defer0) {  // no later octave took it (cannot happen with o_tail > 1): launch it now
+            HIPCHK(hipStreamWaitEvent(aux, c->oct_ev[lane][0], 0));
+            if (launch_blur_detect(p.oct_r[5], defer_f, aux, po) != 0)
+                return fail(SIFT_MI_EHIP, "deferred blur-detect launch declined");
+            defer0 = false;
+        }
+        if (used_aux2) {  // the aux stream's later work (detection, join) follows the second's
+            HIPCHK(hipEventRecord(c->aux2_join, aux2));
+            HIPCHK(hipStreamWaitEvent(aux, c->aux2_join, 0));
+        }
         if (o_tail < p.n_oct) {
             // whole octaves (a row band's restricted rows are a subset: rows
             // outside them depend only on rows outside them, so the exact rows
@@ -1764,8 +1805,10 @@ StreamPool& stream_pool() {
     return *p;
 }
 // the order matters for the queue mapping: lane 0, lane 1, lane 0's aux,
-// the copy stream, lane 1's aux (with 4 queues only the last shares one)
-constexpr int kCtxStreams = 5;
+// the copy stream, lane 1's aux, lane 0's second aux (with 4 queues the last
+// two share the lanes' queues: lane 1's aux is used only when lane 1 is idle,
+// the second aux only while lane 1's stream is: a one-lane / one-chunk call)
+constexpr int kCtxStreams = 6;
 bool take_streams(int dev, hipStream_t (&out)[kCtxStreams]) {
     StreamPool& P = stream_pool();
     {
@@ -1823,8 +1866,10 @@ int sift_mi_create(int device_ordinal, sift_mi_profile profile, sift_mi_ctx** ou
     c->aux[0] = ss[2];
     c->cstream = ss[3];
     c->aux[1] = ss[4];
+    c->aux2 = ss[5];
     c->stream = c->own;
     bool ok = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) == hipSuccess;
+    ok = ok && hipEventCreateWithFlags(&c->aux2_join, hipEventDisableTiming) == hipSuccess;
     for (auto& lane : c->oct_ev)
         for (auto& e : lane) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
     for (auto& S : c->slot) {
@@ -1849,7 +1894,7 @@ void sift_mi_destroy(sift_mi_ctx* c) {
     // stream (it goes back to the pool below), lane 1, both aux streams
     // (octave blurs 4, 5 and detection write the arenas) and the copy stream
     {
-        const hipStream_t ss[] = {c->stream, c->own, c->own2, c->aux[0], c->aux[1], c->cstream, c->dec};
+        const hipStream_t ss[] = {c->stream, c->own, c->own2, c->aux[0], c->aux[1], c->aux2, c->cstream, c->dec};
         for (hipStream_t s : ss)
             if (s) (void)hipStreamSynchronize(s);
     }
@@ -1872,6 +1917,7 @@ void sift_mi_destroy(sift_mi_ctx* c) {
         if (S.oriented) (void)hipEventDestroy(S.oriented);
     }
     if (c->fork) (void)hipEventDestroy(c->fork);
+    if (c->aux2_join) (void)hipEventDestroy(c->aux2_join);
     for (auto& lane : c->oct_ev)
         for (auto& e : lane)
             if (e) (void)hipEventDestroy(e);
@@ -1885,7 +1931,7 @@ void sift_mi_destroy(sift_mi_ctx* c) {
     if (c->gexec) (void)hipGraphExecDestroy(c->gexec);
     if (c->graph) (void)hipGraphDestroy(c->graph);
     if (c->own) {  // the streams go back to the pool (synchronised above)
-        const hipStream_t ss[kCtxStreams] = {c->own, c->own2, c->aux[0], c->cstream, c->aux[1]};
+        const hipStream_t ss[kCtxStreams] = {c->own, c->own2, c->aux[0], c->cstream, c->aux[1], c->aux2};
         give_streams(c->device, ss);
     }
     delete c;

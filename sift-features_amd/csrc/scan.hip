@@ -513,40 +513,44 @@ __global__ __launch_bounds__(256) void k_blur_detect(const BlurDetectLaunch L) {
 
 // PathOpts::fused_detect: 0 keeps blur 5 and detection apart, 2 fuses every
 // octave it can at 32-row segments (test paths)
-int launch_blur_detect(int R, BlurDetectLaunch& L, hipStream_t st, const PathOpts& o) {
-    if (o.fused_detect == 0) return -1;
-    const bool force = o.fused_detect == 2;
+// The segment length the fused pass would use for L (0: it does not apply).
+static int blur_detect_segment(int R, const BlurDetectLaunch& L, const PathOpts& o) {
+    if (o.fused_detect == 0) return 0;
     const bool ok = L.W > R + 1 && L.H > R + 1 && L.W >= 2 * kImageBorder && L.H >= 2 * kImageBorder &&
                     (uint64_t)L.H * (uint64_t)L.pitch * 4 < (1ull << 31) && L.n_img > 0;
-    if (!ok) return -1;
+    if (!ok) return 0;
     const bool ocv = L.profile == kProfileOpenCV;
-    if (!((ocv && R == 13) || (!ocv && R == 7))) return -1;
-    L.nsx = (L.W + DR_COLS - 1) / DR_COLS;
+    if (!((ocv && R == 13) || (!ocv && R == 7))) return 0;
+    if (o.fused_detect == 2) return 32;  // many segment boundaries on test-sized frames
     // row segments: a segment re-filters 2R + 2 halo rows, so long ones, but
     // enough waves to fill the chip (>= ~16 k).  A wave walks its segment row
     // after row, so an octave too small for that at >= 64-row segments (one
     // 1080p frame's octaves, a batch's small octaves) is left to launch_blur +
     // k_detect_rows: there the fused pass is a chain of latency-bound row
     // steps (one frame's octave 4: 54 us against 10 us for its blur 5)
-    int seg = 0;
-    for (int s : {256, 128, 64}) {
-        if ((long)L.nsx * ((L.H + s - 1) / s) * L.n_img >= 16384) {
-            seg = s;
-            break;
-        }
-    }
-    if (force) seg = 32;  // many segment boundaries on test-sized frames
+    const long nsx = (L.W + DR_COLS - 1) / DR_COLS;
+    for (int s : {256, 128, 64})
+        if (nsx * ((L.H + s - 1) / s) * L.n_img >= 16384) return s;
+    return 0;
+}
+
+bool blur_detect_applies(int R, const BlurDetectLaunch& L, const PathOpts& o) {
+    return blur_detect_segment(R, L, o) > 0;
+}
+
+int launch_blur_detect(int R, BlurDetectLaunch& L, hipStream_t st, const PathOpts& o) {
+    const int seg = blur_detect_segment(R, L, o);
     if (!seg) return -1;
+    L.nsx = (L.W + DR_COLS - 1) / DR_COLS;
     L.seg = seg;
     L.nsy = (L.H + seg - 1) / seg;
     const long waves = (long)L.nsx * L.nsy * L.n_img;
     const dim3 grid((uint32_t)((waves + 3) / 4));
-    if (ocv)
+    if (L.profile == kProfileOpenCV)
         hipLaunchKernelGGL((k_blur_detect<13, kProfileOpenCV>), grid, dim3(256), 0, st, L);
     else
         hipLaunchKernelGGL((k_blur_detect<7, kProfileImageproc>), grid, dim3(256), 0, st, L);
     return 0;
 }
-
 
 }  // namespace siftmi

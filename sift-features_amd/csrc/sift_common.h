@@ -59,13 +59,32 @@ struct ExtRec {
 };
 
 // Keypoint with reference orientation (src/lib.rs:58-68 SiftKeyPoint), in
-// 2x-seed pixel units.  48 bytes.
+// 2x-seed pixel units.  48 bytes.  sin_d / cos_d: (sin, cos) of the
+// descriptor's rotation, compute_descriptors' `360 - angle` in radians
+// (src/lib.rs:771, :800-801), as compute_descriptor evaluates them -- computed
+// once per keypoint by k_orient instead of by every lane of k_describe.
 struct KpRec {
     uint64_t key;
-    int32_t img, octave, scale, pad;
+    int32_t img, octave, scale;
+    float sin_d;
     float x, y, size, angle, response;
-    float pad2;
+    float cos_d;
 };
+
+// (sin, cos) of the descriptor rotation for a keypoint angle (degrees):
+// orientation = 360 - angle (src/lib.rs:771), to_radians in f32, then f64
+// sin / cos rounded to f32 (the reference's f32 sin / cos are correctly
+// rounded glibc calls; up to rare near-midpoint ties this is the same value)
+__device__ __forceinline__ void orientation_rotation(float orientation, float& s, float& c) {
+    const float rad = orientation * (3.14159265358979323846f / 180.0f);  // f32::to_radians
+    double sd, cd;
+    sincos((double)rad, &sd, &cd);  // one argument reduction for both
+    s = (float)sd;
+    c = (float)cd;
+}
+__device__ __forceinline__ void desc_rotation(float angle, float& s, float& c) {
+    orientation_rotation(360.0f - angle, s, c);
+}
 
 // Output keypoint (include/sift_mi.h sift_mi_keypoint).
 struct OutKp {

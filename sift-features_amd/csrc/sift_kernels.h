@@ -190,6 +190,8 @@ struct BlurDetectLaunch {
     uint32_t cap;
 };
 int launch_blur_detect(int R, BlurDetectLaunch& L, hipStream_t st, const PathOpts& o = PathOpts{});
+// whether launch_blur_detect would launch (the same test, nothing enqueued)
+bool blur_detect_applies(int R, const BlurDetectLaunch& L, const PathOpts& o = PathOpts{});
 
 // Stage sizes live in device counters (no host round trip between stages):
 // every consumer reads its count from device memory, clamps it to the buffer

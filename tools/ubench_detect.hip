@@ -165,20 +165,44 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_REFINE
         }                                                                        \
     } while (0)
 
-// smooth blobs + a little noise, values in [0, 1]
+// blobs (as sift-features_amd/synth.py: mid grey, ~300 Gaussian blobs of
+// sigma 2..60 px per 1080p frame at 2x) + a gradient + a little noise, in
+// [0, 1]; each 64 x 64 tile sums the blobs whose 3-sigma box reaches it
+__device__ __forceinline__ uint32_t hsh(uint32_t h) {
+    h ^= h >> 16;
+    h *= 0x7feb352dU;
+    h ^= h >> 15;
+    h *= 0x846ca68bU;
+    h ^= h >> 16;
+    return h;
+}
+__device__ __forceinline__ float hf(uint32_t h) { return (float)(hsh(h) & 0xffffff) / 16777216.0f; }
+constexpr int kBlobs = 300;
 __global__ void k_fill_smooth(float* p, int W, int H, int pitch, size_t stride, int n) {
-    const size_t tot = (size_t)n * H * W;
-    for (size_t i = blockIdx.x * 256ull + threadIdx.x; i < tot; i += (size_t)gridDim.x * 256) {
-        const int f = (int)(i / ((size_t)H * W));
-        const size_t r = i - (size_t)f * H * W;
-        const int y = (int)(r / W), x = (int)(r - (size_t)y * W);
-        uint32_t h = (uint32_t)i * 2654435761u;
-        h ^= h >> 15;
-        h *= 2246822519u;
-        h ^= h >> 13;
-        const float fx = x * 0.021f + f, fy = y * 0.017f - f;
-        float v = 0.5f + 0.2f * sinf(fx) * cosf(fy) + 0.1f * sinf(0.37f * fx + 1.3f * fy);
-        v += ((float)(h & 0xff) / 255.0f - 0.5f) * 0.02f;
+    __shared__ float bx[kBlobs], by[kBlobs], bs[kBlobs], ba[kBlobs];
+    __shared__ int nb;
+    const int f = blockIdx.z, tx = blockIdx.x * 64, ty = blockIdx.y * 64;
+    if (threadIdx.x == 0) nb = 0;
+    __syncthreads();
+    for (int k = threadIdx.x; k < kBlobs; k += 256) {
+        const uint32_t s0 = (uint32_t)(f * kBlobs + k) * 4u;
+        const float cx = hf(s0) * W, cy = hf(s0 + 1) * H, sg = 2.0f * (2.0f + 58.0f * hf(s0 + 2) * hf(s0 + 2));
+        const float a = (hf(s0 + 3) - 0.5f) * 2.0f * 80.0f / 255.0f;
+        if (cx + 3 * sg >= tx && cx - 3 * sg < tx + 64 && cy + 3 * sg >= ty && cy - 3 * sg < ty + 64) {
+            const int i = atomicAdd(&nb, 1);
+            bx[i] = cx, by[i] = cy, bs[i] = -0.5f / (sg * sg), ba[i] = a;
+        }
+    }
+    __syncthreads();
+    for (int e = threadIdx.x; e < 64 * 64; e += 256) {
+        const int x = tx + (e & 63), y = ty + (e >> 6);
+        if (x >= W || y >= H) continue;
+        float v = 0.5f + 0.05f * (float)x / W - 0.05f * (float)y / H;
+        for (int k = 0; k < nb; k++) {
+            const float dx = x - bx[k], dy = y - by[k];
+            v += ba[k] * __expf((dx * dx + dy * dy) * bs[k]);
+        }
+        v += (hf((uint32_t)(f * 7919 + y) * 65536u + x) - 0.5f) * 6.0f / 255.0f;
         p[(size_t)f * stride + (size_t)y * pitch + x] = fminf(fmaxf(v, 0.0f), 1.0f);
     }
 }
@@ -205,7 +229,7 @@ int main(int argc, char** argv) {
     const size_t P = (size_t)pitch * H, stride = 6 * P;
     float* g = nullptr;
     CK(hipMalloc(&g, stride * n * sizeof(float)));
-    hipLaunchKernelGGL(k_fill_smooth, dim3(8192), dim3(256), 0, 0, g, W, H, pitch, stride, n);
+    hipLaunchKernelGGL(k_fill_smooth, dim3((W + 63) / 64, (H + 63) / 64, n), dim3(256), 0, 0, g, W, H, pitch, stride, n);
     // OpenCV octave sigmas (host.cpp octave_sigmas / cv_blur_taps): radii 5, 6, 8, 10, 13
     const double sig[6] = {0, 1.2262735, 1.5450078, 1.9465878, 2.4525469, 3.0900155};
     BlurTaps taps[6]{};
@@ -357,14 +381,14 @@ int main(int argc, char** argv) {
     by_key(e_new);
     by_key(e_old);
     const bool same = ne == ne_old && std::memcmp(e_new.data(), e_old.data(), ne * sizeof(ExtRec)) == 0;
-    const double mb = px * 4 / 1e6;  // MB per plane over the batch
+    const double mb = px * 4 / 1e6;  // MB per plane over the batch (MB / ms / 1e3 = TB/s)
     std::printf("octave 0 of %d 1080p frames (%.0f M px)\n", n, px / 1e6);
-    std::printf("blur4 strip R=%d     %8.1f us  %5.2f TB/s (8 B/px)\n", rad[4], t4 * 1e3, 2 * mb / t4 / 1e6);
-    std::printf("blur5 strip R=%d     %8.1f us  %5.2f TB/s (8 B/px)\n", rad[5], t5 * 1e3, 2 * mb / t5 / 1e6);
+    std::printf("blur4 strip R=%d     %8.1f us  %5.2f TB/s (8 B/px)\n", rad[4], t4 * 1e3, 2 * mb / t4 / 1e3);
+    std::printf("blur5 strip R=%d     %8.1f us  %5.2f TB/s (8 B/px)\n", rad[5], t5 * 1e3, 2 * mb / t5 / 1e3);
     std::printf("k_detect_rows        %8.1f us  %5.2f TB/s (24 B/px)  %u candidates\n", td * 1e3,
-                6 * mb / td / 1e6, nc_rows);
+                6 * mb / td / 1e3, nc_rows);
     std::printf("k_blur_detect        %8.1f us  %5.2f TB/s (24 B/px)  %u candidates\n", tbd * 1e3,
-                6 * mb / tbd / 1e6, nc);
+                6 * mb / tbd / 1e3, nc);
     std::printf("blur5 + detect_rows  %8.1f us\n", (t5 + td) * 1e3);
     std::printf("k_blur_detect vs strip blur 5 + k_detect_rows: G_5 %s, candidates %s\n",
                 same_g5 ? "bit-identical" : "DIFFER", same_cand ? "identical" : "DIFFER");
