@@ -179,8 +179,10 @@ typedef enum {
     SIFT_MI_PATH_GRAPH = 7,        /* 1: identical single-chunk calls replayed as a HIP graph (default 0) */
     SIFT_MI_PATH_BAND_DRIFT = 8,   /* row bands: accepted refinement drift, -41..24 rows (default 24;
                                       smaller values force the whole-pyramid re-run) */
-    SIFT_MI_PATH_BOUND_SHRINK = 9  /* k >= 1: first-chunk stage bounds / k (default 1; > 1 forces the
+    SIFT_MI_PATH_BOUND_SHRINK = 9, /* k >= 1: first-chunk stage bounds / k (default 1; > 1 forces the
                                       bound-overflow re-run) */
+    SIFT_MI_PATH_TAIL_SPLIT = 10   /* 0: the small octaves' kernel as one workgroup per frame (default 1:
+                                      a chain and a side workgroup per frame) */
 } sift_mi_path_option;
 int sift_mi_set_path_option(sift_mi_ctx* ctx, int option, int value);
 

@@ -421,8 +421,9 @@ struct Plan {
 // kernels run while the host waits for chunk k and copies its results out.
 struct Slot {
     // [0] candidates [1] extrema [2] keypoints [3] outputs [4..4+F) frame starts
-    // [4+F..4+2F) per-frame outputs [4+2F..4+2F+2) the tail region's counters
-    // (early) [4+2F+2..4+2F+2+kDescWorkWords) descriptor work queues
+    // [4+F..4+2F) per-frame outputs [4+2F..4+2F+kTailWords) the tail
+    // region's counters (early) and the split tail kernel's error word
+    // [4+2F+kTailWords..+kDescWorkWords) descriptor work queues
     DevBuf<uint32_t> counters;
     PinBuf<uint32_t> h_counts;
     DevBuf<OutKp> out_kp;
@@ -491,6 +492,8 @@ struct sift_mi_ctx {
     hipStream_t own2 = nullptr;    // compute stream of pipeline lane 1 (lane 0 runs on `stream`)
     hipStream_t aux[2] = {};       // per lane: blurs 4, 5 of each octave beside the next octave
     hipStream_t aux2 = nullptr;    // lane 0: blurs 4, 5 of octaves >= 1 while octave 0's fused pass runs
+    DevBuf<uint32_t> tail_flags[2];  // per lane: the split tail kernel's G_3 hand-over flags
+    uint32_t tail_epoch = 0;
     hipEvent_t aux2_join = nullptr;
     hipStream_t dec = nullptr;     // JPEG batch decoding: a high-priority stream (its own hardware queue)
     hipEvent_t oct_ev[2][kTailMaxOct + 1] = {};  // per lane: octave o's G_3 done / aux joined
@@ -823,6 +826,7 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
     // the small octaves from o_tail on: one k_octave_tail launch
     // (PathOpts::tail = 0: per-blur launches for every octave)
     const PathOpts& po = c->opts;
+    const int tail_slot = cand_slot;  // the chunk's slot (its counters hold the split tail's error word)
     int o_tail = p.n_oct;
     if (po.tail && p.n_oct <= kTailMaxOct) o_tail = tail_octave_start(p.ow.data(), p.oh.data(), p.n_oct, p.oct_r);
     uint64_t bytes = p.algo_bytes_per_frame;  // per frame, SURVEY.md 8(d)
@@ -1045,6 +1049,21 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
             T.n_oct = p.n_oct;
             T.n_img = (int)nf;
             T.profile = p.profile;
+            // split chain / side workgroups (not under stream capture: the
+            // epoch is a kernel argument, a replay would see the last one's
+            // flags; not for row bands' restricted passes either -- whole
+            // octaves either way, so simply both paths exact)
+            if (po.tail_split && ext_events && tail_slot >= 0) {
+                const size_t need = (size_t)c->plan.chunk * kTailMaxOct;
+                if (c->tail_flags[lane].cap < need) {
+                    CHK(c->tail_flags[lane].ensure(need));
+                    HIPCHK(hipMemsetAsync(c->tail_flags[lane].p, 0, need * sizeof(uint32_t), sm));
+                }
+                T.flags = c->tail_flags[lane].p + (size_t)f0 * kTailMaxOct;
+                T.error = c->slot[tail_slot].counters.p + 4 + 2 * c->slot[tail_slot].m + 2;
+                T.epoch = ++c->tail_epoch;
+                if (T.epoch == 0) T.epoch = ++c->tail_epoch;  // 0 is the flags' initial value
+            }
             for (int s = 1; s < kImagesPerOctave; s++) {
                 T.r[s] = p.oct_r[s];
                 T.taps[s] = p.oct_taps[s];
@@ -1118,6 +1137,7 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
 // is re-run with larger bounds.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kMaxChunk = 256;  // frames per chunk (one workgroup plans the output: k_limit_plan)
+constexpr int kTailWords = 3;        // Slot counters after the per-frame plan: cand_b, ext_b counts, tail error
 
 struct Bounds {
     uint32_t bc, be, bk;
@@ -1159,7 +1179,7 @@ int reserve_chunk(sift_mi_ctx* c, int si, const Bounds& B, uint32_t frames, uint
     const bool grow = B.bc > S.cand.cap || B.be > S.ext.cap || B.bk > S.kp.cap || B.bk > S.keys_a.cap ||
                       bcb > S.cand_b.cap || bcb > S.ext_b.cap ||
                       frames > S.seg_off.cap || B.bk > S.out_kp.cap ||
-                      4 + 2 * frames + kDescWorkWords + 2 > S.counters.cap ||
+                      4 + 2 * frames + kDescWorkWords + kTailWords > S.counters.cap ||
                       (m == 1 && (size_t)B.bk * kDescSize > S.desc_kp.cap);
     if (grow) {
         HIPCHK(hipStreamSynchronize(lane_stream(c, si)));
@@ -1182,8 +1202,8 @@ int reserve_chunk(sift_mi_ctx* c, int si, const Bounds& B, uint32_t frames, uint
     CHK(S.seg_off.ensure(frames));
     CHK(S.out_off.ensure(frames));
     CHK(S.use_resp.ensure(frames));
-    CHK(S.counters.ensure(4 + 2 * frames + kDescWorkWords + 2));
-    CHK(S.h_counts.ensure(4 + 2 * frames + 2));
+    CHK(S.counters.ensure(4 + 2 * frames + kDescWorkWords + kTailWords));
+    CHK(S.h_counts.ensure(4 + 2 * frames + kTailWords));
     CHK(S.out_kp.ensure(B.bk));
     CHK(S.out_desc.ensure((size_t)B.bk * kDescSize));
     CHK(S.out_key.ensure(B.bk));
@@ -1214,7 +1234,7 @@ int prepare_chunk(sift_mi_ctx* c, int si, uint32_t m, uint32_t frame_base, const
     S.early = false;
     uint32_t* cnt = S.counters.p;
     // stage counters, frame starts (~0), descriptor work queues
-    launch_chunk_init(cnt, (int)m, kDescWorkWords + 2, st);  // + the tail region's counters (Slot::early)
+    launch_chunk_init(cnt, (int)m, kDescWorkWords + kTailWords, st);  // + the tail region's words
     HIPCHK(hipGetLastError());
     return 0;
 }
@@ -1314,7 +1334,7 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
     uint32_t* cnt = S.counters.p;
     uint32_t* starts = cnt + 4;
     uint32_t* out_cnt = cnt + 4 + m;
-    uint32_t* work = cnt + 4 + 2 * m + 2;  // descriptor work queues (after the tail region's counters)
+    uint32_t* work = cnt + 4 + 2 * m + kTailWords;  // descriptor work queues (after the tail region's words)
     (void)starts;
     (void)work;
     if (!S.detected) CHK(launch_detection(c, si, 0, m, 0, p.n_oct, st));
@@ -1401,7 +1421,7 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
     HIPCHK(hipGetLastError());
     if (S.staged) HIPCHK(hipEventRecord(S.ev[5], st));
     // the frame plan and the tail region's counters (Slot::early) in one copy
-    HIPCHK(hipMemcpyAsync(S.h_counts.p, cnt, (4 + 2 * m + (S.early ? 2 : 0)) * sizeof(uint32_t),
+    HIPCHK(hipMemcpyAsync(S.h_counts.p, cnt, (4 + 2 * m + kTailWords) * sizeof(uint32_t),
                           hipMemcpyDeviceToHost, st));
     HIPCHK(hipEventRecord(S.ev[6], st));
     return 0;
@@ -1453,6 +1473,8 @@ int finalize_chunk(sift_mi_ctx* c, int si, size_t* offsets, bool only_chunk = fa
     const double fm = (double)m;
     // the tail octaves' region (Slot::early): its counts follow the frame plan
     const uint32_t hb0 = S.early ? h[4 + 2 * m] : 0, hb1 = S.early ? h[4 + 2 * m + 1] : 0;
+    if (h[4 + 2 * m + 2])  // a split tail's side workgroup gave up waiting (never expected)
+        return fail(SIFT_MI_EHIP, "k_octave_tail: a side workgroup timed out waiting for its chain");
     c->pf_cand = std::max(c->pf_cand, (h[0] + hb0) / fm);
     c->pf_ext = std::max(c->pf_ext, (h[1] + hb1) / fm);
     c->pf_kp = std::max(c->pf_kp, h[2] / fm);
@@ -1921,6 +1943,7 @@ void sift_mi_destroy(sift_mi_ctx* c) {
     for (auto& lane : c->oct_ev)
         for (auto& e : lane)
             if (e) (void)hipEventDestroy(e);
+    for (auto& f : c->tail_flags) f.release();
     c->r_kp.release();
     c->r_desc.release();
     c->r_key.release();
@@ -1996,6 +2019,7 @@ int sift_mi_set_path_option(sift_mi_ctx* c, int option, int value) {
         case SIFT_MI_PATH_GRAPH: if (!b) break; o.graph = value; return 0;
         case SIFT_MI_PATH_BAND_DRIFT: if (value < -kBandPatch || value > kBandDrift) break; o.band_drift = value; return 0;
         case SIFT_MI_PATH_BOUND_SHRINK: if (value < 1) break; o.bound_shrink = value; return 0;
+        case SIFT_MI_PATH_TAIL_SPLIT: if (!b) break; o.tail_split = value; return 0;
         default: return fail(SIFT_MI_EINVAL, "unknown path option");
     }
     return fail(SIFT_MI_EINVAL, "path option value out of range");

@@ -52,6 +52,7 @@ struct PathOpts {
     int graph = 0;         // 1: single-chunk calls captured once and replayed as a HIP graph
     int band_drift = 24;   // row bands: refinement drift accepted without a re-run (< 24 forces re-runs)
     int bound_shrink = 1;  // > 1: first-chunk stage bounds divided by it (forces the overflow re-run)
+    int tail_split = 1;    // k_octave_tail as chain + side workgroups per frame (0: one workgroup per frame)
 };
 
 // Image planes are row-pitched: element (y, x) at plane[y * pitch + x].
@@ -122,6 +123,14 @@ struct TailLaunch {
     int o0, n_oct, n_img, profile;
     int r[kImagesPerOctave];
     BlurTaps taps[kImagesPerOctave];
+    // split (flags != null): two workgroups per frame -- the chain (blurs
+    // 1-3 and the next octave's G_0 of every tail octave) and the side (blurs
+    // 4, 5 of each octave once the chain has published its G_3:
+    // flags[frame * kTailMaxOct + o] == epoch); error: set when a side
+    // workgroup gave up waiting (never expected; the host reports it)
+    uint32_t* flags;
+    uint32_t* error;
+    uint32_t epoch;
 };
 // first octave that fits the tail kernel (n_oct: none); radii[1..5] = the
 // octave's blur radii

@@ -273,6 +273,31 @@ def test_world2_gather_device_results(pkg):
 
 
 @pytest.mark.gpu
+def test_batch_tail_split_equal(pkg, oracle):
+    """A one-chunk batch of 6 frames through the split tail kernel (12
+    workgroups: a chain and a side per frame) and through the one-workgroup
+    kernel: identical results, and every tail octave's planes of frames 0
+    and 5 equal the oracle's bit for bit."""
+    import synth
+    fr = synth.frames(6, 640, 480, seed0=60)
+    c = pkg.Context(0, pkg.OpenCVProcessing)
+    c.set_chunk(6)
+    try:
+        split = c.sift_batch(fr)
+        for i in (0, 5):
+            opy = oracle.Pyramid(fr[i], 0)
+            for o in range(opy.n_octaves):
+                assert np.array_equal(c.read_batch_scale_space(i, o), opy.scale_space(o)), (i, o)
+        c.set_path_option("tail_split", 0)
+        whole = c.sift_batch(fr)
+    finally:
+        c.close()
+    for a, b in zip(split, whole):
+        assert a == b
+        assert np.array_equal(a.keys, b.keys)
+
+
+@pytest.mark.gpu
 def test_batch_fused_kernels_equal_single_launches(pkg):
     """The batch path (no DoG planes) with the pair and tail kernels equals the
     batch path with single-blur launches only, bit for bit (1080p frames:
@@ -335,15 +360,17 @@ def test_single_chunk_graph_replay(pkg, ctx, oracle, fetch):
     c.close()
 
 
-@pytest.mark.parametrize("knob", ["early", "desc_first"])
+@pytest.mark.parametrize("knob", ["early", "desc_first", "tail_split"])
 @pytest.mark.parametrize("profile", [0, 1])
 def test_single_chunk_paths_equal(pkg, knob, profile):
     """One-chunk calls take latency paths of their own -- the octaves below
     the tail detected, refined and oriented on the aux stream beside the tail
     kernel with the tail octaves in a region of their own
-    (Slot::early), and the descriptors computed in keypoint index order beside
-    the ordering stage, then gathered (Slot::desc_first) -- whose results must
-    equal the general path's (the knob = 0) bit for bit, incl. keys.  Each
+    (Slot::early), the descriptors computed in keypoint index order beside
+    the ordering stage, then gathered (Slot::desc_first), and the small
+    octaves' kernel as a chain and a side workgroup per frame handing G_3
+    over through device flags (tail_split) -- whose results must equal the
+    general path's (the knob = 0) bit for bit, incl. keys.  Each
     frame runs twice: the second call uses the bounds the first one learned."""
     import synth
     frames = [synth.frame(640, 480, 3), synth.frame(1000, 333, 5),
