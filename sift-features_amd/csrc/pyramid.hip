@@ -1234,14 +1234,17 @@ __device__ __forceinline__ f2v u8_unit2(float a, float b) {
 // constant chunk.
 template <class G, int P, bool NOLOAD = false>
 struct SeedLoader {
-    static constexpr int CW = 12;              // window columns per item
-    static constexpr int NCG = G::IWV / CW;    // column groups (12)
-    // row pairs per loading wave: 4 (48 of its lanes busy); S = 32: all four
-    // waves load, S = 16 (k_seed_pair): waves 0, 1 load and 2, 3 skip the
-    // loader (2 pairs on each of 4 waves left 40 of 64 lanes idle)
-    static constexpr int NPW = 4;
-    static constexpr int NLW = G::S / (2 * NPW);  // loading waves
-    static_assert(G::NW == 4 && G::IWV == 144 && NCG * NPW <= 64 && NLW * NPW * 2 == G::S, "loader item map");
+    // Every wave loads: 48 lanes per wave, NPW row pairs x NCG column groups.
+    // S = 32 (k_seed_strip): items of 12 columns, 4 pairs per wave.  S = 16
+    // (k_seed_pair): items of 6 columns, 2 pairs per wave -- with 12-column
+    // items only waves 0, 1 had any, and the other two waited out the
+    // loader's upsample at the next barrier.
+    static constexpr int CW = G::S == 16 ? 6 : 12;  // window columns per item
+    static constexpr int NCG = G::IWV / CW;         // column groups (24 / 12)
+    static constexpr int NPW = G::S == 16 ? 2 : 4;  // row pairs per wave
+    static constexpr int NLW = G::S / (2 * NPW);    // loading waves (4)
+    static_assert(G::NW == 4 && G::IWV == 144 && NCG * NPW <= 64 && NLW * NPW * 2 == G::S && NLW == G::NW,
+                  "loader item map");
     // border columns: per window column its source offset from the item's
     // first source byte (bits 0-3), single / two taps (bit 4), coefficients
     struct Tables {
@@ -1279,7 +1282,7 @@ struct SeedLoader {
             }
 #pragma unroll
             for (int k = 0; k < CW; k++) t.info[CW * tid + k] = (sx[k] - lo) | (two[k] ? 16 : 0);
-            t.smin[tid] = lo;  // 12 columns span <= 8 sources
+            t.smin[tid] = lo;  // CW (<= 12) columns span <= 8 sources
         }
     }
     __device__ __forceinline__ void init(const uint8_t* src, size_t row_stride_, int sh_, int sw_, int W_, int H_,
@@ -1386,7 +1389,18 @@ struct SeedLoader {
             }
         }
     }
-    // HResizeLinear of one source row's 12 columns from its 8 bytes
+    // one item row of CW floats into the slot (16-B stores for 12 columns, 8-B
+    // for 6: an item's first column is even, so 8-B aligned)
+    __device__ __forceinline__ static void put_row(float* o, const float (&v)[CW]) {
+        if constexpr (CW % 4 == 0) {
+#pragma unroll
+            for (int k = 0; k < CW; k += 4) *reinterpret_cast<float4*>(o + k) = make_float4(v[k], v[k + 1], v[k + 2], v[k + 3]);
+        } else {
+#pragma unroll
+            for (int k = 0; k < CW; k += 2) *reinterpret_cast<float2*>(o + k) = make_float2(v[k], v[k + 1]);
+        }
+    }
+    // HResizeLinear of one source row's CW columns from its (up to) 8 bytes
     __device__ __forceinline__ void hres(const uint32_t (&w)[3], uint32_t sh3, float (&h)[CW]) const {
         float p[8];
         units(w, sh3, p);
@@ -1445,9 +1459,7 @@ struct SeedLoader {
                         v[k] = s0 * b[r][0] + s1 * b[r][1];
                     }
                 }
-#pragma unroll
-                for (int k = 0; k < CW; k += 4)
-                    *reinterpret_cast<float4*>(out + r * G::IWP + k) = make_float4(v[k], v[k + 1], v[k + 2], v[k + 3]);
+                put_row(out + r * G::IWP, v);
             }
         } else {
             // image::imageops::resize Triangle 2x: vertical_sample over the
@@ -1483,9 +1495,7 @@ struct SeedLoader {
                 hmix(vs, v);
 #pragma unroll
                 for (int k = 0; k < CW; k++) v[k] = fminf(fmaxf(v[k], 0.0f), 1.0f);
-#pragma unroll
-                for (int k = 0; k < CW; k += 4)
-                    *reinterpret_cast<float4*>(out + r * G::IWP + k) = make_float4(v[k], v[k + 1], v[k + 2], v[k + 3]);
+                put_row(out + r * G::IWP, v);
             }
         }
     }

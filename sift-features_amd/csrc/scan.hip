@@ -48,6 +48,43 @@ __device__ __forceinline__ float dpp_from_right(float v) {  // lane i <- lane i 
     return __int_as_float(__builtin_amdgcn_mov_dpp(__float_as_int(v), 0x130, 0xf, 0xf, true));
 }
 
+// point_is_local_extremum (src/lib.rs:437-506) for scales 1..3 of row y at
+// this lane's column, from the DoG rows y - 1 (prv), y (mid) and y + 1 (cur)
+// of the five planes.  Bit s - 1 of the result: scale s is a candidate.
+// The reference tests val > threshold (= 0, src/lib.rs:460) and val >= the
+// max of its 8 neighbours in plane s and of the 9 values in planes s - 1 and
+// s + 1 (val < 0: <= the mins).  Here every plane's full 3x3 max / min (the
+// centre included) is formed once -- vertical max3 / min3, then the two lane
+// neighbours through DPP shifts -- and val >= max(P_{s-1}, P_s, P_{s+1}):
+// P_s includes val itself, so val >= P_s is exactly val >= its 8 neighbours.
+// (Comparisons only; no NaN can occur, so the order of max / min operands
+// does not matter.)
+__device__ __forceinline__ uint32_t extremum3(const float (&prv)[kDogPerOctave], const float (&mid)[kDogPerOctave],
+                                              const float (&cur)[kDogPerOctave], bool yin) {
+    const float threshold = floorf(0.5f * kContrastThreshold / (float)kScalesPerOctave);  // 0
+    float pmx[kDogPerOctave], pmn[kDogPerOctave];
+#pragma unroll
+    for (int p = 0; p < kDogPerOctave; p++) {
+        const float vx = fmaxf(fmaxf(prv[p], mid[p]), cur[p]);
+        const float vn = fminf(fminf(prv[p], mid[p]), cur[p]);
+        // max(x - 1, x) then max of that and its right neighbour's: two
+        // v_max_f32_dpp, no shifted copies
+        const float tx = fmaxf(dpp_from_left(vx), vx), tn = fminf(dpp_from_left(vn), vn);
+        pmx[p] = fmaxf(dpp_from_right(tx), tx);
+        pmn[p] = fminf(dpp_from_right(tn), tn);
+    }
+    uint32_t ok3 = 0;
+#pragma unroll
+    for (int s_in = 1; s_in <= kScalesPerOctave; s_in++) {
+        const float val = mid[s_in];
+        const float mx = fmaxf(fmaxf(pmx[s_in - 1], pmx[s_in]), pmx[s_in + 1]);
+        const float mn = fminf(fminf(pmn[s_in - 1], pmn[s_in]), pmn[s_in + 1]);
+        const bool ok = yin && fabsf(val) > threshold && (val > 0.0f ? val >= mx : val <= mn);
+        ok3 |= (uint32_t)ok << (s_in - 1);
+    }
+    return ok3;
+}
+
 // 73 VGPRs, 6 waves per SIMD; forcing 7 spills in the row loop (+30% time)
 #ifndef SIFT_DETECT_WPE
 #define SIFT_DETECT_WPE 1
@@ -76,10 +113,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_DETECT
         const int xc = min(max(x, 0), W - 1);
         const bool xout = lane >= 1 && lane <= DR_COLS && x >= kImageBorder && x < W - kImageBorder;
         const int y0 = L.y_lo + sy * DR_SH, y1 = min(y0 + DR_SH, L.y_hi);
-        // rolling state per plane: row max / min of rows y - 1, y, y + 1
-        float hmx[kDogPerOctave][3], hmn[kDogPerOctave][3];
-        float lrx[kDogPerOctave], lrn[kDogPerOctave], ctr[kDogPerOctave];  // row y (middle planes used)
-        float nv[kImagesPerOctave], nlx[kDogPerOctave], nln[kDogPerOctave];
+        // DoG rows y - 1 (prv) and y (mid) at this lane's column
+        float prv[kDogPerOctave], mid[kDogPerOctave], nv[kImagesPerOctave];
         // one row of G_0..G_5; the loads of row y + 2 stay in flight as raw
         // Gaussians and become D values (to_dog) when the row is consumed
         auto load_row = [&](int yy, float (&g)[kImagesPerOctave]) {
@@ -91,37 +126,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_DETECT
 #pragma unroll
             for (int p = 0; p < kDogPerOctave; p++) v[p] = g[p + 1] - g[p];
         };
-        auto row_stats = [&](const float (&v)[kDogPerOctave], float (&mx)[kDogPerOctave], float (&mn)[kDogPerOctave],
-                             float (&lx)[kDogPerOctave], float (&ln)[kDogPerOctave]) {
-#pragma unroll
-            for (int p = 0; p < kDogPerOctave; p++) {
-                const float l = dpp_from_left(v[p]), r = dpp_from_right(v[p]);
-                lx[p] = fmaxf(l, r);
-                ln[p] = fminf(l, r);
-                mx[p] = fmaxf(lx[p], v[p]);
-                mn[p] = fminf(ln[p], v[p]);
-            }
-        };
-        float v[kDogPerOctave], m0[kDogPerOctave], n0[kDogPerOctave];
-        // rows y0 - 1 and y0
         load_row(y0 - 1, nv);
-        to_dog(nv, v);
-        row_stats(v, m0, n0, nlx, nln);
-#pragma unroll
-        for (int p = 0; p < kDogPerOctave; p++) {
-            hmx[p][0] = m0[p];
-            hmn[p][0] = n0[p];
-        }
+        to_dog(nv, prv);
         load_row(y0, nv);
-        to_dog(nv, v);
-        row_stats(v, m0, n0, lrx, lrn);
-#pragma unroll
-        for (int p = 0; p < kDogPerOctave; p++) {
-            hmx[p][1] = m0[p];
-            hmn[p][1] = n0[p];
-            ctr[p] = v[p];
-        }
-        const float threshold = floorf(0.5f * kContrastThreshold / (float)kScalesPerOctave);
+        to_dog(nv, mid);
         // Two rows in flight (rows y + 1 and y + 2 while row y is tested) in
         // two alternating buffers -- the loop is unrolled by two so neither
         // buffer is copied while its loads are outstanding.
@@ -133,31 +141,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_DETECT
             float cur[kDogPerOctave];
             to_dog(buf, cur);
             if (y + 2 < y1) load_row(y + 3, buf);
-            row_stats(cur, m0, n0, nlx, nln);
-#pragma unroll
-            for (int p = 0; p < kDogPerOctave; p++) {
-                hmx[p][2] = m0[p];
-                hmn[p][2] = n0[p];
-            }
-            // point_is_local_extremum for row y, scales 1..3
             const bool yin = xout && y >= kImageBorder && y < H - kImageBorder;
-            float pmx[kDogPerOctave], pmn[kDogPerOctave];
-#pragma unroll
-            for (int p = 0; p < kDogPerOctave; p++) {
-                pmx[p] = fmaxf(fmaxf(hmx[p][0], hmx[p][1]), hmx[p][2]);
-                pmn[p] = fminf(fminf(hmn[p][0], hmn[p][1]), hmn[p][2]);
-            }
-            uint32_t ok3 = 0;
-#pragma unroll
-            for (int s_in = 1; s_in <= kScalesPerOctave; s_in++) {
-                const float val = ctr[s_in];
-                const float m8 = fmaxf(fmaxf(hmx[s_in][0], hmx[s_in][2]), lrx[s_in]);
-                const float n8 = fminf(fminf(hmn[s_in][0], hmn[s_in][2]), lrn[s_in]);
-                const float mx = fmaxf(fmaxf(pmx[s_in - 1], pmx[s_in + 1]), m8);
-                const float mn = fminf(fminf(pmn[s_in - 1], pmn[s_in + 1]), n8);
-                const bool ok = yin && fabsf(val) > threshold && (val > 0.0f ? val >= mx : val <= mn);
-                ok3 |= (uint32_t)ok << (s_in - 1);
-            }
+            uint32_t ok3 = extremum3(prv, mid, cur, yin);
             if (__ballot(ok3 != 0)) {  // wave-uniform: rare
                 while (ok3) {
                     const int bit = __builtin_ctz(ok3);
@@ -173,16 +158,10 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_DETECT
                     }
                 }
             }
-            // shift rows: y + 1 becomes the centre row
 #pragma unroll
-            for (int p = 0; p < kDogPerOctave; p++) {
-                hmx[p][0] = hmx[p][1];
-                hmn[p][0] = hmn[p][1];
-                hmx[p][1] = hmx[p][2];
-                hmn[p][1] = hmn[p][2];
-                lrx[p] = nlx[p];
-                lrn[p] = nln[p];
-                ctr[p] = cur[p];
+            for (int p = 0; p < kDogPerOctave; p++) {  // y + 1 becomes the centre row
+                prv[p] = mid[p];
+                mid[p] = cur[p];
             }
         };
         for (int y = y0; y < y1; y += 2) {
@@ -335,11 +314,8 @@ __global__ __launch_bounds__(256) void k_blur_detect(const BlurDetectLaunch L) {
             return acc;
         };
         float win[2 * R + 1];  // row-filter outputs of rows r - R .. r + R
-        // rolling detection state (k_detect_rows): row max / min of rows r - 2,
-        // r - 1, r per DoG plane, the left / right max / min and centre of row r - 1
-        float hmx[kDogPerOctave][3], hmn[kDogPerOctave][3];
-        float lrx[kDogPerOctave], lrn[kDogPerOctave], ctr[kDogPerOctave];
-        const float threshold = floorf(0.5f * kContrastThreshold / (float)kScalesPerOctave);
+        // detection state: the DoG rows r - 2 (prv) and r - 1 (mid)
+        float prv[kDogPerOctave] = {}, mid[kDogPerOctave] = {};
         const int q0 = ya - 1 - R, q1 = yb + R;  // G_4 rows filtered: [q0, q1]
         // Row data of one G_4 row q: its ring columns (a, c) and G_0..G_3 of
         // row r = q - R at this lane's column (the window-filling rows r <
@@ -411,35 +387,10 @@ __global__ __launch_bounds__(256) void k_blur_detect(const BlurDetectLaunch L) {
             cur[2] = B.d[3] - B.d[2];
             cur[3] = g4 - B.d[3];
             cur[4] = g5 - g4;
-            float nlx[kDogPerOctave], nln[kDogPerOctave];
-#pragma unroll
-            for (int p = 0; p < kDogPerOctave; p++) {
-                const float l = dpp_from_left(cur[p]), rr = dpp_from_right(cur[p]);
-                nlx[p] = fmaxf(l, rr);
-                nln[p] = fminf(l, rr);
-                hmx[p][2] = fmaxf(nlx[p], cur[p]);
-                hmn[p][2] = fminf(nln[p], cur[p]);
-            }
             const int y = r - 1;  // tested row: rows r - 2, r - 1, r are in
             if (FULL || y >= ya) {  // uniform
                 const bool yin = xout && y >= kImageBorder && y < H - kImageBorder;
-                float pmx[kDogPerOctave], pmn[kDogPerOctave];
-#pragma unroll
-                for (int p = 0; p < kDogPerOctave; p++) {
-                    pmx[p] = fmaxf(fmaxf(hmx[p][0], hmx[p][1]), hmx[p][2]);
-                    pmn[p] = fminf(fminf(hmn[p][0], hmn[p][1]), hmn[p][2]);
-                }
-                uint32_t ok3 = 0;
-#pragma unroll
-                for (int s_in = 1; s_in <= kScalesPerOctave; s_in++) {
-                    const float val = ctr[s_in];
-                    const float m8 = fmaxf(fmaxf(hmx[s_in][0], hmx[s_in][2]), lrx[s_in]);
-                    const float n8 = fminf(fminf(hmn[s_in][0], hmn[s_in][2]), lrn[s_in]);
-                    const float mx = fmaxf(fmaxf(pmx[s_in - 1], pmx[s_in + 1]), m8);
-                    const float mn = fminf(fminf(pmn[s_in - 1], pmn[s_in + 1]), n8);
-                    const bool ok = yin && fabsf(val) > threshold && (val > 0.0f ? val >= mx : val <= mn);
-                    ok3 |= (uint32_t)ok << (s_in - 1);
-                }
+                uint32_t ok3 = extremum3(prv, mid, cur, yin);
                 if (__ballot(ok3 != 0)) {  // wave-uniform: rare
                     while (ok3) {
                         const int bit = __builtin_ctz(ok3);
@@ -458,13 +409,8 @@ __global__ __launch_bounds__(256) void k_blur_detect(const BlurDetectLaunch L) {
             }
 #pragma unroll
             for (int p = 0; p < kDogPerOctave; p++) {
-                hmx[p][0] = hmx[p][1];
-                hmn[p][0] = hmn[p][1];
-                hmx[p][1] = hmx[p][2];
-                hmn[p][1] = hmn[p][2];
-                lrx[p] = nlx[p];
-                lrn[p] = nln[p];
-                ctr[p] = cur[p];
+                prv[p] = mid[p];
+                mid[p] = cur[p];
             }
             shift();
         };
