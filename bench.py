@@ -244,6 +244,18 @@ def main():
     torch.cuda.synchronize()
     serial_ms = 1e3 * (time.perf_counter() - t1) / args.steps
     st = ctx.stats()
+    # The blur kernels alone, for reference: the same serialised steps with
+    # the octaves' last blur as a plain strip launch and the extremum scan in
+    # the detect stage (path option fused_detect = 0; the same bits).  The
+    # product path fuses them, so `roofline` above is the stage as it runs.
+    with ctx.path_options(fused_detect=0):
+        step()
+        torch.cuda.synchronize()
+        ctx.reset_stats()
+        for _ in range(args.steps):
+            step()
+        torch.cuda.synchronize()
+        st_unf = ctx.stats()
     # one more (untimed) step with the measurement-only sample counters: the
     # gradient samples the orientation and descriptor kernels evaluate per
     # step, divided by their serialised-pass stage time above
@@ -320,6 +332,7 @@ def main():
     per_launch_bytes = st["pyramid_bytes"] / max(1, st["pyramid_launches"])
     per_launch_ms = st["pyramid_ms"] / max(1, st["pyramid_launches"])
     fused_bytes = st["pyramid_bytes"] + st["pyramid_scan_bytes"]
+    unf_gbs = st_unf["pyramid_bytes"] / (st_unf["pyramid_ms"] * 1e-3) / 1e9 if st_unf["pyramid_ms"] > 0 else 0.0
     fused_gbs = fused_bytes / (st["pyramid_ms"] * 1e-3) / 1e9 if st["pyramid_ms"] > 0 else 0.0
 
     # the same steps with the results copied to host arrays (PCIe-inclusive)
@@ -453,6 +466,13 @@ def main():
                          "algorithmic_bytes_per_launch": per_launch_bytes,
                          "launches": st["pyramid_launches"],
                          "avg_launch_ms": per_launch_ms},
+            "roofline_blur_kernels_only": {
+                "achieved": unf_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": unf_gbs / HBM_PEAK_GBS,
+                "pyramid_ms_per_step": st_unf["pyramid_ms"] / args.steps,
+                "detect_ms_per_step": st_unf["detect_ms"] / args.steps,
+                "note": "not the product path: the same serialised steps with path option fused_detect=0 "
+                        "(every octave's blur 5 a plain strip launch, its extremum scan in the detect stage), "
+                        "so the stage holds only the blur kernels; same yardstick (SURVEY.md 8(d))"},
             "roofline_fused_stage": {"achieved": fused_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s",
                                      "frac": fused_gbs / HBM_PEAK_GBS,
                                      "bytes_per_launch": fused_bytes / max(1, st["pyramid_launches"]),
