@@ -232,15 +232,6 @@ constexpr int BD_RP = 100;   // ring row pitch (floats): 64 + 2R columns, R <= 1
 #ifndef BD_UNROLL
 #define BD_UNROLL 1  // row groups per steady-state loop iteration
 #endif
-#ifndef BD_DEPTH
-#define BD_DEPTH 2  // row-buffer pairs: loads issued 2 (2 pairs) or 4 (3 pairs) rows ahead
-#endif
-#ifndef BD_WPE
-#define BD_WPE 1
-#endif
-#ifndef BD_RSPLIT
-#define BD_RSPLIT 0
-#endif
 
 template <int P>
 __device__ __forceinline__ int bd_index(int p, int n) {
@@ -257,7 +248,7 @@ __device__ __forceinline__ uint32_t xcd_block_1d() {
 }
 
 template <int R, int P>
-__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BD_WPE))) void k_blur_detect(const BlurDetectLaunch L) {
+__global__ __launch_bounds__(256) void k_blur_detect(const BlurDetectLaunch L) {
     static_assert(64 + 2 * R <= BD_RP && R + 3 <= BD_RING, "ring geometry");
     __shared__ float ring[4][BD_RING * BD_RP];
     __shared__ uint64_t lcand[DR_LCAP];
@@ -312,25 +303,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BD_WPE))) v
         auto rowpass = [&](int q) -> float {
             const float* p = rg + (q & (BD_RING - 1)) * BD_RP + lane;
             float v[2 * R + 1];
-            // BD_RSPLIT: the taps' LDS reads in two halves (fewer live values)
-            constexpr int H1 = BD_RSPLIT ? R : 2 * R;
 #pragma unroll
-            for (int t = 0; t <= H1; t++) v[t] = p[t];
+            for (int t = 0; t <= 2 * R; t++) v[t] = p[t];
             float acc = v[0] * L.taps.k[R];
 #pragma unroll
-            for (int t = 1; t <= H1; t++) {
+            for (int t = 1; t <= 2 * R; t++) {
                 const float kt = L.taps.k[t > R ? t - R : R - t];
                 acc = P == kProfileOpenCV ? __builtin_fmaf(v[t], kt, acc) : acc + v[t] * kt;
-            }
-            if constexpr (H1 < 2 * R) {
-                __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-                for (int t = H1 + 1; t <= 2 * R; t++) v[t] = p[t];
-#pragma unroll
-                for (int t = H1 + 1; t <= 2 * R; t++) {
-                    const float kt = L.taps.k[t > R ? t - R : R - t];
-                    acc = P == kProfileOpenCV ? __builtin_fmaf(v[t], kt, acc) : acc + v[t] * kt;
-                }
             }
             return acc;
         };
@@ -435,36 +414,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BD_WPE))) v
             }
             shift();
         };
-#if BD_DEPTH == 3
-        // rows q, q + 1 from (A0, A1) while q + 2 .. q + 5 are in flight into
-        // (B0, B1), (C0, C1): loads issued four rows ahead
-        RowBuf A0, A1, B0, B1, C0, C1;
-        constexpr int GROUP = 6;
-        auto group = [&](int q, auto full_tag) {
-            load(q + 4, C0, 0);
-            load(q + 5, C1, 1);
-            __builtin_amdgcn_sched_barrier(0);
-            step(q, A0, full_tag);
-            step(q + 1, A1, full_tag);
-            __builtin_amdgcn_sched_barrier(0);
-            load(q + 6, A0, 0);
-            load(q + 7, A1, 1);
-            __builtin_amdgcn_sched_barrier(0);
-            step(q + 2, B0, full_tag);
-            step(q + 3, B1, full_tag);
-            __builtin_amdgcn_sched_barrier(0);
-            load(q + 8, B0, 0);
-            load(q + 9, B1, 1);
-            __builtin_amdgcn_sched_barrier(0);
-            step(q + 4, C0, full_tag);
-            step(q + 5, C1, full_tag);
-            __builtin_amdgcn_sched_barrier(0);
-        };
-        load(q0, A0, 0);
-        load(q0 + 1, A1, 1);
-        load(q0 + 2, B0, 0);
-        load(q0 + 3, B1, 1);
-#else
         // rows q, q + 1 from (A0, A1) while q + 2, q + 3 load into (B0, B1),
         // then the other way round (even / odd rows: par 0 / 1)
         RowBuf A0, A1, B0, B1;
@@ -485,7 +434,6 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(BD_WPE))) v
         };
         load(q0, A0, 0);
         load(q0 + 1, A1, 1);
-#endif
         // window fill: rows q0 .. ya + R (2R + 2 rows), then the steady rows
         // a group at a time, the last rows guarded again (a guarded step is
         // exact at any row, so the fill may run past ya + R)

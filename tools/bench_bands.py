@@ -10,6 +10,7 @@ per keypoint) comes on top.  Frames are the tiled synthetic frames of
 tests/test_gpu_large.py (8192 x 8192 by default, configs #5).
 
     python tools/bench_bands.py [--size 8192] [--reps 5]
+    python tools/bench_bands.py --gloo-from /tmp/sift_bands_parts   (no GPU)
 
 Each band is timed twice: results left in HBM (`device_ms`, as a GPU
 consumer -- matching, the all-gather over RCCL -- takes them; n = 1 is then
@@ -38,7 +39,8 @@ def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--size", type=int, default=8192)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--parts-dir", default=os.path.join(ROOT, "gpurun_out", "bands_parts"))
+    # outside gpurun_out/: the parts are ~45 MB per band count
+    ap.add_argument("--parts-dir", default="/tmp/sift_bands_parts")
     ap.add_argument("--gloo-from", default=None, help="time the gloo all-gather of saved band results (no GPU)")
     a = ap.parse_args()
     if a.gloo_from:
