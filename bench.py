@@ -64,6 +64,8 @@ def parse():
     p.add_argument("--no-cpu-baseline", action="store_true")
     p.add_argument("--no-latency", action="store_true")
     p.add_argument("--no-configs", action="store_true", help="skip the other single-GPU BASELINE configs")
+    p.add_argument("--no-unfused", action="store_true",
+                   help="skip the blur-kernels-only reference pass (profiles: product kernels only)")
     p.add_argument("--no-jpeg", action="store_true", help="skip the JPEG -> keypoints end-to-end field")
     return p.parse_args()
 
@@ -248,14 +250,16 @@ def main():
     # the octaves' last blur as a plain strip launch and the extremum scan in
     # the detect stage (path option fused_detect = 0; the same bits).  The
     # product path fuses them, so `roofline` above is the stage as it runs.
-    with ctx.path_options(fused_detect=0):
-        step()
-        torch.cuda.synchronize()
-        ctx.reset_stats()
-        for _ in range(args.steps):
+    st_unf = None
+    if not args.no_unfused:
+        with ctx.path_options(fused_detect=0):
             step()
-        torch.cuda.synchronize()
-        st_unf = ctx.stats()
+            torch.cuda.synchronize()
+            ctx.reset_stats()
+            for _ in range(args.steps):
+                step()
+            torch.cuda.synchronize()
+            st_unf = ctx.stats()
     # one more (untimed) step with the measurement-only sample counters: the
     # gradient samples the orientation and descriptor kernels evaluate per
     # step, divided by their serialised-pass stage time above
@@ -332,7 +336,8 @@ def main():
     per_launch_bytes = st["pyramid_bytes"] / max(1, st["pyramid_launches"])
     per_launch_ms = st["pyramid_ms"] / max(1, st["pyramid_launches"])
     fused_bytes = st["pyramid_bytes"] + st["pyramid_scan_bytes"]
-    unf_gbs = st_unf["pyramid_bytes"] / (st_unf["pyramid_ms"] * 1e-3) / 1e9 if st_unf["pyramid_ms"] > 0 else 0.0
+    unf_gbs = (st_unf["pyramid_bytes"] / (st_unf["pyramid_ms"] * 1e-3) / 1e9
+               if st_unf and st_unf["pyramid_ms"] > 0 else 0.0)
     fused_gbs = fused_bytes / (st["pyramid_ms"] * 1e-3) / 1e9 if st["pyramid_ms"] > 0 else 0.0
 
     # the same steps with the results copied to host arrays (PCIe-inclusive)
@@ -466,7 +471,7 @@ def main():
                          "algorithmic_bytes_per_launch": per_launch_bytes,
                          "launches": st["pyramid_launches"],
                          "avg_launch_ms": per_launch_ms},
-            "roofline_blur_kernels_only": {
+            "roofline_blur_kernels_only": None if st_unf is None else {
                 "achieved": unf_gbs, "peak": HBM_PEAK_GBS, "unit": "GB/s", "frac": unf_gbs / HBM_PEAK_GBS,
                 "pyramid_ms_per_step": st_unf["pyramid_ms"] / args.steps,
                 "detect_ms_per_step": st_unf["detect_ms"] / args.steps,

@@ -60,19 +60,52 @@ __device__ __forceinline__ void load_nbhd(const gfloat* g0, size_t P, int pitch,
         }
 }
 
-// On success n holds the neighbourhood of the converged point (scale, y, x),
-// which extremum_contrast / extremum_is_on_edge read next.
-__device__ __forceinline__ bool interpolate(const gfloat* g0, size_t P, int W, int H, int pitch, int& scale, int& x,
-                                            int& y, float& os, float& ox, float& oy, Nbhd& n, uint32_t* band_flag,
-                                            int vlo, int vhi) {
-    for (int it = 0; it < kMaxInterpSteps; it++) {
-        // row bands with a restricted pyramid (host.cpp run_pyramid): the
-        // rows read here must be computed ones, else the host recomputes the
-        // band on the whole-frame pyramid
-        if (band_flag && (y - 1 < vlo || y + 1 >= vhi)) atomicOr(band_flag, 1u);
-        load_nbhd(g0, P, pitch, scale, y, x, n);
-        // AT(plane, dy, dx): plane 0 / 1 / 2 = prev / curr / next
+// ---------------------------------------------------------------------------
+// k_refine: interpolate_extremum, extremum_contrast, extremum_is_on_edge
+// (src/lib.rs:334-367, 525-653) for the candidate list.
+//
+// interpolate_extremum takes 1 Newton step for ~78% of candidates but up to 5
+// (a candidate that keeps moving; ~9% hit the cap), and every step is a round
+// trip of dependent loads.  With one candidate per lane for its whole
+// refinement, a wave would run as many steps as its slowest lane -- nearly
+// always 5.  Here a lane holds a refinement STATE (candidate, current scale /
+// row / column, steps taken) and the wave advances all its lanes by one step
+// per loop trip; a lane whose candidate is decided (accepted, rejected, or
+// out of steps) takes the next candidate of the wave's range at once.  Each
+// candidate runs exactly the reference's sequence of steps (same expressions,
+// same order), so the extrema are those of the one-candidate-per-lane
+// kernel bit for bit; only their append order differs (sorted by key later).
+// ---------------------------------------------------------------------------
+struct RefineState {
+    uint64_t key;
+    int sc, xi, yi, it;  // current scale, column, row; Newton steps taken
+};
+
+// One step for state st.  Returns 1 (accepted: e filled), -1 (rejected) or 0
+// (moved: another step follows).
+__device__ __forceinline__ int refine_step(const RefineLaunch& L, RefineState& st, ExtRec& e) {
+    const uint64_t key = st.key;
+    const int b = (int)(key >> kKeyImgShift);
+    const int o = (int)((key >> kKeyOctShift) & 15);
+    const int W = L.ow[o], H = L.oh[o], pitch = L.opitch[o];
+    const gfloat* g0 = as_global(L.gauss[o]) + (size_t)(b - L.img_base) * L.g_img_stride[o];
+    const size_t P = (size_t)pitch * H;
+    int vlo = 0, vhi = H;  // rows of this octave's Gaussians that are exact
+    if (L.band_flag) {
+        vlo = max(0, (int)((uint64_t)H * L.band_r / L.band_n) - 1 - L.band_margin);
+        vhi = min(H, (int)((uint64_t)H * (L.band_r + 1) / L.band_n) + 1 + L.band_margin);
+    }
+    const int x = st.xi, y = st.yi, scale = st.sc;
+    // row bands with a restricted pyramid (host.cpp run_pyramid): the rows
+    // read here must be computed ones, else the host recomputes the band on
+    // the whole-frame pyramid
+    if (L.band_flag && (y - 1 < vlo || y + 1 >= vhi)) atomicOr(L.band_flag, 1u);
+    Nbhd n;
+    load_nbhd(g0, P, pitch, scale, y, x, n);
+    // interpolate_extremum (src/lib.rs:525-603), one iteration
+    // AT(plane, dy, dx): plane 0 / 1 / 2 = prev / curr / next
 #define AT(a, dy, dx) n.d[a][(dy) + 1][(dx) + 1]
+    {
         const float g1 = (AT(2, 0, 0) - AT(0, 0, 0)) / 2.f;
         const float g2 = (AT(1, 1, 0) - AT(1, -1, 0)) / 2.f;
         const float g3 = (AT(1, 0, 1) - AT(1, 0, -1)) / 2.f;
@@ -83,7 +116,6 @@ __device__ __forceinline__ bool interpolate(const gfloat* g0, size_t P, int W, i
         const float h22 = AT(1, 1, 0) + AT(1, -1, 0) - v2;
         const float h33 = AT(1, 0, 1) + AT(1, 0, -1) - v2;
         const float h23 = (AT(1, 1, 1) - AT(1, 1, -1) - AT(1, -1, 1) + AT(1, -1, -1)) / 4.f;
-#undef AT
         const float det =
             h11 * h22 * h33 - h11 * h23 * h23 - h12 * h12 * h33 + 2.f * h12 * h13 * h23 - h13 * h13 * h22;
         const float i11 = (h22 * h33 - h23 * h23) / det;
@@ -95,108 +127,102 @@ __device__ __forceinline__ bool interpolate(const gfloat* g0, size_t P, int W, i
         const float s_ = -(i11 * g1 + i12 * g2 + i13 * g3);
         const float x_ = -(i13 * g1 + i23 * g2 + i33 * g3);
         const float y_ = -(i12 * g1 + i22 * g2 + i23 * g3);
-        if (fabsf(s_) < 0.5f && fabsf(x_) < 0.5f && fabsf(y_) < 0.5f) {
-            os = s_;
-            ox = x_;
-            oy = y_;
-            return true;
+        if (!(fabsf(s_) < 0.5f && fabsf(x_) < 0.5f && fabsf(y_) < 0.5f)) {
+            // `x as isize + offset.round() as isize` (saturating), then bounds
+            const int64_t LIM = (int64_t)1 << 40;
+            const int64_t rx = sat_i64(roundf(x_)), ry = sat_i64(roundf(y_)), rs = sat_i64(roundf(s_));
+            if (rx > LIM || rx < -LIM || ry > LIM || ry < -LIM || rs > LIM || rs < -LIM) return -1;
+            const int64_t nx = x + rx, ny = y + ry, ns = scale + rs;
+            if (!(ns >= 1 && ns <= kScalesPerOctave) || nx < kImageBorder || nx >= W - kImageBorder ||
+                ny < kImageBorder || ny >= H - kImageBorder)
+                return -1;
+            st.xi = (int)nx;
+            st.yi = (int)ny;
+            st.sc = (int)ns;
+            return ++st.it < kMaxInterpSteps ? 0 : -1;
         }
-        // `x as isize + offset.round() as isize` (saturating), then bounds
-        const int64_t LIM = (int64_t)1 << 40;
-        const int64_t rx = sat_i64(roundf(x_)), ry = sat_i64(roundf(y_)), rs = sat_i64(roundf(s_));
-        if (rx > LIM || rx < -LIM || ry > LIM || ry < -LIM || rs > LIM || rs < -LIM) return false;
-        const int64_t nx = x + rx, ny = y + ry, ns = scale + rs;
-        if (!(ns >= 1 && ns <= kScalesPerOctave) || nx < kImageBorder || nx >= W - kImageBorder ||
-            ny < kImageBorder || ny >= H - kImageBorder)
-            return false;
-        x = (int)nx;
-        y = (int)ny;
-        scale = (int)ns;
+        e.off_s = s_;
+        e.off_x = x_;
+        e.off_y = y_;
     }
-    return false;
-}
-
-// ---------------------------------------------------------------------------
-// k_refine: one thread per candidate extremum -- interpolate_extremum,
-// extremum_contrast, extremum_is_on_edge (src/lib.rs:334-367); accepted
-// extrema are appended with one atomic per wave.
-// ---------------------------------------------------------------------------
-__device__ __forceinline__ bool refine_one(const RefineLaunch& L, uint64_t key, ExtRec& e) {
-    const int b = (int)(key >> kKeyImgShift);
-    const int o = (int)((key >> kKeyOctShift) & 15);
-    const int s_in = (int)((key >> kKeyScaleShift) & 3);
-    const int y = (int)((key >> kKeyYShift) & kKeyCoordMask);
-    const int x = (int)((key >> kKeyXShift) & kKeyCoordMask);
-    const int W = L.ow[o], H = L.oh[o], pitch = L.opitch[o];
-    const gfloat* g0 = as_global(L.gauss[o]) + (size_t)(b - L.img_base) * L.g_img_stride[o];
-    const size_t P = (size_t)pitch * H;
-    int sc = s_in, xi = x, yi = y;
-    float os, ox, oy;
-    Nbhd n;
-    int vlo = 0, vhi = H;  // rows of this octave's Gaussians that are exact
-    if (L.band_flag) {
-        vlo = max(0, (int)((uint64_t)H * L.band_r / L.band_n) - 1 - L.band_margin);
-        vhi = min(H, (int)((uint64_t)H * (L.band_r + 1) / L.band_n) + 1 + L.band_margin);
-    }
-    if (!interpolate(g0, P, W, H, pitch, sc, xi, yi, os, ox, oy, n, L.band_flag, vlo, vhi)) return false;
-    // the converged point's neighbourhood is n (the last step did not move)
-#define PREV(dy, dx) n.d[0][(dy) + 1][(dx) + 1]
-#define CURR(dy, dx) n.d[1][(dy) + 1][(dx) + 1]
-#define NEXT(dy, dx) n.d[2][(dy) + 1][(dx) + 1]
-    // extremum_contrast (src/lib.rs:606-626)
-    const float g1 = (NEXT(0, 0) - PREV(0, 0)) / 2.f;
-    const float g2 = (CURR(1, 0) - CURR(-1, 0)) / 2.f;
-    const float g3 = (CURR(0, 1) - CURR(0, -1)) / 2.f;
-    const float interp = os * g1 + oy * g2 + ox * g3;
-    const float contrast = fabsf(CURR(0, 0) + interp / 2.f);
-    if (contrast * (float)kScalesPerOctave <= kContrastThreshold) return false;
+    // converged: extremum_contrast (src/lib.rs:606-626) on the same neighbourhood
+    const float g1 = (AT(2, 0, 0) - AT(0, 0, 0)) / 2.f;
+    const float g2 = (AT(1, 1, 0) - AT(1, -1, 0)) / 2.f;
+    const float g3 = (AT(1, 0, 1) - AT(1, 0, -1)) / 2.f;
+    const float interp = e.off_s * g1 + e.off_y * g2 + e.off_x * g3;
+    const float contrast = fabsf(AT(1, 0, 0) + interp / 2.f);
+    if (contrast * (float)kScalesPerOctave <= kContrastThreshold) return -1;
     // extremum_is_on_edge (src/lib.rs:630-653)
-    const float v2 = CURR(0, 0) * 2.0f;
-    const float h11 = CURR(1, 0) + CURR(-1, 0) - v2;
-    const float d22 = CURR(0, 1) + CURR(0, -1) - v2;
-    const float h12 = (CURR(1, 1) - CURR(1, -1) - CURR(-1, 1) + CURR(-1, -1)) / 4.f;
-#undef PREV
-#undef CURR
-#undef NEXT
+    const float v2 = AT(1, 0, 0) * 2.0f;
+    const float h11 = AT(1, 1, 0) + AT(1, -1, 0) - v2;
+    const float d22 = AT(1, 0, 1) + AT(1, 0, -1) - v2;
+    const float h12 = (AT(1, 1, 1) - AT(1, 1, -1) - AT(1, -1, 1) + AT(1, -1, -1)) / 4.f;
+#undef AT
     const float tr = d22 + h11;
     const float det = d22 * h11 - h12 * h12;
-    if (det <= 0.f) return false;
-    if ((tr * tr * kEdgeThreshold) > (kEdgeThreshold + 1.0f) * (kEdgeThreshold + 1.0f) * det) return false;
+    if (det <= 0.f) return -1;
+    if ((tr * tr * kEdgeThreshold) > (kEdgeThreshold + 1.0f) * (kEdgeThreshold + 1.0f) * det) return -1;
     // an accepted keypoint's orientation / descriptor patch must be exact too
     // (at the image's own top / bottom rows the patch reads clamp, so no limit)
-    if (L.band_flag && ((vlo > 0 && yi - L.band_patch < vlo) || (vhi < H && yi + L.band_patch >= vhi)))
+    if (L.band_flag && ((vlo > 0 && y - L.band_patch < vlo) || (vhi < H && y + L.band_patch >= vhi)))
         atomicOr(L.band_flag, 1u);
     e.key = key;
     e.img = b;
     e.octave = o;
-    e.scale = sc;
-    e.x = xi;
-    e.y = yi;
-    e.off_s = os;
-    e.off_x = ox;
-    e.off_y = oy;
+    e.scale = scale;
+    e.x = x;
+    e.y = y;
     e.response = contrast;
     e.pad = 0;
-    return true;
+    return 1;
 }
 
 #ifndef SIFT_REFINE_WPE
 #define SIFT_REFINE_WPE 1
 #endif
+// Persistent waves: wave w owns candidates [n*w/NW, n*(w+1)/NW) and refills
+// its decided lanes from that range (ballot rank + a wave cursor), so every
+// loop trip advances up to 64 live refinements by one Newton step.
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_REFINE_WPE))) void k_refine(const RefineLaunch L) {
     const uint32_t n = min(*L.n_cand, L.cand_cap);
     const int lane = threadIdx.x & 63;
-    for (uint32_t base = blockIdx.x * 256; base < n; base += gridDim.x * 256) {
-        const uint32_t i = base + threadIdx.x;
+    const uint32_t nw = gridDim.x * 4u, w = blockIdx.x * 4u + (threadIdx.x >> 6);
+    uint32_t cur = (uint32_t)(((uint64_t)n * w) / nw);
+    const uint32_t end = (uint32_t)(((uint64_t)n * (w + 1)) / nw);
+    RefineState st{};
+    bool live = false;
+    for (;;) {
+        // refill decided lanes, in lane order, from the wave's range
+        const uint64_t need = __ballot(!live);
+        if (need && cur < end) {
+            const uint32_t rank = (uint32_t)__popcll(need & ((1ull << lane) - 1ull));
+            const uint32_t i = cur + rank;
+            if (!live && i < end) {
+                const uint64_t key = L.cand[i];
+                st.key = key;
+                st.sc = (int)((key >> kKeyScaleShift) & 3);
+                st.yi = (int)((key >> kKeyYShift) & kKeyCoordMask);
+                st.xi = (int)((key >> kKeyXShift) & kKeyCoordMask);
+                st.it = 0;
+                live = true;
+            }
+            cur = min(end, cur + (uint32_t)__popcll(need));
+        }
+        if (!__ballot(live)) break;  // wave-uniform: range done, no refinement left
         ExtRec e;
-        const bool keep = i < n && refine_one(L, L.cand[i], e);
+        int r = 0;
+        if (live) {
+            r = refine_step(L, st, e);
+            if (r != 0) live = false;
+        }
+        const bool keep = r > 0;
         const uint64_t mask = __ballot(keep);
         if (!mask) continue;
         const int leader = __ffsll((unsigned long long)mask) - 1;
-        uint32_t b = 0;
-        if (lane == leader) b = atomicAdd(L.counter, (uint32_t)__popcll(mask));
-        b = __shfl(b, leader);
-        const uint32_t slot = b + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+        uint32_t base = 0;
+        if (lane == leader) base = atomicAdd(L.counter, (uint32_t)__popcll(mask));
+        base = __shfl(base, leader);
+        const uint32_t slot = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
         if (keep && slot < L.cap) L.out[slot] = e;
     }
 }

@@ -2013,7 +2013,7 @@ int sift_mi_set_path_option(sift_mi_ctx* c, int option, int value) {
         case SIFT_MI_PATH_PAIR_BLUR: if (!b) break; o.pair = value; return 0;
         case SIFT_MI_PATH_SEED_PAIR: if (!b) break; o.seed_pair = value; return 0;
         case SIFT_MI_PATH_TAIL: if (!b) break; o.tail = value; return 0;
-        case SIFT_MI_PATH_FUSED_DETECT: if (value < 0 || value > 2) break; o.fused_detect = value; return 0;
+        case SIFT_MI_PATH_FUSED_DETECT: if (value < 0 || value > 3) break; o.fused_detect = value; return 0;
         case SIFT_MI_PATH_EARLY: if (!b) break; o.early = value; return 0;
         case SIFT_MI_PATH_DESC_FIRST: if (!b) break; o.desc_first = value; return 0;
         case SIFT_MI_PATH_GRAPH: if (!b) break; o.graph = value; return 0;

@@ -2206,7 +2206,9 @@ __global__ __launch_bounds__(1024) void k_octave_tail(const TailLaunch L) {
             // wait for the chain's G_3 of this octave, then read it into A
             if (tid == 0) {
                 uint32_t spins = 0;
-                while (__hip_atomic_load(flag, __ATOMIC_ACQUIRE, __HIP_MEMORY_SCOPE_AGENT) != L.epoch) {
+                // relaxed polls (an acquire load would invalidate this XCD's
+                // L2 on every poll); the acquire fence below follows the last
+                while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != L.epoch) {
                     __builtin_amdgcn_s_sleep(2);
                     if (++spins == (1u << 24)) {  // ~1 s: give up (the host reports it)
                         gave_up = 1;

@@ -46,7 +46,7 @@ struct PathOpts {
     int pair = 1;          // 0: no pair kernels (k_blur2_strip, k_seed_pair)
     int seed_pair = 1;     // 0: k_seed_strip, then blur 1 like the other octaves
     int tail = 1;          // 0: per-blur launches for the small octaves (no k_octave_tail)
-    int fused_detect = 1;  // 0: blur 5 and the extremum scan apart; 2: fused at 32-row segments wherever it applies
+    int fused_detect = 1;  // 0: blur 5 and the extremum scan apart; 2: fused at 32-row segments wherever it applies; 3: no one-large-frame rule
     int early = 1;         // one-chunk calls: detection of the octaves below the tail beside the tail kernel
     int desc_first = 1;    // one-frame calls: descriptors beside the ordering stage
     int graph = 0;         // 1: single-chunk calls captured once and replayed as a HIP graph

@@ -16,7 +16,7 @@ mkdir -p "$OUT"
 export TMPDIR=/tmp
 # the default bench workload only: no CPU baseline, no latency probe, no
 # other-config runs (they would mix other frame sizes into the PMC means)
-CMD="python3 bench.py --steps 3 --warmup 1 --frames $FRAMES --width $W --height $H --no-cpu-baseline --no-latency --no-configs"
+CMD="python3 bench.py --steps 3 --warmup 1 --frames $FRAMES --width $W --height $H --no-cpu-baseline --no-latency --no-configs --no-unfused"
 pass() {  # name, rocprofv3 options
   local name=$1; shift
   rm -rf "$OUT/$name"

@@ -25,18 +25,25 @@ def main():
     ap.add_argument("--width", type=int, default=1920)
     ap.add_argument("--height", type=int, default=1080)
     ap.add_argument("--octaves", type=int, default=0)
+    ap.add_argument("--frames", type=int, default=1, help="frames per call (batch A/B runs)")
+    ap.add_argument("--opt", action="append", default=[], help="path option name=value (A/B runs)")
     a = ap.parse_args()
     import torch
     import pkg_loader
     import synth
     pkg = pkg_loader.load()
     W, H = a.width, a.height
-    fr = synth.frames_torch(1, W, H, seed0=1000, device=torch.device("cuda", 0))
+    fr = synth.frames_torch(a.frames, W, H, seed0=1000, device=torch.device("cuda", 0))
     torch.cuda.synchronize()
     c = pkg.Context(0, pkg.OpenCVProcessing)
     if a.octaves:
         c.set_max_octaves(a.octaves)
-    call = (fr.data_ptr(), 1, W, H, fr.stride(1), fr.stride(0))
+    opts = {}
+    for kv in a.opt:
+        k, v = kv.split("=")
+        opts[k] = int(v)
+        c.set_path_option(k, int(v))
+    call = (fr.data_ptr(), a.frames, W, H, fr.stride(1), fr.stride(0))
     for _ in range(10):
         c.sift_batch_device(*call, fetch=False)
     torch.cuda.synchronize()
@@ -46,8 +53,8 @@ def main():
         kp += int(c.sift_batch_device(*call, fetch=False)[0][-1])
         ts.append(time.perf_counter() - t)
     c.close()
-    print(json.dumps({"frame": f"{W}x{H}", "calls": a.calls, "ms_per_call": 1e3 * float(np.mean(ts)),
-                      "ms_per_call_median": 1e3 * float(np.median(ts)), "keypoints_per_call": kp / a.calls}))
+    print(json.dumps({"frame": f"{W}x{H}", "frames_per_call": a.frames, "calls": a.calls, "ms_per_call": 1e3 * float(np.mean(ts)),
+                      "ms_per_call_median": 1e3 * float(np.median(ts)), "keypoints_per_call": kp / a.calls, "path_options": opts}))
 
 
 if __name__ == "__main__":

@@ -154,6 +154,140 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_REFINE
     }
 }
 
+// the first round-5 k_refine (one candidate per lane for its whole refinement), for A/B
+// On success n holds the neighbourhood of the converged point (scale, y, x),
+// which extremum_contrast / extremum_is_on_edge read next.
+__device__ __forceinline__ bool interpolate_r5a(const gfloat* g0, size_t P, int W, int H, int pitch, int& scale, int& x,
+                                            int& y, float& os, float& ox, float& oy, Nbhd& n, uint32_t* band_flag,
+                                            int vlo, int vhi) {
+    for (int it = 0; it < kMaxInterpSteps; it++) {
+        // row bands with a restricted pyramid (host.cpp run_pyramid): the
+        // rows read here must be computed ones, else the host recomputes the
+        // band on the whole-frame pyramid
+        if (band_flag && (y - 1 < vlo || y + 1 >= vhi)) atomicOr(band_flag, 1u);
+        load_nbhd(g0, P, pitch, scale, y, x, n);
+        // AT(plane, dy, dx): plane 0 / 1 / 2 = prev / curr / next
+#define AT(a, dy, dx) n.d[a][(dy) + 1][(dx) + 1]
+        const float g1 = (AT(2, 0, 0) - AT(0, 0, 0)) / 2.f;
+        const float g2 = (AT(1, 1, 0) - AT(1, -1, 0)) / 2.f;
+        const float g3 = (AT(1, 0, 1) - AT(1, 0, -1)) / 2.f;
+        const float v2 = AT(1, 0, 0) * 2.f;
+        const float h11 = AT(2, 0, 0) + AT(0, 0, 0) - v2;
+        const float h12 = (AT(2, 1, 0) - AT(2, -1, 0) - AT(0, 1, 0) + AT(0, -1, 0)) / 4.f;
+        const float h13 = (AT(2, 0, 1) - AT(2, 0, -1) - AT(0, 0, 1) + AT(0, 0, -1)) / 4.f;
+        const float h22 = AT(1, 1, 0) + AT(1, -1, 0) - v2;
+        const float h33 = AT(1, 0, 1) + AT(1, 0, -1) - v2;
+        const float h23 = (AT(1, 1, 1) - AT(1, 1, -1) - AT(1, -1, 1) + AT(1, -1, -1)) / 4.f;
+#undef AT
+        const float det =
+            h11 * h22 * h33 - h11 * h23 * h23 - h12 * h12 * h33 + 2.f * h12 * h13 * h23 - h13 * h13 * h22;
+        const float i11 = (h22 * h33 - h23 * h23) / det;
+        const float i12 = (h13 * h23 - h12 * h33) / det;
+        const float i13 = (h12 * h23 - h13 * h22) / det;
+        const float i22 = (h11 * h33 - h13 * h13) / det;
+        const float i23 = (h12 * h13 - h11 * h23) / det;
+        const float i33 = (h11 * h22 - h12 * h12) / det;
+        const float s_ = -(i11 * g1 + i12 * g2 + i13 * g3);
+        const float x_ = -(i13 * g1 + i23 * g2 + i33 * g3);
+        const float y_ = -(i12 * g1 + i22 * g2 + i23 * g3);
+        if (fabsf(s_) < 0.5f && fabsf(x_) < 0.5f && fabsf(y_) < 0.5f) {
+            os = s_;
+            ox = x_;
+            oy = y_;
+            return true;
+        }
+        // `x as isize + offset.round() as isize` (saturating), then bounds
+        const int64_t LIM = (int64_t)1 << 40;
+        const int64_t rx = sat_i64(roundf(x_)), ry = sat_i64(roundf(y_)), rs = sat_i64(roundf(s_));
+        if (rx > LIM || rx < -LIM || ry > LIM || ry < -LIM || rs > LIM || rs < -LIM) return false;
+        const int64_t nx = x + rx, ny = y + ry, ns = scale + rs;
+        if (!(ns >= 1 && ns <= kScalesPerOctave) || nx < kImageBorder || nx >= W - kImageBorder ||
+            ny < kImageBorder || ny >= H - kImageBorder)
+            return false;
+        x = (int)nx;
+        y = (int)ny;
+        scale = (int)ns;
+    }
+    return false;
+}
+
+__device__ __forceinline__ bool refine_one_r5a(const RefineLaunch& L, uint64_t key, ExtRec& e) {
+    const int b = (int)(key >> kKeyImgShift);
+    const int o = (int)((key >> kKeyOctShift) & 15);
+    const int s_in = (int)((key >> kKeyScaleShift) & 3);
+    const int y = (int)((key >> kKeyYShift) & kKeyCoordMask);
+    const int x = (int)((key >> kKeyXShift) & kKeyCoordMask);
+    const int W = L.ow[o], H = L.oh[o], pitch = L.opitch[o];
+    const gfloat* g0 = as_global(L.gauss[o]) + (size_t)(b - L.img_base) * L.g_img_stride[o];
+    const size_t P = (size_t)pitch * H;
+    int sc = s_in, xi = x, yi = y;
+    float os, ox, oy;
+    Nbhd n;
+    int vlo = 0, vhi = H;  // rows of this octave's Gaussians that are exact
+    if (L.band_flag) {
+        vlo = max(0, (int)((uint64_t)H * L.band_r / L.band_n) - 1 - L.band_margin);
+        vhi = min(H, (int)((uint64_t)H * (L.band_r + 1) / L.band_n) + 1 + L.band_margin);
+    }
+    if (!interpolate_r5a(g0, P, W, H, pitch, sc, xi, yi, os, ox, oy, n, L.band_flag, vlo, vhi)) return false;
+    // the converged point's neighbourhood is n (the last step did not move)
+#define PREV(dy, dx) n.d[0][(dy) + 1][(dx) + 1]
+#define CURR(dy, dx) n.d[1][(dy) + 1][(dx) + 1]
+#define NEXT(dy, dx) n.d[2][(dy) + 1][(dx) + 1]
+    // extremum_contrast (src/lib.rs:606-626)
+    const float g1 = (NEXT(0, 0) - PREV(0, 0)) / 2.f;
+    const float g2 = (CURR(1, 0) - CURR(-1, 0)) / 2.f;
+    const float g3 = (CURR(0, 1) - CURR(0, -1)) / 2.f;
+    const float interp = os * g1 + oy * g2 + ox * g3;
+    const float contrast = fabsf(CURR(0, 0) + interp / 2.f);
+    if (contrast * (float)kScalesPerOctave <= kContrastThreshold) return false;
+    // extremum_is_on_edge (src/lib.rs:630-653)
+    const float v2 = CURR(0, 0) * 2.0f;
+    const float h11 = CURR(1, 0) + CURR(-1, 0) - v2;
+    const float d22 = CURR(0, 1) + CURR(0, -1) - v2;
+    const float h12 = (CURR(1, 1) - CURR(1, -1) - CURR(-1, 1) + CURR(-1, -1)) / 4.f;
+#undef PREV
+#undef CURR
+#undef NEXT
+    const float tr = d22 + h11;
+    const float det = d22 * h11 - h12 * h12;
+    if (det <= 0.f) return false;
+    if ((tr * tr * kEdgeThreshold) > (kEdgeThreshold + 1.0f) * (kEdgeThreshold + 1.0f) * det) return false;
+    // an accepted keypoint's orientation / descriptor patch must be exact too
+    // (at the image's own top / bottom rows the patch reads clamp, so no limit)
+    if (L.band_flag && ((vlo > 0 && yi - L.band_patch < vlo) || (vhi < H && yi + L.band_patch >= vhi)))
+        atomicOr(L.band_flag, 1u);
+    e.key = key;
+    e.img = b;
+    e.octave = o;
+    e.scale = sc;
+    e.x = xi;
+    e.y = yi;
+    e.off_s = os;
+    e.off_x = ox;
+    e.off_y = oy;
+    e.response = contrast;
+    e.pad = 0;
+    return true;
+}
+
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_REFINE_WPE))) void k_refine_r5a(const RefineLaunch L) {
+    const uint32_t n = min(*L.n_cand, L.cand_cap);
+    const int lane = threadIdx.x & 63;
+    for (uint32_t base = blockIdx.x * 256; base < n; base += gridDim.x * 256) {
+        const uint32_t i = base + threadIdx.x;
+        ExtRec e;
+        const bool keep = i < n && refine_one_r5a(L, L.cand[i], e);
+        const uint64_t mask = __ballot(keep);
+        if (!mask) continue;
+        const int leader = __ffsll((unsigned long long)mask) - 1;
+        uint32_t b = 0;
+        if (lane == leader) b = atomicAdd(L.counter, (uint32_t)__popcll(mask));
+        b = __shfl(b, leader);
+        const uint32_t slot = b + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+        if (keep && slot < L.cap) L.out[slot] = e;
+    }
+}
+
 }  // namespace siftmi
 
 #define CK(x)                                                                    \
@@ -319,16 +453,13 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(&nc, cnt, 4, hipMemcpyDeviceToHost));
     std::vector<uint64_t> c_bd(nc);
     CK(hipMemcpy(c_bd.data(), cand, nc * 8, hipMemcpyDeviceToHost));
+    const std::vector<uint64_t> c_raw = c_bd;  // k_blur_detect's append order
     std::sort(c_bd.begin(), c_bd.end());
     CK(hipMemcpy(g5c.data(), g + 5 * P, P * 4, hipMemcpyDeviceToHost));
     CK(hipMemcpy(g5d.data(), g + (size_t)(n - 1) * stride + 5 * P, P * 4, hipMemcpyDeviceToHost));
     const bool same_g5 = std::memcmp(g5a.data(), g5c.data(), P * 4) == 0 && std::memcmp(g5b.data(), g5d.data(), P * 4) == 0;
     const bool same_cand = c_rows == c_bd;
-    // the candidates must be refined from a consistent order: restore k_detect_rows' list
-    CK(hipMemcpy(cand, c_rows.data(), nc_rows * 8, hipMemcpyHostToDevice));
-    CK(hipMemcpy(cnt, &nc_rows, 4, hipMemcpyHostToDevice));
-    nc = nc_rows;
-    // refine the candidates
+    // refine the candidates, in sorted and in k_blur_detect's append order
     const float** dg = nullptr;
     size_t* dgs = nullptr;
     int *dw = nullptr, *dh = nullptr, *dp = nullptr;
@@ -343,6 +474,7 @@ int main(int argc, char** argv) {
     CK(hipMemcpy(dw, &W, 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(dh, &H, 4, hipMemcpyHostToDevice));
     CK(hipMemcpy(dp, &pitch, 4, hipMemcpyHostToDevice));
+    nc = nc_rows;
     ExtRec* ext = nullptr;
     CK(hipMalloc(&ext, (size_t)nc * sizeof(ExtRec) + 64));
     RefineLaunch R{};
@@ -358,44 +490,58 @@ int main(int argc, char** argv) {
     R.counter = cnt + 1;
     R.cap = nc;
     R.band_n = 1;
-    const float tr = timeit([&] {
-        CK(hipMemsetAsync(cnt + 1, 0, 4, 0));
-        launch_refine(R, 0);
-    });
-    uint32_t ne = 0;
-    CK(hipMemcpy(&ne, cnt + 1, 4, hipMemcpyDeviceToHost));
-    std::vector<ExtRec> e_new(ne);
-    CK(hipMemcpy(e_new.data(), ext, ne * sizeof(ExtRec), hipMemcpyDeviceToHost));
-    const float tro = timeit([&] {
-        CK(hipMemsetAsync(cnt + 1, 0, 4, 0));
-        hipLaunchKernelGGL(k_refine_old, dim3(std::min<uint32_t>((R.cand_cap + 255) / 256, 2048)), dim3(256), 0, 0, R);
-    });
-    uint32_t ne_old = 0;
-    CK(hipMemcpy(&ne_old, cnt + 1, 4, hipMemcpyDeviceToHost));
-    std::vector<ExtRec> e_old(ne_old);
-    CK(hipMemcpy(e_old.data(), ext, ne_old * sizeof(ExtRec), hipMemcpyDeviceToHost));
     // the same extrema (the append order differs run to run): sort by key
-    auto by_key = [](std::vector<ExtRec>& v) {
+    auto fetch_sorted = [&]() {
+        uint32_t ne = 0;
+        CK(hipMemcpy(&ne, cnt + 1, 4, hipMemcpyDeviceToHost));
+        std::vector<ExtRec> v(ne);
+        CK(hipMemcpy(v.data(), ext, ne * sizeof(ExtRec), hipMemcpyDeviceToHost));
         std::sort(v.begin(), v.end(), [](const ExtRec& a, const ExtRec& b) { return a.key < b.key; });
+        return v;
     };
-    by_key(e_new);
-    by_key(e_old);
-    const bool same = ne == ne_old && std::memcmp(e_new.data(), e_old.data(), ne * sizeof(ExtRec)) == 0;
-    const double mb = px * 4 / 1e6;  // MB per plane over the batch (MB / ms / 1e3 = TB/s)
+    const uint32_t grid = std::min<uint32_t>((R.cand_cap + 255) / 256, 2048);
+    bool same = true;
+    const std::vector<uint64_t>* orders[2] = {&c_rows, &c_raw};
+    const char* oname[2] = {"sorted", "append order"};
     std::printf("octave 0 of %d 1080p frames (%.0f M px)\n", n, px / 1e6);
+    for (int k = 0; k < 2; k++) {
+        CK(hipMemcpy(cand, orders[k]->data(), nc * 8, hipMemcpyHostToDevice));
+        CK(hipMemcpy(cnt, &nc, 4, hipMemcpyHostToDevice));
+        const float tr = timeit([&] {
+            CK(hipMemsetAsync(cnt + 1, 0, 4, 0));
+            launch_refine(R, 0);
+        });
+        const std::vector<ExtRec> e_new = fetch_sorted();
+        const float tr5 = timeit([&] {
+            CK(hipMemsetAsync(cnt + 1, 0, 4, 0));
+            hipLaunchKernelGGL(k_refine_r5a, dim3(grid), dim3(256), 0, 0, R);
+        });
+        const std::vector<ExtRec> e_r5 = fetch_sorted();
+        const float tro = timeit([&] {
+            CK(hipMemsetAsync(cnt + 1, 0, 4, 0));
+            hipLaunchKernelGGL(k_refine_old, dim3(grid), dim3(256), 0, 0, R);
+        });
+        const std::vector<ExtRec> e_old = fetch_sorted();
+        auto eq = [](const std::vector<ExtRec>& a, const std::vector<ExtRec>& b) {
+            return a.size() == b.size() && std::memcmp(a.data(), b.data(), a.size() * sizeof(ExtRec)) == 0;
+        };
+        const bool s1 = eq(e_new, e_old), s2 = eq(e_r5, e_old);
+        same = same && s1 && s2;
+        std::printf("k_refine (%s)    %8.1f us  %u candidates -> %zu extrema; identical to round 4: %s\n", oname[k],
+                    tr * 1e3, nc, e_new.size(), s1 ? "yes" : "NO");
+        std::printf("k_refine r5a (%s) %8.1f us  identical: %s\n", oname[k], tr5 * 1e3, s2 ? "yes" : "NO");
+        std::printf("k_refine r4 (%s)  %8.1f us\n", oname[k], tro * 1e3);
+    }
+    const double mb = px * 4 / 1e6;  // MB per plane over the batch (MB / ms / 1e3 = TB/s)
     std::printf("blur4 strip R=%d     %8.1f us  %5.2f TB/s (8 B/px)\n", rad[4], t4 * 1e3, 2 * mb / t4 / 1e3);
     std::printf("blur5 strip R=%d     %8.1f us  %5.2f TB/s (8 B/px)\n", rad[5], t5 * 1e3, 2 * mb / t5 / 1e3);
     std::printf("k_detect_rows        %8.1f us  %5.2f TB/s (24 B/px)  %u candidates\n", td * 1e3,
                 6 * mb / td / 1e3, nc_rows);
     std::printf("k_blur_detect        %8.1f us  %5.2f TB/s (24 B/px)  %u candidates\n", tbd * 1e3,
-                6 * mb / tbd / 1e3, nc);
+                6 * mb / tbd / 1e3, (unsigned)c_raw.size());
     std::printf("blur5 + detect_rows  %8.1f us\n", (t5 + td) * 1e3);
     std::printf("k_blur_detect vs strip blur 5 + k_detect_rows: G_5 %s, candidates %s\n",
                 same_g5 ? "bit-identical" : "DIFFER", same_cand ? "identical" : "DIFFER");
     if (!same_g5 || !same_cand) return 4;
-    std::printf("k_refine             %8.1f us  %u candidates -> %u extrema\n", tr * 1e3, nc, ne);
-    std::printf("k_refine (round 4)   %8.1f us  %u extrema; identical records: %s\n", tro * 1e3, ne_old,
-                same ? "yes" : "NO");
     return same ? 0 : 3;
-    return 0;
 }
