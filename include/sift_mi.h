@@ -173,8 +173,7 @@ typedef enum {
     SIFT_MI_PATH_SEED_PAIR = 2,    /* 0: seed and blur 1 as two launches (default 1) */
     SIFT_MI_PATH_TAIL = 3,         /* 0: per-blur launches for the small octaves (default 1) */
     SIFT_MI_PATH_FUSED_DETECT = 4, /* 0: blur 5 and the extremum scan apart; 2: fused wherever it
-                                      applies, at 32-row segments; 3: as 1 without the one-large-frame
-                                      rule (default 1: where it fills the chip) */
+                                      applies, at 32-row segments (default 1: where it fills the chip) */
     SIFT_MI_PATH_EARLY = 5,        /* 0: one-chunk calls detect every octave after the tail (default 1) */
     SIFT_MI_PATH_DESC_FIRST = 6,   /* 0: one-frame calls order, then describe (default 1) */
     SIFT_MI_PATH_GRAPH = 7,        /* 1: identical single-chunk calls replayed as a HIP graph (default 0) */
@@ -182,8 +181,8 @@ typedef enum {
                                       smaller values force the whole-pyramid re-run) */
     SIFT_MI_PATH_BOUND_SHRINK = 9, /* k >= 1: first-chunk stage bounds / k (default 1; > 1 forces the
                                       bound-overflow re-run) */
-    SIFT_MI_PATH_TAIL_SPLIT = 10   /* 0: the small octaves' kernel as one workgroup per frame (default 1:
-                                      a chain and a side workgroup per frame) */
+    SIFT_MI_PATH_TAIL_SPLIT = 10   /* the small octaves' kernel as a chain and a side workgroup per frame:
+                                      1 (default) for chunks of <= 8 frames, 2 always, 0 never */
 } sift_mi_path_option;
 int sift_mi_set_path_option(sift_mi_ctx* ctx, int option, int value);
 

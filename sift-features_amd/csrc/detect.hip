@@ -78,23 +78,41 @@ __device__ __forceinline__ void load_nbhd(const gfloat* g0, size_t P, int pitch,
 // ---------------------------------------------------------------------------
 struct RefineState {
     uint64_t key;
+    const gfloat* g0;    // G_0 of the candidate's frame and octave
+    int W, H, pitch;     // the octave's geometry
+    int vlo, vhi;        // rows of the octave's Gaussians that are exact (row bands)
     int sc, xi, yi, it;  // current scale, column, row; Newton steps taken
 };
+
+// A new candidate's state: its key decoded and its octave's geometry loaded
+// once (a Newton step then issues only the neighbourhood loads).
+__device__ __forceinline__ void refine_start(const RefineLaunch& L, uint64_t key, RefineState& st) {
+    const int b = (int)(key >> kKeyImgShift);
+    const int o = (int)((key >> kKeyOctShift) & 15);
+    st.key = key;
+    st.W = L.ow[o];
+    st.H = L.oh[o];
+    st.pitch = L.opitch[o];
+    st.g0 = as_global(L.gauss[o]) + (size_t)(b - L.img_base) * L.g_img_stride[o];
+    st.vlo = 0;
+    st.vhi = st.H;
+    if (L.band_flag) {
+        st.vlo = max(0, (int)((uint64_t)st.H * L.band_r / L.band_n) - 1 - L.band_margin);
+        st.vhi = min(st.H, (int)((uint64_t)st.H * (L.band_r + 1) / L.band_n) + 1 + L.band_margin);
+    }
+    st.sc = (int)((key >> kKeyScaleShift) & 3);
+    st.yi = (int)((key >> kKeyYShift) & kKeyCoordMask);
+    st.xi = (int)((key >> kKeyXShift) & kKeyCoordMask);
+    st.it = 0;
+}
 
 // One step for state st.  Returns 1 (accepted: e filled), -1 (rejected) or 0
 // (moved: another step follows).
 __device__ __forceinline__ int refine_step(const RefineLaunch& L, RefineState& st, ExtRec& e) {
     const uint64_t key = st.key;
-    const int b = (int)(key >> kKeyImgShift);
-    const int o = (int)((key >> kKeyOctShift) & 15);
-    const int W = L.ow[o], H = L.oh[o], pitch = L.opitch[o];
-    const gfloat* g0 = as_global(L.gauss[o]) + (size_t)(b - L.img_base) * L.g_img_stride[o];
+    const int W = st.W, H = st.H, pitch = st.pitch, vlo = st.vlo, vhi = st.vhi;
+    const gfloat* g0 = st.g0;
     const size_t P = (size_t)pitch * H;
-    int vlo = 0, vhi = H;  // rows of this octave's Gaussians that are exact
-    if (L.band_flag) {
-        vlo = max(0, (int)((uint64_t)H * L.band_r / L.band_n) - 1 - L.band_margin);
-        vhi = min(H, (int)((uint64_t)H * (L.band_r + 1) / L.band_n) + 1 + L.band_margin);
-    }
     const int x = st.xi, y = st.yi, scale = st.sc;
     // row bands with a restricted pyramid (host.cpp run_pyramid): the rows
     // read here must be computed ones, else the host recomputes the band on
@@ -167,8 +185,8 @@ __device__ __forceinline__ int refine_step(const RefineLaunch& L, RefineState& s
     if (L.band_flag && ((vlo > 0 && y - L.band_patch < vlo) || (vhi < H && y + L.band_patch >= vhi)))
         atomicOr(L.band_flag, 1u);
     e.key = key;
-    e.img = b;
-    e.octave = o;
+    e.img = (int)(key >> kKeyImgShift);
+    e.octave = (int)((key >> kKeyOctShift) & 15);
     e.scale = scale;
     e.x = x;
     e.y = y;
@@ -198,12 +216,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_REFINE
             const uint32_t rank = (uint32_t)__popcll(need & ((1ull << lane) - 1ull));
             const uint32_t i = cur + rank;
             if (!live && i < end) {
-                const uint64_t key = L.cand[i];
-                st.key = key;
-                st.sc = (int)((key >> kKeyScaleShift) & 3);
-                st.yi = (int)((key >> kKeyYShift) & kKeyCoordMask);
-                st.xi = (int)((key >> kKeyXShift) & kKeyCoordMask);
-                st.it = 0;
+                refine_start(L, L.cand[i], st);
                 live = true;
             }
             cur = min(end, cur + (uint32_t)__popcll(need));

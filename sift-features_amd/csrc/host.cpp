@@ -1053,7 +1053,12 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
             // epoch is a kernel argument, a replay would see the last one's
             // flags; not for row bands' restricted passes either -- whole
             // octaves either way, so simply both paths exact)
-            if (po.tail_split && ext_events && tail_slot >= 0) {
+            // the split pays on the latency path (one frame: 3 + 2 blurs per
+            // octave in parallel); on a batch chunk the one-workgroup kernel
+            // is faster (256 x 640x480: 10.0-10.2 vs 10.65 ms per call; the
+            // side workgroups hold a CU's LDS each while they wait)
+            const bool split = po.tail_split == 2 || (po.tail_split == 1 && nf <= kTailSplitMaxFrames);
+            if (split && ext_events && tail_slot >= 0) {
                 const size_t need = (size_t)c->plan.chunk * kTailMaxOct;
                 if (c->tail_flags[lane].cap < need) {
                     CHK(c->tail_flags[lane].ensure(need));
@@ -2013,13 +2018,13 @@ int sift_mi_set_path_option(sift_mi_ctx* c, int option, int value) {
         case SIFT_MI_PATH_PAIR_BLUR: if (!b) break; o.pair = value; return 0;
         case SIFT_MI_PATH_SEED_PAIR: if (!b) break; o.seed_pair = value; return 0;
         case SIFT_MI_PATH_TAIL: if (!b) break; o.tail = value; return 0;
-        case SIFT_MI_PATH_FUSED_DETECT: if (value < 0 || value > 3) break; o.fused_detect = value; return 0;
+        case SIFT_MI_PATH_FUSED_DETECT: if (value < 0 || value > 2) break; o.fused_detect = value; return 0;
         case SIFT_MI_PATH_EARLY: if (!b) break; o.early = value; return 0;
         case SIFT_MI_PATH_DESC_FIRST: if (!b) break; o.desc_first = value; return 0;
         case SIFT_MI_PATH_GRAPH: if (!b) break; o.graph = value; return 0;
         case SIFT_MI_PATH_BAND_DRIFT: if (value < -kBandPatch || value > kBandDrift) break; o.band_drift = value; return 0;
         case SIFT_MI_PATH_BOUND_SHRINK: if (value < 1) break; o.bound_shrink = value; return 0;
-        case SIFT_MI_PATH_TAIL_SPLIT: if (!b) break; o.tail_split = value; return 0;
+        case SIFT_MI_PATH_TAIL_SPLIT: if (value < 0 || value > 2) break; o.tail_split = value; return 0;
         default: return fail(SIFT_MI_EINVAL, "unknown path option");
     }
     return fail(SIFT_MI_EINVAL, "path option value out of range");

@@ -232,9 +232,6 @@ constexpr int BD_RP = 100;   // ring row pitch (floats): 64 + 2R columns, R <= 1
 #ifndef BD_UNROLL
 #define BD_UNROLL 1  // row groups per steady-state loop iteration
 #endif
-#ifndef BD_PACK
-#define BD_PACK 0  // row pairs in packed f32 (v_pk_fma_f32) row / column passes
-#endif
 
 template <int P>
 __device__ __forceinline__ int bd_index(int p, int n) {
@@ -338,112 +335,6 @@ __global__ __launch_bounds__(256) void k_blur_detect(const BlurDetectLaunch L) {
             ld4(qq, B.a, B.c);
             ld03(r >= ya - 1 ? min(r, yb) : ya - 1 + par, B.d);
         };
-#if BD_PACK
-        // Row pairs (q even, q + 1): both G_4 rows go to the ring, one
-        // packed row pass (v_pk_fma_f32: each half an individually rounded
-        // f32 FMA, the same chain as the scalar one) filters both -- each
-        // ds_read2_b32 fetches tap t of row q and of row q + 1 as one
-        // register pair -- and one packed column pass yields G_5 of rows
-        // r = q - R and r + 1.  The window holds the row-filter outputs as
-        // row pairs; a column-pass operand {w[j], w[j + 1]} with odd j
-        // straddles two of them (one v_pk_mov).
-        float w[2 * R + 2];  // w[j]: row q - 2R + j
-        auto M = [&](int j) __attribute__((always_inline)) -> f2v { return f2v{w[j], w[j + 1]}; };
-        // the ring holds row pairs interleaved: pair slot (q & 15) / 2, column
-        // c at floats 2c (row q) and 2c + 1 (row q + 1), so one ds_read_b64
-        // is an aligned register pair {row q, row q + 1}
-        auto pair_slot = [&](int q) __attribute__((always_inline)) -> f2v* {
-            return reinterpret_cast<f2v*>(rg + ((q & (BD_RING - 1)) >> 1) * (2 * BD_RP));
-        };
-        auto rowpass2 = [&](int q) __attribute__((always_inline)) -> f2v {
-            const f2v* p = pair_slot(q) + lane;
-            f2v acc = p[0] * L.taps.k[R];
-#pragma unroll
-            for (int t = 1; t <= 2 * R; t++) {
-                const float kt = L.taps.k[t > R ? t - R : R - t];
-                const f2v v = p[t];
-                if constexpr (P == kProfileOpenCV)
-                    acc = __builtin_elementwise_fma(v, f2v{kt, kt}, acc);
-                else
-                    acc = acc + v * kt;
-            }
-            return acc;
-        };
-        // row q's G_5 value g5 (row r = q - R): store, DoG, the test of row
-        // r - 1 (the per-row part of step() below)
-        auto finish = [&](int q, const RowBuf& B, float g5, auto full_tag) __attribute__((always_inline)) {
-            constexpr bool FULL = decltype(full_tag)::value;
-            const bool on = FULL || q <= q1;  // uniform
-            const int r = q - R;
-            const uint32_t bad = ((FULL || (on && r >= ya)) && r < yb && xst) ? 0u : 0xfffffff0u;
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, g5), rg5,
-                                                  ((uint32_t)(r * pitch * 4) + (uint32_t)vx) | bad, 0, 2 /* nt */);
-            if (!FULL && !(on && r >= ya - 1)) return;  // uniform
-            const float g4 = pair_slot(r)[lane + R][r & 1];
-            float cur[kDogPerOctave];
-            cur[0] = B.d[1] - B.d[0];
-            cur[1] = B.d[2] - B.d[1];
-            cur[2] = B.d[3] - B.d[2];
-            cur[3] = g4 - B.d[3];
-            cur[4] = g5 - g4;
-            const int y = r - 1;
-            if (FULL || y >= ya) {  // uniform
-                const bool yin = xout && y >= kImageBorder && y < H - kImageBorder;
-                uint32_t ok3 = extremum3(prv, mid, cur, yin);
-                if (__ballot(ok3 != 0)) {  // wave-uniform: rare
-                    while (ok3) {
-                        const int bit = __builtin_ctz(ok3);
-                        ok3 &= ok3 - 1;
-                        const uint64_t key = make_key((uint32_t)(L.img_base + b), (uint32_t)L.octave,
-                                                      (uint32_t)(bit + 1), (uint32_t)y, (uint32_t)x);
-                        const uint32_t li = atomicAdd(&lcount, 1u);
-                        if (li < DR_LCAP) {
-                            lcand[li] = key;
-                        } else {
-                            const uint32_t slot = atomicAdd(L.counter, 1u);
-                            if (slot < L.cap) L.cand[slot] = key;
-                        }
-                    }
-                }
-            }
-#pragma unroll
-            for (int p = 0; p < kDogPerOctave; p++) {
-                prv[p] = mid[p];
-                mid[p] = cur[p];
-            }
-        };
-        auto step2 = [&](int q, const RowBuf& B0, const RowBuf& B1, auto full_tag) __attribute__((always_inline)) {
-            constexpr bool FULL = decltype(full_tag)::value;
-            f2v g5 = {0.0f, 0.0f};
-            if (FULL || q <= q1) {  // uniform (past q1 no later row needs the window)
-                f2v* wp = pair_slot(q);
-                wp[lane] = f2v{B0.a, B1.a};
-                if (lane < 2 * R) wp[64 + lane] = f2v{B0.c, B1.c};
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
-                __builtin_amdgcn_wave_barrier();
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
-#pragma unroll
-                for (int j = 0; j < 2 * R; j++) w[j] = w[j + 2];
-                const f2v h = rowpass2(q);
-                w[2 * R] = h.x;
-                w[2 * R + 1] = h.y;
-                if constexpr (P == kProfileOpenCV) {
-                    g5 = M(R) * L.taps.k[0];
-#pragma unroll
-                    for (int t = 1; t <= R; t++) {
-                        const float kt = L.taps.k[t];
-                        g5 = __builtin_elementwise_fma(M(R + t) + M(R - t), f2v{kt, kt}, g5);
-                    }
-                } else {
-                    g5 = M(0) * L.taps.k[R];
-#pragma unroll
-                    for (int t = 1; t <= 2 * R; t++) g5 = g5 + M(t) * L.taps.k[t > R ? t - R : R - t];
-                }
-            }
-            finish(q, B0, g5.x, full_tag);
-            finish(q + 1, B1, g5.y, full_tag);
-        };
-#else
         auto shift = [&]() {
 #pragma unroll
             for (int j = 0; j < 2 * R; j++) win[j] = win[j + 1];
@@ -523,7 +414,6 @@ __global__ __launch_bounds__(256) void k_blur_detect(const BlurDetectLaunch L) {
             }
             shift();
         };
-#endif
         // rows q, q + 1 from (A0, A1) while q + 2, q + 3 load into (B0, B1),
         // then the other way round (even / odd rows: par 0 / 1)
         RowBuf A0, A1, B0, B1;
@@ -532,22 +422,14 @@ __global__ __launch_bounds__(256) void k_blur_detect(const BlurDetectLaunch L) {
             load(q + 2, B0, 0);
             load(q + 3, B1, 1);
             __builtin_amdgcn_sched_barrier(0);
-#if BD_PACK
-            step2(q, A0, A1, full_tag);
-#else
             step(q, A0, full_tag);
             step(q + 1, A1, full_tag);
-#endif
             __builtin_amdgcn_sched_barrier(0);
             load(q + 4, A0, 0);
             load(q + 5, A1, 1);
             __builtin_amdgcn_sched_barrier(0);
-#if BD_PACK
-            step2(q + 2, B0, B1, full_tag);
-#else
             step(q + 2, B0, full_tag);
             step(q + 3, B1, full_tag);
-#endif
             __builtin_amdgcn_sched_barrier(0);
         };
         load(q0, A0, 0);
@@ -574,8 +456,7 @@ __global__ __launch_bounds__(256) void k_blur_detect(const BlurDetectLaunch L) {
 }
 
 // PathOpts::fused_detect: 0 keeps blur 5 and detection apart, 2 fuses every
-// octave it can at 32-row segments (test paths), 3 is 1 without the
-// one-large-frame rule (A/B)
+// octave it can at 32-row segments (test paths)
 // The segment length the fused pass would use for L (0: it does not apply).
 static int blur_detect_segment(int R, const BlurDetectLaunch& L, const PathOpts& o) {
     if (o.fused_detect == 0) return 0;
@@ -594,11 +475,6 @@ static int blur_detect_segment(int R, const BlurDetectLaunch& L, const PathOpts&
     const long nsx = (L.W + DR_COLS - 1) / DR_COLS;
     for (int s : {256, 128, 64})
         if (nsx * ((L.H + s - 1) / s) * L.n_img >= 16384) return s;
-    // one large frame (octave 0 of a 1080p frame: ~4 k waves at 32-row
-    // segments, 4 per SIMD): the pass replaces blur 5 and that octave's share
-    // of the scan launch on the one-frame critical path, although a segment
-    // re-filters its 2R + 2 halo rows (PathOpts::fused_detect = 3: not)
-    if (o.fused_detect == 1 && L.n_img == 1 && nsx * ((L.H + 31) / 32) >= 4096) return 32;
     return 0;
 }
 

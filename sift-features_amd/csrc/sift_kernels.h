@@ -41,18 +41,21 @@ enum : int { kProfileOpenCV = 0, kProfileImageproc = 1 };
 // exists so the tests can hold each kernel family against the oracle.  They
 // live in the context (no process-wide state, nothing read from the
 // environment).
+constexpr uint32_t kTailSplitMaxFrames = 8;
+
 struct PathOpts {
     int tile_blur = 0;     // 1: one-tile-per-workgroup blurs everywhere (no strip / pair kernels)
     int pair = 1;          // 0: no pair kernels (k_blur2_strip, k_seed_pair)
     int seed_pair = 1;     // 0: k_seed_strip, then blur 1 like the other octaves
     int tail = 1;          // 0: per-blur launches for the small octaves (no k_octave_tail)
-    int fused_detect = 1;  // 0: blur 5 and the extremum scan apart; 2: fused at 32-row segments wherever it applies; 3: no one-large-frame rule
+    int fused_detect = 1;  // 0: blur 5 and the extremum scan apart; 2: fused at 32-row segments wherever it applies
     int early = 1;         // one-chunk calls: detection of the octaves below the tail beside the tail kernel
     int desc_first = 1;    // one-frame calls: descriptors beside the ordering stage
     int graph = 0;         // 1: single-chunk calls captured once and replayed as a HIP graph
     int band_drift = 24;   // row bands: refinement drift accepted without a re-run (< 24 forces re-runs)
     int bound_shrink = 1;  // > 1: first-chunk stage bounds divided by it (forces the overflow re-run)
-    int tail_split = 1;    // k_octave_tail as chain + side workgroups per frame (0: one workgroup per frame)
+    int tail_split = 1;    // k_octave_tail as chain + side workgroups per frame: 1 for chunks of
+                           // <= kTailSplitMaxFrames frames, 2 always, 0 never (one workgroup per frame)
 };
 
 // Image planes are row-pitched: element (y, x) at plane[y * pitch + x].

@@ -115,20 +115,3 @@ def test_read_batch_scale_space_state(pkg):
         c.read_batch_scale_space(0, 0)
     c.close()
 
-
-def test_fused_one_large_frame(pkg, oracle):
-    """One 1080p frame: octave 0 (3840x2160) takes the fused pass at 32-row
-    segments (the one-large-frame rule of fused_detect = 1); its planes equal
-    the oracle's, and the result equals the run without the rule
-    (fused_detect = 3) bit for bit."""
-    import synth
-    img = synth.frame(1920, 1080, 11)
-    c = pkg.Context(0, pkg.OpenCVProcessing)
-    res = c.sift(img)
-    opy = oracle.Pyramid(img, 0)
-    go = opy.scale_space(0)
-    assert np.array_equal(c.read_batch_scale_space(0, 0), go)
-    c.set_path_option("fused_detect", 3)
-    ref = c.sift(img)
-    c.close()
-    assert res == ref
