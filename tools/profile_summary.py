@@ -154,12 +154,19 @@ def launch_blurs(k):
 
 
 def pos_info(seq):
-    """(octave, first blur, actual HBM bytes) per launch of a chunk, from the
-    kernel sequence: the seed reads the u8 frame and writes G_0; a blur reads
-    G_{s-1} and writes G_s (8 B/px), a pair reads G_{s-1} and writes G_s,
-    G_{s+1} (12 B/px); blur s = 3 also writes the next octave's G_0 (1 B/px);
-    the tail reads G_0 of its first octave and writes everything after it."""
-    out, done = [], 0
+    """(octave, blurs, actual HBM bytes) per launch of a chunk, from the
+    kernel sequence in enqueue order: the seed reads the u8 frame and writes
+    G_0; a blur reads G_{s-1} and writes G_s (8 B/px), a pair reads G_{s-1}
+    and writes G_s, G_{s+1} (12 B/px); blur s = 3 also writes the next
+    octave's G_0 (1 B/px); k_blur_detect (blur 5 + the scan) reads G_0..G_4
+    and writes G_5 (24 B/px); the tail reads G_0 of its first octave and
+    writes everything after it.  The first n octaves' blur 5 is a
+    k_blur_detect launch, n = the number of those in the chunk; octave 0's is
+    enqueued late (deferred until octave 1's G_3), so every launch is placed
+    in the lowest octave with a blur it can perform pending."""
+    n_fused = sum(1 for k in seq if k.startswith("k_blur_detect"))
+    nxt = [1] * n_oct  # next blur (1..5; 6 = octave done) per octave
+    out = []
     for k in seq:
         nb = launch_blurs(k)
         if nb == 0:
@@ -167,22 +174,31 @@ def pos_info(seq):
             continue
         if nb == -1:  # k_seed_pair: u8 read, G_0 and G_1 written
             out.append((0, "seed,1", chunk * (W * H + 8 * dims[0][0] * dims[0][1])))
-            done = 1
+            nxt[0] = 2
             continue
-        o, s = done // 5, done % 5 + 1
-        if nb is None:
+        if nb is None:  # the tail: every octave not done
+            o = next((i for i in range(n_oct) if nxt[i] <= 5), n_oct - 1)
             by = 4 * dims[o][0] * dims[o][1]
             for oo in range(o, n_oct):
                 by += 4 * 5 * dims[oo][0] * dims[oo][1] + (4 * dims[oo + 1][0] * dims[oo + 1][1] if oo + 1 < n_oct else 0)
             out.append((o, f"{o}..{n_oct - 1}", chunk * by))
-            done = 5 * n_oct
+            for oo in range(o, n_oct):
+                nxt[oo] = 6
             continue
+        if k.startswith("k_blur_detect"):
+            o = next(i for i in range(n_oct) if nxt[i] == 5)
+            px = dims[o][0] * dims[o][1]
+            out.append((o, "5+scan", chunk * 24 * px))
+            nxt[o] = 6
+            continue
+        # a strip blur / pair: the lowest octave with such a blur pending (a
+        # fused octave's blur 5 is left to its k_blur_detect)
+        o = next(i for i in range(n_oct) if nxt[i] <= (4 if i < n_fused else 5))
+        s = nxt[o]
         px = dims[o][0] * dims[o][1]
         by = (4 + 4 * nb) * px + (px if (s <= 3 < s + nb) and o + 1 < n_oct else 0)
-        if k.startswith("k_blur_detect"):  # blur 5 + the scan: G_0..G_4 read, G_5 written
-            by = 24 * px
         out.append((o, f"{s}" if nb == 1 else f"{s},{s + 1}", chunk * by))
-        done += nb
+        nxt[o] = s + nb
     return out
 
 
