@@ -450,6 +450,11 @@ struct Slot {
     // keypoint index order (desc_kp) while lane 1's stream orders the
     // keypoints; k_gather_out then writes the outputs in emission order
     bool desc_first = false;
+    // early, two lanes: the aux stream's join event (oct_ev[lane][kTailMaxOct])
+    // is recorded but the lane stream has not waited for it yet; the keypoint
+    // stage either waits first or, with desc_first, runs the descriptors on
+    // the aux stream itself (no cross-stream hop before them)
+    bool join_pending = false;
     uint32_t bcb = 0;
     DevBuf<uint64_t> cand_b;
     DevBuf<ExtRec> ext_b;
@@ -1108,7 +1113,10 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
         }
         if (ov && o_tail > 0) {  // join: the aux stream's work before what follows on sm
             HIPCHK(hipEventRecord(c->oct_ev[lane][kTailMaxOct], aux));
-            HIPCHK(hipStreamWaitEvent(sm, c->oct_ev[lane][kTailMaxOct], 0));
+            if (early && c->lanes == 2)
+                c->slot[detect_slot].join_pending = true;  // enqueue_keypoints joins
+            else
+                HIPCHK(hipStreamWaitEvent(sm, c->oct_ev[lane][kTailMaxOct], 0));
         }
         return 0;
     };
@@ -1237,6 +1245,7 @@ int prepare_chunk(sift_mi_ctx* c, int si, uint32_t m, uint32_t frame_base, const
     S.fused_mask = 0;
     S.graph_run = false;
     S.early = false;
+    S.join_pending = false;
     uint32_t* cnt = S.counters.p;
     // stage counters, frame starts (~0), descriptor work queues
     launch_chunk_init(cnt, (int)m, kDescWorkWords + kTailWords, st);  // + the tail region's words
@@ -1342,6 +1351,16 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
     uint32_t* work = cnt + 4 + 2 * m + kTailWords;  // descriptor work queues (after the tail region's words)
     (void)starts;
     (void)work;
+    // one frame, no limit, early detection: the descriptors are computed in
+    // keypoint index order beside the ordering stage, which runs on lane 1's
+    // idle stream; k_gather_out then writes the outputs in emission order
+    // (PathOpts::desc_first = 0: order, then describe in emission order)
+    S.desc_first = S.early && m == 1 && limit < 0 && si == 0 && c->lanes == 2 &&
+                   S.desc_kp.cap >= (size_t)B.bk * kDescSize && c->opts.desc_first;
+    const bool join_pending = S.join_pending;
+    S.join_pending = false;
+    hipEvent_t aux_done = c->oct_ev[si][kTailMaxOct];  // the aux stream's early stages (join_pending)
+    if (join_pending && !S.desc_first) HIPCHK(hipStreamWaitEvent(st, aux_done, 0));
     if (!S.detected) CHK(launch_detection(c, si, 0, m, 0, p.n_oct, st));
     // (early: refinement and orientation were enqueued inside the pyramid)
     if (!S.early) CHK(launch_refine_stage(c, si, S.cand.p, cnt + 0, B.bc, S.ext.p, cnt + 1, B.be, st));
@@ -1349,16 +1368,21 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
     if (!S.early) CHK(launch_orient_stage(c, si, S.ext.p, cnt + 1, B.be, B.bk, st));
     HIPCHK(hipGetLastError());
     if (S.staged) HIPCHK(hipEventRecord(S.ev[3], st));
-    // one frame, no limit, early detection: the descriptors are computed in
-    // keypoint index order beside the ordering stage, which runs on lane 1's
-    // idle stream; k_gather_out then writes the outputs in emission order
-    // (PathOpts::desc_first = 0: order, then describe in emission order)
-    S.desc_first = S.early && m == 1 && limit < 0 && si == 0 && c->lanes == 2 &&
-                   S.desc_kp.cap >= (size_t)B.bk * kDescSize && c->opts.desc_first;
     hipStream_t os = S.desc_first ? c->own2 : st;  // the ordering stage's stream
+    hipStream_t ds = st;                            // the descriptor stage's stream
     if (S.desc_first) {
+        // the ordering stage needs every keypoint: the lane stream's (tail
+        // octaves) and, when the join is pending, the aux stream's; the
+        // descriptors then run on the aux stream right after its orientation
+        // (the lane stream's is long done by then), saving the cross-stream
+        // hop in front of them (~15 us per one-frame call)
         HIPCHK(hipEventRecord(S.oriented, st));
         HIPCHK(hipStreamWaitEvent(os, S.oriented, 0));
+        if (join_pending) {
+            HIPCHK(hipStreamWaitEvent(os, aux_done, 0));
+            ds = c->aux[si];
+            HIPCHK(hipStreamWaitEvent(ds, S.oriented, 0));
+        }
     }
     // emission order: radix sort of the keys (padding sorts last)
     const uint32_t* order = S.vals_b.p;  // emission order -> kp index
@@ -1398,7 +1422,7 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
     if (S.desc_first) HIPCHK(hipEventRecord(S.ordered, os));
     if (S.staged) HIPCHK(hipEventRecord(S.ev[4], st));
     // descriptors into this slot's outputs, once its previous copy-out is done
-    if (S.pending_copy) HIPCHK(hipStreamWaitEvent(st, S.copied, 0));
+    if (S.pending_copy) HIPCHK(hipStreamWaitEvent(ds, S.copied, 0));
     DescLaunch DL{};
     DL.kp = S.kp.p;
     DL.idx = S.desc_first ? nullptr : order;
@@ -1417,18 +1441,20 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
     DL.out_desc = S.desc_first ? S.desc_kp.p : S.out_desc.p;
     DL.exact = c->exact_descriptors;
     DL.samples = c->count_samples ? c->samples.p + 8 : nullptr;
-    launch_describe(DL, st);
+    launch_describe(DL, ds);
     if (S.desc_first) {
-        HIPCHK(hipStreamWaitEvent(st, S.ordered, 0));
+        HIPCHK(hipStreamWaitEvent(ds, S.ordered, 0));
         launch_gather_out(S.kp.p, order, cnt + 3, B.bk, S.desc_kp.p, S.out_desc.p, S.out_kp.p, S.out_key.p,
-                          DL.key_base, st);
+                          DL.key_base, ds);
     }
     HIPCHK(hipGetLastError());
     if (S.staged) HIPCHK(hipEventRecord(S.ev[5], st));
     // the frame plan and the tail region's counters (Slot::early) in one copy
     HIPCHK(hipMemcpyAsync(S.h_counts.p, cnt, (4 + 2 * m + kTailWords) * sizeof(uint32_t),
-                          hipMemcpyDeviceToHost, st));
-    HIPCHK(hipEventRecord(S.ev[6], st));
+                          hipMemcpyDeviceToHost, ds));
+    HIPCHK(hipEventRecord(S.ev[6], ds));
+    // the lane stream's next work follows this chunk (and a capture rejoins)
+    if (ds != st) HIPCHK(hipStreamWaitEvent(st, S.ev[6], 0));
     return 0;
 }
 
