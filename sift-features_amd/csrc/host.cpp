@@ -1113,7 +1113,8 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
         }
         if (ov && o_tail > 0) {  // join: the aux stream's work before what follows on sm
             HIPCHK(hipEventRecord(c->oct_ev[lane][kTailMaxOct], aux));
-            if (early && c->lanes == 2)
+            // (not under stream capture: a capture keeps the plain join)
+            if (early && c->lanes == 2 && ext_events)
                 c->slot[detect_slot].join_pending = true;  // enqueue_keypoints joins
             else
                 HIPCHK(hipStreamWaitEvent(sm, c->oct_ev[lane][kTailMaxOct], 0));
