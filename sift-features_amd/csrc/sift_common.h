@@ -169,6 +169,14 @@ __device__ __forceinline__ TileId xcd_tile() {
     return {(int)(rem - (rem / tx) * tx), (int)(rem / tx), (int)z};
 }
 
+// The same bijection for a 1-D range of n items dealt round robin to the 8
+// XCDs by index (item `orig` runs on XCD orig % 8): item orig becomes the
+// returned index, so each XCD takes a contiguous range of [0, n).
+__device__ __forceinline__ uint32_t xcd_remap(uint32_t orig, uint32_t n) {
+    const uint32_t q = n / 8, r = n % 8, xcd = orig % 8;
+    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
+}
+
 __host__ __device__ __forceinline__ int clamp_idx(int p, int len) { return p < 0 ? 0 : (p >= len ? len - 1 : p); }
 
 // image 0.25.2 imageops::resize clamps every f32 output to [DEFAULT_MIN_VALUE,
