@@ -181,10 +181,8 @@ typedef enum {
                                       smaller values force the whole-pyramid re-run) */
     SIFT_MI_PATH_BOUND_SHRINK = 9, /* k >= 1: first-chunk stage bounds / k (default 1; > 1 forces the
                                       bound-overflow re-run) */
-    SIFT_MI_PATH_TAIL_SPLIT = 10,  /* the small octaves' kernel as a chain and a side workgroup per frame:
+    SIFT_MI_PATH_TAIL_SPLIT = 10   /* the small octaves' kernel as a chain and a side workgroup per frame:
                                       1 (default) for chunks of <= 8 frames, 2 always, 0 never */
-    SIFT_MI_PATH_XCD_LOCAL = 11    /* 0: orientation / descriptor work interleaved over the XCDs (default 1:
-                                      contiguous keypoint ranges per XCD) */
 } sift_mi_path_option;
 int sift_mi_set_path_option(sift_mi_ctx* ctx, int option, int value);
 

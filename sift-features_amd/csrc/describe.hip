@@ -671,20 +671,11 @@ __global__ __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(kMode == 0 ?
     auto issue = [&]() {
         if (lane == 0) pend = atomicAdd(L.work + q * kDescQueueStride, 1u);
     };
-    // xcd_local: queue q is the contiguous range [n q / 8, n (q + 1) / 8) --
-    // consecutive keypoints (neighbours in emission order, overlapping
-    // patches) on one XCD's L2; otherwise keypoints q, q + 8, ...
     auto take = [&]() -> uint32_t {  // resolves the claim in flight: keypoint index, or n when all queues are empty
         for (;;) {
             const uint32_t j = __builtin_amdgcn_readfirstlane(__shfl(pend, 0));
-            uint32_t i, end = n;
-            if (L.xcd_local) {
-                i = (uint32_t)(((uint64_t)n * q) / kDescQueues) + j;
-                end = (uint32_t)(((uint64_t)n * (q + 1)) / kDescQueues);
-            } else {
-                i = j * kDescQueues + q;
-            }
-            if (i < end) return __builtin_amdgcn_readfirstlane(i);
+            const uint32_t i = j * kDescQueues + q;
+            if (i < n) return __builtin_amdgcn_readfirstlane(i);
             if (++drained == kDescQueues) return n;
             q = (q + 1) & (kDescQueues - 1);
             issue();

@@ -274,13 +274,13 @@ __global__ __launch_bounds__(256, SIFT_ORIENT_MIN_WAVES) void k_orient(const Ori
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
     const uint32_t n_ext = min(*L.n_ext, L.ext_cap);
     // one group of 4 extrema per workgroup; the grid covers the bound, the
-    // device count ends it early (block-uniform).  xcd_local: the live groups
-    // remapped so each XCD takes a contiguous range of them (neighbouring
-    // extrema share patch rows in that XCD's L2)
+    // device count ends it early (block-uniform).  (Round 5: the groups
+    // remapped to contiguous ranges per XCD measured slower, together with
+    // the same for the descriptor queues: 32.5-32.9 vs 32.2-32.4 ms per 128
+    // 1080p frames, profiles/r05_xcd_local_ab.log.)
     {
-        const uint32_t ng = (n_ext + 3) / 4;
-        if (blockIdx.x >= ng) return;
-        const uint32_t rg = (L.xcd_local ? xcd_remap(blockIdx.x, ng) : blockIdx.x) * 4;
+        const uint32_t rg = blockIdx.x * 4;
+        if (rg >= n_ext) return;
         const uint32_t r = rg + wave;
         const bool active = r < n_ext;
         ExtRec e;

@@ -1336,7 +1336,6 @@ int launch_orient_stage(sift_mi_ctx* c, int si, const ExtRec* ext, const uint32_
     O.img_base = 0;
     O.cap = kp_cap;
     O.samples = c->count_samples ? c->samples.p : nullptr;
-    O.xcd_local = c->opts.xcd_local;
     launch_orient(O, st);
     HIPCHK(hipGetLastError());
     return 0;
@@ -1443,7 +1442,6 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
     DL.out_desc = S.desc_first ? S.desc_kp.p : S.out_desc.p;
     DL.exact = c->exact_descriptors;
     DL.samples = c->count_samples ? c->samples.p + 8 : nullptr;
-    DL.xcd_local = c->opts.xcd_local;
     launch_describe(DL, ds);
     if (S.desc_first) {
         HIPCHK(hipStreamWaitEvent(ds, S.ordered, 0));
@@ -2054,7 +2052,6 @@ int sift_mi_set_path_option(sift_mi_ctx* c, int option, int value) {
         case SIFT_MI_PATH_BAND_DRIFT: if (value < -kBandPatch || value > kBandDrift) break; o.band_drift = value; return 0;
         case SIFT_MI_PATH_BOUND_SHRINK: if (value < 1) break; o.bound_shrink = value; return 0;
         case SIFT_MI_PATH_TAIL_SPLIT: if (value < 0 || value > 2) break; o.tail_split = value; return 0;
-        case SIFT_MI_PATH_XCD_LOCAL: if (!b) break; o.xcd_local = value; return 0;
         default: return fail(SIFT_MI_EINVAL, "unknown path option");
     }
     return fail(SIFT_MI_EINVAL, "path option value out of range");

@@ -241,11 +241,7 @@ __device__ __forceinline__ int bd_index(int p, int n) {
 
 // 1-D block id remapped so each XCD walks a contiguous range (neighbouring
 // strips of one row segment share their G_4 halo columns in that XCD's L2)
-__device__ __forceinline__ uint32_t xcd_block_1d() {
-    const uint32_t nwg = gridDim.x, orig = blockIdx.x;
-    const uint32_t q = nwg / 8, r = nwg % 8, xcd = orig % 8;
-    return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + orig / 8;
-}
+__device__ __forceinline__ uint32_t xcd_block_1d() { return xcd_remap(blockIdx.x, gridDim.x); }
 
 template <int R, int P>
 __global__ __launch_bounds__(256) void k_blur_detect(const BlurDetectLaunch L) {

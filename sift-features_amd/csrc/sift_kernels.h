@@ -54,7 +54,6 @@ struct PathOpts {
     int graph = 0;         // 1: single-chunk calls captured once and replayed as a HIP graph
     int band_drift = 24;   // row bands: refinement drift accepted without a re-run (< 24 forces re-runs)
     int bound_shrink = 1;  // > 1: first-chunk stage bounds divided by it (forces the overflow re-run)
-    int xcd_local = 1;     // orientation / descriptor work in contiguous keypoint ranges per XCD (0: interleaved)
     int tail_split = 1;    // k_octave_tail as chain + side workgroups per frame: 1 for chunks of
                            // <= kTailSplitMaxFrames frames, 2 always, 0 never (one workgroup per frame)
 };
@@ -245,7 +244,6 @@ struct OrientLaunch {
     int img_base;
     uint32_t cap;
     unsigned long long* samples;  // 8 counters (measurement only; null: off)
-    int xcd_local;  // workgroup -> extrema group remapped so each XCD takes a contiguous range
 };
 void launch_orient(const OrientLaunch& L, hipStream_t st);
 
@@ -314,7 +312,6 @@ struct DescLaunch {
     uint8_t* out_desc;
     int exact;         // 1: bit-exact bin-owner accumulation (describe_wave_exact)
     unsigned long long* samples;  // 8 counters (measurement only; null: off)
-    int xcd_local;     // queue q holds keypoints [n q / 8, n (q + 1) / 8) (0: i % 8 == q)
 };
 void launch_describe(const DescLaunch& L, hipStream_t st);
 

@@ -360,7 +360,7 @@ def test_single_chunk_graph_replay(pkg, ctx, oracle, fetch):
     c.close()
 
 
-@pytest.mark.parametrize("knob", ["early", "desc_first", "tail_split", "xcd_local"])
+@pytest.mark.parametrize("knob", ["early", "desc_first", "tail_split"])
 @pytest.mark.parametrize("profile", [0, 1])
 def test_single_chunk_paths_equal(pkg, knob, profile):
     """One-chunk calls take latency paths of their own -- the octaves below
