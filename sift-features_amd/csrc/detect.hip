@@ -84,16 +84,26 @@ struct RefineState {
     int sc, xi, yi, it;  // current scale, column, row; Newton steps taken
 };
 
-// A new candidate's state: its key decoded and its octave's geometry loaded
-// once (a Newton step then issues only the neighbourhood loads).
-__device__ __forceinline__ void refine_start(const RefineLaunch& L, uint64_t key, RefineState& st) {
+// The octaves' geometry, staged in LDS once per workgroup (a refill then
+// costs the key load only, not a second round trip for its octave's entries)
+struct RefineOct {
+    const float* g;
+    size_t stride;
+    int W, H, pitch;
+};
+
+// A new candidate's state: its key decoded and its octave's geometry looked
+// up once (a Newton step then issues only the neighbourhood loads).
+__device__ __forceinline__ void refine_start(const RefineLaunch& L, const RefineOct* geo, uint64_t key,
+                                             RefineState& st) {
     const int b = (int)(key >> kKeyImgShift);
     const int o = (int)((key >> kKeyOctShift) & 15);
+    const RefineOct& g = geo[o];
     st.key = key;
-    st.W = L.ow[o];
-    st.H = L.oh[o];
-    st.pitch = L.opitch[o];
-    st.g0 = as_global(L.gauss[o]) + (size_t)(b - L.img_base) * L.g_img_stride[o];
+    st.W = g.W;
+    st.H = g.H;
+    st.pitch = g.pitch;
+    st.g0 = as_global(g.g) + (size_t)(b - L.img_base) * g.stride;
     st.vlo = 0;
     st.vhi = st.H;
     if (L.band_flag) {
@@ -202,6 +212,11 @@ __device__ __forceinline__ int refine_step(const RefineLaunch& L, RefineState& s
 // its decided lanes from that range (ballot rank + a wave cursor), so every
 // loop trip advances up to 64 live refinements by one Newton step.
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_REFINE_WPE))) void k_refine(const RefineLaunch L) {
+    __shared__ RefineOct geo[16];
+    if ((int)threadIdx.x < L.n_oct && threadIdx.x < 16)
+        geo[threadIdx.x] = RefineOct{L.gauss[threadIdx.x], L.g_img_stride[threadIdx.x], L.ow[threadIdx.x],
+                                     L.oh[threadIdx.x], L.opitch[threadIdx.x]};
+    __syncthreads();
     const uint32_t n = min(*L.n_cand, L.cand_cap);
     const int lane = threadIdx.x & 63;
     const uint32_t nw = gridDim.x * 4u, w = blockIdx.x * 4u + (threadIdx.x >> 6);
@@ -209,19 +224,37 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_REFINE
     const uint32_t end = (uint32_t)(((uint64_t)n * (w + 1)) / nw);
     RefineState st{};
     bool live = false;
+    // each lane holds its next candidate's key (loaded one refill ahead)
+    uint64_t nk = 0;
+    bool nk_ok = false;
+    {
+        const uint32_t i0 = cur + (uint32_t)lane, i1 = i0 + 64u;
+        if (i0 < end) {
+            refine_start(L, geo, L.cand[i0], st);
+            live = true;
+        }
+        if (i1 < end) {
+            nk = L.cand[i1];
+            nk_ok = true;
+        }
+        cur = min(end, cur + 128u);
+    }
     for (;;) {
-        // refill decided lanes, in lane order, from the wave's range
-        const uint64_t need = __ballot(!live);
-        if (need && cur < end) {
-            const uint32_t rank = (uint32_t)__popcll(need & ((1ull << lane) - 1ull));
-            const uint32_t i = cur + rank;
-            if (!live && i < end) {
-                refine_start(L, L.cand[i], st);
+        // a decided lane starts its prefetched candidate and claims the next
+        // one of the wave's range (in lane order)
+        const bool take = !live && nk_ok;
+        const uint64_t need = __ballot(take);
+        if (need) {
+            if (take) {
+                refine_start(L, geo, nk, st);
                 live = true;
+                const uint32_t i = cur + (uint32_t)__popcll(need & ((1ull << lane) - 1ull));
+                nk_ok = i < end;
+                if (nk_ok) nk = L.cand[i];
             }
             cur = min(end, cur + (uint32_t)__popcll(need));
         }
-        if (!__ballot(live)) break;  // wave-uniform: range done, no refinement left
+        if (!__ballot(live)) break;  // wave-uniform: no refinement left (and no prefetched candidate)
         ExtRec e;
         int r = 0;
         if (live) {

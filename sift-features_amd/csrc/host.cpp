@@ -1309,6 +1309,7 @@ int launch_refine_stage(sift_mi_ctx* c, int si, const uint64_t* cand, const uint
     R.ow = p.d_ow.p;
     R.oh = p.d_oh.p;
     R.opitch = p.d_opitch.p;
+    R.n_oct = p.n_oct;
     R.img_base = 0;
     R.out = ext;
     R.counter = counter;

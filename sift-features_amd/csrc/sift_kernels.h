@@ -223,6 +223,7 @@ struct RefineLaunch {
     const int* ow;
     const int* oh;
     const int* opitch;
+    int n_oct;  // entries of the device arrays above
     int img_base;
     ExtRec* out;
     uint32_t* counter;

@@ -486,6 +486,7 @@ int main(int argc, char** argv) {
     R.ow = dw;
     R.oh = dh;
     R.opitch = dp;
+    R.n_oct = 1;
     R.out = ext;
     R.counter = cnt + 1;
     R.cap = nc;
