@@ -62,19 +62,11 @@ __device__ __forceinline__ void load_nbhd(const gfloat* g0, size_t P, int pitch,
 
 // ---------------------------------------------------------------------------
 // k_refine: interpolate_extremum, extremum_contrast, extremum_is_on_edge
-// (src/lib.rs:334-367, 525-653) for the candidate list.
-//
-// interpolate_extremum takes 1 Newton step for ~78% of candidates but up to 5
-// (a candidate that keeps moving; ~9% hit the cap), and every step is a round
-// trip of dependent loads.  With one candidate per lane for its whole
-// refinement, a wave would run as many steps as its slowest lane -- nearly
-// always 5.  Here a lane holds a refinement STATE (candidate, current scale /
-// row / column, steps taken) and the wave advances all its lanes by one step
-// per loop trip; a lane whose candidate is decided (accepted, rejected, or
-// out of steps) takes the next candidate of the wave's range at once.  Each
-// candidate runs exactly the reference's sequence of steps (same expressions,
-// same order), so the extrema are those of the one-candidate-per-lane
-// kernel bit for bit; only their append order differs (sorted by key later).
+// (src/lib.rs:334-367, 525-653) for the candidate list.  A refinement is a
+// STATE (candidate, current scale / row / column, steps taken, the octave's
+// geometry) advanced by refine_step one Newton step at a time: exactly the
+// reference's sequence of steps (same expressions, same order), decided after
+// at most kMaxInterpSteps of them.
 // ---------------------------------------------------------------------------
 struct RefineState {
     uint64_t key;
@@ -84,8 +76,9 @@ struct RefineState {
     int sc, xi, yi, it;  // current scale, column, row; Newton steps taken
 };
 
-// The octaves' geometry, staged in LDS once per workgroup (a refill then
-// costs the key load only, not a second round trip for its octave's entries)
+// The octaves' geometry, staged in LDS once per workgroup (a candidate's
+// start then costs its key load only, not a second round trip for its
+// octave's entries)
 struct RefineOct {
     const float* g;
     size_t stride;
@@ -208,9 +201,14 @@ __device__ __forceinline__ int refine_step(const RefineLaunch& L, RefineState& s
 #ifndef SIFT_REFINE_WPE
 #define SIFT_REFINE_WPE 1
 #endif
-// Persistent waves: wave w owns candidates [n*w/NW, n*(w+1)/NW) and refills
-// its decided lanes from that range (ballot rank + a wave cursor), so every
-// loop trip advances up to 64 live refinements by one Newton step.
+// One candidate per lane for its whole refinement, the block's lanes
+// grid-striding over the list.  (Round 5 also built persistent waves that
+// refill a decided lane at once, so a wave never waits for its slowest
+// lane's five steps -- with the next key prefetched and the geometry in LDS
+// as here -- and measured them slower: 26.8-28.6 vs 23.3-25.4 us on octave 0
+// of 64 frames, detect_ms 1.36-1.58 vs 1.19 per 128 frames.  The stage moves
+// ~12 scattered 64-byte sectors per step; keeping more steps in flight per
+// wave does not shorten that.)
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_REFINE_WPE))) void k_refine(const RefineLaunch L) {
     __shared__ RefineOct geo[16];
     if ((int)threadIdx.x < L.n_oct && threadIdx.x < 16)
@@ -219,56 +217,25 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_REFINE
     __syncthreads();
     const uint32_t n = min(*L.n_cand, L.cand_cap);
     const int lane = threadIdx.x & 63;
-    const uint32_t nw = gridDim.x * 4u, w = blockIdx.x * 4u + (threadIdx.x >> 6);
-    uint32_t cur = (uint32_t)(((uint64_t)n * w) / nw);
-    const uint32_t end = (uint32_t)(((uint64_t)n * (w + 1)) / nw);
-    RefineState st{};
-    bool live = false;
-    // each lane holds its next candidate's key (loaded one refill ahead)
-    uint64_t nk = 0;
-    bool nk_ok = false;
-    {
-        const uint32_t i0 = cur + (uint32_t)lane, i1 = i0 + 64u;
-        if (i0 < end) {
-            refine_start(L, geo, L.cand[i0], st);
-            live = true;
-        }
-        if (i1 < end) {
-            nk = L.cand[i1];
-            nk_ok = true;
-        }
-        cur = min(end, cur + 128u);
-    }
-    for (;;) {
-        // a decided lane starts its prefetched candidate and claims the next
-        // one of the wave's range (in lane order)
-        const bool take = !live && nk_ok;
-        const uint64_t need = __ballot(take);
-        if (need) {
-            if (take) {
-                refine_start(L, geo, nk, st);
-                live = true;
-                const uint32_t i = cur + (uint32_t)__popcll(need & ((1ull << lane) - 1ull));
-                nk_ok = i < end;
-                if (nk_ok) nk = L.cand[i];
-            }
-            cur = min(end, cur + (uint32_t)__popcll(need));
-        }
-        if (!__ballot(live)) break;  // wave-uniform: no refinement left (and no prefetched candidate)
+    for (uint32_t base = blockIdx.x * 256; base < n; base += gridDim.x * 256) {
+        const uint32_t i = base + threadIdx.x;
         ExtRec e;
-        int r = 0;
-        if (live) {
-            r = refine_step(L, st, e);
-            if (r != 0) live = false;
+        int r = -1;
+        if (i < n) {
+            RefineState st;
+            refine_start(L, geo, L.cand[i], st);
+            do {
+                r = refine_step(L, st, e);  // <= kMaxInterpSteps steps
+            } while (r == 0);
         }
         const bool keep = r > 0;
         const uint64_t mask = __ballot(keep);
         if (!mask) continue;
         const int leader = __ffsll((unsigned long long)mask) - 1;
-        uint32_t base = 0;
-        if (lane == leader) base = atomicAdd(L.counter, (uint32_t)__popcll(mask));
-        base = __shfl(base, leader);
-        const uint32_t slot = base + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
+        uint32_t b = 0;
+        if (lane == leader) b = atomicAdd(L.counter, (uint32_t)__popcll(mask));
+        b = __shfl(b, leader);
+        const uint32_t slot = b + (uint32_t)__popcll(mask & ((1ull << lane) - 1ull));
         if (keep && slot < L.cap) L.out[slot] = e;
     }
 }
