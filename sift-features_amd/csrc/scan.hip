@@ -25,7 +25,7 @@ namespace siftmi {
 // ---------------------------------------------------------------------------
 // k_detect_rows: point_is_local_extremum (src/lib.rs:437-506) over all three
 // scale triples of an octave, with no LDS staging.  A wave owns a strip of 64
-// columns (62 outputs: lanes 1..62, the edge lanes are halo) and DR_SH rows;
+// columns (62 outputs: lanes 1..62, the edge lanes are halo) and ML.sh rows;
 // it walks down the strip, loading one row of the 5 DoG planes per step (one
 // coalesced 256-B load per plane), forming the 3-wide row max / min with DPP
 // wave shifts and keeping the last 3 rows in registers.  Every DoG byte is
@@ -34,7 +34,7 @@ namespace siftmi {
 // in LDS ran 1.8x longer: latency-bound, 62% of wave cycles waiting.)
 // Extrema are appended as packed emission keys for k_refine.
 // ---------------------------------------------------------------------------
-constexpr int DR_SH = 32;       // rows per strip
+constexpr int DR_SH = 32;       // rows per strip (fewer for launches that cannot fill the chip)
 constexpr int DR_COLS = 62;     // output columns per wave
 constexpr int DR_LCAP = 256;    // per-block LDS candidate list
 
@@ -98,7 +98,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_DETECT
     const DetectOctave& L = ML.oct[oi];
     const int W = L.W, H = L.H, pitch = L.pitch;
     const int tid = threadIdx.x, lane = tid & 63, wave = tid >> 6;
-    const int nsx = (W + DR_COLS - 1) / DR_COLS, nsy = (L.y_hi - L.y_lo + DR_SH - 1) / DR_SH;
+    const int SH = ML.sh;
+    const int nsx = (W + DR_COLS - 1) / DR_COLS, nsy = (L.y_hi - L.y_lo + SH - 1) / SH;
     const uint32_t g = (blockIdx.x - ML.block0[oi]) * 4 + wave;  // strip index: frame-major, then row band, then column
     const uint32_t per = (uint32_t)(nsx * nsy);
     const int b = (int)(g / per);
@@ -112,7 +113,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_DETECT
         const int x = sx * DR_COLS - 1 + lane;  // this lane's column
         const int xc = min(max(x, 0), W - 1);
         const bool xout = lane >= 1 && lane <= DR_COLS && x >= kImageBorder && x < W - kImageBorder;
-        const int y0 = L.y_lo + sy * DR_SH, y1 = min(y0 + DR_SH, L.y_hi);
+        const int y0 = L.y_lo + sy * SH, y1 = min(y0 + SH, L.y_hi);
         // DoG rows y - 1 (prv) and y (mid) at this lane's column
         float prv[kDogPerOctave], mid[kDogPerOctave], nv[kImagesPerOctave];
         // one row of G_0..G_5; the loads of row y + 2 stay in flight as raw
@@ -188,12 +189,29 @@ void launch_detect(DetectLaunch& L, hipStream_t st) {
         L.oct[k++] = d;
     }
     L.n_oct = k;
+    // A wave walks its strip row after row (~1 us per row at low occupancy):
+    // a launch too small to fill the chip twice over at 32-row strips (one
+    // frame's octaves) takes shorter ones, down to 4 rows, until it has ~8 k
+    // waves
+    auto total = [&](int sh) {
+        uint32_t nb = 0;
+        for (int i = 0; i < k; i++) {
+            const DetectOctave& d = L.oct[i];
+            const uint32_t strips =
+                (uint32_t)((d.W + DR_COLS - 1) / DR_COLS) * ((d.y_hi - d.y_lo + sh - 1) / sh) * L.n_img;
+            nb += (strips + 3) / 4;
+        }
+        return nb;
+    };
+    int sh = DR_SH;
+    while (sh > 4 && total(sh) * 4 < 8192) sh /= 2;
+    L.sh = sh;
     uint32_t nb = 0;
     for (int i = 0; i < k; i++) {
         const DetectOctave& d = L.oct[i];
         L.block0[i] = nb;
         const uint32_t strips =
-            (uint32_t)((d.W + DR_COLS - 1) / DR_COLS) * ((d.y_hi - d.y_lo + DR_SH - 1) / DR_SH) * L.n_img;
+            (uint32_t)((d.W + DR_COLS - 1) / DR_COLS) * ((d.y_hi - d.y_lo + sh - 1) / sh) * L.n_img;
         nb += (strips + 3) / 4;
     }
     L.block0[k] = nb;

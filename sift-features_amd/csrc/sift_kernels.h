@@ -54,8 +54,9 @@ struct PathOpts {
     int graph = 0;         // 1: single-chunk calls captured once and replayed as a HIP graph
     int band_drift = 24;   // row bands: refinement drift accepted without a re-run (< 24 forces re-runs)
     int bound_shrink = 1;  // > 1: first-chunk stage bounds divided by it (forces the overflow re-run)
-    int tail_split = 1;    // k_octave_tail as chain + side workgroups per frame: 1 for chunks of
-                           // <= kTailSplitMaxFrames frames, 2 always, 0 never (one workgroup per frame)
+    int tail_split = 0;    // k_octave_tail as chain + side workgroups per frame: 1 for chunks of
+                           // <= kTailSplitMaxFrames frames, 2 always, 0 never (one workgroup per frame:
+                           // faster in every case measured)
 };
 
 // Image planes are row-pitched: element (y, x) at plane[y * pitch + x].
@@ -181,11 +182,12 @@ struct DetectLaunch {
     DetectOctave oct[kTailMaxOct];
     uint32_t block0[kTailMaxOct + 1];
     int n_oct, n_img, img_base;
+    int sh;          // rows per strip (filled by launch_detect)
     uint64_t* cand;  // packed candidate keys (frame, octave, scale, y, x)
     uint32_t* counter;
     uint32_t cap;
 };
-// octaves L.oct[0 .. n_oct) (block0 is filled here)
+// octaves L.oct[0 .. n_oct) (block0 and sh are filled here)
 void launch_detect(DetectLaunch& L, hipStream_t st);
 // The octave's blur 5 (G_4 -> G_5, radius R, whole planes) and its
 // detection in one pass (k_blur_detect); -1 when it does not apply (the

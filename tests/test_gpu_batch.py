@@ -282,6 +282,7 @@ def test_batch_tail_split_equal(pkg, oracle):
     fr = synth.frames(6, 640, 480, seed0=60)
     c = pkg.Context(0, pkg.OpenCVProcessing)
     c.set_chunk(6)
+    c.set_path_option("tail_split", 2)
     try:
         split = c.sift_batch(fr)
         for i in (0, 5):
@@ -360,9 +361,9 @@ def test_single_chunk_graph_replay(pkg, ctx, oracle, fetch):
     c.close()
 
 
-@pytest.mark.parametrize("knob", ["early", "desc_first", "tail_split"])
+@pytest.mark.parametrize("knob,on", [("early", 1), ("desc_first", 1), ("tail_split", 1)])
 @pytest.mark.parametrize("profile", [0, 1])
-def test_single_chunk_paths_equal(pkg, knob, profile):
+def test_single_chunk_paths_equal(pkg, knob, on, profile):
     """One-chunk calls take latency paths of their own -- the octaves below
     the tail detected, refined and oriented on the aux stream beside the tail
     kernel with the tail octaves in a region of their own
@@ -370,13 +371,15 @@ def test_single_chunk_paths_equal(pkg, knob, profile):
     the ordering stage, then gathered (Slot::desc_first), and the small
     octaves' kernel as a chain and a side workgroup per frame handing G_3
     over through device flags (tail_split) -- whose results must equal the
-    general path's (the knob = 0) bit for bit, incl. keys.  Each
+    general path's (the knob = 0) bit for bit, incl. keys.  tail_split is
+    off by default (measured slower), so it is switched on here.  Each
     frame runs twice: the second call uses the bounds the first one learned."""
     import synth
     frames = [synth.frame(640, 480, 3), synth.frame(1000, 333, 5),
               np.random.default_rng(5).integers(0, 256, (96, 128), dtype=np.uint8)]
     prof = pkg.OpenCVProcessing if profile == 0 else pkg.ImageprocProcessing
     c = pkg.Context(0, prof)
+    c.set_path_option(knob, on)
     got = [c.sift(f) for f in frames for _ in range(2)]
     c.set_path_option(knob, 0)
     ref = [c.sift(f) for f in frames for _ in range(2)]

@@ -1,0 +1,11 @@
+cd "$GRAFT_REPO_ROOT" || exit 2
+mkdir -p gpurun_out
+export TMPDIR=/tmp
+for r in 1 2 3; do
+  for ts in 3 0 1; do
+    timeout -k 10 120 python3 tools/single_frame.py --calls 300 --opt tail_split=$ts >> gpurun_out/r05_single17.log 2>&1 || exit 1
+  done
+done
+grep frames_per_call gpurun_out/r05_single17.log
+timeout -k 10 300 python -u -m pytest tests/test_gpu_batch.py -x -q -k "tail_split or single_chunk" --timeout 120 --timeout-method thread -p no:cacheprovider > gpurun_out/r05_pytest17.log 2>&1
+rc=$?; echo "pytest rc=$rc"; tail -2 gpurun_out/r05_pytest17.log
