@@ -16,6 +16,7 @@
 #include <algorithm>
 #include <type_traits>
 
+#include "launch_ext.h"
 #include "sift_common.h"
 #include "sift_kernels.h"
 
@@ -536,7 +537,7 @@ __global__ __launch_bounds__(256, SIFT_ORIENT_MIN_WAVES) void k_orient(const Ori
 void launch_orient(const OrientLaunch& L, hipStream_t st) {
     if (L.ext_cap == 0) return;
     dim3 grid((L.ext_cap + 3) / 4);
-    hipLaunchKernelGGL(k_orient, grid, dim3(256), 0, st, L);
+    klaunch(k_orient, grid, dim3(256), st, L);  // may carry a completion event (set_launch_done_event)
 }
 
 }  // namespace siftmi

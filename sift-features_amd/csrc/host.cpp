@@ -455,6 +455,9 @@ struct Slot {
     // stage either waits first or, with desc_first, runs the descriptors on
     // the aux stream itself (no cross-stream hop before them)
     bool join_pending = false;
+    // the chunk's counter reset is launched right after the seed pass
+    // (run_pyramid) instead of before it: the seed does not touch them
+    bool init_pending = false;
     uint32_t bcb = 0;
     DevBuf<uint64_t> cand_b;
     DevBuf<ExtRec> ext_b;
@@ -782,6 +785,9 @@ constexpr int kBandDrift = 24, kBandPatch = 41;
 // cand_slot >= 0 (the keypoint stages follow): octaves whose blur 5 and
 // detection run as one pass (k_blur_detect) append their candidates to that
 // slot's buffer from here, whatever detect_slot is (Slot::fused_mask).
+constexpr int kTailWords = 3;        // Slot counters after the per-frame plan: cand_b, ext_b counts, tail error
+void flush_chunk_init(sift_mi_ctx* c, int si);
+
 int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_pitch, size_t row_stride,
                 uint32_t n, bool full, int detect_slot = -1, int cand_slot = -1) {
     Plan& p = c->plan;
@@ -905,9 +911,17 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
         S.taps = p.seed_taps;
         S.y0 = seed_y0;
         S.y1 = seed_y1;
+        // the chunk's counter reset rides on the seed pass (its first workgroup)
+        Slot* is = (tail_slot >= 0 && f0 == 0 && c->slot[tail_slot].init_pending) ? &c->slot[tail_slot] : nullptr;
+        if (is) {
+            S.init_cnt = is->counters.p;
+            S.init_m = (int)is->m;
+            S.init_words = kDescWorkWords + kTailWords;
+        }
         // G_0 and G_1 in one pass where it applies (whole planes: not for a
         // restricted row band); G_0 is then never read back from HBM
         seed_pair = p.n_oct > 0 && launch_seed_pair(p.seed_r, p.oct_r[1], S, blur_launch(0, 1, f0, nf), sm, po) == 0;
+        if (seed_pair && is) is->init_pending = false;
         if (seed_pair) {
             launches++;
             return 0;
@@ -1024,9 +1038,11 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
         return 0;
     };
     auto part = [&](uint32_t f0, uint32_t nf, hipStream_t sm, bool ov) -> int {
+        bool aux_done_signalled = false;  // the aux orientation's launch carries the join event
         const bool early =
             detect_slot >= 0 && ov && o_tail > 0 && o_tail < p.n_oct && c->slot[detect_slot].bcb && po.early;
         CHK(seed(f0, nf, sm));
+        if (tail_slot >= 0 && f0 == 0) flush_chunk_init(c, tail_slot);  // the chunk's counters, behind the seed
         CHK(octaves(f0, nf, 0, o_tail, sm, ov));
         if (defer0) {  // no later octave took it (cannot happen with o_tail > 1): launch it now
             HIPCHK(hipStreamWaitEvent(aux, c->oct_ev[lane][0], 0));
@@ -1100,7 +1116,13 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
             uint32_t* cb = cnt + 4 + 2 * S.m;
             CHK(launch_detection(c, detect_slot, f0, nf, 0, o_tail, aux));
             CHK(launch_refine_stage(c, detect_slot, S.cand.p, cnt + 0, S.bc, S.ext.p, cnt + 1, S.be, aux));
-            CHK(launch_orient_stage(c, detect_slot, S.ext.p, cnt + 1, S.be, S.bk, aux));
+            // the aux orientation signals the join event itself (no marker on
+            // the aux stream's critical path; not under stream capture)
+            if (ov && o_tail > 0 && ext_events) set_launch_done_event(c->oct_ev[lane][kTailMaxOct]);
+            const int rc_o = launch_orient_stage(c, detect_slot, S.ext.p, cnt + 1, S.be, S.bk, aux);
+            aux_done_signalled = ov && o_tail > 0 && ext_events && !launch_done_pending();
+            set_launch_done_event(nullptr);
+            CHK(rc_o);
             CHK(launch_detection(c, detect_slot, f0, nf, o_tail, p.n_oct, sm, S.cand_b.p, cb + 0, S.bcb));
             CHK(launch_refine_stage(c, detect_slot, S.cand_b.p, cb + 0, S.bcb, S.ext_b.p, cb + 1, S.bcb, sm));
             CHK(launch_orient_stage(c, detect_slot, S.ext_b.p, cb + 1, S.bcb, S.bk, sm));
@@ -1112,7 +1134,7 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
             CHK(launch_detection(c, detect_slot, f0, nf, o_tail, p.n_oct, sm));
         }
         if (ov && o_tail > 0) {  // join: the aux stream's work before what follows on sm
-            HIPCHK(hipEventRecord(c->oct_ev[lane][kTailMaxOct], aux));
+            if (!aux_done_signalled) HIPCHK(hipEventRecord(c->oct_ev[lane][kTailMaxOct], aux));
             // (not under stream capture: a capture keeps the plain join)
             if (early && c->lanes == 2 && ext_events)
                 c->slot[detect_slot].join_pending = true;  // enqueue_keypoints joins
@@ -1151,7 +1173,6 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
 // is re-run with larger bounds.
 // ---------------------------------------------------------------------------
 constexpr uint32_t kMaxChunk = 256;  // frames per chunk (one workgroup plans the output: k_limit_plan)
-constexpr int kTailWords = 3;        // Slot counters after the per-frame plan: cand_b, ext_b counts, tail error
 
 struct Bounds {
     uint32_t bc, be, bk;
@@ -1233,7 +1254,14 @@ int img_bits_for(uint32_t m) {
 
 // Per-chunk state and zeroed counters of slot si, before any of its kernels
 // (detection may start inside the pyramid: stage overlap).
-int prepare_chunk(sift_mi_ctx* c, int si, uint32_t m, uint32_t frame_base, const Bounds& B) {
+void flush_chunk_init(sift_mi_ctx* c, int si) {
+    Slot& S = c->slot[si];
+    if (!S.init_pending) return;
+    S.init_pending = false;
+    launch_chunk_init(S.counters.p, (int)S.m, kDescWorkWords + kTailWords, lane_stream(c, si));  // + the tail region's words
+}
+
+int prepare_chunk(sift_mi_ctx* c, int si, uint32_t m, uint32_t frame_base, const Bounds& B, bool defer_init) {
     Slot& S = c->slot[si];
     hipStream_t st = lane_stream(c, si);
     S.m = m;
@@ -1247,9 +1275,10 @@ int prepare_chunk(sift_mi_ctx* c, int si, uint32_t m, uint32_t frame_base, const
     S.graph_run = false;
     S.early = false;
     S.join_pending = false;
-    uint32_t* cnt = S.counters.p;
+    (void)st;
     // stage counters, frame starts (~0), descriptor work queues
-    launch_chunk_init(cnt, (int)m, kDescWorkWords + kTailWords, st);  // + the tail region's words
+    S.init_pending = true;
+    if (!defer_init) flush_chunk_init(c, si);
     HIPCHK(hipGetLastError());
     return 0;
 }
@@ -1361,6 +1390,9 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
                    S.desc_kp.cap >= (size_t)B.bk * kDescSize && c->opts.desc_first;
     const bool join_pending = S.join_pending;
     S.join_pending = false;
+    // completion events carried by kernel launches (not under stream capture)
+    hipStreamCaptureStatus cap = hipStreamCaptureStatusNone;
+    const bool ext_events = hipStreamIsCapturing(st, &cap) == hipSuccess && cap == hipStreamCaptureStatusNone;
     hipEvent_t aux_done = c->oct_ev[si][kTailMaxOct];  // the aux stream's early stages (join_pending)
     if (join_pending && !S.desc_first) HIPCHK(hipStreamWaitEvent(st, aux_done, 0));
     if (!S.detected) CHK(launch_detection(c, si, 0, m, 0, p.n_oct, st));
@@ -1408,8 +1440,13 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
         return fail(SIFT_MI_EHIP, "radix sort failed");
     launch_frame_starts(S.keys_b.p, cnt + 2, B.bk, starts, os);
     // features_limit (src/lib.rs:156-161): per-frame plan on the device
+    // (desc_first: the plan's launch signals S.ordered, no marker after it)
+    const bool ordered_ext = S.desc_first && ext_events && limit < 0;
+    if (ordered_ext) set_launch_done_event(S.ordered);
     launch_limit_plan(starts, cnt + 2, B.bk, (int)m, limit, out_cnt, S.seg_off.p, S.out_off.p, S.use_resp.p,
                       cnt + 3, os);
+    const bool ordered_signalled = ordered_ext && !launch_done_pending();
+    set_launch_done_event(nullptr);
     if (limit >= 0) {
         // stable sort: response-descending within each frame, emission order on ties
         launch_make_resp_keys(S.kp.p, order, cnt + 2, B.bk, 0, rpad, S.keys_a.p, S.vals_a.p, os);
@@ -1421,7 +1458,7 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
         order = S.vals_a.p;
     }
     HIPCHK(hipGetLastError());
-    if (S.desc_first) HIPCHK(hipEventRecord(S.ordered, os));
+    if (S.desc_first && !ordered_signalled) HIPCHK(hipEventRecord(S.ordered, os));
     if (S.staged) HIPCHK(hipEventRecord(S.ev[4], st));
     // descriptors into this slot's outputs, once its previous copy-out is done
     if (S.pending_copy) HIPCHK(hipStreamWaitEvent(ds, S.copied, 0));
@@ -1444,17 +1481,23 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
     DL.exact = c->exact_descriptors;
     DL.samples = c->count_samples ? c->samples.p + 8 : nullptr;
     launch_describe(DL, ds);
+    const int count_words = 4 + 2 * m + kTailWords;  // the frame plan and the tail region's counters (Slot::early)
+    bool counts_copied = false;  // by k_gather_out, which then signals ev[6] itself
     if (S.desc_first) {
         HIPCHK(hipStreamWaitEvent(ds, S.ordered, 0));
+        const bool in_gather = ext_events && !S.staged;
+        if (in_gather) set_launch_done_event(S.ev[6]);
         launch_gather_out(S.kp.p, order, cnt + 3, B.bk, S.desc_kp.p, S.out_desc.p, S.out_kp.p, S.out_key.p,
-                          DL.key_base, ds);
+                          DL.key_base, in_gather ? cnt : nullptr, in_gather ? S.h_counts.p : nullptr, count_words, ds);
+        counts_copied = in_gather && !launch_done_pending();
+        set_launch_done_event(nullptr);
     }
     HIPCHK(hipGetLastError());
     if (S.staged) HIPCHK(hipEventRecord(S.ev[5], st));
-    // the frame plan and the tail region's counters (Slot::early) in one copy
-    HIPCHK(hipMemcpyAsync(S.h_counts.p, cnt, (4 + 2 * m + kTailWords) * sizeof(uint32_t),
-                          hipMemcpyDeviceToHost, ds));
-    HIPCHK(hipEventRecord(S.ev[6], ds));
+    if (!counts_copied) {
+        HIPCHK(hipMemcpyAsync(S.h_counts.p, cnt, count_words * sizeof(uint32_t), hipMemcpyDeviceToHost, ds));
+        HIPCHK(hipEventRecord(S.ev[6], ds));
+    }
     // the lane stream's next work follows this chunk (and a capture rejoins)
     if (ds != st) HIPCHK(hipStreamWaitEvent(st, S.ev[6], 0));
     return 0;
@@ -1485,12 +1528,13 @@ int enqueue_chunk(sift_mi_ctx* c, int si, const uint8_t* d_frames, size_t frame_
     hipStream_t st = lane_stream(c, si);
     S.staged = c->lanes == 1;
     if (S.staged) HIPCHK(hipEventRecord(S.ev[0], st));
-    CHK(prepare_chunk(c, si, m, frame_base, B));
+    CHK(prepare_chunk(c, si, m, frame_base, B, pyramid));
     // stage overlap (two-lane mode; the one-lane mode times the stages apart):
     // detection starts inside the pyramid (run_pyramid), so ev[1]..ev[2] is
     // then only the refinement
     const bool fused = pyramid && c->lanes == 2;
     if (pyramid) CHK(run_pyramid(c, si, d_frames, frame_pitch, stride, m, false, fused ? si : -1, si));
+    flush_chunk_init(c, si);  // (run_pyramid launched it after the seed)
     if (S.staged) HIPCHK(hipEventRecord(S.ev[1], st));
     return enqueue_keypoints(c, si, m, limit, frame_base, B);
 }
@@ -1895,6 +1939,8 @@ extern "C" {
 const char* sift_mi_version(void) { return "sift_mi 0.4.0 (gfx950)"; }
 const char* sift_mi_last_error(void) { return g_err.c_str(); }
 
+bool create_sync_events(sift_mi_ctx* c);
+
 int sift_mi_create(int device_ordinal, sift_mi_profile profile, sift_mi_ctx** out) {
     if (!out) return fail(SIFT_MI_EINVAL, "out is null");
     *out = nullptr;
@@ -1923,15 +1969,10 @@ int sift_mi_create(int device_ordinal, sift_mi_profile profile, sift_mi_ctx** ou
     c->aux[1] = ss[4];
     c->aux2 = ss[5];
     c->stream = c->own;
-    bool ok = hipEventCreateWithFlags(&c->fork, hipEventDisableTiming) == hipSuccess;
-    ok = ok && hipEventCreateWithFlags(&c->aux2_join, hipEventDisableTiming) == hipSuccess;
-    for (auto& lane : c->oct_ev)
-        for (auto& e : lane) ok = ok && hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+    bool ok = create_sync_events(c);
     for (auto& S : c->slot) {
         for (auto& e : S.ev) ok = ok && hipEventCreate(&e) == hipSuccess;
         ok = ok && hipEventCreateWithFlags(&S.copied, hipEventDisableTiming) == hipSuccess;
-        ok = ok && hipEventCreateWithFlags(&S.ordered, hipEventDisableTiming) == hipSuccess;
-        ok = ok && hipEventCreateWithFlags(&S.oriented, hipEventDisableTiming) == hipSuccess;
     }
     if (!ok) {
         sift_mi_destroy(c);
@@ -2033,6 +2074,24 @@ int sift_mi_set_row_band(sift_mi_ctx* c, uint32_t band, uint32_t n_bands) {
     c->band_r = band;
     c->band_n = n_bands;
     return 0;
+}
+
+// The events that only order the context's streams on the device (octave
+// hand-overs, forks, joins, the one-frame path's oriented / ordered).
+// (Measured: a device-scope release, hipEventReleaseToDevice, changed nothing
+// -- 0.581-0.583 ms per 1080p frame either way; a signalling kernel still
+// costs its stream ~5 us before the next one starts)
+bool create_sync_events(sift_mi_ctx* c) {
+    auto make = [&](hipEvent_t& e) {
+        if (e) (void)hipEventDestroy(e);
+        e = nullptr;
+        return hipEventCreateWithFlags(&e, hipEventDisableTiming) == hipSuccess;
+    };
+    bool ok = make(c->fork) && make(c->aux2_join);
+    for (auto& lane : c->oct_ev)
+        for (auto& e : lane) ok = ok && make(e);
+    for (auto& S : c->slot) ok = ok && make(S.ordered) && make(S.oriented);
+    return ok;
 }
 
 int sift_mi_set_path_option(sift_mi_ctx* c, int option, int value) {

@@ -11,6 +11,7 @@
 
 #include <algorithm>
 
+#include "launch_ext.h"
 #include "sift_common.h"
 #include "sift_kernels.h"
 
@@ -126,8 +127,8 @@ __global__ __launch_bounds__(kLimitPlanFrames) void k_limit_plan(const uint32_t*
 void launch_limit_plan(const uint32_t* starts, const uint32_t* n_kp, uint32_t bound, int n_img, int64_t limit,
                        uint32_t* out_cnt, uint32_t* seg_off, uint32_t* out_off, uint8_t* use_resp, uint32_t* n_out,
                        hipStream_t st) {
-    hipLaunchKernelGGL(k_limit_plan, dim3(1), dim3(kLimitPlanFrames), 0, st, starts, n_kp, bound, n_img, limit,
-                       out_cnt, seg_off, out_off, use_resp, n_out);
+    klaunch(k_limit_plan, dim3(1), dim3(kLimitPlanFrames), st, starts, n_kp, bound, n_img, limit, out_cnt, seg_off,
+            out_off, use_resp, n_out);
 }
 
 // key = (frame << 32) | ~bits(response)  (response >= 0, so bit order == value order)
@@ -186,12 +187,20 @@ void launch_select(const uint32_t* emis_order, const uint32_t* resp_order, const
 // (one-frame calls: k_describe runs beside the ordering stage): row j of the
 // outputs is keypoint order[j] -- its descriptor (16 bytes per thread), its
 // KeyPoint (src/lib.rs:163-176: x, y, size * DELTA_MIN) and its emission key.
+// Block 0 also copies the chunk's counters (cnt_words words) to the host's
+// pinned buffer, written back to host memory before the kernel ends (system
+// fence): no copy command after the kernel (~4 us plus its dispatch).
 __global__ void k_gather_out(const KpRec* __restrict__ kp, const uint32_t* __restrict__ order,
                              const uint32_t* __restrict__ n_out, uint32_t bound, const uint4* __restrict__ desc_in,
                              uint4* __restrict__ desc_out, OutKp* __restrict__ out_kp, uint64_t* __restrict__ out_key,
-                             uint64_t key_base) {
+                             uint64_t key_base, const uint32_t* __restrict__ cnt, uint32_t* __restrict__ h_cnt,
+                             int cnt_words) {
     constexpr uint32_t kParts = kDescSize / 16;
     const uint32_t t = blockIdx.x * blockDim.x + threadIdx.x;
+    if (h_cnt && blockIdx.x == 0) {
+        for (int w = threadIdx.x; w < cnt_words; w += blockDim.x) h_cnt[w] = cnt[w];
+        __threadfence_system();
+    }
     const uint32_t j = t / kParts, part = t % kParts;
     const uint32_t n = min(*n_out, bound);
     if (j >= n) return;
@@ -212,12 +221,12 @@ __global__ void k_gather_out(const KpRec* __restrict__ kp, const uint32_t* __res
 
 void launch_gather_out(const KpRec* kp, const uint32_t* order, const uint32_t* n_out, uint32_t bound,
                        const uint8_t* desc_in, uint8_t* desc_out, OutKp* out_kp, uint64_t* out_key, uint64_t key_base,
-                       hipStream_t st) {
+                       const uint32_t* cnt, uint32_t* h_cnt, int cnt_words, hipStream_t st) {
     if (!bound) return;
     const uint64_t threads = (uint64_t)bound * (kDescSize / 16);
-    hipLaunchKernelGGL(k_gather_out, dim3((unsigned)((threads + 255) / 256)), dim3(256), 0, st, kp, order, n_out,
-                       bound, reinterpret_cast<const uint4*>(desc_in), reinterpret_cast<uint4*>(desc_out), out_kp,
-                       out_key, key_base);
+    klaunch(k_gather_out, dim3((unsigned)((threads + 255) / 256)), dim3(256), st, kp, order, n_out, bound,
+            reinterpret_cast<const uint4*>(desc_in), reinterpret_cast<uint4*>(desc_out), out_kp, out_key, key_base, cnt,
+            h_cnt, cnt_words);
 }
 
 }  // namespace siftmi

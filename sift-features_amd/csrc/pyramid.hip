@@ -24,8 +24,7 @@
 //                 (nearest 1/2 = pixel (2x, 2y)).
 // The stage is HBM-bound: per octave pixel the reference materialises 6 G + 5 D
 // images (44 B); see DESIGN.md for the roofline accounting.
-#include <hip/hip_ext.h>
-
+#include "launch_ext.h"
 #include "sift_common.h"
 #include "sift_kernels.h"
 
@@ -35,35 +34,8 @@
 
 namespace siftmi {
 
-// The next kernel a launcher below enqueues from this host thread signals
-// t_done on completion (hipExtLaunchKernel's stop event, no marker packet of
-// its own: a marker between two kernels costs ~7 us of the stream's
-// timeline).
-static thread_local hipEvent_t t_done = nullptr;
 void set_launch_done_event(hipEvent_t e) { t_done = e; }
 bool launch_done_pending() { return t_done != nullptr; }
-
-template <class F, class... A>
-static void klaunch(F kernel, dim3 grid, dim3 block, hipStream_t st, A... args) {
-    if (t_done) {
-        hipEvent_t e = t_done;
-        t_done = nullptr;
-        // hipExtLaunchKernelGGL's packing, with its status checked: on failure
-        // the kernel goes out plainly and e is recorded after it
-        auto tup_ = std::tuple<A...>{args...};
-        auto tup = validateArgsCountType(kernel, tup_);
-        void* kargs[sizeof...(A) > 0 ? sizeof...(A) : 1];
-        pArgs<0>(tup, kargs);
-        if (hipExtLaunchKernel(reinterpret_cast<void*>(kernel), grid, block, kargs, 0, st, nullptr, e, 0) !=
-            hipSuccess) {
-            (void)hipGetLastError();
-            hipLaunchKernelGGL(kernel, grid, block, 0, st, args...);
-            (void)hipEventRecord(e, st);
-        }
-    } else {
-        hipLaunchKernelGGL(kernel, grid, block, 0, st, args...);
-    }
-}
 
 
 // ---------------------------------------------------------------------------
@@ -1518,13 +1490,18 @@ template <int Ra, int Rb, int P>
 __global__ __launch_bounds__(256, (PairGeom<Ra, Rb, 8>::MINB)) void k_seed_pair(
     const uint8_t* __restrict__ frames, size_t frame_pitch, size_t row_stride, int sh, int sw,
     float* __restrict__ dst_a, float* __restrict__ dst_b, size_t img_stride, int W, int H, int pitch,
-    const BlurTaps taps_a, const BlurTaps taps_b, int ya, int yb, int seg) {
+    const BlurTaps taps_a, const BlurTaps taps_b, int ya, int yb, int seg, uint32_t* __restrict__ init_cnt,
+    int init_m, int init_words) {
     using Q = PairGeom<Ra, Rb, 8>;
     using GA = typename Q::GA;
     using L = SeedLoader<GA, P>;
     __shared__ __attribute__((aligned(16))) float lds[Q::LDS_FLOATS];
     __shared__ typename L::Tables tabs;
     const int tid = threadIdx.x, lane = tid & 63;
+    if (init_cnt && blockIdx.x == 0 && blockIdx.y == 0 && blockIdx.z == 0) {  // the chunk's counters (k_chunk_init)
+        for (int i = tid; i < 4 + init_m + init_words; i += 256)
+            init_cnt[i < 4 + init_m ? i : i + init_m] = (i >= 4 && i < 4 + init_m) ? 0xffffffffu : 0u;
+    }
     const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
     const TileId tile = xcd_tile();
     const int X = tile.x * Q::TWO;
@@ -1941,7 +1918,7 @@ static void launch_seed_pair_rr(const SeedLaunch& S, const BlurLaunch& B, hipStr
     const int nseg = (S.H + seg - 1) / seg;
     klaunch((k_seed_pair<Ra, Rb, P>), dim3(strips, nseg, S.n_img), dim3(256), st, S.frames,
                        S.frame_pitch, S.row_stride, S.sh, S.sw, S.dst, B.dst, S.dst_img_stride, S.W, S.H, S.pitch,
-                       S.taps, B.taps, 0, S.H, seg);
+                       S.taps, B.taps, 0, S.H, seg, S.init_cnt, S.init_m, S.init_words);
 }
 
 int launch_seed_pair(int rs, int rb, const SeedLaunch& S, const BlurLaunch& B, hipStream_t st, const PathOpts& o) {

@@ -90,6 +90,10 @@ struct SeedLaunch {
     int n_img;
     int y0, y1;  // output rows [y0, y1) only (rounded out to tiles); y1 <= y0: all rows
     BlurTaps taps;
+    // k_seed_pair's first workgroup also resets a chunk's counters (k_chunk_init's
+    // words: 4 zeros, init_m x ~0, init_words zeros) when init_cnt is set
+    uint32_t* init_cnt = nullptr;
+    int init_m = 0, init_words = 0;
 };
 
 
@@ -278,7 +282,7 @@ void launch_make_resp_keys(const KpRec* kp, const uint32_t* order, const uint32_
 // then row j of the outputs = keypoint order[j] (descriptor, KeyPoint, key)
 void launch_gather_out(const KpRec* kp, const uint32_t* order, const uint32_t* n_out, uint32_t bound,
                        const uint8_t* desc_in, uint8_t* desc_out, OutKp* out_kp, uint64_t* out_key, uint64_t key_base,
-                       hipStream_t st);
+                       const uint32_t* cnt, uint32_t* h_cnt, int cnt_words, hipStream_t st);
 void launch_select(const uint32_t* emis_order, const uint32_t* resp_order, const uint32_t* seg_off,
                    const uint32_t* out_off, const uint8_t* use_resp, int n_img, const uint32_t* n_out, uint32_t bound,
                    uint32_t* final_idx, hipStream_t st);
