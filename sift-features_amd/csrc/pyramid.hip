@@ -2256,16 +2256,15 @@ __global__ __launch_bounds__(1024) void k_octave_tail(const TailLaunch L) {
         if constexpr (SPLIT) {
             // publish G_3: every wave's stores visible device-wide (an
             // agent-scope release per wave: its own stores complete, the L2
-            // written back for a reader on another XCD), then the flag
-            // every wave waits for its own stores to reach L2 (vmcnt(0)),
-            // then one agent-scope release -- one L2 write-back, not one per
-            // wave (0.599 vs 0.604 ms per 1080p frame) -- before the flag
-            __builtin_amdgcn_s_waitcnt(0x0F70);  // gfx9 encoding: vmcnt(0), expcnt / lgkmcnt untouched
+            // written back for a reader on another XCD), then the flag.
+            // (A variant with a raw s_waitcnt vmcnt(0) per wave and a single
+            // release by thread 0 -- 0.599 vs 0.604 ms per 1080p frame -- gave
+            // a wrong count once in ~10 runs of test_single_chunk_paths_equal:
+            // the builtin wait does not order the compiler's stores, so the
+            // one write-back could miss another wave's G_3 rows.)
+            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
             __syncthreads();
-            if (tid == 0) {
-                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-                __hip_atomic_store(flag, L.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
-            }
+            if (tid == 0) __hip_atomic_store(flag, L.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
