@@ -1807,8 +1807,12 @@ int extract_device(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, 
         HIPCHK(hipEventRecord(c->fork, c->own2));
         HIPCHK(hipStreamWaitEvent(c->stream, c->fork, 0));
     }
-    HIPCHK(hipStreamSynchronize(c->cstream));
-    for (auto& S2 : c->slot) S2.pending_copy = false;  // every copy of the call is done
+    // every copy of the call done (a device-resident one-chunk call copied
+    // nothing: no synchronisation, whose marker round trip costs a few us)
+    bool copies = false;
+    for (auto& S2 : c->slot) copies = copies || S2.pending_copy;
+    if (copies) HIPCHK(hipStreamSynchronize(c->cstream));
+    for (auto& S2 : c->slot) S2.pending_copy = false;
     if (offsets) offsets[n] = c->n_result;
     c->have_result = true;
     if (n_chunks == 1 && !c->band_restricted) {
