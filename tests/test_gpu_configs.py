@@ -146,3 +146,23 @@ def test_stage_bound_overflow_rerun(pkg, ctx, lanes):
     assert st["stage_reruns"] >= (2 if lanes == 2 else 1), st
     assert st["frames"] == 7 and st["keypoints"] == sum(len(r) for r in ref)
     assert all(a == b for a, b in zip(got, ref))
+
+
+def test_stage_bound_overflow_rerun_one_frame(pkg, ctx):
+    """The one-frame path (early detection, descriptors beside the ordering,
+    the chunk's counters copied to the host by k_gather_out) overflows its
+    first-call bounds (bound_shrink) and re-runs; the results equal a
+    context's whose bounds were learned."""
+    import synth
+    frames = [synth.frame(640, 480, 11), synth.frame(1920, 1080, 12)]
+    ref = [ctx.sift(f) for f in frames]
+    for f, r in zip(frames, ref):
+        c = pkg.Context(0, pkg.OpenCVProcessing)  # no high-water marks yet
+        c.set_path_option("bound_shrink", 1000)
+        got = c.sift(f)
+        st = c.stats()
+        again = c.sift(f)  # bounds learned now
+        c.close()
+        assert st["stage_reruns"] >= 1, st
+        assert got == r and again == r
+        assert np.array_equal(got.keys, r.keys)
