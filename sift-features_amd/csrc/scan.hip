@@ -262,7 +262,14 @@ __device__ __forceinline__ int bd_index(int p, int n) {
 __device__ __forceinline__ uint32_t xcd_block_1d() { return xcd_remap(blockIdx.x, gridDim.x); }
 
 template <int R, int P>
-__global__ __launch_bounds__(256) void k_blur_detect(const BlurDetectLaunch L) {
+#ifndef SIFT_BD_WPE
+// waves per SIMD the register budget must allow (1: unconstrained, 104 VGPRs
+// = 4 waves).  5 (96 VGPRs, 13 dwords spilled): 4159 / 4176 vs 3213 / 3083 us
+// on octave 0 of 64 frames (profiles/r05_ubd31.log)
+#define SIFT_BD_WPE 1
+#endif
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_BD_WPE))) void k_blur_detect(
+    const BlurDetectLaunch L) {
     static_assert(64 + 2 * R <= BD_RP && R + 3 <= BD_RING, "ring geometry");
     __shared__ float ring[4][BD_RING * BD_RP];
     __shared__ uint64_t lcand[DR_LCAP];
