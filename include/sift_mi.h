@@ -181,8 +181,10 @@ typedef enum {
                                       smaller values force the whole-pyramid re-run) */
     SIFT_MI_PATH_BOUND_SHRINK = 9, /* k >= 1: first-chunk stage bounds / k (default 1; > 1 forces the
                                       bound-overflow re-run) */
-    SIFT_MI_PATH_TAIL_SPLIT = 10   /* the small octaves' kernel as a chain and a side workgroup per frame:
+    SIFT_MI_PATH_TAIL_SPLIT = 10,  /* the small octaves' kernel as a chain and a side workgroup per frame:
                                       1 for chunks of <= 8 frames, 2 always, 0 never (default 0) */
+    SIFT_MI_PATH_LARGE_FIRST = 11  /* 0: one-chunk calls orient the extrema in refinement order, not
+                                      those with large windows first (default 1) */
 } sift_mi_path_option;
 int sift_mi_set_path_option(sift_mi_ctx* ctx, int option, int value);
 

@@ -230,6 +230,24 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_REFINE
             } while (r == 0);
         }
         const bool keep = r > 0;
+        if (L.counter_hi) {  // two-ended: large windows from the front, the others from the back
+            const bool large = keep && (float)e.scale + e.off_s >= kLargeWindowScale;
+            const uint64_t ml = __ballot(large), ms = __ballot(keep && !large);
+            uint32_t bl = 0, bs = 0;
+            if (ml && lane == __ffsll((unsigned long long)ml) - 1) bl = atomicAdd(L.counter, (uint32_t)__popcll(ml));
+            if (ms && lane == __ffsll((unsigned long long)ms) - 1) bs = atomicAdd(L.counter_hi, (uint32_t)__popcll(ms));
+            if (ml) bl = __shfl(bl, __ffsll((unsigned long long)ml) - 1);
+            if (ms) bs = __shfl(bs, __ffsll((unsigned long long)ms) - 1);
+            const uint64_t below = (1ull << lane) - 1ull;
+            if (large) {
+                const uint32_t slot = bl + (uint32_t)__popcll(ml & below);
+                if (slot < L.cap) L.out[slot] = e;
+            } else if (keep) {
+                const uint32_t j = bs + (uint32_t)__popcll(ms & below);
+                if (j < L.cap) L.out[L.cap - 1 - j] = e;
+            }
+            continue;
+        }
         const uint64_t mask = __ballot(keep);
         if (!mask) continue;
         const int leader = __ffsll((unsigned long long)mask) - 1;
@@ -273,7 +291,11 @@ __global__ __launch_bounds__(256, SIFT_ORIENT_MIN_WAVES) void k_orient(const Ori
     __shared__ float swt[4][OR_WT];  // per-wave Gaussian weight table
     __shared__ uint32_t wcount[4], wbase, wsamp[4];
     const int wave = threadIdx.x >> 6, lane = threadIdx.x & 63;
-    const uint32_t n_ext = min(*L.n_ext, L.ext_cap);
+    // two-ended ext (RefineLaunch::counter_hi): wave r < n_lo takes ext[r],
+    // the next n_hi waves ext[cap - 1 - (r - n_lo)] (a total above the cap is
+    // an overflow the host re-runs)
+    const uint32_t n_lo = min(*L.n_ext, L.ext_cap);
+    const uint32_t n_ext = L.n_ext_hi ? min(n_lo + min(*L.n_ext_hi, L.ext_cap), L.ext_cap) : n_lo;
     // one group of 4 extrema per workgroup; the grid covers the bound, the
     // device count ends it early (block-uniform).  (Round 5: the groups
     // remapped to contiguous ranges per XCD measured slower, together with
@@ -290,7 +312,7 @@ __global__ __launch_bounds__(256, SIFT_ORIENT_MIN_WAVES) void k_orient(const Ori
         float kp_scale = 0.f, kp_x = 0.f, kp_y = 0.f, osf = 1.f;
         float acc = 0.0f;  // lane k < 36: raw_hist[k + 2]
         if (active) {
-            e = L.ext[r];
+            e = L.ext[r < n_lo ? r : L.ext_cap - 1 - (r - n_lo)];
             W = L.ow[e.octave];
             H = L.oh[e.octave];
             pitch = L.opitch[e.octave];

@@ -752,10 +752,11 @@ int launch_detection(sift_mi_ctx* c, int si, uint32_t f0, uint32_t nf, int o0, i
                      uint64_t* cand = nullptr, uint32_t* counter = nullptr, uint32_t cap = 0);
 // refinement of the candidates (cand, *n_cand <= cand_cap) into ext (*counter,
 // cap), and orientation of those extrema into the slot's keypoints
+// (counter_hi / n_ext_hi: two-ended extremum append, RefineLaunch::counter_hi)
 int launch_refine_stage(sift_mi_ctx* c, int si, const uint64_t* cand, const uint32_t* n_cand, uint32_t cand_cap,
-                        ExtRec* ext, uint32_t* counter, uint32_t cap, hipStream_t st);
+                        ExtRec* ext, uint32_t* counter, uint32_t cap, hipStream_t st, uint32_t* counter_hi = nullptr);
 int launch_orient_stage(sift_mi_ctx* c, int si, const ExtRec* ext, const uint32_t* n_ext, uint32_t ext_cap,
-                        uint32_t kp_cap, hipStream_t st);
+                        uint32_t kp_cap, hipStream_t st, const uint32_t* n_ext_hi = nullptr);
 
 // Row bands with a restricted pyramid: rows a refined keypoint may drift from
 // its detection row and still be exact without a re-run, and the rows its
@@ -785,7 +786,8 @@ constexpr int kBandDrift = 24, kBandPatch = 41;
 // cand_slot >= 0 (the keypoint stages follow): octaves whose blur 5 and
 // detection run as one pass (k_blur_detect) append their candidates to that
 // slot's buffer from here, whatever detect_slot is (Slot::fused_mask).
-constexpr int kTailWords = 3;        // Slot counters after the per-frame plan: cand_b, ext_b counts, tail error
+constexpr int kTailWords = 4;        // Slot counters after the per-frame plan: cand_b, ext_b counts, tail error,
+                                     // the two-ended ext's back count (PathOpts::large_first)
 void flush_chunk_init(sift_mi_ctx* c, int si);
 
 int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_pitch, size_t row_stride,
@@ -1115,11 +1117,14 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
             uint32_t* cnt = S.counters.p;
             uint32_t* cb = cnt + 4 + 2 * S.m;
             CHK(launch_detection(c, detect_slot, f0, nf, 0, o_tail, aux));
-            CHK(launch_refine_stage(c, detect_slot, S.cand.p, cnt + 0, S.bc, S.ext.p, cnt + 1, S.be, aux));
+            // (PathOpts::large_first: two-ended extremum append, large
+            // descriptor windows first)
+            uint32_t* ext_hi = po.large_first ? cb + 3 : nullptr;
+            CHK(launch_refine_stage(c, detect_slot, S.cand.p, cnt + 0, S.bc, S.ext.p, cnt + 1, S.be, aux, ext_hi));
             // the aux orientation signals the join event itself (no marker on
             // the aux stream's critical path; not under stream capture)
             if (ov && o_tail > 0 && ext_events) set_launch_done_event(c->oct_ev[lane][kTailMaxOct]);
-            const int rc_o = launch_orient_stage(c, detect_slot, S.ext.p, cnt + 1, S.be, S.bk, aux);
+            const int rc_o = launch_orient_stage(c, detect_slot, S.ext.p, cnt + 1, S.be, S.bk, aux, ext_hi);
             aux_done_signalled = ov && o_tail > 0 && ext_events && !launch_done_pending();
             set_launch_done_event(nullptr);
             CHK(rc_o);
@@ -1318,9 +1323,10 @@ int launch_detection(sift_mi_ctx* c, int si, uint32_t f0, uint32_t nf, int o0, i
 }
 
 int launch_refine_stage(sift_mi_ctx* c, int si, const uint64_t* cand, const uint32_t* n_cand, uint32_t cand_cap,
-                        ExtRec* ext, uint32_t* counter, uint32_t cap, hipStream_t st) {
+                        ExtRec* ext, uint32_t* counter, uint32_t cap, hipStream_t st, uint32_t* counter_hi) {
     Plan& p = c->plan;
     RefineLaunch R{};
+    R.counter_hi = counter_hi;
     R.cand = cand;
     R.n_cand = n_cand;
     R.cand_cap = cand_cap;
@@ -1349,11 +1355,12 @@ int launch_refine_stage(sift_mi_ctx* c, int si, const uint64_t* cand, const uint
 }
 
 int launch_orient_stage(sift_mi_ctx* c, int si, const ExtRec* ext, const uint32_t* n_ext, uint32_t ext_cap,
-                        uint32_t kp_cap, hipStream_t st) {
+                        uint32_t kp_cap, hipStream_t st, const uint32_t* n_ext_hi) {
     Plan& p = c->plan;
     Slot& S = c->slot[si];
     OrientLaunch O{};
     O.ext = ext;
+    O.n_ext_hi = n_ext_hi;
     O.n_ext = n_ext;
     O.ext_cap = ext_cap;
     O.gauss = p.d_gauss[arena_of(c, si)].p;
@@ -1550,13 +1557,15 @@ int finalize_chunk(sift_mi_ctx* c, int si, size_t* offsets, bool only_chunk = fa
     const double fm = (double)m;
     // the tail octaves' region (Slot::early): its counts follow the frame plan
     const uint32_t hb0 = S.early ? h[4 + 2 * m] : 0, hb1 = S.early ? h[4 + 2 * m + 1] : 0;
+    // the main region's extrema (a two-ended append keeps its back count in the tail words)
+    const uint32_t h1 = h[1] + (S.early ? h[4 + 2 * m + 3] : 0);
     if (h[4 + 2 * m + 2])  // a split tail's side workgroup gave up waiting (never expected)
         return fail(SIFT_MI_EHIP, "k_octave_tail: a side workgroup timed out waiting for its chain");
     c->pf_cand = std::max(c->pf_cand, (h[0] + hb0) / fm);
-    c->pf_ext = std::max(c->pf_ext, (h[1] + hb1) / fm);
+    c->pf_ext = std::max(c->pf_ext, (h1 + hb1) / fm);
     c->pf_kp = std::max(c->pf_kp, h[2] / fm);
     c->pf_cand_b = std::max(c->pf_cand_b, std::max(hb0, hb1) / fm);
-    if (h[0] > S.bc || h[1] > S.be || h[2] > S.bk || hb0 > S.bcb || hb1 > S.bcb) {
+    if (h[0] > S.bc || h1 > S.be || h[2] > S.bk || hb0 > S.bcb || hb1 > S.bcb) {
         c->stats.stage_reruns++;
         return 1;
     }
@@ -1617,7 +1626,7 @@ int finalize_chunk(sift_mi_ctx* c, int si, size_t* offsets, bool only_chunk = fa
         }
     }
     c->n_result = base + n_out;
-    c->stats.extrema += h[1] + hb1;
+    c->stats.extrema += h1 + hb1;
     c->stats.keypoints += n_out;
     c->stats.frames += m;
     return 0;
@@ -2116,6 +2125,7 @@ int sift_mi_set_path_option(sift_mi_ctx* c, int option, int value) {
         case SIFT_MI_PATH_BAND_DRIFT: if (value < -kBandPatch || value > kBandDrift) break; o.band_drift = value; return 0;
         case SIFT_MI_PATH_BOUND_SHRINK: if (value < 1) break; o.bound_shrink = value; return 0;
         case SIFT_MI_PATH_TAIL_SPLIT: if (value < 0 || value > 2) break; o.tail_split = value; return 0;
+        case SIFT_MI_PATH_LARGE_FIRST: if (!b) break; o.large_first = value; return 0;
         default: return fail(SIFT_MI_EINVAL, "unknown path option");
     }
     return fail(SIFT_MI_EINVAL, "path option value out of range");

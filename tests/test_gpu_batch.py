@@ -361,7 +361,7 @@ def test_single_chunk_graph_replay(pkg, ctx, oracle, fetch):
     c.close()
 
 
-@pytest.mark.parametrize("knob,on", [("early", 1), ("desc_first", 1), ("tail_split", 1)])
+@pytest.mark.parametrize("knob,on", [("early", 1), ("desc_first", 1), ("tail_split", 1), ("large_first", 1)])
 @pytest.mark.parametrize("profile", [0, 1])
 def test_single_chunk_paths_equal(pkg, knob, on, profile):
     """One-chunk calls take latency paths of their own -- the octaves below

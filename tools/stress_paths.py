@@ -25,7 +25,7 @@ def main():
     for r in range(a.rounds):
         for prof in (pkg.OpenCVProcessing, pkg.ImageprocProcessing):
             res = {}
-            for knob, val in (("tail_split", 1), ("tail_split", 0), ("early", 0)):
+            for knob, val in (("tail_split", 1), ("tail_split", 0), ("early", 0), ("large_first", 1)):
                 c = pkg.Context(0, prof)
                 c.set_path_option(knob, val)
                 res[(knob, val)] = [c.sift(f) for f in frames for _ in range(2)]
