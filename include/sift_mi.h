@@ -183,8 +183,10 @@ typedef enum {
                                       bound-overflow re-run) */
     SIFT_MI_PATH_TAIL_SPLIT = 10,  /* the small octaves' kernel as a chain and a side workgroup per frame:
                                       1 for chunks of <= 8 frames, 2 always, 0 never (default 0) */
-    SIFT_MI_PATH_LARGE_FIRST = 11  /* 0: one-chunk calls orient the extrema in refinement order, not
+    SIFT_MI_PATH_LARGE_FIRST = 11, /* 0: one-chunk calls orient the extrema in refinement order, not
                                       those with large windows first (default 1) */
+    SIFT_MI_PATH_ONESWEEP = 12     /* the emission-order sorts with rocprim's Onesweep radix sort: 1 at
+                                      every size, 0 never, 2 from 131072 keys (default 2) */
 } sift_mi_path_option;
 int sift_mi_set_path_option(sift_mi_ctx* ctx, int option, int value);
 

@@ -1430,11 +1430,12 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
     const int img_bits = img_bits_for(m);
     const int end_bit = kKeyImgShift + img_bits;
     const uint64_t pad = (end_bit >= 64) ? ~0ull : ((1ull << end_bit) - 1);
-    size_t tmp = sort_pairs_u64(nullptr, 0, S.keys_a.p, S.keys_b.p, S.vals_a.p, S.vals_b.p, B.bk, end_bit, os);
+    const bool onesweep = c->opts.onesweep == 1 || (c->opts.onesweep == 2 && B.bk >= kOnesweepMinKeys);
+    size_t tmp = sort_pairs_u64(nullptr, 0, S.keys_a.p, S.keys_b.p, S.vals_a.p, S.vals_b.p, B.bk, end_bit, os, onesweep);
     const int rb = 32 + img_bits;
     const uint64_t rpad = (1ull << rb) - 1;
     if (limit >= 0)
-        tmp = std::max(tmp, sort_pairs_u64(nullptr, 0, S.keys_a.p, S.keys_b.p, S.vals_a.p, S.fin.p, B.bk, rb, os));
+        tmp = std::max(tmp, sort_pairs_u64(nullptr, 0, S.keys_a.p, S.keys_b.p, S.vals_a.p, S.fin.p, B.bk, rb, os, onesweep));
     if (!tmp) return fail(SIFT_MI_EHIP, "radix sort sizing failed");
     if (tmp > S.sort_tmp.cap) {
         HIPCHK(hipStreamSynchronize(st));
@@ -1443,7 +1444,7 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
     }
     launch_make_sort_keys(S.kp.p, cnt + 2, B.bk, pad, S.keys_a.p, S.vals_a.p, os);
     if (!sort_pairs_u64(S.sort_tmp.p, S.sort_tmp.cap, S.keys_a.p, S.keys_b.p, S.vals_a.p, S.vals_b.p, B.bk,
-                        end_bit, os))
+                        end_bit, os, onesweep))
         return fail(SIFT_MI_EHIP, "radix sort failed");
     launch_frame_starts(S.keys_b.p, cnt + 2, B.bk, starts, os);
     // features_limit (src/lib.rs:156-161): per-frame plan on the device
@@ -1458,7 +1459,7 @@ int enqueue_keypoints(sift_mi_ctx* c, int si, uint32_t m, int64_t limit, uint32_
         // stable sort: response-descending within each frame, emission order on ties
         launch_make_resp_keys(S.kp.p, order, cnt + 2, B.bk, 0, rpad, S.keys_a.p, S.vals_a.p, os);
         if (!sort_pairs_u64(S.sort_tmp.p, S.sort_tmp.cap, S.keys_a.p, S.keys_b.p, S.vals_a.p, S.fin.p, B.bk, rb,
-                            os))
+                            os, onesweep))
             return fail(SIFT_MI_EHIP, "response sort failed");
         launch_select(order, S.fin.p, S.seg_off.p, S.out_off.p, S.use_resp.p, (int)m, cnt + 3, B.bk, S.vals_a.p,
                       os);
@@ -2126,6 +2127,7 @@ int sift_mi_set_path_option(sift_mi_ctx* c, int option, int value) {
         case SIFT_MI_PATH_BOUND_SHRINK: if (value < 1) break; o.bound_shrink = value; return 0;
         case SIFT_MI_PATH_TAIL_SPLIT: if (value < 0 || value > 2) break; o.tail_split = value; return 0;
         case SIFT_MI_PATH_LARGE_FIRST: if (!b) break; o.large_first = value; return 0;
+        case SIFT_MI_PATH_ONESWEEP: if (value < 0 || value > 2) break; o.onesweep = value; return 0;
         default: return fail(SIFT_MI_EINVAL, "unknown path option");
     }
     return fail(SIFT_MI_EINVAL, "path option value out of range");

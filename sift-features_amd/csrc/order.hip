@@ -8,6 +8,7 @@
 // exceeds the limit are re-sorted by response, descending (src/lib.rs:156-161,
 // stable w.r.t. emission order for ties) and truncated.
 #include <hipcub/hipcub.hpp>
+#include <rocprim/device/device_radix_sort.hpp>
 
 #include <algorithm>
 
@@ -17,12 +18,21 @@
 
 namespace siftmi {
 
+// onesweep: rocprim's Onesweep radix sort for every size above one block
+// (merge_sort_limit 0); otherwise the library default, which takes a block
+// radix sort of 1024-key tiles plus merge passes up to 1 M keys
 size_t sort_pairs_u64(void* temp, size_t temp_bytes, const uint64_t* kin, uint64_t* kout, const uint32_t* vin,
-                      uint32_t* vout, uint32_t n, int end_bit, hipStream_t st) {
+                      uint32_t* vout, uint32_t n, int end_bit, hipStream_t st, bool onesweep) {
     size_t bytes = temp_bytes;
-    if (hipcub::DeviceRadixSort::SortPairs(temp, bytes, kin, kout, vin, vout, (int)n, 0, end_bit, st) != hipSuccess)
-        return 0;
-    return bytes;
+    hipError_t e;
+    if (onesweep) {
+        using Cfg = rocprim::radix_sort_config<rocprim::default_config, rocprim::default_config,
+                                               rocprim::default_config, 0>;
+        e = rocprim::radix_sort_pairs<Cfg>(temp, bytes, kin, kout, vin, vout, n, 0u, (unsigned)end_bit, st);
+    } else {
+        e = hipcub::DeviceRadixSort::SortPairs(temp, bytes, kin, kout, vin, vout, (int)n, 0, end_bit, st);
+    }
+    return e == hipSuccess ? bytes : 0;
 }
 
 // Per-chunk counters in one launch (instead of three memsets): cnt[0..3] = 0,

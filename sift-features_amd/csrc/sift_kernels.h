@@ -42,6 +42,11 @@ enum : int { kProfileOpenCV = 0, kProfileImageproc = 1 };
 // live in the context (no process-wide state, nothing read from the
 // environment).
 constexpr uint32_t kTailSplitMaxFrames = 8;
+// Onesweep from this many sort keys (PathOpts::onesweep = 2): below it rocprim's
+// block sort + merge path is faster (one 1080p frame, ~12 k keys: 0.578 vs
+// 0.71 ms per call; 128 x 1080p in 64-frame chunks: 31.32 / 30.90 vs 31.54 /
+// 30.96 ms per call with Onesweep)
+constexpr uint32_t kOnesweepMinKeys = 1u << 17;
 
 struct PathOpts {
     int tile_blur = 0;     // 1: one-tile-per-workgroup blurs everywhere (no strip / pair kernels)
@@ -58,6 +63,8 @@ struct PathOpts {
                            // <= kTailSplitMaxFrames frames, 2 always, 0 never (one workgroup per frame:
                            // faster in every case measured)
     int large_first = 1;   // one-chunk early path: two-ended extremum append (RefineLaunch::counter_hi)
+    int onesweep = 2;      // emission-order sorts with rocprim's Onesweep: 1 always, 0 never, 2 for
+                           // bounds >= kOnesweepMinKeys (batch chunks; one frame: the library default)
 };
 
 // Image planes are row-pitched: element (y, x) at plane[y * pitch + x].
@@ -268,7 +275,8 @@ void launch_orient(const OrientLaunch& L, hipStream_t st);
 // order.hip
 // keys/vals for the emission-order sort; returns temp bytes when temp == null.
 size_t sort_pairs_u64(void* temp, size_t temp_bytes, const uint64_t* kin, uint64_t* kout, const uint32_t* vin,
-                      uint32_t* vout, uint32_t n, int end_bit, hipStream_t st);
+                      uint32_t* vout, uint32_t n, int end_bit, hipStream_t st,
+                      bool onesweep = false);
 // keys[i] = emission key of kp i for i < min(*n, bound); keys beyond are
 // padded with `pad` (sorts last); vals[i] = i
 void launch_chunk_init(uint32_t* cnt, int m, int work_words, hipStream_t st);

@@ -361,7 +361,8 @@ def test_single_chunk_graph_replay(pkg, ctx, oracle, fetch):
     c.close()
 
 
-@pytest.mark.parametrize("knob,on", [("early", 1), ("desc_first", 1), ("tail_split", 1), ("large_first", 1)])
+@pytest.mark.parametrize("knob,on", [("early", 1), ("desc_first", 1), ("tail_split", 1), ("large_first", 1),
+                                     ("onesweep", 1)])
 @pytest.mark.parametrize("profile", [0, 1])
 def test_single_chunk_paths_equal(pkg, knob, on, profile):
     """One-chunk calls take latency paths of their own -- the octaves below
@@ -383,6 +384,23 @@ def test_single_chunk_paths_equal(pkg, knob, on, profile):
     got = [c.sift(f) for f in frames for _ in range(2)]
     c.set_path_option(knob, 0)
     ref = [c.sift(f) for f in frames for _ in range(2)]
+    c.close()
+    for a, b in zip(got, ref):
+        assert a == b
+        assert np.array_equal(a.keys, b.keys)
+
+
+@pytest.mark.parametrize("limit", [None, 40])
+def test_batch_onesweep_equal(pkg, ctx, limit):
+    """Path option onesweep = 1 (rocprim's Onesweep radix sort for the
+    emission-order and response sorts at every size) gives the same results
+    as the default sort path, chunked batches and features_limit included."""
+    fr = _frames()
+    ref = ctx.sift_batch(fr, features_limit=limit)
+    c = pkg.Context(0)
+    c.set_chunk(2)
+    c.set_path_option("onesweep", 1)
+    got = c.sift_batch(fr, features_limit=limit)
     c.close()
     for a, b in zip(got, ref):
         assert a == b
