@@ -43,10 +43,11 @@ enum : int { kProfileOpenCV = 0, kProfileImageproc = 1 };
 // environment).
 constexpr uint32_t kTailSplitMaxFrames = 8;
 // Onesweep from this many sort keys (PathOpts::onesweep = 2): below it rocprim's
-// block sort + merge path is faster (one 1080p frame, ~12 k keys: 0.578 vs
-// 0.71 ms per call; 128 x 1080p in 64-frame chunks: 31.32 / 30.90 vs 31.54 /
-// 30.96 ms per call with Onesweep)
-constexpr uint32_t kOnesweepMinKeys = 1u << 17;
+// block sort + merge path is faster.  One 1080p frame (~12 k keys): 0.578 vs
+// 0.71 ms per call with Onesweep; 256 x VGA (128-frame chunks, ~206 k keys):
+// 10.08-10.29 vs 9.93-10.15 ms; 128 x 1080p (64-frame chunks, ~715 k keys):
+// 31.69-31.73 vs 31.68-31.89 ms (profiles/r05_batch35.log, r05_vga35.log)
+constexpr uint32_t kOnesweepMinKeys = 1u << 19;
 
 struct PathOpts {
     int tile_blur = 0;     // 1: one-tile-per-workgroup blurs everywhere (no strip / pair kernels)
