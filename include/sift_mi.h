@@ -186,7 +186,7 @@ typedef enum {
     SIFT_MI_PATH_LARGE_FIRST = 11, /* 0: one-chunk calls orient the extrema in refinement order, not
                                       those with large windows first (default 1) */
     SIFT_MI_PATH_ONESWEEP = 12     /* the emission-order sorts with rocprim's Onesweep radix sort: 1 at
-                                      every size, 0 never, 2 from 524288 keys (default 2) */
+                                      every size, 0 never, 2 from 524288 keys (default 0) */
 } sift_mi_path_option;
 int sift_mi_set_path_option(sift_mi_ctx* ctx, int option, int value);
 

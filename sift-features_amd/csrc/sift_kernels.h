@@ -64,8 +64,8 @@ struct PathOpts {
                            // <= kTailSplitMaxFrames frames, 2 always, 0 never (one workgroup per frame:
                            // faster in every case measured)
     int large_first = 1;   // one-chunk early path: two-ended extremum append (RefineLaunch::counter_hi)
-    int onesweep = 2;      // emission-order sorts with rocprim's Onesweep: 1 always, 0 never, 2 for
-                           // bounds >= kOnesweepMinKeys (batch chunks; one frame: the library default)
+    int onesweep = 0;      // emission-order sorts with rocprim's Onesweep: 1 always, 0 never (the
+                           // library default path), 2 for bounds >= kOnesweepMinKeys
 };
 
 // Image planes are row-pitched: element (y, x) at plane[y * pitch + x].

@@ -269,7 +269,7 @@ class Context:
                     "fused_detect": (4, 1), "early": (5, 1), "desc_first": (6, 1), "graph": (7, 0),
                     "band_drift": (8, 24), "bound_shrink": (9, 1), "tail_split": (10, 0),
                     "large_first": (11, 1),
-                    "onesweep": (12, 2)}
+                    "onesweep": (12, 0)}
 
     def set_path_option(self, name, value):
         """One kernel-path switch (sift_mi_set_path_option), e.g.
