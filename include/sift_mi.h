@@ -181,12 +181,16 @@ typedef enum {
                                       smaller values force the whole-pyramid re-run) */
     SIFT_MI_PATH_BOUND_SHRINK = 9, /* k >= 1: first-chunk stage bounds / k (default 1; > 1 forces the
                                       bound-overflow re-run) */
-    SIFT_MI_PATH_TAIL_SPLIT = 10,  /* the small octaves' kernel as a chain and a side workgroup per frame:
-                                      1 for chunks of <= 8 frames, 2 always, 0 never (default 0) */
+    /* 10: retired (the round-5 split tail kernel, removed in round 6); setting it returns
+       SIFT_MI_EINVAL */
     SIFT_MI_PATH_LARGE_FIRST = 11, /* 0: one-chunk calls orient the extrema in refinement order, not
                                       those with large windows first (default 1) */
-    SIFT_MI_PATH_ONESWEEP = 12     /* the emission-order sorts with rocprim's Onesweep radix sort: 1 at
+    SIFT_MI_PATH_ONESWEEP = 12,    /* the emission-order sorts with rocprim's Onesweep radix sort: 1 at
                                       every size, 0 never, 2 from 524288 keys (default 0) */
+    SIFT_MI_PATH_BD_PAIR = 13,     /* the fused blur 5 + extremum scan with two column strips per lane
+                                      (packed f32): 1 on, 0 the one-column kernel */
+    SIFT_MI_PATH_BD_WAVES = 14     /* the pair kernel's fewest waves per launch when choosing its row
+                                      segments, 1024..65536 */
 } sift_mi_path_option;
 int sift_mi_set_path_option(sift_mi_ctx* ctx, int option, int value);
 

@@ -422,7 +422,7 @@ struct Plan {
 struct Slot {
     // [0] candidates [1] extrema [2] keypoints [3] outputs [4..4+F) frame starts
     // [4+F..4+2F) per-frame outputs [4+2F..4+2F+kTailWords) the tail
-    // region's counters (early) and the split tail kernel's error word
+    // region's counters (early)
     // [4+2F+kTailWords..+kDescWorkWords) descriptor work queues
     DevBuf<uint32_t> counters;
     PinBuf<uint32_t> h_counts;
@@ -500,8 +500,6 @@ struct sift_mi_ctx {
     hipStream_t own2 = nullptr;    // compute stream of pipeline lane 1 (lane 0 runs on `stream`)
     hipStream_t aux[2] = {};       // per lane: blurs 4, 5 of each octave beside the next octave
     hipStream_t aux2 = nullptr;    // lane 0: blurs 4, 5 of octaves >= 1 while octave 0's fused pass runs
-    DevBuf<uint32_t> tail_flags[2];  // per lane: the split tail kernel's G_3 hand-over flags
-    uint32_t tail_epoch = 0;
     hipEvent_t aux2_join = nullptr;
     hipStream_t dec = nullptr;     // JPEG batch decoding: a high-priority stream (its own hardware queue)
     hipEvent_t oct_ev[2][kTailMaxOct + 1] = {};  // per lane: octave o's G_3 done / aux joined
@@ -786,7 +784,7 @@ constexpr int kBandDrift = 24, kBandPatch = 41;
 // cand_slot >= 0 (the keypoint stages follow): octaves whose blur 5 and
 // detection run as one pass (k_blur_detect) append their candidates to that
 // slot's buffer from here, whatever detect_slot is (Slot::fused_mask).
-constexpr int kTailWords = 4;        // Slot counters after the per-frame plan: cand_b, ext_b counts, tail error,
+constexpr int kTailWords = 4;        // Slot counters after the per-frame plan: cand_b, ext_b counts, (unused),
                                      // the two-ended ext's back count (PathOpts::large_first)
 void flush_chunk_init(sift_mi_ctx* c, int si);
 
@@ -839,7 +837,7 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
     // the small octaves from o_tail on: one k_octave_tail launch
     // (PathOpts::tail = 0: per-blur launches for every octave)
     const PathOpts& po = c->opts;
-    const int tail_slot = cand_slot;  // the chunk's slot (its counters hold the split tail's error word)
+    const int tail_slot = cand_slot;  // the chunk's slot
     int o_tail = p.n_oct;
     if (po.tail && p.n_oct <= kTailMaxOct) o_tail = tail_octave_start(p.ow.data(), p.oh.data(), p.n_oct, p.oct_r);
     uint64_t bytes = p.algo_bytes_per_frame;  // per frame, SURVEY.md 8(d)
@@ -1072,26 +1070,6 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
             T.n_oct = p.n_oct;
             T.n_img = (int)nf;
             T.profile = p.profile;
-            // split chain / side workgroups (not under stream capture: the
-            // epoch is a kernel argument, a replay would see the last one's
-            // flags; not for row bands' restricted passes either -- whole
-            // octaves either way, so simply both paths exact)
-            // the split pays on the latency path (one frame: 3 + 2 blurs per
-            // octave in parallel); on a batch chunk the one-workgroup kernel
-            // is faster (256 x 640x480: 10.0-10.2 vs 10.65 ms per call; the
-            // side workgroups hold a CU's LDS each while they wait)
-            const bool split = po.tail_split == 2 || (po.tail_split == 1 && nf <= kTailSplitMaxFrames);
-            if (split && ext_events && tail_slot >= 0) {
-                const size_t need = (size_t)c->plan.chunk * kTailMaxOct;
-                if (c->tail_flags[lane].cap < need) {
-                    CHK(c->tail_flags[lane].ensure(need));
-                    HIPCHK(hipMemsetAsync(c->tail_flags[lane].p, 0, need * sizeof(uint32_t), sm));
-                }
-                T.flags = c->tail_flags[lane].p + (size_t)f0 * kTailMaxOct;
-                T.error = c->slot[tail_slot].counters.p + 4 + 2 * c->slot[tail_slot].m + 2;
-                T.epoch = ++c->tail_epoch;
-                if (T.epoch == 0) T.epoch = ++c->tail_epoch;  // 0 is the flags' initial value
-            }
             for (int s = 1; s < kImagesPerOctave; s++) {
                 T.r[s] = p.oct_r[s];
                 T.taps[s] = p.oct_taps[s];
@@ -1560,8 +1538,6 @@ int finalize_chunk(sift_mi_ctx* c, int si, size_t* offsets, bool only_chunk = fa
     const uint32_t hb0 = S.early ? h[4 + 2 * m] : 0, hb1 = S.early ? h[4 + 2 * m + 1] : 0;
     // the main region's extrema (a two-ended append keeps its back count in the tail words)
     const uint32_t h1 = h[1] + (S.early ? h[4 + 2 * m + 3] : 0);
-    if (h[4 + 2 * m + 2])  // a split tail's side workgroup gave up waiting (never expected)
-        return fail(SIFT_MI_EHIP, "k_octave_tail: a side workgroup timed out waiting for its chain");
     c->pf_cand = std::max(c->pf_cand, (h[0] + hb0) / fm);
     c->pf_ext = std::max(c->pf_ext, (h1 + hb1) / fm);
     c->pf_kp = std::max(c->pf_kp, h[2] / fm);
@@ -2031,7 +2007,6 @@ void sift_mi_destroy(sift_mi_ctx* c) {
     for (auto& lane : c->oct_ev)
         for (auto& e : lane)
             if (e) (void)hipEventDestroy(e);
-    for (auto& f : c->tail_flags) f.release();
     c->r_kp.release();
     c->r_desc.release();
     c->r_key.release();
@@ -2125,9 +2100,10 @@ int sift_mi_set_path_option(sift_mi_ctx* c, int option, int value) {
         case SIFT_MI_PATH_GRAPH: if (!b) break; o.graph = value; return 0;
         case SIFT_MI_PATH_BAND_DRIFT: if (value < -kBandPatch || value > kBandDrift) break; o.band_drift = value; return 0;
         case SIFT_MI_PATH_BOUND_SHRINK: if (value < 1) break; o.bound_shrink = value; return 0;
-        case SIFT_MI_PATH_TAIL_SPLIT: if (value < 0 || value > 2) break; o.tail_split = value; return 0;
         case SIFT_MI_PATH_LARGE_FIRST: if (!b) break; o.large_first = value; return 0;
         case SIFT_MI_PATH_ONESWEEP: if (value < 0 || value > 2) break; o.onesweep = value; return 0;
+        case SIFT_MI_PATH_BD_PAIR: if (!b) break; o.bd_pair = value; return 0;
+        case SIFT_MI_PATH_BD_WAVES: if (value < 1024 || value > 65536) break; o.bd_waves = value; return 0;
         default: return fail(SIFT_MI_EINVAL, "unknown path option");
     }
     return fail(SIFT_MI_EINVAL, "path option value out of range");

@@ -2147,25 +2147,13 @@ __device__ __forceinline__ void tail_blur(float* __restrict__ A, float* __restri
     }
 }
 
-// SPLIT: workgroup 2f is frame f's chain -- blurs 1-3 of each tail octave,
-// the next octave's G_0 from G_3 -- and 2f + 1 its side: blurs 4, 5 of each
-// octave, which need only that octave's G_3.  The chain publishes G_3 (its
-// global stores, then a device-scope release of flags[f][o] = epoch), the
-// side acquires the flag and reads G_3 back (L2-resident).  One 1080p frame:
-// octaves 5-9 as 3 + 2 blurs in parallel instead of 5 in a row.  The side
-// waits only for a workgroup dispatched before it (lower index; and with
-// workgroups dealt round robin over the 8 XCDs, chains and sides never share
-// an XCD), and gives up after ~1 s (error flag, reported by the host).
-template <int P, bool SPLIT>
+template <int P>
 __global__ __launch_bounds__(1024) void k_octave_tail(const TailLaunch L) {
     __shared__ float lds[kTailLdsFloats];
-    __shared__ uint32_t gave_up;
     const int tid = threadIdx.x;
-    const int b = SPLIT ? (int)(blockIdx.x >> 1) : (int)blockIdx.x;
-    const bool side = SPLIT && (blockIdx.x & 1);
+    const int b = (int)blockIdx.x;
     int Rm = 0;
     for (int s = 1; s < kImagesPerOctave; s++) Rm = max(Rm, L.r[s]);
-    if (SPLIT && tid == 0) gave_up = 0;
     for (int o = L.o0; o < L.n_oct; o++) {
         const int W = L.ow[o], H = L.oh[o], pitch = L.pitch[o], PA = tail_pa(W, Rm);
         float* A = lds;                         // G_{s-1}
@@ -2178,45 +2166,6 @@ __global__ __launch_bounds__(1024) void k_octave_tail(const TailLaunch L) {
         const int wn = has_next ? L.ow[o + 1] : 0, hn = has_next ? L.oh[o + 1] : 0;
         float* gn = has_next ? L.gauss[o + 1] + (size_t)b * L.gstride[o + 1] : nullptr;
         const int pn = has_next ? L.pitch[o + 1] : 0;
-        uint32_t* flag = SPLIT ? L.flags + (size_t)b * kTailMaxOct + o : nullptr;
-        if (side) {
-            // wait for the chain's G_3 of this octave, then read it into A
-            if (tid == 0) {
-                uint32_t spins = 0;
-                // relaxed polls (an acquire load would invalidate this XCD's
-                // L2 on every poll); the acquire fence below follows the last
-                while (__hip_atomic_load(flag, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) != L.epoch) {
-                    __builtin_amdgcn_s_sleep(2);
-                    if (++spins == (1u << 24)) {  // ~1 s: give up (the host reports it)
-                        gave_up = 1;
-                        atomicOr(L.error, 1u);
-                        break;
-                    }
-                }
-                // one invalidate of this CU's L1 / XCD's L2 for the whole
-                // workgroup (no stale G_3 lines; the barrier below orders
-                // every wave's reads after it)
-                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "agent");
-            }
-            __syncthreads();
-            if (gave_up) return;
-            const float* g3 = g + 3 * plane;
-            for (int y = tid >> 6; y < H; y += 16)
-                for (int x = tid & 63; x < W; x += 64) A[y * PA + Rm + x] = g3[(size_t)y * pitch + x];
-            __syncthreads();
-            tail_fill_cols<P>(A, W, H, Rm, L.r[4]);
-            __syncthreads();
-#pragma unroll 1
-            for (int s = 4; s < kImagesPerOctave; s++) {
-                tail_blur<P>(A, T, B, L.taps[s], L.r[s], s + 1 < kImagesPerOctave ? L.r[s + 1] : 0, Rm, W, H,
-                             g + s * plane, pitch, false, N, gn, wn, hn, pn);
-                float* t = A;
-                A = B;
-                B = t;
-            }
-            __syncthreads();  // A / B are reloaded for the next octave
-            continue;
-        }
         // G_0: from HBM (first tail octave) or from the previous octave's N
         // (which overlaps this octave's A / B: copy through registers)
         if (o == L.o0) {
@@ -2244,27 +2193,13 @@ __global__ __launch_bounds__(1024) void k_octave_tail(const TailLaunch L) {
         __syncthreads();
         tail_fill_cols<P>(A, W, H, Rm, L.r[1]);
         __syncthreads();
-        constexpr int s_end = SPLIT ? 4 : kImagesPerOctave;  // the chain stops at G_3
 #pragma unroll 1
-        for (int s = 1; s < s_end; s++) {
+        for (int s = 1; s < kImagesPerOctave; s++) {
             tail_blur<P>(A, T, B, L.taps[s], L.r[s], s + 1 < kImagesPerOctave ? L.r[s + 1] : 0, Rm, W, H,
                          g + s * plane, pitch, s == 3 && has_next, N, gn, wn, hn, pn);
             float* t = A;
             A = B;
             B = t;
-        }
-        if constexpr (SPLIT) {
-            // publish G_3: every wave's stores visible device-wide (an
-            // agent-scope release per wave: its own stores complete, the L2
-            // written back for a reader on another XCD), then the flag.
-            // (A variant with a raw s_waitcnt vmcnt(0) per wave and a single
-            // release by thread 0 -- 0.599 vs 0.604 ms per 1080p frame -- gave
-            // a wrong count once in ~10 runs of test_single_chunk_paths_equal:
-            // the builtin wait does not order the compiler's stores, so the
-            // one write-back could miss another wave's G_3 rows.)
-            __builtin_amdgcn_fence(__ATOMIC_RELEASE, "agent");
-            __syncthreads();
-            if (tid == 0) __hip_atomic_store(flag, L.epoch, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
         }
     }
 }
@@ -2287,17 +2222,10 @@ int tail_octave_start(const int* ow, const int* oh, int n_oct, const int* radii)
 
 void launch_octave_tail(const TailLaunch& L, hipStream_t st) {
     if (L.o0 >= L.n_oct || L.n_img <= 0) return;
-    if (L.flags) {
-        if (L.profile == kProfileImageproc)
-            klaunch(k_octave_tail<kProfileImageproc, true>, dim3(2 * L.n_img), dim3(1024), st, L);
-        else
-            klaunch(k_octave_tail<kProfileOpenCV, true>, dim3(2 * L.n_img), dim3(1024), st, L);
-        return;
-    }
     if (L.profile == kProfileImageproc)
-        klaunch(k_octave_tail<kProfileImageproc, false>, dim3(L.n_img), dim3(1024), st, L);
+        klaunch(k_octave_tail<kProfileImageproc>, dim3(L.n_img), dim3(1024), st, L);
     else
-        klaunch(k_octave_tail<kProfileOpenCV, false>, dim3(L.n_img), dim3(1024), st, L);
+        klaunch(k_octave_tail<kProfileOpenCV>, dim3(L.n_img), dim3(1024), st, L);
 }
 
 // ---------------------------------------------------------------------------

@@ -476,13 +476,266 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_BD_WPE
         if (gbase + i < L.cap) L.cand[gbase + i] = lcand[i];
 }
 
+// ---------------------------------------------------------------------------
+// k_blur_detect_pair: k_blur_detect with two column strips per lane.  Lane l
+// owns columns x0 = xb - 1 + l and x1 = x0 + 62, so a wave covers 124 output
+// columns (two 62-column halves, lanes 0 / 63 the halo of each).  The blur's
+// arithmetic runs on the pair {x0, x1} as packed f32 (v_pk_fma_f32 /
+// v_pk_mul_f32 / v_pk_add_f32: two lanes' worth per instruction, each half
+// the same IEEE operation sequence as the single-column kernel, so G_5 is
+// bit-identical); the ring row's taps for the pair are ring[t] and
+// ring[t + 62], one ds_read2_b32 into a register pair.  The DoG differences
+// are packed too; the extremum scan runs on each half (max / min have no
+// packed form).  The test is branch-free: each scale's verdict is a lane mask
+// (val == the 27-value max or min on its side of 0, val != 0), and the
+// per-lane key bits are formed only when some lane of the wave has one.
+// ---------------------------------------------------------------------------
+typedef float bd_f2 __attribute__((ext_vector_type(2)));
+constexpr int BD2_COLS = 2 * DR_COLS;  // output columns per wave
+// The G_4 ring holds a row as 90 column pairs {c, c + 62} (8-byte slots, the
+// taps of the two halves side by side): slot j of a lane's tap t is j = lane
+// + t, read with one ds_read_b64 straight into the register pair the packed
+// FMA takes.
+constexpr int BD2_SLOTS = DR_COLS + 2 + 2 * 13;  // 90: lanes 0..63 plus the 2R taps (R <= 13)
+
+// The scan of one half: three lane masks, scale s of row y - 1 at this
+// lane's column a candidate (rows prv, mid, cur of the five DoG planes).
+struct ScanMasks {
+    bool s1, s2, s3;
+};
+__device__ __forceinline__ ScanMasks extremum3_masks(const float (&prv)[kDogPerOctave], const float (&mid)[kDogPerOctave],
+                                                     const float (&cur)[kDogPerOctave], bool yin) {
+    float pmx[kDogPerOctave], pmn[kDogPerOctave];
+#pragma unroll
+    for (int p = 0; p < kDogPerOctave; p++) {
+        const float vx = fmaxf(fmaxf(prv[p], mid[p]), cur[p]);
+        const float vn = fminf(fminf(prv[p], mid[p]), cur[p]);
+        const float tx = fmaxf(dpp_from_left(vx), vx), tn = fminf(dpp_from_left(vn), vn);
+        pmx[p] = fmaxf(dpp_from_right(tx), tx);
+        pmn[p] = fminf(dpp_from_right(tn), tn);
+    }
+    bool ok[kScalesPerOctave];
+#pragma unroll
+    for (int s_in = 1; s_in <= kScalesPerOctave; s_in++) {
+        // threshold 0 (src/lib.rs:460): val != 0, then val >= the max (val > 0)
+        // or <= the min (val < 0).  The max / min include val, so >= / <= is
+        // equality with the side's extreme.
+        const float val = mid[s_in];
+        const float mx = fmaxf(fmaxf(pmx[s_in - 1], pmx[s_in]), pmx[s_in + 1]);
+        const float mn = fminf(fminf(pmn[s_in - 1], pmn[s_in]), pmn[s_in + 1]);
+        const float ext = val > 0.0f ? mx : mn;
+        ok[s_in - 1] = yin & (val != 0.0f) & (val == ext);
+    }
+    return ScanMasks{ok[0], ok[1], ok[2]};
+}
+
+#ifndef SIFT_BD2_WPE
+#define SIFT_BD2_WPE 1
+#endif
+template <int R, int P>
+__global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_BD2_WPE))) void k_blur_detect_pair(
+    const BlurDetectLaunch L) {
+    static_assert(R <= 13 && R + 3 <= BD_RING, "ring geometry");
+    __shared__ bd_f2 ring[4][BD_RING * BD2_SLOTS];
+    __shared__ uint64_t lcand[DR_LCAP];
+    __shared__ uint32_t lcount, gbase;
+    const int tid = threadIdx.x, lane = tid & 63, wave = __builtin_amdgcn_readfirstlane(tid >> 6);
+    const int W = L.W, H = L.H, pitch = L.pitch;
+    const uint32_t g = xcd_block_1d() * 4 + wave;  // strip index: frame-major, then row segment, then column
+    const uint32_t per = (uint32_t)(L.nsx * L.nsy);
+    const int b = (int)(g / per);
+    const uint32_t rem = g - (uint32_t)b * per;
+    const int sy = (int)(rem / (uint32_t)L.nsx), sx = (int)(rem % (uint32_t)L.nsx);
+    if (tid == 0) lcount = 0;
+    __syncthreads();
+    if (b < L.n_img) {
+        const size_t P_ = (size_t)pitch * H;
+        const int pb = (int)((uint32_t)P_ * 4u);  // plane bytes (6 planes < 2^31: launch_blur_detect)
+        // one resource over the frame's six planes; the plane is a scalar offset
+        const __amdgpu_buffer_rsrc_t rgs = uniform_rsrc(L.gauss + (size_t)b * L.img_stride, (uint32_t)(6 * pb));
+        const int xb = sx * BD2_COLS;
+        const int x0 = xb - 1 + lane, x1 = x0 + DR_COLS;  // this lane's two columns
+        const int vx0 = min(max(x0, 0), W - 1) * 4, vx1 = min(max(x1, 0), W - 1) * 4;
+        const bool edge = lane >= 1 && lane <= DR_COLS;
+        const bool xout0 = edge && x0 >= kImageBorder && x0 < W - kImageBorder;
+        const bool xout1 = edge && x1 >= kImageBorder && x1 < W - kImageBorder;
+        const uint32_t xbad0 = (edge && x0 < W) ? 0u : 0xfffffff0u, xbad1 = (edge && x1 < W) ? 0u : 0xfffffff0u;
+        const int ya = sy * L.seg, yb = min(ya + L.seg, H);
+        // ring slot j = {column xb - 1 - R + j, the same + 62}: lane l fills
+        // slot l and (l < 26) slot l + 64
+        const int ca = xb - 1 - R + lane;
+        const int va = bd_index<P>(ca, W) * 4, vb = bd_index<P>(ca + DR_COLS, W) * 4,
+                  vc = bd_index<P>(ca + 64, W) * 4, vd = bd_index<P>(ca + 64 + DR_COLS, W) * 4;
+        const bool second = lane < BD2_SLOTS - 64;
+        bd_f2* rg = ring[wave];
+        struct RowBuf {
+            bd_f2 s0, s1;  // ring slots lane, lane + 64
+            bd_f2 d[4];    // G_0..G_3 at the two columns
+        };
+        const int q0 = ya - 1 - R, q1 = yb + R;  // G_4 rows filtered: [q0, q1]
+        auto load = [&](int q, RowBuf& B, int par) {
+            const int qq = min(q, q1), r = qq - R;
+            const int so = bd_index<P>(qq, H) * pitch * 4 + 4 * pb;
+            B.s0 = bd_f2{buffer_load_f32(rgs, va, so), buffer_load_f32(rgs, vb, so)};
+            B.s1 = bd_f2{buffer_load_f32(rgs, vc, so), buffer_load_f32(rgs, vd, so)};
+            const int rr = r >= ya - 1 ? min(r, yb) : ya - 1 + par;
+            const int sd = min(max(rr, 0), H - 1) * pitch * 4;
+#pragma unroll
+            for (int p = 0; p < 4; p++)
+                B.d[p] = bd_f2{buffer_load_f32(rgs, vx0, sd + p * pb), buffer_load_f32(rgs, vx1, sd + p * pb)};
+        };
+        // row filter of G_4 row q at this lane's two columns
+        auto rowpass = [&](int q) -> bd_f2 {
+            const bd_f2* p = rg + (q & (BD_RING - 1)) * BD2_SLOTS + lane;
+            bd_f2 v[2 * R + 1];
+#pragma unroll
+            for (int t = 0; t <= 2 * R; t++) v[t] = p[t];
+            bd_f2 acc = v[0] * L.taps.k[R];
+#pragma unroll
+            for (int t = 1; t <= 2 * R; t++) {
+                const float kt = L.taps.k[t > R ? t - R : R - t];
+                if constexpr (P == kProfileOpenCV)
+                    acc = __builtin_elementwise_fma(v[t], (bd_f2)kt, acc);
+                else
+                    acc = acc + v[t] * kt;
+            }
+            return acc;
+        };
+        bd_f2 win[2 * R + 1];
+        float prv0[kDogPerOctave] = {}, mid0[kDogPerOctave] = {}, prv1[kDogPerOctave] = {}, mid1[kDogPerOctave] = {};
+        auto shift = [&]() {
+#pragma unroll
+            for (int j = 0; j < 2 * R; j++) win[j] = win[j + 1];
+        };
+        auto emit = [&](const ScanMasks& m, int y, int x) {
+            uint32_t ok3 = (uint32_t)m.s1 | ((uint32_t)m.s2 << 1) | ((uint32_t)m.s3 << 2);
+            while (ok3) {
+                const int bit = __builtin_ctz(ok3);
+                ok3 &= ok3 - 1;
+                const uint64_t key = make_key((uint32_t)(L.img_base + b), (uint32_t)L.octave, (uint32_t)(bit + 1),
+                                              (uint32_t)y, (uint32_t)x);
+                const uint32_t li = atomicAdd(&lcount, 1u);
+                if (li < DR_LCAP) {
+                    lcand[li] = key;
+                } else {
+                    const uint32_t slot = atomicAdd(L.counter, 1u);
+                    if (slot < L.cap) L.cand[slot] = key;
+                }
+            }
+        };
+        auto step = [&](int q, const RowBuf& B, auto full_tag) {
+            constexpr bool FULL = decltype(full_tag)::value;
+            const bool on = FULL || q <= q1;  // uniform
+            const int r = q - R;
+            bd_f2 g5 = bd_f2{0.0f, 0.0f};
+            if (on) {
+                bd_f2* wp = rg + (q & (BD_RING - 1)) * BD2_SLOTS;
+                wp[lane] = B.s0;
+                if (second) wp[64 + lane] = B.s1;
+                __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+                __builtin_amdgcn_wave_barrier();
+                __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+                win[2 * R] = rowpass(q);
+                if constexpr (P == kProfileOpenCV) {
+                    g5 = win[R] * L.taps.k[0];
+#pragma unroll
+                    for (int t = 1; t <= R; t++)
+                        g5 = __builtin_elementwise_fma(win[R + t] + win[R - t], (bd_f2)L.taps.k[t], g5);
+                } else {
+                    g5 = win[0] * L.taps.k[R];
+#pragma unroll
+                    for (int t = 1; t <= 2 * R; t++) g5 = g5 + win[t] * L.taps.k[t > R ? t - R : R - t];
+                }
+            }
+            const uint32_t rbad = ((FULL || (on && r >= ya)) && r < yb) ? 0u : 0xfffffff0u;
+            const int so5 = r * pitch * 4 + 5 * pb;
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, g5.x), rgs, (uint32_t)vx0 | rbad | xbad0,
+                                                  so5, 2 /* nt */);
+            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, g5.y), rgs, (uint32_t)vx1 | rbad | xbad1,
+                                                  so5, 2 /* nt */);
+            if (!FULL && !(on && r >= ya - 1)) {  // uniform
+                shift();
+                return;
+            }
+            // row r's DoG values (G_4 from the ring: row r is resident)
+            const bd_f2 g4 = rg[(r & (BD_RING - 1)) * BD2_SLOTS + lane + R];
+            bd_f2 cur[kDogPerOctave];
+            cur[0] = B.d[1] - B.d[0];
+            cur[1] = B.d[2] - B.d[1];
+            cur[2] = B.d[3] - B.d[2];
+            cur[3] = g4 - B.d[3];
+            cur[4] = g5 - g4;
+            float c0[kDogPerOctave], c1[kDogPerOctave];
+#pragma unroll
+            for (int p = 0; p < kDogPerOctave; p++) {
+                c0[p] = cur[p].x;
+                c1[p] = cur[p].y;
+            }
+            const int y = r - 1;  // tested row: rows r - 2, r - 1, r are in
+            if (FULL || y >= ya) {  // uniform
+                const bool yin = y >= kImageBorder && y < H - kImageBorder;
+                const ScanMasks m0 = extremum3_masks(prv0, mid0, c0, yin && xout0);
+                const ScanMasks m1 = extremum3_masks(prv1, mid1, c1, yin && xout1);
+                if (__builtin_amdgcn_ballot_w64(m0.s1 | m0.s2 | m0.s3 | m1.s1 | m1.s2 | m1.s3)) {  // rare
+                    emit(m0, y, x0);
+                    emit(m1, y, x1);
+                }
+            }
+#pragma unroll
+            for (int p = 0; p < kDogPerOctave; p++) {
+                prv0[p] = mid0[p];
+                mid0[p] = c0[p];
+                prv1[p] = mid1[p];
+                mid1[p] = c1[p];
+            }
+            shift();
+        };
+        RowBuf A0, A1, B0, B1;
+        constexpr int GROUP = 4;
+        auto group = [&](int q, auto full_tag) {
+            load(q + 2, B0, 0);
+            load(q + 3, B1, 1);
+            __builtin_amdgcn_sched_barrier(0);
+            step(q, A0, full_tag);
+            step(q + 1, A1, full_tag);
+            __builtin_amdgcn_sched_barrier(0);
+            load(q + 4, A0, 0);
+            load(q + 5, A1, 1);
+            __builtin_amdgcn_sched_barrier(0);
+            step(q + 2, B0, full_tag);
+            step(q + 3, B1, full_tag);
+            __builtin_amdgcn_sched_barrier(0);
+        };
+        load(q0, A0, 0);
+        load(q0 + 1, A1, 1);
+        int q = q0;
+        for (; q < ya + R + 1; q += GROUP) group(q, std::false_type{});
+        // three groups per iteration: the rolling DoG rows (a 3-cycle) and
+        // the buffer pairs (a 2-cycle) return to their registers, no moves
+        for (; q + 3 * GROUP - 1 <= q1; q += 3 * GROUP) {
+            group(q, std::true_type{});
+            group(q + GROUP, std::true_type{});
+            group(q + 2 * GROUP, std::true_type{});
+        }
+        for (; q + GROUP - 1 <= q1; q += GROUP) group(q, std::true_type{});
+        for (; q <= q1; q += GROUP) group(q, std::false_type{});
+    }
+    __syncthreads();
+    const uint32_t nl = lcount < DR_LCAP ? lcount : DR_LCAP;
+    if (nl == 0) return;
+    if (tid == 0) gbase = atomicAdd(L.counter, nl);
+    __syncthreads();
+    for (uint32_t i = tid; i < nl; i += 256)
+        if (gbase + i < L.cap) L.cand[gbase + i] = lcand[i];
+}
+
 // PathOpts::fused_detect: 0 keeps blur 5 and detection apart, 2 fuses every
 // octave it can at 32-row segments (test paths)
 // The segment length the fused pass would use for L (0: it does not apply).
 static int blur_detect_segment(int R, const BlurDetectLaunch& L, const PathOpts& o) {
     if (o.fused_detect == 0) return 0;
     const bool ok = L.W > R + 1 && L.H > R + 1 && L.W >= 2 * kImageBorder && L.H >= 2 * kImageBorder &&
-                    (uint64_t)L.H * (uint64_t)L.pitch * 4 < (1ull << 31) && L.n_img > 0;
+                    (uint64_t)L.H * (uint64_t)L.pitch * 4 * (o.bd_pair ? 6 : 1) < (1ull << 31) && L.n_img > 0;
     if (!ok) return 0;
     const bool ocv = L.profile == kProfileOpenCV;
     if (!((ocv && R == 13) || (!ocv && R == 7))) return 0;
@@ -496,10 +749,12 @@ static int blur_detect_segment(int R, const BlurDetectLaunch& L, const PathOpts&
     // The octave's rows split into nsy equal segments, not nsy - 1 full ones
     // and a remainder (octave 0 of 64 1080p frames: 3240 vs 3290 us; 384- or
     // 512-row segments, fewer and longer: 3290-3320 us)
-    const long nsx = (L.W + DR_COLS - 1) / DR_COLS;
+    const int cols = o.bd_pair ? BD2_COLS : DR_COLS;
+    const long nsx = (L.W + cols - 1) / cols;
+    const long want = o.bd_pair ? o.bd_waves : 16384;
     for (int s : {256, 128, 64}) {
         const int nsy = (L.H + s - 1) / s;
-        if (nsx * nsy * L.n_img >= 16384) return (L.H + nsy - 1) / nsy;
+        if (nsx * nsy * L.n_img >= want) return (L.H + nsy - 1) / nsy;
     }
     return 0;
 }
@@ -511,12 +766,18 @@ bool blur_detect_applies(int R, const BlurDetectLaunch& L, const PathOpts& o) {
 int launch_blur_detect(int R, BlurDetectLaunch& L, hipStream_t st, const PathOpts& o) {
     const int seg = blur_detect_segment(R, L, o);
     if (!seg) return -1;
-    L.nsx = (L.W + DR_COLS - 1) / DR_COLS;
+    const int cols = o.bd_pair ? BD2_COLS : DR_COLS;
+    L.nsx = (L.W + cols - 1) / cols;
     L.seg = seg;
     L.nsy = (L.H + seg - 1) / seg;
     const long waves = (long)L.nsx * L.nsy * L.n_img;
     const dim3 grid((uint32_t)((waves + 3) / 4));
-    if (L.profile == kProfileOpenCV)
+    if (o.bd_pair) {
+        if (L.profile == kProfileOpenCV)
+            hipLaunchKernelGGL((k_blur_detect_pair<13, kProfileOpenCV>), grid, dim3(256), 0, st, L);
+        else
+            hipLaunchKernelGGL((k_blur_detect_pair<7, kProfileImageproc>), grid, dim3(256), 0, st, L);
+    } else if (L.profile == kProfileOpenCV)
         hipLaunchKernelGGL((k_blur_detect<13, kProfileOpenCV>), grid, dim3(256), 0, st, L);
     else
         hipLaunchKernelGGL((k_blur_detect<7, kProfileImageproc>), grid, dim3(256), 0, st, L);

@@ -41,7 +41,6 @@ enum : int { kProfileOpenCV = 0, kProfileImageproc = 1 };
 // exists so the tests can hold each kernel family against the oracle.  They
 // live in the context (no process-wide state, nothing read from the
 // environment).
-constexpr uint32_t kTailSplitMaxFrames = 8;
 // Onesweep from this many sort keys (PathOpts::onesweep = 2): below it rocprim's
 // block sort + merge path is faster.  One 1080p frame (~12 k keys): 0.578 vs
 // 0.71 ms per call with Onesweep; 256 x VGA (128-frame chunks, ~206 k keys):
@@ -60,10 +59,9 @@ struct PathOpts {
     int graph = 0;         // 1: single-chunk calls captured once and replayed as a HIP graph
     int band_drift = 24;   // row bands: refinement drift accepted without a re-run (< 24 forces re-runs)
     int bound_shrink = 1;  // > 1: first-chunk stage bounds divided by it (forces the overflow re-run)
-    int tail_split = 0;    // k_octave_tail as chain + side workgroups per frame: 1 for chunks of
-                           // <= kTailSplitMaxFrames frames, 2 always, 0 never (one workgroup per frame:
-                           // faster in every case measured)
     int large_first = 1;   // one-chunk early path: two-ended extremum append (RefineLaunch::counter_hi)
+    int bd_pair = 0;       // 1: k_blur_detect_pair (two column strips per lane, packed f32 blur)
+    int bd_waves = 8192;   // k_blur_detect_pair: fewest waves per launch at the chosen row segments
     int onesweep = 0;      // emission-order sorts with rocprim's Onesweep: 1 always, 0 never (the
                            // library default path), 2 for bounds >= kOnesweepMinKeys
 };
@@ -140,14 +138,6 @@ struct TailLaunch {
     int o0, n_oct, n_img, profile;
     int r[kImagesPerOctave];
     BlurTaps taps[kImagesPerOctave];
-    // split (flags != null): two workgroups per frame -- the chain (blurs
-    // 1-3 and the next octave's G_0 of every tail octave) and the side (blurs
-    // 4, 5 of each octave once the chain has published its G_3:
-    // flags[frame * kTailMaxOct + o] == epoch); error: set when a side
-    // workgroup gave up waiting (never expected; the host reports it)
-    uint32_t* flags;
-    uint32_t* error;
-    uint32_t epoch;
 };
 // first octave that fits the tail kernel (n_oct: none); radii[1..5] = the
 // octave's blur radii

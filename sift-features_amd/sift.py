@@ -128,6 +128,7 @@ class Context:
         self._h = h
         self._generation = 0
         self._keep_dev = False  # sift_mi_set_keep_on_device state
+        self._path_values = {}  # sift_mi_set_path_option values set through this object
 
     def close(self):
         if getattr(self, "_h", None):
@@ -267,26 +268,33 @@ class Context:
     # diagnostic only; the defaults are the product path
     PATH_OPTIONS = {"tile_blur": (0, 0), "pair_blur": (1, 1), "seed_pair": (2, 1), "tail": (3, 1),
                     "fused_detect": (4, 1), "early": (5, 1), "desc_first": (6, 1), "graph": (7, 0),
-                    "band_drift": (8, 24), "bound_shrink": (9, 1), "tail_split": (10, 0),
+                    "band_drift": (8, 24), "bound_shrink": (9, 1),
                     "large_first": (11, 1),
-                    "onesweep": (12, 0)}
+                    "onesweep": (12, 0), "bd_pair": (13, 0), "bd_waves": (14, 8192)}
 
     def set_path_option(self, name, value):
         """One kernel-path switch (sift_mi_set_path_option), e.g.
         set_path_option("pair_blur", 0)."""
         check(lib().sift_mi_set_path_option(self._h, self.PATH_OPTIONS[name][0], int(value)))
+        self._path_values[name] = int(value)
+
+    def path_option(self, name):
+        """The switch's current value (as last set through this object, else
+        its default)."""
+        return self._path_values.get(name, self.PATH_OPTIONS[name][1])
 
     @contextlib.contextmanager
     def path_options(self, **opts):
         """Kernel-path switches for the duration of a with-block, then the
-        defaults again."""
+        values they had before it."""
+        before = {k: self.path_option(k) for k in opts}
         try:
             for k, v in opts.items():
                 self.set_path_option(k, v)
             yield self
         finally:
-            for k in opts:
-                self.set_path_option(k, self.PATH_OPTIONS[k][1])
+            for k, v in before.items():
+                self.set_path_option(k, v)
 
     # -- precompute_images / sift_with_precomputed (src/lib.rs:123-177) ------
     def precompute_images(self, img):

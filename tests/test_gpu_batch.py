@@ -273,29 +273,22 @@ def test_world2_gather_device_results(pkg):
 
 
 @pytest.mark.gpu
-def test_batch_tail_split_equal(pkg, oracle):
-    """A one-chunk batch of 6 frames through the split tail kernel (12
-    workgroups: a chain and a side per frame) and through the one-workgroup
-    kernel: identical results, and every tail octave's planes of frames 0
-    and 5 equal the oracle's bit for bit."""
+def test_batch_tail_planes_exact(pkg, oracle):
+    """A one-chunk batch of 6 frames: every octave's planes of frames 0 and
+    5, the tail octaves' from k_octave_tail (one workgroup per frame), equal
+    the oracle's bit for bit."""
     import synth
     fr = synth.frames(6, 640, 480, seed0=60)
     c = pkg.Context(0, pkg.OpenCVProcessing)
     c.set_chunk(6)
-    c.set_path_option("tail_split", 2)
     try:
-        split = c.sift_batch(fr)
+        c.sift_batch(fr)
         for i in (0, 5):
             opy = oracle.Pyramid(fr[i], 0)
             for o in range(opy.n_octaves):
                 assert np.array_equal(c.read_batch_scale_space(i, o), opy.scale_space(o)), (i, o)
-        c.set_path_option("tail_split", 0)
-        whole = c.sift_batch(fr)
     finally:
         c.close()
-    for a, b in zip(split, whole):
-        assert a == b
-        assert np.array_equal(a.keys, b.keys)
 
 
 @pytest.mark.gpu
@@ -361,20 +354,17 @@ def test_single_chunk_graph_replay(pkg, ctx, oracle, fetch):
     c.close()
 
 
-@pytest.mark.parametrize("knob,on", [("early", 1), ("desc_first", 1), ("tail_split", 1), ("large_first", 1),
-                                     ("onesweep", 1)])
+@pytest.mark.parametrize("knob,on", [("early", 1), ("desc_first", 1), ("large_first", 1), ("onesweep", 1)])
 @pytest.mark.parametrize("profile", [0, 1])
 def test_single_chunk_paths_equal(pkg, knob, on, profile):
     """One-chunk calls take latency paths of their own -- the octaves below
     the tail detected, refined and oriented on the aux stream beside the tail
     kernel with the tail octaves in a region of their own
     (Slot::early), the descriptors computed in keypoint index order beside
-    the ordering stage, then gathered (Slot::desc_first), and the small
-    octaves' kernel as a chain and a side workgroup per frame handing G_3
-    over through device flags (tail_split) -- whose results must equal the
-    general path's (the knob = 0) bit for bit, incl. keys.  tail_split is
-    off by default (measured slower), so it is switched on here.  Each
-    frame runs twice: the second call uses the bounds the first one learned."""
+    the ordering stage, then gathered (Slot::desc_first) -- whose results
+    must equal the general path's (the knob = 0) bit for bit, incl. keys.
+    Each frame runs twice: the second call uses the bounds the first one
+    learned."""
     import synth
     frames = [synth.frame(640, 480, 3), synth.frame(1000, 333, 5),
               np.random.default_rng(5).integers(0, 256, (96, 128), dtype=np.uint8)]

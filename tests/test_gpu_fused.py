@@ -10,8 +10,9 @@ pin both of its outputs:
     build_gaussian_scale_space (src/lib.rs:213-267);
   * the keypoints of the same calls against the oracle with the fused pass
     on (forced onto every octave it applies to, at 32-row segments:
-    path option fused_detect = 2) and off (fused_detect = 0: launch_blur +
-    k_detect_rows), across frame shapes that exercise partial strips, short
+    path option fused_detect = 2), in its one-column (k_blur_detect) and
+    two-strips-per-lane (k_blur_detect_pair, path option bd_pair) forms, and
+    off (fused_detect = 0: launch_blur + k_detect_rows), across frame shapes that exercise partial strips, short
     row segments, reflect-101 / clamp-to-edge borders and both profiles, and
     white noise (dense extrema, plateaus).
 """
@@ -31,15 +32,26 @@ def _frame(name, seed=7):
     return synth.frame(w, h, seed)
 
 
-@pytest.mark.parametrize("fused", [2, 0])
+MODES = {"pair": dict(fused_detect=2, bd_pair=1), "single": dict(fused_detect=2, bd_pair=0),
+         "apart": dict(fused_detect=0)}
+
+
+def _context(pkg, profile, mode):
+    c = pkg.Context(0, pkg.OpenCVProcessing if profile == 0 else pkg.ImageprocProcessing)
+    for k, v in MODES[mode].items():
+        c.set_path_option(k, v)
+    return c
+
+
+@pytest.mark.parametrize("fused", list(MODES))
 @pytest.mark.parametrize("profile", [0, 1])
 @pytest.mark.parametrize("name", SHAPES)
 def test_batch_pyramid_bit_exact(pkg, oracle, fused, profile, name):
     """Every Gaussian plane the batch path leaves in its arena (G_5 from
-    k_blur_detect when fused) equals the oracle's, bit for bit."""
+    k_blur_detect / k_blur_detect_pair when fused) equals the oracle's, bit
+    for bit."""
     img = _frame(name)
-    c = pkg.Context(0, pkg.OpenCVProcessing if profile == 0 else pkg.ImageprocProcessing)
-    c.set_path_option("fused_detect", fused)
+    c = _context(pkg, profile, fused)
     c.sift(img)
     opy = oracle.Pyramid(img, profile)
     for o in range(opy.n_octaves):
@@ -50,7 +62,7 @@ def test_batch_pyramid_bit_exact(pkg, oracle, fused, profile, name):
     c.close()
 
 
-@pytest.mark.parametrize("fused", [2, 0])
+@pytest.mark.parametrize("fused", list(MODES))
 @pytest.mark.parametrize("profile", [0, 1])
 @pytest.mark.parametrize("name", SHAPES + ["noise"])
 def test_fused_detect_parity(pkg, oracle, fused, profile, name):
@@ -58,21 +70,22 @@ def test_fused_detect_parity(pkg, oracle, fused, profile, name):
     oracle with and without the fused pass."""
     from test_gpu_parity import assert_parity
     img = _frame(name)
-    c = pkg.Context(0, pkg.OpenCVProcessing if profile == 0 else pkg.ImageprocProcessing)
-    c.set_path_option("fused_detect", fused)
+    c = _context(pkg, profile, fused)
     res = c.sift(img)
     c.close()
     kp_o, desc_o, ext_o = oracle.sift(img, profile=profile, internal=True)
     assert_parity(pkg, res, kp_o, desc_o, ext_o)
 
 
-def test_batch_pyramid_multi_frame(pkg, oracle):
+@pytest.mark.parametrize("pair", [1, 0])
+def test_batch_pyramid_multi_frame(pkg, oracle, pair):
     """Frames of one chunk (the fused pass's frame index and image stride):
     every frame's planes of a 5-frame single-chunk batch equal the oracle's."""
     import synth
     fr = synth.frames(5, 320, 240, seed0=21)
     c = pkg.Context(0, pkg.OpenCVProcessing)
     c.set_path_option("fused_detect", 2)
+    c.set_path_option("bd_pair", pair)
     c.set_chunk(5)
     got = c.sift_batch(fr)
     for i in (0, 2, 4):

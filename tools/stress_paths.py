@@ -1,5 +1,5 @@
 #!/usr/bin/env python3
-"""Repeats the one-frame path comparisons (split tail on / off, early off)
+"""Repeats the one-frame path comparisons (default, early off, large_first)
 in one process, fresh contexts each round, and prints any mismatch: a check
 for rare ordering races.  python tools/stress_paths.py [--rounds 8]"""
 import argparse
@@ -25,12 +25,12 @@ def main():
     for r in range(a.rounds):
         for prof in (pkg.OpenCVProcessing, pkg.ImageprocProcessing):
             res = {}
-            for knob, val in (("tail_split", 1), ("tail_split", 0), ("early", 0), ("large_first", 1)):
+            for knob, val in (("early", 1), ("early", 0), ("large_first", 0)):
                 c = pkg.Context(0, prof)
                 c.set_path_option(knob, val)
                 res[(knob, val)] = [c.sift(f) for f in frames for _ in range(2)]
                 c.close()
-            ref = res[("tail_split", 0)]
+            ref = res[("early", 1)]
             for k, v in res.items():
                 for i, (x, y) in enumerate(zip(v, ref)):
                     if not (x == y and np.array_equal(x.keys, y.keys)):

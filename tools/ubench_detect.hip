@@ -449,6 +449,47 @@ int main(int argc, char** argv) {
         BlurDetectLaunch f = F;
         launch_blur_detect(rad[5], f, 0);
     });
+    // the pair kernel (two column strips per lane): time, then G_5 and candidates
+    const int bdw = getenv("BD_WAVES") ? atoi(getenv("BD_WAVES")) : 8192;
+    PathOpts po2{};
+    po2.bd_pair = 1;
+    po2.bd_waves = bdw;
+    CK(hipMemset(g + 5 * P, 0, P * 4));
+    const float tbp = timeit([&] {
+        CK(hipMemsetAsync(cnt, 0, 4, 0));
+        BlurDetectLaunch f = F;
+        launch_blur_detect(rad[5], f, 0, po2);
+    });
+    {
+        uint32_t np = 0;
+        CK(hipMemcpy(&np, cnt, 4, hipMemcpyDeviceToHost));
+        std::vector<uint64_t> c_p(np);
+        CK(hipMemcpy(c_p.data(), cand, np * 8, hipMemcpyDeviceToHost));
+        std::sort(c_p.begin(), c_p.end());
+        std::vector<float> g5e(P), g5f(P);
+        CK(hipMemcpy(g5e.data(), g + 5 * P, P * 4, hipMemcpyDeviceToHost));
+        CK(hipMemcpy(g5f.data(), g + (size_t)(n - 1) * stride + 5 * P, P * 4, hipMemcpyDeviceToHost));
+        const bool sg = std::memcmp(g5a.data(), g5e.data(), P * 4) == 0 && std::memcmp(g5b.data(), g5f.data(), P * 4) == 0;
+        BlurDetectLaunch f = F;
+        launch_blur_detect(rad[5], f, 0, po2);  // fills nsx / seg for the report
+        std::printf("k_blur_detect_pair   %8.1f us  %5.2f TB/s (24 B/px)  %u candidates  seg %d  G_5 %s, candidates %s\n",
+                    tbp * 1e3, 6 * (double)W * H * n * 4 / 1e6 / tbp / 1e3, np, f.seg,
+                    sg ? "bit-identical" : "DIFFER", c_p == c_rows ? "identical" : "DIFFER");
+        if (!sg || c_p != c_rows) {
+            size_t bad = 0, first = 0;
+            for (size_t i = 0; i < P; i++)
+                if (g5a[i] != g5e[i]) { if (!bad) first = i; bad++; }
+            std::printf("  G_5 frame 0: %zu differ, first at y %zu x %zu (%g vs %g)\n", bad, first / pitch, first % pitch,
+                        bad ? g5a[first] : 0.f, bad ? g5e[first] : 0.f);
+        }
+    }
+    CK(hipDeviceSynchronize());
+    {
+        // restore k_blur_detect's outputs for the refine comparisons below
+        CK(hipMemsetAsync(cnt, 0, 4, 0));
+        BlurDetectLaunch f = F;
+        launch_blur_detect(rad[5], f, 0);
+    }
     uint32_t nc = 0;
     CK(hipMemcpy(&nc, cnt, 4, hipMemcpyDeviceToHost));
     std::vector<uint64_t> c_bd(nc);
