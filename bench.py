@@ -67,7 +67,23 @@ def parse():
     p.add_argument("--no-unfused", action="store_true",
                    help="skip the blur-kernels-only reference pass (profiles: product kernels only)")
     p.add_argument("--no-jpeg", action="store_true", help="skip the JPEG -> keypoints end-to-end field")
-    return p.parse_args()
+    p.add_argument("--opt", action="append", default=[],
+                   help="path option name=value on every context (A/B runs; default: the product path)")
+    a = p.parse_args()
+    for kv in a.opt:
+        k, v = kv.split("=")
+        PATH_OPTS[k] = int(v)
+    return a
+
+
+PATH_OPTS = {}  # --opt name=value
+
+
+def new_context(pkg, device_index, processing):
+    c = pkg.Context(device_index, processing)
+    for k, v in PATH_OPTS.items():
+        c.set_path_option(k, v)
+    return c
 
 
 def run_config(pkg, synth, dev, device_index, n, W, H, steps, seed0=1000, max_octaves=0, processing=None):
@@ -80,7 +96,7 @@ def run_config(pkg, synth, dev, device_index, n, W, H, steps, seed0=1000, max_oc
     import torch
     fr = synth.frames_torch(n, W, H, seed0=seed0, device=dev)
     torch.cuda.synchronize()
-    c = pkg.Context(device_index, processing or pkg.OpenCVProcessing)
+    c = new_context(pkg, device_index, processing or pkg.OpenCVProcessing)
     if max_octaves:
         c.set_max_octaves(max_octaves)
     call = (fr.data_ptr(), n, W, H, fr.stride(1), fr.stride(0))
@@ -139,8 +155,8 @@ def run_jpeg_e2e(pkg, synth, device_index, n, W, H, steps, threads):
         b = io.BytesIO()
         Image.fromarray(rgb).save(b, "JPEG", quality=90, subsampling=2)
         datas.append(b.getvalue())
-    ctx = pkg.Context(device_index, pkg.OpenCVProcessing)
-    dctx = pkg.Context(device_index, pkg.OpenCVProcessing)
+    ctx = new_context(pkg, device_index, pkg.OpenCVProcessing)
+    dctx = new_context(pkg, device_index, pkg.OpenCVProcessing)
     bufs = [torch.empty((n, H, W), dtype=torch.uint8, device="cuda") for _ in range(2)]
     fp, rs = bufs[0].stride(0), bufs[0].stride(1)
 
@@ -201,7 +217,7 @@ def main():
     f0, f1 = shard.shard_range(world * B, rank, world)
     frames = synth.frames_torch(f1 - f0, W, H, seed0=f0, device=dev)
     torch.cuda.synchronize()
-    ctx = pkg.Context(local, pkg.OpenCVProcessing)
+    ctx = new_context(pkg, local, pkg.OpenCVProcessing)
     if args.chunk:
         ctx.set_chunk(args.chunk)
     ptr, stride, pitch = frames.data_ptr(), frames.stride(1), frames.stride(0)
@@ -453,7 +469,8 @@ def main():
             "data": "synthetic (seeded procedural blob frames generated on device, synth.py)",
             "config": {"workload": f"batch of {B} x {W}x{H} u8 frames per GPU (configs[3] shard), full sift()",
                        "frames_per_gpu": B, "frame": f"{W}x{H}", "octaves": n_oct, "profile": "opencv",
-                       "parallelism": f"dp{world} (frames sharded, no collective)"},
+                       "parallelism": f"dp{world} (frames sharded, no collective)",
+                       **({"path_options": dict(PATH_OPTS)} if PATH_OPTS else {})},
             "frames_per_s": total_frames / dt_max,
             "keypoints_per_frame": total_kp / max(1.0, total_frames),
             "stage_ms_per_step": {k: st[k] / args.steps for k in

@@ -2102,7 +2102,7 @@ int sift_mi_set_path_option(sift_mi_ctx* c, int option, int value) {
         case SIFT_MI_PATH_BOUND_SHRINK: if (value < 1) break; o.bound_shrink = value; return 0;
         case SIFT_MI_PATH_LARGE_FIRST: if (!b) break; o.large_first = value; return 0;
         case SIFT_MI_PATH_ONESWEEP: if (value < 0 || value > 2) break; o.onesweep = value; return 0;
-        case SIFT_MI_PATH_BD_PAIR: if (!b) break; o.bd_pair = value; return 0;
+        case SIFT_MI_PATH_BD_PAIR: if (value < 0 || value > 2) break; o.bd_pair = value; return 0;
         case SIFT_MI_PATH_BD_WAVES: if (value < 1024 || value > 65536) break; o.bd_waves = value; return 0;
         default: return fail(SIFT_MI_EINVAL, "unknown path option");
     }

@@ -532,7 +532,7 @@ __device__ __forceinline__ ScanMasks extremum3_masks(const float (&prv)[kDogPerO
 #ifndef SIFT_BD2_WPE
 #define SIFT_BD2_WPE 1
 #endif
-template <int R, int P>
+template <int R, int P, int NB>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_BD2_WPE))) void k_blur_detect_pair(
     const BlurDetectLaunch L) {
     static_assert(R <= 13 && R + 3 <= BD_RING, "ring geometry");
@@ -649,10 +649,13 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_BD2_WP
             }
             const uint32_t rbad = ((FULL || (on && r >= ya)) && r < yb) ? 0u : 0xfffffff0u;
             const int so5 = r * pitch * 4 + 5 * pb;
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, g5.x), rgs, (uint32_t)vx0 | rbad | xbad0,
-                                                  so5, 2 /* nt */);
-            __builtin_amdgcn_raw_buffer_store_b32(__builtin_bit_cast(uint32_t, g5.y), rgs, (uint32_t)vx1 | rbad | xbad1,
-                                                  so5, 2 /* nt */);
+            // (the halves through scalars: a __builtin_bit_cast of g5.y, an
+            // element of a vector lvalue, reads element 0 in this clang)
+            const float g5x = g5.x, g5y = g5.y;
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(g5x), rgs, (uint32_t)vx0 | rbad | xbad0, so5,
+                                                  2 /* nt */);
+            __builtin_amdgcn_raw_buffer_store_b32(__float_as_uint(g5y), rgs, (uint32_t)vx1 | rbad | xbad1, so5,
+                                                  2 /* nt */);
             if (!FULL && !(on && r >= ya - 1)) {  // uniform
                 shift();
                 return;
@@ -690,32 +693,36 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_BD2_WP
             }
             shift();
         };
-        RowBuf A0, A1, B0, B1;
-        constexpr int GROUP = 4;
+        // NB buffer pairs: rows q, q + 1 are processed from one pair while
+        // the next NB - 1 pairs' loads (rows up to q + 2 NB - 1) are in flight
+        RowBuf buf[NB][2];
+        constexpr int GROUP = 2 * NB;
         auto group = [&](int q, auto full_tag) {
-            load(q + 2, B0, 0);
-            load(q + 3, B1, 1);
-            __builtin_amdgcn_sched_barrier(0);
-            step(q, A0, full_tag);
-            step(q + 1, A1, full_tag);
-            __builtin_amdgcn_sched_barrier(0);
-            load(q + 4, A0, 0);
-            load(q + 5, A1, 1);
-            __builtin_amdgcn_sched_barrier(0);
-            step(q + 2, B0, full_tag);
-            step(q + 3, B1, full_tag);
-            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int k = 0; k < NB; k++) {
+                load(q + 2 * k + 2 * (NB - 1), buf[(k + NB - 1) % NB][0], 0);
+                load(q + 2 * k + 2 * (NB - 1) + 1, buf[(k + NB - 1) % NB][1], 1);
+                __builtin_amdgcn_sched_barrier(0);
+                step(q + 2 * k, buf[k][0], full_tag);
+                step(q + 2 * k + 1, buf[k][1], full_tag);
+                __builtin_amdgcn_sched_barrier(0);
+            }
         };
-        load(q0, A0, 0);
-        load(q0 + 1, A1, 1);
+#pragma unroll
+        for (int k = 0; k < NB - 1; k++) {
+            load(q0 + 2 * k, buf[k][0], 0);
+            load(q0 + 2 * k + 1, buf[k][1], 1);
+        }
         int q = q0;
         for (; q < ya + R + 1; q += GROUP) group(q, std::false_type{});
-        // three groups per iteration: the rolling DoG rows (a 3-cycle) and
-        // the buffer pairs (a 2-cycle) return to their registers, no moves
-        for (; q + 3 * GROUP - 1 <= q1; q += 3 * GROUP) {
-            group(q, std::true_type{});
-            group(q + GROUP, std::true_type{});
-            group(q + 2 * GROUP, std::true_type{});
+        if constexpr (NB == 2) {
+            // three groups per iteration: the rolling DoG rows (a 3-cycle)
+            // and the buffer pairs (a 2-cycle) return to their registers
+            for (; q + 3 * GROUP - 1 <= q1; q += 3 * GROUP) {
+                group(q, std::true_type{});
+                group(q + GROUP, std::true_type{});
+                group(q + 2 * GROUP, std::true_type{});
+            }
         }
         for (; q + GROUP - 1 <= q1; q += GROUP) group(q, std::true_type{});
         for (; q <= q1; q += GROUP) group(q, std::false_type{});
@@ -772,11 +779,16 @@ int launch_blur_detect(int R, BlurDetectLaunch& L, hipStream_t st, const PathOpt
     L.nsy = (L.H + seg - 1) / seg;
     const long waves = (long)L.nsx * L.nsy * L.n_img;
     const dim3 grid((uint32_t)((waves + 3) / 4));
-    if (o.bd_pair) {
+    if (o.bd_pair == 2) {
         if (L.profile == kProfileOpenCV)
-            hipLaunchKernelGGL((k_blur_detect_pair<13, kProfileOpenCV>), grid, dim3(256), 0, st, L);
+            hipLaunchKernelGGL((k_blur_detect_pair<13, kProfileOpenCV, 3>), grid, dim3(256), 0, st, L);
         else
-            hipLaunchKernelGGL((k_blur_detect_pair<7, kProfileImageproc>), grid, dim3(256), 0, st, L);
+            hipLaunchKernelGGL((k_blur_detect_pair<7, kProfileImageproc, 3>), grid, dim3(256), 0, st, L);
+    } else if (o.bd_pair) {
+        if (L.profile == kProfileOpenCV)
+            hipLaunchKernelGGL((k_blur_detect_pair<13, kProfileOpenCV, 2>), grid, dim3(256), 0, st, L);
+        else
+            hipLaunchKernelGGL((k_blur_detect_pair<7, kProfileImageproc, 2>), grid, dim3(256), 0, st, L);
     } else if (L.profile == kProfileOpenCV)
         hipLaunchKernelGGL((k_blur_detect<13, kProfileOpenCV>), grid, dim3(256), 0, st, L);
     else

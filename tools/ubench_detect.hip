@@ -451,8 +451,9 @@ int main(int argc, char** argv) {
     });
     // the pair kernel (two column strips per lane): time, then G_5 and candidates
     const int bdw = getenv("BD_WAVES") ? atoi(getenv("BD_WAVES")) : 8192;
+    for (int mode = 1; mode <= 2; mode++) {
     PathOpts po2{};
-    po2.bd_pair = 1;
+    po2.bd_pair = mode;
     po2.bd_waves = bdw;
     CK(hipMemset(g + 5 * P, 0, P * 4));
     const float tbp = timeit([&] {
@@ -472,8 +473,8 @@ int main(int argc, char** argv) {
         const bool sg = std::memcmp(g5a.data(), g5e.data(), P * 4) == 0 && std::memcmp(g5b.data(), g5f.data(), P * 4) == 0;
         BlurDetectLaunch f = F;
         launch_blur_detect(rad[5], f, 0, po2);  // fills nsx / seg for the report
-        std::printf("k_blur_detect_pair   %8.1f us  %5.2f TB/s (24 B/px)  %u candidates  seg %d  G_5 %s, candidates %s\n",
-                    tbp * 1e3, 6 * (double)W * H * n * 4 / 1e6 / tbp / 1e3, np, f.seg,
+        std::printf("k_blur_detect_pair%d  %8.1f us  %5.2f TB/s (24 B/px)  %u candidates  seg %d  G_5 %s, candidates %s\n",
+                    mode, tbp * 1e3, 6 * (double)W * H * n * 4 / 1e6 / tbp / 1e3, np, f.seg,
                     sg ? "bit-identical" : "DIFFER", c_p == c_rows ? "identical" : "DIFFER");
         if (!sg || c_p != c_rows) {
             size_t bad = 0, first = 0;
@@ -481,7 +482,9 @@ int main(int argc, char** argv) {
                 if (g5a[i] != g5e[i]) { if (!bad) first = i; bad++; }
             std::printf("  G_5 frame 0: %zu differ, first at y %zu x %zu (%g vs %g)\n", bad, first / pitch, first % pitch,
                         bad ? g5a[first] : 0.f, bad ? g5e[first] : 0.f);
+            return 5;
         }
+    }
     }
     CK(hipDeviceSynchronize());
     {
