@@ -188,7 +188,8 @@ typedef enum {
     SIFT_MI_PATH_ONESWEEP = 12,    /* the emission-order sorts with rocprim's Onesweep radix sort: 1 at
                                       every size, 0 never, 2 from 524288 keys (default 0) */
     SIFT_MI_PATH_BD_PAIR = 13,     /* the fused blur 5 + extremum scan with two column strips per lane
-                                      (packed f32): 1 on, 0 the one-column kernel */
+                                      (packed f32): 1 (default) / 2 its two loop forms, 0 the one-column
+                                      kernel */
     SIFT_MI_PATH_BD_WAVES = 14     /* the pair kernel's fewest waves per launch when choosing its row
                                       segments, 1024..65536 */
 } sift_mi_path_option;

@@ -532,7 +532,7 @@ __device__ __forceinline__ ScanMasks extremum3_masks(const float (&prv)[kDogPerO
 #ifndef SIFT_BD2_WPE
 #define SIFT_BD2_WPE 1
 #endif
-template <int R, int P, int NB>
+template <int R, int P, int NB, int U>
 __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_BD2_WPE))) void k_blur_detect_pair(
     const BlurDetectLaunch L) {
     static_assert(R <= 13 && R + 3 <= BD_RING, "ring geometry");
@@ -625,8 +625,8 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_BD2_WP
         };
         auto step = [&](int q, const RowBuf& B, auto full_tag) {
             constexpr bool FULL = decltype(full_tag)::value;
-            const bool on = FULL || q <= q1;  // uniform
-            const int r = q - R;
+            const bool on = FULL || q <= q1;  // uniform: G_4 row q is row-filtered
+            const int r = q - R;              // the G_5 row this step forms
             bd_f2 g5 = bd_f2{0.0f, 0.0f};
             if (on) {
                 bd_f2* wp = rg + (q & (BD_RING - 1)) * BD2_SLOTS;
@@ -715,7 +715,7 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_BD2_WP
         }
         int q = q0;
         for (; q < ya + R + 1; q += GROUP) group(q, std::false_type{});
-        if constexpr (NB == 2) {
+        if constexpr (NB == 2 && U == 3) {
             // three groups per iteration: the rolling DoG rows (a 3-cycle)
             // and the buffer pairs (a 2-cycle) return to their registers
             for (; q + 3 * GROUP - 1 <= q1; q += 3 * GROUP) {
@@ -781,14 +781,14 @@ int launch_blur_detect(int R, BlurDetectLaunch& L, hipStream_t st, const PathOpt
     const dim3 grid((uint32_t)((waves + 3) / 4));
     if (o.bd_pair == 2) {
         if (L.profile == kProfileOpenCV)
-            hipLaunchKernelGGL((k_blur_detect_pair<13, kProfileOpenCV, 3>), grid, dim3(256), 0, st, L);
+            hipLaunchKernelGGL((k_blur_detect_pair<13, kProfileOpenCV, 2, 1>), grid, dim3(256), 0, st, L);
         else
-            hipLaunchKernelGGL((k_blur_detect_pair<7, kProfileImageproc, 3>), grid, dim3(256), 0, st, L);
+            hipLaunchKernelGGL((k_blur_detect_pair<7, kProfileImageproc, 2, 1>), grid, dim3(256), 0, st, L);
     } else if (o.bd_pair) {
         if (L.profile == kProfileOpenCV)
-            hipLaunchKernelGGL((k_blur_detect_pair<13, kProfileOpenCV, 2>), grid, dim3(256), 0, st, L);
+            hipLaunchKernelGGL((k_blur_detect_pair<13, kProfileOpenCV, 2, 3>), grid, dim3(256), 0, st, L);
         else
-            hipLaunchKernelGGL((k_blur_detect_pair<7, kProfileImageproc, 2>), grid, dim3(256), 0, st, L);
+            hipLaunchKernelGGL((k_blur_detect_pair<7, kProfileImageproc, 2, 3>), grid, dim3(256), 0, st, L);
     } else if (L.profile == kProfileOpenCV)
         hipLaunchKernelGGL((k_blur_detect<13, kProfileOpenCV>), grid, dim3(256), 0, st, L);
     else

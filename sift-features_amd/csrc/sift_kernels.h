@@ -60,8 +60,8 @@ struct PathOpts {
     int band_drift = 24;   // row bands: refinement drift accepted without a re-run (< 24 forces re-runs)
     int bound_shrink = 1;  // > 1: first-chunk stage bounds divided by it (forces the overflow re-run)
     int large_first = 1;   // one-chunk early path: two-ended extremum append (RefineLaunch::counter_hi)
-    int bd_pair = 1;       // k_blur_detect_pair (two column strips per lane, packed f32): 1 two buffer pairs,
-                           // 2 three (loads 4 rows ahead: slower, round 6); 0 the one-column k_blur_detect
+    int bd_pair = 1;       // k_blur_detect_pair (two column strips per lane, packed f32): 1 its steady loop
+                           // unrolled by 12 rows, 2 by 4; 0 the one-column k_blur_detect
     int bd_waves = 8192;   // k_blur_detect_pair: fewest waves per launch at the chosen row segments
     int onesweep = 0;      // emission-order sorts with rocprim's Onesweep: 1 always, 0 never (the
                            // library default path), 2 for bounds >= kOnesweepMinKeys

@@ -32,7 +32,8 @@ def _frame(name, seed=7):
     return synth.frame(w, h, seed)
 
 
-MODES = {"pair": dict(fused_detect=2, bd_pair=1), "single": dict(fused_detect=2, bd_pair=0),
+MODES = {"pair": dict(fused_detect=2, bd_pair=1), "pair_u1": dict(fused_detect=2, bd_pair=2),
+         "single": dict(fused_detect=2, bd_pair=0),
          "apart": dict(fused_detect=0)}
 
 
@@ -77,7 +78,7 @@ def test_fused_detect_parity(pkg, oracle, fused, profile, name):
     assert_parity(pkg, res, kp_o, desc_o, ext_o)
 
 
-@pytest.mark.parametrize("pair", [1, 0])
+@pytest.mark.parametrize("pair", [2, 1, 0])
 def test_batch_pyramid_multi_frame(pkg, oracle, pair):
     """Frames of one chunk (the fused pass's frame index and image stride):
     every frame's planes of a 5-frame single-chunk batch equal the oracle's."""
