@@ -738,12 +738,20 @@ __global__ __launch_bounds__(256) __attribute__((amdgpu_waves_per_eu(SIFT_BD2_WP
 
 // PathOpts::fused_detect: 0 keeps blur 5 and detection apart, 2 fuses every
 // octave it can at 32-row segments (test paths)
+// Whether L runs as k_blur_detect_pair (its one buffer resource spans the
+// frame's six planes: < 2^31 bytes; larger octaves -- octave 0 of an 8192^2
+// frame -- take the one-column kernel, whose resources are per plane).
+static bool blur_detect_pair(const BlurDetectLaunch& L, const PathOpts& o) {
+    return o.bd_pair && (uint64_t)L.H * (uint64_t)L.pitch * 4 * 6 < (1ull << 31);
+}
+
 // The segment length the fused pass would use for L (0: it does not apply).
 static int blur_detect_segment(int R, const BlurDetectLaunch& L, const PathOpts& o) {
     if (o.fused_detect == 0) return 0;
     const bool ok = L.W > R + 1 && L.H > R + 1 && L.W >= 2 * kImageBorder && L.H >= 2 * kImageBorder &&
-                    (uint64_t)L.H * (uint64_t)L.pitch * 4 * (o.bd_pair ? 6 : 1) < (1ull << 31) && L.n_img > 0;
+                    (uint64_t)L.H * (uint64_t)L.pitch * 4 < (1ull << 31) && L.n_img > 0;
     if (!ok) return 0;
+    const bool pair = blur_detect_pair(L, o);
     const bool ocv = L.profile == kProfileOpenCV;
     if (!((ocv && R == 13) || (!ocv && R == 7))) return 0;
     if (o.fused_detect == 2) return 32;  // many segment boundaries on test-sized frames
@@ -756,9 +764,9 @@ static int blur_detect_segment(int R, const BlurDetectLaunch& L, const PathOpts&
     // The octave's rows split into nsy equal segments, not nsy - 1 full ones
     // and a remainder (octave 0 of 64 1080p frames: 3240 vs 3290 us; 384- or
     // 512-row segments, fewer and longer: 3290-3320 us)
-    const int cols = o.bd_pair ? BD2_COLS : DR_COLS;
+    const int cols = pair ? BD2_COLS : DR_COLS;
     const long nsx = (L.W + cols - 1) / cols;
-    const long want = o.bd_pair ? o.bd_waves : 16384;
+    const long want = pair ? o.bd_waves : 16384;
     for (int s : {256, 128, 64}) {
         const int nsy = (L.H + s - 1) / s;
         if (nsx * nsy * L.n_img >= want) return (L.H + nsy - 1) / nsy;
@@ -773,18 +781,19 @@ bool blur_detect_applies(int R, const BlurDetectLaunch& L, const PathOpts& o) {
 int launch_blur_detect(int R, BlurDetectLaunch& L, hipStream_t st, const PathOpts& o) {
     const int seg = blur_detect_segment(R, L, o);
     if (!seg) return -1;
-    const int cols = o.bd_pair ? BD2_COLS : DR_COLS;
+    const bool pair = blur_detect_pair(L, o);
+    const int cols = pair ? BD2_COLS : DR_COLS;
     L.nsx = (L.W + cols - 1) / cols;
     L.seg = seg;
     L.nsy = (L.H + seg - 1) / seg;
     const long waves = (long)L.nsx * L.nsy * L.n_img;
     const dim3 grid((uint32_t)((waves + 3) / 4));
-    if (o.bd_pair == 2) {
+    if (pair && o.bd_pair == 2) {
         if (L.profile == kProfileOpenCV)
             hipLaunchKernelGGL((k_blur_detect_pair<13, kProfileOpenCV, 2, 1>), grid, dim3(256), 0, st, L);
         else
             hipLaunchKernelGGL((k_blur_detect_pair<7, kProfileImageproc, 2, 1>), grid, dim3(256), 0, st, L);
-    } else if (o.bd_pair) {
+    } else if (pair) {
         if (L.profile == kProfileOpenCV)
             hipLaunchKernelGGL((k_blur_detect_pair<13, kProfileOpenCV, 2, 3>), grid, dim3(256), 0, st, L);
         else
