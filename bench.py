@@ -67,6 +67,8 @@ def parse():
     p.add_argument("--no-unfused", action="store_true",
                    help="skip the blur-kernels-only reference pass (profiles: product kernels only)")
     p.add_argument("--no-jpeg", action="store_true", help="skip the JPEG -> keypoints end-to-end field")
+    p.add_argument("--rehearse-one-gpu", action="store_true",
+                   help="N > 1 rehearsal on a one-GPU box: every rank on cuda:0, gloo transport (not a measurement)")
     p.add_argument("--opt", action="append", default=[],
                    help="path option name=value on every context (A/B runs; default: the product path)")
     a = p.parse_args()
@@ -199,9 +201,14 @@ def main():
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
+    if args.rehearse_one_gpu:
+        local = 0  # every rank shares the one card; the gather goes over gloo
     if world > 1:
         torch.cuda.set_device(local)
-        dist.init_process_group("nccl", device_id=torch.device("cuda", local))
+        if args.rehearse_one_gpu:
+            dist.init_process_group("gloo")
+        else:
+            dist.init_process_group("nccl", device_id=torch.device("cuda", local))
     else:
         torch.cuda.set_device(local)
     dev = torch.device("cuda", local)
@@ -470,7 +477,9 @@ def main():
             "config": {"workload": f"batch of {B} x {W}x{H} u8 frames per GPU (configs[3] shard), full sift()",
                        "frames_per_gpu": B, "frame": f"{W}x{H}", "octaves": n_oct, "profile": "opencv",
                        "parallelism": f"dp{world} (frames sharded, no collective)",
-                       **({"path_options": dict(PATH_OPTS)} if PATH_OPTS else {})},
+                       **({"path_options": dict(PATH_OPTS)} if PATH_OPTS else {}),
+                       **({"rehearsal": "every rank on cuda:0, gloo transport: not a measurement"}
+                          if args.rehearse_one_gpu else {})},
             "frames_per_s": total_frames / dt_max,
             "keypoints_per_frame": total_kp / max(1.0, total_frames),
             "stage_ms_per_step": {k: st[k] / args.steps for k in

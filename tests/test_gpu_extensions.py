@@ -133,3 +133,26 @@ def test_run_sift_cli(pkg, oracle, name):
                           "--processing", "opencv"], capture_output=True, text=True, timeout=300, env=env)
     assert out.returncode == 0, out.stderr
     assert out.stdout.strip() == {"bird_small": "225 keypoints", "tree_small": "1270 keypoints"}[name]
+
+
+def test_path_option_validation_and_restore(pkg):
+    """sift_mi_set_path_option rejects the retired split-tail option (10) and
+    out-of-range values of the round-6 options; Context.path_options()
+    restores the values the options had before the block, not the defaults
+    (ADVICE r05)."""
+    c = pkg.Context(0)
+    try:
+        L = pkg.lib()
+        assert L.sift_mi_set_path_option(c._h, 10, 0) != 0  # split tail: retired
+        assert L.sift_mi_set_path_option(c._h, 13, 3) != 0  # bd_pair: 0..2
+        assert L.sift_mi_set_path_option(c._h, 14, 100) != 0  # bd_waves: 1024..65536
+        assert L.sift_mi_set_path_option(c._h, 99, 0) != 0
+        c.set_path_option("graph", 1)
+        c.set_path_option("bd_waves", 4096)
+        with c.path_options(graph=0, bd_pair=2, bd_waves=16384):
+            assert c.path_option("graph") == 0 and c.path_option("bd_pair") == 2
+        assert c.path_option("graph") == 1
+        assert c.path_option("bd_pair") == pkg.Context.PATH_OPTIONS["bd_pair"][1]
+        assert c.path_option("bd_waves") == 4096
+    finally:
+        c.close()
