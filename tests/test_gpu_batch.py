@@ -272,6 +272,69 @@ def test_world2_gather_device_results(pkg):
     assert all(r[0] == "ok" and r[2] for r in res), res
 
 
+def _nccl_worker(port, q):
+    import os
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    sys.path.insert(0, root)
+    sys.path.insert(0, os.path.join(root, "sift-features_amd"))
+    import torch
+    import torch.distributed as dist
+    import pkg_loader
+    import shard
+    import synth
+    os.environ["MASTER_ADDR"] = "127.0.0.1"
+    os.environ["MASTER_PORT"] = str(port)
+    torch.cuda.set_device(0)
+    dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+    try:
+        pkg = pkg_loader.load()
+        ctx = pkg.Context(0, pkg.OpenCVProcessing)
+        ctx.set_chunk(2)
+        t = torch.from_numpy(synth.frames(3, 640, 480, seed0=7)).cuda()
+        torch.cuda.synchronize()
+        offs, _ = ctx.sift_batch_device(t.data_ptr(), 3, 640, 480, t.stride(1), t.stride(0), fetch=False)
+        k, d = shard.device_results(ctx)
+        g = shard.gather_device_results(k, d, offs, dist, dst=0)
+        dist.barrier()
+        ref = ctx.sift_batch(synth.frames(3, 640, 480, seed0=7))
+        kh, dh, oh = (x.cpu().numpy() for x in g)
+        ok = g[0].is_cuda and len(oh) == 4 and int(oh[-1]) == sum(len(r) for r in ref)
+        for i in range(3):
+            a, b = int(oh[i]), int(oh[i + 1])
+            ok = ok and np.array_equal(kh[a:b], ref[i].keypoints_array) and np.array_equal(dh[a:b], ref[i].descriptors)
+        # the bench's max-over-ranks reduction as a real RCCL all-reduce
+        x = torch.tensor([1.5], dtype=torch.float64, device="cuda")
+        dist.all_reduce(x, op=dist.ReduceOp.MAX)
+        ok = ok and float(x.item()) == 1.5
+        q.put(("ok", 0, bool(ok)))
+        ctx.close()
+    except Exception as e:  # pragma: no cover - surfaced by the assert below
+        q.put(("err", 0, repr(e)))
+    finally:
+        dist.destroy_process_group()
+
+
+@pytest.mark.gpu
+@pytest.mark.timeout(120)
+def test_nccl_world1_gather_device_results(pkg):
+    """The RCCL (backend "nccl") side of the N > 1 path on the one card a
+    test box has: a one-rank process group initialised the way bench.py does
+    (device_id given), the size all-gather of gather_device_results, a
+    barrier and an all-reduce on device tensors; the gathered device results
+    equal sift_batch's.  (Two ranks cannot share one GPU under RCCL; the
+    point-to-point rows are covered on gloo by the test above.)"""
+    import multiprocessing as mp
+    mpc = mp.get_context("spawn")
+    q = mpc.Queue()
+    p = mpc.Process(target=_nccl_worker, args=(_free_port(), q))
+    p.start()
+    res = q.get(timeout=110)
+    p.join(timeout=30)
+    assert p.exitcode == 0
+    assert res[0] == "ok" and res[2], res
+
+
 @pytest.mark.gpu
 def test_batch_tail_planes_exact(pkg, oracle):
     """A one-chunk batch of 6 frames: every octave's planes of frames 0 and
