@@ -1966,6 +1966,25 @@ int launch_seed_pair(int rs, int rb, const SeedLaunch& S, const BlurLaunch& B, h
 // columns), so its reads of A and writes of T hit distinct banks; the column
 // pass maps lanes along a row.
 // ---------------------------------------------------------------------------
+// Phase timestamps of workgroup 0's thread 0 (s_memrealtime / s_memtime)
+// for tools/ubench_kernels built with -DSIFT_TAIL_PROF (tools/ubench_tailprof);
+// the product build does not define it and the marks compile to nothing
+#ifdef SIFT_TAIL_PROF
+__device__ unsigned long long g_tail_prof[2048];
+__shared__ int tail_prof_n;
+#define TAIL_MARK(tag)                                                                                  \
+    do {                                                                                                \
+        if (threadIdx.x == 0 && blockIdx.x == 0 && tail_prof_n < 1024) {                                \
+            g_tail_prof[2 * tail_prof_n] = wall_clock64();                                              \
+            g_tail_prof[2 * tail_prof_n + 1] = (unsigned long long)(tag) | ((unsigned long long)clock64() << 8); \
+            tail_prof_n++;                                                                              \
+        }                                                                                               \
+    } while (0)
+#else
+#define TAIL_MARK(tag) \
+    do {               \
+    } while (0)
+#endif
 template <int P>
 __device__ __forceinline__ int tail_index(int p, int n) {
     return P == kProfileOpenCV ? reflect101(p, n) : clamp_idx(p, n);
@@ -2050,6 +2069,7 @@ __device__ __forceinline__ void tail_blur_r(float* __restrict__ A, float* __rest
         }
     }
     __syncthreads();
+    TAIL_MARK(1);
     if (!rows_direct) {  // T's halo rows [-R, 0) and [H, H + R)
         for (int i = threadIdx.x; i < 2 * R * W; i += 1024) {
             const int j = i / W, x = i - j * W;
@@ -2057,6 +2077,7 @@ __device__ __forceinline__ void tail_blur_r(float* __restrict__ A, float* __rest
             T[(p + Rm) * TP + x] = T[(tail_index<P>(p, H) + Rm) * TP + x];
         }
         __syncthreads();
+        TAIL_MARK(2);
     }
     // column pass: centre product + fma of the (below + above) pair sums
     // (OpenCV) / the unfused chain from the first tap (imageproc); item =
@@ -2117,9 +2138,11 @@ __device__ __forceinline__ void tail_blur_r(float* __restrict__ A, float* __rest
         }
     }
     __syncthreads();
+    TAIL_MARK(3);
     if (Rn > 0 && !cols_direct) {  // B's halo columns for the next blur
         tail_fill_cols<P>(B, W, H, Rm, Rn);
         __syncthreads();
+        TAIL_MARK(4);
     }
 }
 
@@ -2154,7 +2177,12 @@ __global__ __launch_bounds__(1024) void k_octave_tail(const TailLaunch L) {
     const int b = (int)blockIdx.x;
     int Rm = 0;
     for (int s = 1; s < kImagesPerOctave; s++) Rm = max(Rm, L.r[s]);
+#ifdef SIFT_TAIL_PROF
+    if (tid == 0) tail_prof_n = 0;
+    TAIL_MARK(0);
+#endif
     for (int o = L.o0; o < L.n_oct; o++) {
+        TAIL_MARK(10 + o);
         const int W = L.ow[o], H = L.oh[o], pitch = L.pitch[o], PA = tail_pa(W, Rm);
         float* A = lds;                         // G_{s-1}
         float* B = A + PA * H;                  // G_s
@@ -2191,8 +2219,10 @@ __global__ __launch_bounds__(1024) void k_octave_tail(const TailLaunch L) {
             }
         }
         __syncthreads();
+        TAIL_MARK(5);
         tail_fill_cols<P>(A, W, H, Rm, L.r[1]);
         __syncthreads();
+        TAIL_MARK(6);
 #pragma unroll 1
         for (int s = 1; s < kImagesPerOctave; s++) {
             tail_blur<P>(A, T, B, L.taps[s], L.r[s], s + 1 < kImagesPerOctave ? L.r[s + 1] : 0, Rm, W, H,
@@ -2202,6 +2232,7 @@ __global__ __launch_bounds__(1024) void k_octave_tail(const TailLaunch L) {
             B = t;
         }
     }
+    TAIL_MARK(99);
 }
 
 int tail_octave_start(const int* ow, const int* oh, int n_oct, const int* radii) {

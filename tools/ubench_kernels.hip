@@ -209,6 +209,28 @@ void bench_tail(int N) {
         CK(hipEventElapsedTime(&ms, a, b));
         return ms / 10;
     };
+#ifdef SIFT_TAIL_PROF
+    {
+        L.o0 = 5;
+        L.n_oct = 10;
+        for (int rep = 0; rep < 3; rep++) {
+            launch_octave_tail(L, 0);
+            CK(hipDeviceSynchronize());
+        }
+        std::vector<unsigned long long> pr(2048);
+        CK(hipMemcpyFromSymbol(pr.data(), HIP_SYMBOL(g_tail_prof), 2048 * 8));
+        std::printf("tail phases (workgroup 0, 100 MHz clock, us since start): tag dt\n");
+        unsigned long long t0 = pr[0], tp = pr[0], cp = pr[1] >> 8;
+        for (int k = 0; k < 1024; k++) {
+            const unsigned long long t = pr[2 * k], tag = pr[2 * k + 1] & 255, c = pr[2 * k + 1] >> 8;
+            std::printf("  %3llu %7.2f  +%5.2f us  +%6llu clk  (%.2f GHz)\n", tag, (t - t0) / 100.0, (t - tp) / 100.0,
+                        c - cp, t > tp ? (c - cp) / ((t - tp) * 10.0) : 0.0);
+            tp = t;
+            cp = c;
+            if (tag == 99) break;
+        }
+    }
+#endif
     std::printf("octave tail, %d frames (1080p seed geometry)\n", N);
     std::printf("  octaves 5..9: %8.1f us\n", 1e3 * timeit(5, 10));
     for (int o = 5; o < 10; o++) std::printf("  octave %d alone (%dx%d): %8.1f us\n", o, L.ow[o], L.oh[o], 1e3 * timeit(o, o + 1));
