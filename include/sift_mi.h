@@ -190,8 +190,12 @@ typedef enum {
     SIFT_MI_PATH_BD_PAIR = 13,     /* the fused blur 5 + extremum scan with two column strips per lane
                                       (packed f32): 1 (default) / 2 its two loop forms, 0 the one-column
                                       kernel */
-    SIFT_MI_PATH_BD_WAVES = 14     /* the pair kernel's fewest waves per launch when choosing its row
+    SIFT_MI_PATH_BD_WAVES = 14,    /* the pair kernel's fewest waves per launch when choosing its row
                                       segments, 1024..65536 */
+    SIFT_MI_PATH_CHUNK_MODE = 15   /* automatic chunking: 1 (default) as few chunks as ~64 GB of pyramid
+                                      and ~1062 M seed pixels per chunk allow (128 x 1080p: one chunk);
+                                      0 at least two chunks per multi-frame call (both pipeline lanes
+                                      busy), <= ~32 GB / ~531 M seed pixels each (rounds 1-5) */
 } sift_mi_path_option;
 int sift_mi_set_path_option(sift_mi_ctx* ctx, int option, int value);
 

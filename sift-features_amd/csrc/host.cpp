@@ -583,8 +583,14 @@ int set_device(sift_mi_ctx* c) {
     return 0;
 }
 
-uint32_t auto_chunk(const Plan& p_probe_w_h, uint32_t w, uint32_t h, uint32_t n) {
+uint32_t auto_chunk(const Plan& p_probe_w_h, uint32_t w, uint32_t h, uint32_t n, int mode) {
     (void)p_probe_w_h;
+    // mode 1 (path option chunk_mode, the default since round 6): twice the
+    // caps below and no forced second chunk -- a 128-frame 1080p call is one
+    // chunk.  Against mode 0's two overlapped 64-frame chunks: 34.49-34.53 vs
+    // 34.12-34.43 M keypoints/s, VGA 256 30.32-30.43 vs 30.00-30.21 M
+    // (profiles/r06_ab_runs.md): each stage's launches twice as large beat
+    // the overlap of two half-size chunks.
     // Up to ~32 GB of pyramid per chunk (two lanes: ~64 GB of the 288 GB HBM)
     // and at most kMaxChunk frames, in balanced chunks, at least two when the
     // batch has two frames (the lanes overlap consecutive chunks).  Bigger
@@ -599,14 +605,15 @@ uint32_t auto_chunk(const Plan& p_probe_w_h, uint32_t w, uint32_t h, uint32_t n)
         oh /= 2;
     }
     const double per_frame = 44.0 * sum_p;
-    uint32_t cmax = (uint32_t)std::max(1.0, std::floor(32e9 / per_frame));
+    const double scale = mode == 1 ? 2.0 : 1.0;
+    uint32_t cmax = (uint32_t)std::max(1.0, std::floor(scale * 32e9 / per_frame));
     // and ~531 M seed pixels (64 frames at 1080p): smaller frames get more
     // frames per chunk, so their octave launches are as large (VGA: 256
     // frames in two chunks of 128 instead of four of 64)
     const double seed_px = 4.0 * w * h;
-    cmax = std::min<uint32_t>(cmax, (uint32_t)std::max(1.0, std::floor(64.0 * 3840.0 * 2160.0 / seed_px)));
+    cmax = std::min<uint32_t>(cmax, (uint32_t)std::max(1.0, std::floor(scale * 64.0 * 3840.0 * 2160.0 / seed_px)));
     cmax = std::min<uint32_t>(cmax, 256);
-    uint32_t k = std::max<uint32_t>((n + cmax - 1) / cmax, n >= 2 ? 2u : 1u);  // chunks
+    uint32_t k = std::max<uint32_t>((n + cmax - 1) / cmax, (n >= 2 && mode != 1) ? 2u : 1u);  // chunks
     return std::max<uint32_t>(1, (n + k - 1) / k);
 }
 
@@ -1739,7 +1746,7 @@ int extract_device(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, 
     if (c->band_n > 1 && limit >= 0)
         return fail(SIFT_MI_EINVAL, "features_limit ranks a whole frame's keypoints: apply it after merging row bands");
     const uint32_t chunk =
-        std::min(kMaxChunk, c->chunk_override ? std::min(c->chunk_override, n) : auto_chunk(c->plan, w, h, n));
+        std::min(kMaxChunk, c->chunk_override ? std::min(c->chunk_override, n) : auto_chunk(c->plan, w, h, n, c->opts.chunk_mode));
     CHK(ensure_plan(c, w, h, chunk));
     c->have_pyramid = false;
     c->n_result = 0;
@@ -2104,6 +2111,7 @@ int sift_mi_set_path_option(sift_mi_ctx* c, int option, int value) {
         case SIFT_MI_PATH_ONESWEEP: if (value < 0 || value > 2) break; o.onesweep = value; return 0;
         case SIFT_MI_PATH_BD_PAIR: if (value < 0 || value > 2) break; o.bd_pair = value; return 0;
         case SIFT_MI_PATH_BD_WAVES: if (value < 1024 || value > 65536) break; o.bd_waves = value; return 0;
+        case SIFT_MI_PATH_CHUNK_MODE: if (value < 0 || value > 1) break; o.chunk_mode = value; return 0;
         default: return fail(SIFT_MI_EINVAL, "unknown path option");
     }
     return fail(SIFT_MI_EINVAL, "path option value out of range");

@@ -63,6 +63,7 @@ struct PathOpts {
     int bd_pair = 1;       // k_blur_detect_pair (two column strips per lane, packed f32): 1 its steady loop
                            // unrolled by 12 rows, 2 by 4; 0 the one-column k_blur_detect
     int bd_waves = 8192;   // k_blur_detect_pair: fewest waves per launch at the chosen row segments
+    int chunk_mode = 1;    // automatic chunking (SIFT_MI_PATH_CHUNK_MODE)
     int onesweep = 0;      // emission-order sorts with rocprim's Onesweep: 1 always, 0 never (the
                            // library default path), 2 for bounds >= kOnesweepMinKeys
 };

@@ -270,7 +270,8 @@ class Context:
                     "fused_detect": (4, 1), "early": (5, 1), "desc_first": (6, 1), "graph": (7, 0),
                     "band_drift": (8, 24), "bound_shrink": (9, 1),
                     "large_first": (11, 1),
-                    "onesweep": (12, 0), "bd_pair": (13, 1), "bd_waves": (14, 8192)}
+                    "onesweep": (12, 0), "bd_pair": (13, 1), "bd_waves": (14, 8192),
+                    "chunk_mode": (15, 1)}
 
     def set_path_option(self, name, value):
         """One kernel-path switch (sift_mi_set_path_option), e.g.

@@ -2,15 +2,15 @@
 
 * config #2: one 1920x1080 frame, `sift()` vs the oracle directly;
 * config #3: 256 x 640x480 frames through the device-resident batch path
-  (`sift_batch_device(..., fetch=False)`: 2 chunks of 128 -- chunks are
-  sized by seed pixels, ~531 M per chunk -- over both pipeline lanes),
-  frames spread over both chunks (the last included) vs the oracle, every
-  frame vs per-frame `sift()`;
+  (`sift_batch_device(..., fetch=False)`: one chunk of 256 under the default
+  automatic chunking, or -- chunk_mode 0 -- 2 chunks of 128 over both
+  pipeline lanes), frames spread over the chunks (the last included) vs the
+  oracle, every frame vs per-frame `sift()`;
 * chunks of more than 64 frames with a features_limit (the per-frame output
   plan is one 256-thread workgroup, k_limit_plan);
 * config #4, one GPU's shard: bench.py's exact call (128 x 1920x1080, auto
-  chunks, results kept in HBM), 2 frames vs the oracle, every frame vs
-  per-frame `sift()`;
+  chunks -- one of 128, or two of 64 under chunk_mode 0 -- results kept in
+  HBM), 2 frames vs the oracle, every frame vs per-frame `sift()`;
 * the stage-bound overflow re-run (host.cpp finalize_chunk rc == 1): with
   path option bound_shrink every chunk enqueued before a high-water mark exists
   overflows; the re-run chunks must equal per-frame results.
@@ -71,18 +71,21 @@ def test_config2_single_1080p(pkg, ctx, oracle):
     assert_parity(pkg, res, kp_o, desc_o, ext_o)
 
 
-def test_config3_vga_256_device(pkg, ctx, oracle):
+@pytest.mark.parametrize("chunk_mode", [1, 0])
+def test_config3_vga_256_device(pkg, ctx, oracle, chunk_mode):
     import synth
     import torch
     t = synth.frames_torch(256, 640, 480, seed0=0, device="cuda")
     torch.cuda.synchronize()
     host = t.cpu().numpy()
-    c, offs, kp, desc = _device_batch(pkg, t)
+    c = pkg.Context(0, pkg.OpenCVProcessing)
+    c.set_path_option("chunk_mode", chunk_mode)
+    c, offs, kp, desc = _device_batch(pkg, t, c)
     st = c.stats()
     assert st["frames"] == 256
     c.close()
     assert np.all(np.diff(offs) > 0)
-    for i in (0, 63, 64, 127, 128, 200, 255):  # both 128-frame chunks (lanes), the last frame
+    for i in (0, 63, 64, 127, 128, 200, 255):  # both 128-frame chunks (mode 0: lanes), the last frame
         a, b = int(offs[i]), int(offs[i + 1])
         kp_o, desc_o = oracle.sift(host[i])
         _parity_rows(kp[a:b], desc[a:b], kp_o, desc_o)
@@ -93,14 +96,18 @@ def test_config3_vga_256_device(pkg, ctx, oracle):
         assert np.array_equal(desc[a:b], r.descriptors), i
 
 
-def test_config4_bench_shard_1080p(pkg, ctx, oracle):
-    """bench.py's step: 128 device-resident 1080p frames, auto chunks (two
-    64-frame chunks, one per lane), results kept in the device arena."""
+@pytest.mark.parametrize("chunk_mode", [1, 0])
+def test_config4_bench_shard_1080p(pkg, ctx, oracle, chunk_mode):
+    """bench.py's step: 128 device-resident 1080p frames, auto chunks (one
+    128-frame chunk; chunk_mode 0: two 64-frame chunks, one per lane),
+    results kept in the device arena."""
     import synth
     import torch
     t = synth.frames_torch(128, 1920, 1080, seed0=0, device="cuda")
     torch.cuda.synchronize()
-    c, offs, kp, desc = _device_batch(pkg, t)
+    c = pkg.Context(0, pkg.OpenCVProcessing)
+    c.set_path_option("chunk_mode", chunk_mode)
+    c, offs, kp, desc = _device_batch(pkg, t, c)
     c.close()
     host = t.cpu().numpy()
     del t

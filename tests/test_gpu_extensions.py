@@ -146,6 +146,7 @@ def test_path_option_validation_and_restore(pkg):
         assert L.sift_mi_set_path_option(c._h, 10, 0) != 0  # split tail: retired
         assert L.sift_mi_set_path_option(c._h, 13, 3) != 0  # bd_pair: 0..2
         assert L.sift_mi_set_path_option(c._h, 14, 100) != 0  # bd_waves: 1024..65536
+        assert L.sift_mi_set_path_option(c._h, 15, 2) != 0  # chunk_mode: 0..1
         assert L.sift_mi_set_path_option(c._h, 99, 0) != 0
         c.set_path_option("graph", 1)
         c.set_path_option("bd_waves", 4096)
@@ -154,5 +155,25 @@ def test_path_option_validation_and_restore(pkg):
         assert c.path_option("graph") == 1
         assert c.path_option("bd_pair") == pkg.Context.PATH_OPTIONS["bd_pair"][1]
         assert c.path_option("bd_waves") == 4096
+    finally:
+        c.close()
+
+
+@pytest.mark.gpu
+def test_chunk_mode_results_equal(pkg):
+    """Automatic chunking mode 1 (as few chunks as memory allows: the five
+    640x480 frames in one chunk instead of 3 + 2 over both lanes) returns
+    the same keypoints and descriptors, frame for frame."""
+    import synth
+    fr = synth.frames(5, 640, 480, seed0=40)
+    c = pkg.Context(0, pkg.OpenCVProcessing)
+    try:
+        ref = c.sift_batch(fr)
+        with c.path_options(chunk_mode=1):
+            got = c.sift_batch(fr)
+        assert len(ref) == len(got) == 5
+        for a, b in zip(ref, got):
+            assert np.array_equal(a.keypoints_array, b.keypoints_array)
+            assert np.array_equal(a.descriptors, b.descriptors)
     finally:
         c.close()

@@ -107,7 +107,8 @@ def test_read_batch_scale_space_state(pkg):
     import synth
     fr = synth.frames(4, 96, 64, seed0=3)
     c = pkg.Context(0, pkg.OpenCVProcessing)
-    c.sift_batch(fr)  # auto chunking: two chunks over both lanes
+    c.set_path_option("chunk_mode", 0)
+    c.sift_batch(fr)  # auto chunking (mode 0): two chunks over both lanes
     with pytest.raises(pkg.SiftMiError):
         c.read_batch_scale_space(0, 0, (192, 128))
     c.sift(fr[0])

@@ -117,9 +117,11 @@ n_oct = int(round(math.log2(min(2 * W, 2 * H)) - 2)) + 1
 dims = [((2 * W) >> o, (2 * H) >> o) for o in range(n_oct)]
 sum_p = sum(w * h for w, h in dims)
 algo_pf = W * H + 44 * sum_p  # u8 read once, G_0..G_5 + D_0..D_4 written once
-cmax = min(256, max(1, int(32e9 // (44.0 * sum_p))),  # host auto_chunk
-           max(1, int(64.0 * 3840 * 2160 // (4.0 * W * H))))
-nck = max(-(-FRAMES // cmax), 2 if FRAMES >= 2 else 1)
+CHUNK_MODE = int(os.environ.get("CHUNK_MODE", "1"))  # host auto_chunk, path option chunk_mode
+scale = 2.0 if CHUNK_MODE == 1 else 1.0
+cmax = min(256, max(1, int(scale * 32e9 // (44.0 * sum_p))),
+           max(1, int(scale * 64.0 * 3840 * 2160 // (4.0 * W * H))))
+nck = max(-(-FRAMES // cmax), 2 if FRAMES >= 2 and CHUNK_MODE != 1 else 1)
 chunk = -(-FRAMES // nck)
 
 pos = defaultdict(list)     # launch position in the chunk (enqueue order) -> (start, duration) (us)
