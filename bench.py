@@ -477,6 +477,9 @@ def main():
             "config": {"workload": f"batch of {B} x {W}x{H} u8 frames per GPU (configs[3] shard), full sift()",
                        "frames_per_gpu": B, "frame": f"{W}x{H}", "octaves": n_oct, "profile": "opencv",
                        "parallelism": f"dp{world} (frames sharded, no collective)",
+                       "chunking": (f"--chunk {args.chunk}" if args.chunk else
+                                    "auto (path option chunk_mode, default 1: as few chunks as ~64 GB of pyramid "
+                                    "allows; 128 x 1080p runs as one chunk)"),
                        **({"path_options": dict(PATH_OPTS)} if PATH_OPTS else {}),
                        **({"rehearsal": "every rank on cuda:0, gloo transport: not a measurement"}
                           if args.rehearse_one_gpu else {})},
