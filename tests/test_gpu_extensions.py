@@ -177,3 +177,22 @@ def test_chunk_mode_results_equal(pkg):
             assert np.array_equal(a.descriptors, b.descriptors)
     finally:
         c.close()
+
+
+@pytest.mark.gpu
+def test_chunk_mode1_multi_chunk_lanes(pkg, ctx):
+    """Under the default automatic chunking (mode 1) a call larger than one
+    chunk still splits into balanced chunks over both pipeline lanes: 300
+    tiny frames exceed the 256-frame cap (two chunks of 150); every frame
+    equals its per-frame sift()."""
+    import synth
+    fr = synth.frames(300, 64, 48, seed0=900)
+    c = pkg.Context(0, pkg.OpenCVProcessing)
+    try:
+        got = c.sift_batch(fr)
+        st = c.stats()
+    finally:
+        c.close()
+    assert st["frames"] == 300
+    ref = [ctx.sift(f) for f in fr]
+    assert all(a == b for a, b in zip(got, ref))
