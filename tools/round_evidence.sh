@@ -1,5 +1,5 @@
 #!/bin/bash
-# round-6 evidence (run via gpurun): the default bench line, then the round
+# Round evidence (run via gpurun): the default bench line, then the round
 # profile (trace + PMC passes) of the same workload
 cd "$GRAFT_REPO_ROOT" || exit 2
 mkdir -p gpurun_out
@@ -10,5 +10,5 @@ d=json.loads(sys.stdin.readline())
 print('value', d['value'], 'ms', d['ms_per_step'], 'frac', d['roofline']['frac'], 'stages', d['stage_ms_per_step'])
 print('latency', d.get('latency_1frame_ms'), 'cpu', d['cpu_baseline'])
 print('configs', json.dumps(d.get('configs'))[:1500])"
-bash tools/round_profile.sh r06 128 || exit 1
-head -12 gpurun_out/rp_r06/summary.md
+bash tools/round_profile.sh ${1:-r06} 128 || exit 1
+head -12 gpurun_out/rp_${1:-r06}/summary.md
