@@ -583,7 +583,7 @@ int set_device(sift_mi_ctx* c) {
     return 0;
 }
 
-uint32_t auto_chunk(const Plan& p_probe_w_h, uint32_t w, uint32_t h, uint32_t n, int mode) {
+uint32_t auto_chunk(const Plan& p_probe_w_h, uint32_t w, uint32_t h, uint32_t n, int mode, double avail_bytes) {
     (void)p_probe_w_h;
     // mode 1 (path option chunk_mode, the default since round 6): twice the
     // caps below and no forced second chunk -- a 128-frame 1080p call is one
@@ -607,6 +607,10 @@ uint32_t auto_chunk(const Plan& p_probe_w_h, uint32_t w, uint32_t h, uint32_t n,
     const double per_frame = 44.0 * sum_p;
     const double scale = mode == 1 ? 2.0 : 1.0;
     uint32_t cmax = (uint32_t)std::max(1.0, std::floor(scale * 32e9 / per_frame));
+    // and at most 40% of the device memory this context could use (free +
+    // its own arenas) per chunk: the two lanes' arenas stay below 80% however
+    // much other work holds (no effect on an idle 288 GB MI355X)
+    if (avail_bytes > 0) cmax = std::min<uint32_t>(cmax, (uint32_t)std::max(1.0, std::floor(0.4 * avail_bytes / per_frame)));
     // and ~531 M seed pixels (64 frames at 1080p): smaller frames get more
     // frames per chunk, so their octave launches are as large (VGA: 256
     // frames in two chunks of 128 instead of four of 64)
@@ -679,7 +683,12 @@ int ensure_plan(sift_mi_ctx* c, uint32_t w, uint32_t h, uint32_t chunk) {
         p.goff[o] = total;
         total += (size_t)chunk * kImagesPerOctave * p.P[o];
         p.doff[o] = total;
-        total += (size_t)chunk * kDogPerOctave * p.P[o];
+        // D_0..D_4 for ONE frame: only precompute_images materialises the
+        // DoG (run_pyramid's `full`, one frame on lane 0); the batch path
+        // forms D where it reads it.  (Rounds 1-5 reserved them per chunk
+        // frame: 5 / 11 of the arena never written -- 28 GB per lane at 128 x
+        // 1080p.)
+        total += (size_t)kDogPerOctave * p.P[o];
         total = (total + 63) & ~(size_t)63;  // 256-B aligned octave arenas
         if (o + 1 < p.n_oct) {
             // nearest 1/2 must be source pixel (2x, 2y) (OpenCV INTER_NEAREST)
@@ -798,6 +807,7 @@ void flush_chunk_init(sift_mi_ctx* c, int si);
 int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_pitch, size_t row_stride,
                 uint32_t n, bool full, int detect_slot = -1, int cand_slot = -1) {
     Plan& p = c->plan;
+    if (full && n != 1) return fail(SIFT_MI_EINVAL, "the DoG planes are materialised for one frame");
     hipStream_t st = lane_stream(c, lane);
     lane = arena_of(c, lane);
     hipStream_t aux = c->aux[lane];
@@ -958,7 +968,7 @@ int run_pyramid(sift_mi_ctx* c, int lane, const uint8_t* d_frames, size_t frame_
         for (int o = o0; o < o1; o++) {
             bool g3_signalled = false;
             float* G = p.gauss(o, lane) + (size_t)f0 * p.gstride(o);
-            float* D = p.dog(o, lane) + (size_t)f0 * p.dstride(o);
+            float* D = full ? p.dog(o, lane) + (size_t)f0 * p.dstride(o) : nullptr;  // one frame's D (ensure_plan)
             const size_t P = p.P[o];
             // octave 0 after k_seed_pair starts at blur 2
             for (int s = (o == 0 && seed_pair) ? 2 : 1; s < kImagesPerOctave; s++) {
@@ -1745,8 +1755,14 @@ int extract_device(sift_mi_ctx* c, const uint8_t* d_frames, size_t frame_pitch, 
     }
     if (c->band_n > 1 && limit >= 0)
         return fail(SIFT_MI_EINVAL, "features_limit ranks a whole frame's keypoints: apply it after merging row bands");
-    const uint32_t chunk =
-        std::min(kMaxChunk, c->chunk_override ? std::min(c->chunk_override, n) : auto_chunk(c->plan, w, h, n, c->opts.chunk_mode));
+    double avail = 0;  // device memory this context could hold: free + its own arenas
+    if (!c->chunk_override && n > 1) {  // (one frame is one chunk: no query on the latency path)
+        size_t free_b = 0, total_b = 0;
+        if (hipMemGetInfo(&free_b, &total_b) == hipSuccess)
+            avail = (double)free_b + 4.0 * ((double)c->plan.arena[0].cap + (double)c->plan.arena[1].cap);
+    }
+    const uint32_t chunk = std::min(kMaxChunk, c->chunk_override ? std::min(c->chunk_override, n)
+                                                                 : auto_chunk(c->plan, w, h, n, c->opts.chunk_mode, avail));
     CHK(ensure_plan(c, w, h, chunk));
     c->have_pyramid = false;
     c->n_result = 0;
