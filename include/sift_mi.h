@@ -193,9 +193,11 @@ typedef enum {
     SIFT_MI_PATH_BD_WAVES = 14,    /* the pair kernel's fewest waves per launch when choosing its row
                                       segments, 1024..65536 */
     SIFT_MI_PATH_CHUNK_MODE = 15   /* automatic chunking: 1 (default) as few chunks as ~64 GB of pyramid
-                                      and ~1062 M seed pixels per chunk allow (128 x 1080p: one chunk);
-                                      0 at least two chunks per multi-frame call (both pipeline lanes
-                                      busy), <= ~32 GB / ~531 M seed pixels each (rounds 1-5) */
+                                      (counted at 44 B per octave pixel) and ~1062 M seed pixels per chunk
+                                      allow (128 x 1080p: one chunk); 0 at least two chunks per
+                                      multi-frame call (both pipeline lanes busy), <= ~32 GB / ~531 M
+                                      seed pixels each (rounds 1-5).  Either way a chunk is capped at
+                                      40% of the device memory the context could use */
 } sift_mi_path_option;
 int sift_mi_set_path_option(sift_mi_ctx* ctx, int option, int value);
 
